@@ -1,0 +1,385 @@
+// Reference harness (TEST INFRASTRUCTURE ONLY).
+//
+// Drives the *reference* CPU executor path of shacklettbp/gpu-ecs-madrona
+// (compiled from the untouched sources under /root/reference by
+// oracle/Makefile.ref) in single-world mode, which is the only mode in which
+// the reference physics reads the right columns.  Every
+// world owns a StateManager + StateCache + TaskGraph, exactly the recipe of
+// SURVEY.md Appendix B.  The world definition below is the "collisions"
+// physics workload of SURVEY.md §8(d) written against the reference's own
+// registration API (registerTypes / setupTasks / world ctor).
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load
+// the resulting oracle/_ref/libmadrona_ref.so.  Nothing here is product code.
+
+#include <madrona/taskgraph.hpp>
+#include <madrona/custom_context.hpp>
+#include <madrona/components.hpp>
+#include <madrona/physics.hpp>
+#include <madrona/state.hpp>
+
+#include "core/worker_init.hpp"
+#include "physics/physics_impl.hpp"
+
+#include <cfloat>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+using namespace madrona;
+using namespace madrona::math;
+using namespace madrona::base;
+using namespace madrona::phys;
+
+namespace refh {
+
+// Body archetype: column order is the reference physics ABI (Cols 1..12,
+// include/madrona/physics.hpp:449-464).
+struct PhysicsBody : Archetype<
+    Position, Rotation, Scale, Velocity, ObjectID, ResponseType,
+    solver::SubstepPrevState, solver::PreSolvePositional,
+    solver::PreSolveVelocity, ExternalForce, ExternalTorque,
+    broadphase::LeafID> {};
+
+struct RefPhysConfig {
+    int32_t numCubes;
+    int32_t numSubsteps;
+    float deltaT;
+    float gravityZ;
+    int32_t maxContacts;
+    float cubeInvMass;
+    float cubeInvInertia;
+    float muS;
+    float muD;
+};
+
+struct WorldInit {
+    const float *pos;   // numCubes * 3
+    const float *rot;   // numCubes * 4 (w, x, y, z)
+};
+
+class Engine;
+
+struct PhysWorld : public WorldBase {
+    PhysWorld(Engine &ctx, ObjectManager *mgr, const RefPhysConfig &cfg,
+              const WorldInit &init);
+};
+
+class Engine : public CustomContext<Engine, PhysWorld> {
+public:
+    using CustomContext::CustomContext;
+};
+
+static void registerWorldTypes(ECSRegistry &reg)
+{
+    base::registerTypes(reg);
+    RigidBodyPhysicsSystem::registerTypes(reg);
+    reg.registerArchetype<PhysicsBody>();
+}
+
+static void setupTasks(TaskGraph::Builder &builder, int32_t num_substeps)
+{
+    auto bp = RigidBodyPhysicsSystem::setupBroadphaseTasks(builder, {});
+    auto sub = RigidBodyPhysicsSystem::setupSubstepTasks(builder, {bp},
+                                                         num_substeps);
+    RigidBodyPhysicsSystem::setupCleanupTasks(builder, {sub});
+}
+
+PhysWorld::PhysWorld(Engine &ctx, ObjectManager *mgr,
+                     const RefPhysConfig &cfg, const WorldInit &init)
+    : WorldBase(ctx)
+{
+    RigidBodyPhysicsSystem::init(ctx, mgr, cfg.deltaT, cfg.numSubsteps,
+        Vector3 { 0.f, 0.f, cfg.gravityZ }, cfg.numCubes + 1,
+        cfg.maxContacts, 16);
+
+    auto setup = [&](Entity e, Vector3 p, Quat q, int32_t obj,
+                     ResponseType rt) {
+        ctx.getUnsafe<Position>(e) = Position { p };
+        ctx.getUnsafe<Rotation>(e) = Rotation { q };
+        ctx.getUnsafe<Scale>(e) = Scale { Diag3x3 { 1.f, 1.f, 1.f } };
+        ctx.getUnsafe<Velocity>(e) = Velocity { Vector3::zero(),
+                                                Vector3::zero() };
+        ctx.getUnsafe<ObjectID>(e) = ObjectID { obj };
+        ctx.getUnsafe<ResponseType>(e) = rt;
+        ctx.getUnsafe<solver::SubstepPrevState>(e) = { p, q };
+        ctx.getUnsafe<solver::PreSolvePositional>(e) = { p, q };
+        ctx.getUnsafe<solver::PreSolveVelocity>(e) = {
+            Vector3::zero(), Vector3::zero() };
+        ctx.getUnsafe<ExternalForce>(e) = ExternalForce { Vector3::zero() };
+        ctx.getUnsafe<ExternalTorque>(e) = ExternalTorque { Vector3::zero() };
+        ctx.getUnsafe<broadphase::LeafID>(e) =
+            RigidBodyPhysicsSystem::registerEntity(ctx, e, ObjectID { obj });
+    };
+
+    for (int32_t i = 0; i < cfg.numCubes; i++) {
+        Entity e = ctx.makeEntityNow<PhysicsBody>();
+        Vector3 p { init.pos[3 * i], init.pos[3 * i + 1], init.pos[3 * i + 2] };
+        Quat q { init.rot[4 * i], init.rot[4 * i + 1], init.rot[4 * i + 2],
+                 init.rot[4 * i + 3] };
+        setup(e, p, q, 0, ResponseType::Dynamic);
+    }
+
+    Entity plane = ctx.makeEntityNow<PhysicsBody>();
+    setup(plane, Vector3::zero(), Quat { 1.f, 0.f, 0.f, 0.f }, 1,
+          ResponseType::Static);
+
+    ctx.getSingleton<broadphase::BVH>().rebuildOnUpdate();
+}
+
+// Object table: object 0 = cube hull (half extent 1), object 1 = plane.
+static ObjectManager * makeObjectManager(const RefPhysConfig &cfg)
+{
+    auto *mgr = new ObjectManager {};
+    mgr->metadata = new RigidBodyMetadata[2];
+    mgr->aabbs = new AABB[2];
+    mgr->primitives = new CollisionPrimitive[2];
+
+    const Vector3 verts[8] = {
+        { -1, -1, -1 }, {  1, -1, -1 }, {  1,  1, -1 }, { -1,  1, -1 },
+        { -1, -1,  1 }, {  1, -1,  1 }, {  1,  1,  1 }, { -1,  1,  1 },
+    };
+    const uint32_t faces[6][4] = {
+        { 0, 3, 2, 1 }, { 4, 5, 6, 7 }, { 0, 1, 5, 4 },
+        { 3, 7, 6, 2 }, { 0, 4, 7, 3 }, { 1, 2, 6, 5 },
+    };
+
+    geometry::FastPolygonList pl {};
+    pl.allocate(6 * 5);
+    pl.polygonCount = 0;
+    pl.edgeCount = 0;
+    for (int f = 0; f < 6; f++) {
+        pl.addPolygon(Span<const uint32_t>(faces[f], 4));
+    }
+
+    mgr->primitives[0].type = CollisionPrimitive::Type::Hull;
+    mgr->primitives[0].hull.halfEdgeMesh.construct(pl, 8, verts);
+
+    mgr->metadata[0] = RigidBodyMetadata {
+        { cfg.cubeInvInertia, cfg.cubeInvInertia, cfg.cubeInvInertia },
+        cfg.cubeInvMass, cfg.muS, cfg.muD,
+    };
+    mgr->aabbs[0] = AABB { { -1, -1, -1 }, { 1, 1, 1 } };
+
+    mgr->primitives[1].type = CollisionPrimitive::Type::Plane;
+    mgr->metadata[1] = RigidBodyMetadata {
+        { 0.f, 0.f, 0.f }, 0.f, cfg.muS, cfg.muD,
+    };
+    mgr->aabbs[1] = AABB {
+        { -FLT_MAX, -FLT_MAX, -FLT_MAX },
+        { FLT_MAX, FLT_MAX, 0.f },
+    };
+
+    return mgr;
+}
+
+struct RefWorld {
+    StateManager sm;
+    StateCache sc;
+    PhysWorld *world;
+    Engine *ctx;
+    TaskGraph *graph;
+};
+
+struct RefPhys {
+    RefPhysConfig cfg;
+    ObjectManager *mgr;
+    std::vector<RefWorld *> worlds;
+};
+
+// Mirror of broadphase::BVH's private layout (include/madrona/physics.hpp:
+// 303-396) so the harness can read node / leaf arrays without editing the
+// reference headers.
+struct BVHMirror {
+    void *nodes;
+    CountT numNodes;
+    CountT numAllocatedNodes;
+    Entity *leafEntities;
+    CollisionPrimitive **leafPrimitives;
+    AABB *leafAABBs;
+    void *leafTransforms;
+    uint32_t *leafParents;
+    int32_t *sortedLeaves;
+    AtomicI32 numLeaves;
+    int32_t numAllocatedLeaves;
+    float leafVelocityExpansion;
+    float leafAccelExpansion;
+    bool forceRebuild;
+};
+static_assert(sizeof(BVHMirror) == sizeof(broadphase::BVH));
+
+}
+
+using namespace refh;
+
+extern "C" {
+
+struct RefBodyState {
+    uint32_t gen;
+    int32_t id;
+    float pos[3];
+    float rot[4];
+    float vel[6];
+    float prevPos[3];
+    float prevRot[4];
+    float presolvePos[3];
+    float presolveRot[4];
+    float presolveVel[6];
+    int32_t leafID;
+    int32_t objID;
+    uint32_t responseType;
+};
+
+MADRONA_EXPORT void * ref_phys_create(int32_t num_worlds,
+                                      const RefPhysConfig *cfg,
+                                      const float *init_pos,
+                                      const float *init_rot)
+{
+    auto *h = new RefPhys {};
+    h->cfg = *cfg;
+    h->mgr = makeObjectManager(*cfg);
+
+    for (int32_t w = 0; w < num_worlds; w++) {
+        auto *rw = new RefWorld {};
+        ECSRegistry reg(&rw->sm, nullptr);
+        registerWorldTypes(reg);
+
+        rw->world = (PhysWorld *)::operator new(sizeof(PhysWorld));
+        rw->ctx = new Engine(rw->world, WorkerInit { &rw->sm, &rw->sc });
+
+        WorldInit init {
+            init_pos + (size_t)w * cfg->numCubes * 3,
+            init_rot + (size_t)w * cfg->numCubes * 4,
+        };
+        new (rw->world) PhysWorld(*rw->ctx, h->mgr, *cfg, init);
+
+        TaskGraph::Builder builder(*rw->ctx);
+        setupTasks(builder, cfg->numSubsteps);
+        rw->graph = new TaskGraph(builder.build());
+        h->worlds.push_back(rw);
+    }
+
+    return h;
+}
+
+MADRONA_EXPORT void ref_phys_step(void *handle, int32_t num_steps)
+{
+    auto *h = (RefPhys *)handle;
+    for (int32_t s = 0; s < num_steps; s++) {
+        for (RefWorld *rw : h->worlds) {
+            SolverData &solver = rw->ctx->getSingleton<SolverData>();
+            // Poison the contact array so a reader can tell which prefix
+            // the last substep wrote.
+            memset((void *)solver.contacts, 0xFF,
+                   sizeof(Contact) * solver.maxContacts);
+            rw->graph->run(rw->ctx);
+        }
+    }
+}
+
+MADRONA_EXPORT int32_t ref_phys_num_bodies(void *handle)
+{
+    auto *h = (RefPhys *)handle;
+    return h->cfg.numCubes + 1;
+}
+
+MADRONA_EXPORT void ref_phys_read_bodies(void *handle, int32_t world,
+                                         RefBodyState *out)
+{
+    auto *h = (RefPhys *)handle;
+    RefWorld *rw = h->worlds[world];
+    Engine &ctx = *rw->ctx;
+
+    Query<Entity, Position, Rotation, Velocity, solver::SubstepPrevState,
+          solver::PreSolvePositional, solver::PreSolveVelocity,
+          broadphase::LeafID, ObjectID, ResponseType> q =
+        ctx.query<Entity, Position, Rotation, Velocity,
+                  solver::SubstepPrevState, solver::PreSolvePositional,
+                  solver::PreSolveVelocity, broadphase::LeafID, ObjectID,
+                  ResponseType>();
+
+    int32_t idx = 0;
+    ctx.forEach(q, [&](Entity e, Position &p, Rotation &r, Velocity &v,
+                       solver::SubstepPrevState &prev,
+                       solver::PreSolvePositional &psp,
+                       solver::PreSolveVelocity &psv,
+                       broadphase::LeafID &leaf, ObjectID &obj,
+                       ResponseType &rt) {
+        RefBodyState &o = out[idx++];
+        o.gen = e.gen;
+        o.id = e.id;
+        memcpy(o.pos, &p, 12);
+        memcpy(o.rot, &r, 16);
+        memcpy(o.vel, &v, 24);
+        memcpy(o.prevPos, &prev.prevPosition, 12);
+        memcpy(o.prevRot, &prev.prevRotation, 16);
+        memcpy(o.presolvePos, &psp.x, 12);
+        memcpy(o.presolveRot, &psp.q, 16);
+        memcpy(o.presolveVel, &psv, 24);
+        o.leafID = leaf.id;
+        o.objID = obj.idx;
+        o.responseType = (uint32_t)rt;
+    });
+}
+
+// BVH snapshot: node array (116 B / node), leaf AABBs (24 B / leaf),
+// leaf parents, sorted leaves.  Returns the number of nodes.
+MADRONA_EXPORT int32_t ref_phys_read_bvh(void *handle, int32_t world,
+                                         void *nodes_out,
+                                         float *leaf_aabbs_out,
+                                         uint32_t *leaf_parents_out,
+                                         int32_t *sorted_leaves_out)
+{
+    auto *h = (RefPhys *)handle;
+    RefWorld *rw = h->worlds[world];
+    auto &bvh = rw->ctx->getSingleton<broadphase::BVH>();
+    auto *m = (BVHMirror *)&bvh;
+    int32_t num_leaves = m->numLeaves.load_relaxed();
+    if (nodes_out) {
+        memcpy(nodes_out, m->nodes, 116 * m->numNodes);
+    }
+    if (leaf_aabbs_out) {
+        memcpy(leaf_aabbs_out, m->leafAABBs, sizeof(AABB) * num_leaves);
+    }
+    if (leaf_parents_out) {
+        memcpy(leaf_parents_out, m->leafParents, 4 * num_leaves);
+    }
+    if (sorted_leaves_out) {
+        memcpy(sorted_leaves_out, m->sortedLeaves, 4 * num_leaves);
+    }
+    return (int32_t)m->numNodes;
+}
+
+// Raw contact array (maxContacts * 112 B).  Entries written by the last
+// substep form a prefix; untouched entries are 0xFF-poisoned.
+MADRONA_EXPORT int32_t ref_phys_read_contacts(void *handle, int32_t world,
+                                              void *out)
+{
+    auto *h = (RefPhys *)handle;
+    RefWorld *rw = h->worlds[world];
+    SolverData &solver = rw->ctx->getSingleton<SolverData>();
+    memcpy(out, (void *)solver.contacts, sizeof(Contact) * solver.maxContacts);
+    return (int32_t)solver.maxContacts;
+}
+
+MADRONA_EXPORT int32_t ref_sizeof(int32_t what)
+{
+    switch (what) {
+    case 0: return sizeof(Contact);
+    case 1: return sizeof(RefBodyState);
+    case 2: return sizeof(JointConstraint);
+    case 3: return sizeof(CandidateCollision);
+    default: return -1;
+    }
+}
+
+MADRONA_EXPORT void ref_phys_destroy(void *handle)
+{
+    // The reference has no teardown path for worlds that is safe to call
+    // piecemeal (TaskGraph / StateManager own raw allocations); the harness
+    // is process-scoped, so leak deliberately.
+    (void)handle;
+}
+
+}

@@ -1,0 +1,24 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _build_oracle():
+    """Build the oracle restatement (and the reference harness when the
+    reference sources are present) once per session.  CPU-only, seconds."""
+    orc = os.path.join(ROOT, "oracle", "_build", "liborc.so")
+    if not os.path.exists(orc) or os.environ.get("MW_REBUILD_ORACLE"):
+        import subprocess
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    yield

@@ -1,0 +1,60 @@
+"""Generate golden fixtures from the REFERENCE itself (oracle/_ref, built from
+/root/reference by oracle/Makefile.ref).  Run in the build container only:
+
+    make -C oracle && python tests/golden/make_golden.py
+
+Writes tests/golden/collisions_ref.npz: inputs (init positions / rotations,
+config) and the reference's outputs (per-body state after selected steps, the
+BVH after step 1, the last substep's contact prefix).  These pin both the C++
+restatement (oracle/) and, through it, the HIP path.
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+from oracle_lib import (ReferencePhys, default_phys_config,  # noqa: E402
+                        gen_collisions_inits)
+
+NUM_WORLDS = 3
+SNAP_STEPS = (1, 2, 5, 10, 30)
+CONTACT_STEPS = (1, 10, 30)
+
+
+def main():
+    cfg = default_phys_config(num_cubes=128, num_substeps=4, max_contacts=1024)
+    pos, rot = gen_collisions_inits(NUM_WORLDS, 128, seed=0)
+    ref = ReferencePhys(cfg, pos, rot)
+    out = {
+        "init_pos": pos, "init_rot": rot,
+        "cfg": np.array([cfg.numCubes, cfg.numSubsteps, cfg.maxContacts], np.int32),
+        "cfg_f": np.array([cfg.deltaT, cfg.gravityZ, cfg.cubeInvMass, cfg.cubeInvInertia,
+                           cfg.muS, cfg.muD], np.float32),
+        "snap_steps": np.array(SNAP_STEPS, np.int32),
+    }
+    step = 0
+    for target in SNAP_STEPS:
+        ref.step(target - step)
+        step = target
+        bodies = np.stack([ref.bodies(w) for w in range(NUM_WORLDS)])
+        out[f"bodies_{step}"] = bodies.view(np.uint8).reshape(NUM_WORLDS, -1)
+        if step == 1:
+            for w in range(NUM_WORLDS):
+                nodes, aabbs, parents, sorted_l = ref.bvh(w)
+                out[f"bvh_leaf_aabbs_{w}"] = aabbs
+                out[f"bvh_leaf_parents_{w}"] = parents
+                out[f"bvh_sorted_{w}"] = sorted_l
+        if step in CONTACT_STEPS:
+            for w in range(NUM_WORLDS):
+                raw = ref.contacts_raw(w)
+                n = int((raw["ref"][:, 0] != 0xFFFFFFFF).sum())
+                out[f"contacts_{step}_{w}"] = raw[:n].view(np.uint8).reshape(n, -1)
+    path = os.path.join(HERE, "collisions_ref.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+if __name__ == "__main__":
+    main()

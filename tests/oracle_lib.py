@@ -1,0 +1,196 @@
+"""ctypes bindings for the oracle libraries (TEST INFRASTRUCTURE ONLY).
+
+oracle/_build/liborc.so      -- our C++ restatement of the reference path
+oracle/_ref/libmadrona_ref.so -- the reference itself (built from /root/reference)
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORC_PATH = os.path.join(ROOT, "oracle", "_build", "liborc.so")
+REF_PATH = os.path.join(ROOT, "oracle", "_ref", "libmadrona_ref.so")
+
+
+class PhysConfig(ctypes.Structure):
+    _fields_ = [
+        ("numCubes", ctypes.c_int32),
+        ("numSubsteps", ctypes.c_int32),
+        ("deltaT", ctypes.c_float),
+        ("gravityZ", ctypes.c_float),
+        ("maxContacts", ctypes.c_int32),
+        ("cubeInvMass", ctypes.c_float),
+        ("cubeInvInertia", ctypes.c_float),
+        ("muS", ctypes.c_float),
+        ("muD", ctypes.c_float),
+    ]
+
+
+def default_phys_config(num_cubes=128, num_substeps=4, max_contacts=4096):
+    return PhysConfig(num_cubes, num_substeps, 1.0 / 60.0, -9.8, max_contacts,
+                      1.0, 1.5, 0.5, 0.5)
+
+
+# Per-body record (matches RefBodyState / OrcBodyState): 38 x 4 bytes.
+BODY_DTYPE = np.dtype([
+    ("gen", np.uint32), ("id", np.int32),
+    ("pos", np.float32, 3), ("rot", np.float32, 4), ("vel", np.float32, 6),
+    ("prevPos", np.float32, 3), ("prevRot", np.float32, 4),
+    ("presolvePos", np.float32, 3), ("presolveRot", np.float32, 4),
+    ("presolveVel", np.float32, 6),
+    ("leafID", np.int32), ("objID", np.int32), ("responseType", np.uint32),
+])
+assert BODY_DTYPE.itemsize == 152
+
+CONTACT_DTYPE = np.dtype([
+    ("ref", np.uint32, 2), ("alt", np.uint32, 2), ("points", np.float32, (4, 4)),
+    ("numPoints", np.int32), ("normal", np.float32, 3), ("lambdaN", np.float32, 4),
+])
+assert CONTACT_DTYPE.itemsize == 112
+
+BVH_NODE_DTYPE = np.dtype([
+    ("minX", np.float32, 4), ("minY", np.float32, 4), ("minZ", np.float32, 4),
+    ("maxX", np.float32, 4), ("maxY", np.float32, 4), ("maxZ", np.float32, 4),
+    ("children", np.int32, 4), ("parentID", np.int32),
+])
+assert BVH_NODE_DTYPE.itemsize == 116
+
+
+def _vp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def gen_collisions_inits(num_worlds, num_cubes=128, seed=0):
+    lib = load_orc()
+    pos = np.zeros((num_worlds, num_cubes, 3), np.float32)
+    rot = np.zeros((num_worlds, num_cubes, 4), np.float32)
+    lib.orc_gen_collisions_inits(num_worlds, num_cubes, ctypes.c_uint32(seed),
+                                 _vp(pos), _vp(rot))
+    return pos, rot
+
+
+_ORC = None
+_REF = None
+
+
+def load_orc():
+    global _ORC
+    if _ORC is None:
+        lib = ctypes.CDLL(ORC_PATH)
+        lib.orc_phys_create.restype = ctypes.c_void_p
+        lib.orc_phys_create.argtypes = [ctypes.c_int32, ctypes.POINTER(PhysConfig),
+                                        ctypes.c_void_p, ctypes.c_void_p]
+        lib.orc_phys_step.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+        lib.orc_phys_read_bodies.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+        lib.orc_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 4
+        lib.orc_phys_read_candidates.argtypes = [ctypes.c_void_p, ctypes.c_int32,
+                                                 ctypes.c_void_p, ctypes.c_int32]
+        lib.orc_phys_read_contacts.argtypes = [ctypes.c_void_p, ctypes.c_int32,
+                                               ctypes.c_void_p, ctypes.c_int32]
+        lib.orc_phys_destroy.argtypes = [ctypes.c_void_p]
+        lib.orc_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
+                                                 ctypes.c_void_p, ctypes.c_void_p]
+        _ORC = lib
+    return _ORC
+
+
+def ref_available():
+    return os.path.exists(REF_PATH)
+
+
+def load_ref():
+    global _REF
+    if _REF is None:
+        lib = ctypes.CDLL(REF_PATH)
+        lib.ref_phys_create.restype = ctypes.c_void_p
+        lib.ref_phys_create.argtypes = [ctypes.c_int32, ctypes.POINTER(PhysConfig),
+                                        ctypes.c_void_p, ctypes.c_void_p]
+        lib.ref_phys_step.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        lib.ref_phys_read_bodies.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+        lib.ref_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 4
+        lib.ref_phys_read_contacts.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+        _REF = lib
+    return _REF
+
+
+class OraclePhys:
+    """Restated CPU physics (oracle/mw_oracle.cpp)."""
+
+    def __init__(self, cfg, pos, rot):
+        self.lib = load_orc()
+        self.cfg = cfg
+        self.num_worlds = pos.shape[0]
+        self.nb = cfg.numCubes + 1
+        pos = np.ascontiguousarray(pos, np.float32)
+        rot = np.ascontiguousarray(rot, np.float32)
+        self.h = self.lib.orc_phys_create(self.num_worlds, ctypes.byref(cfg), _vp(pos), _vp(rot))
+
+    def step(self, n=1, threads=1):
+        self.lib.orc_phys_step(self.h, n, threads)
+
+    def bodies(self, w):
+        out = np.zeros(self.nb, BODY_DTYPE)
+        self.lib.orc_phys_read_bodies(self.h, w, _vp(out))
+        return out
+
+    def bvh(self, w):
+        nodes = np.zeros(4 * self.nb + 8, BVH_NODE_DTYPE)
+        aabbs = np.zeros((self.nb, 6), np.float32)
+        parents = np.zeros(self.nb, np.uint32)
+        sorted_l = np.zeros(self.nb, np.int32)
+        n = self.lib.orc_phys_read_bvh(self.h, w, _vp(nodes), _vp(aabbs), _vp(parents), _vp(sorted_l))
+        return nodes[:n], aabbs, parents, sorted_l
+
+    def candidates(self, w, cap=1 << 16):
+        out = np.zeros((cap, 4), np.int32)
+        n = self.lib.orc_phys_read_candidates(self.h, w, _vp(out), cap)
+        return out[:n]
+
+    def contacts(self, w):
+        out = np.zeros(self.cfg.maxContacts, CONTACT_DTYPE)
+        n = self.lib.orc_phys_read_contacts(self.h, w, _vp(out), self.cfg.maxContacts)
+        return out[:n]
+
+    def __del__(self):
+        try:
+            self.lib.orc_phys_destroy(self.h)
+        except Exception:
+            pass
+
+
+class ReferencePhys:
+    """The reference itself (oracle/_ref/libmadrona_ref.so)."""
+
+    def __init__(self, cfg, pos, rot):
+        self.lib = load_ref()
+        self.cfg = cfg
+        self.num_worlds = pos.shape[0]
+        self.nb = cfg.numCubes + 1
+        self._pos = np.ascontiguousarray(pos, np.float32)
+        self._rot = np.ascontiguousarray(rot, np.float32)
+        self.h = self.lib.ref_phys_create(self.num_worlds, ctypes.byref(cfg),
+                                          _vp(self._pos), _vp(self._rot))
+
+    def step(self, n=1):
+        self.lib.ref_phys_step(self.h, n)
+
+    def bodies(self, w):
+        out = np.zeros(self.nb, BODY_DTYPE)
+        self.lib.ref_phys_read_bodies(self.h, w, _vp(out))
+        return out
+
+    def bvh(self, w):
+        nodes = np.zeros(4 * self.nb + 8, BVH_NODE_DTYPE)
+        aabbs = np.zeros((self.nb, 6), np.float32)
+        parents = np.zeros(self.nb, np.uint32)
+        sorted_l = np.zeros(self.nb, np.int32)
+        n = self.lib.ref_phys_read_bvh(self.h, w, _vp(nodes), _vp(aabbs), _vp(parents), _vp(sorted_l))
+        return nodes[:n], aabbs, parents, sorted_l
+
+    def contacts_raw(self, w):
+        out = np.zeros(self.cfg.maxContacts, CONTACT_DTYPE)
+        self.lib.ref_phys_read_contacts(self.h, w, _vp(out))
+        return out

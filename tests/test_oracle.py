@@ -1,0 +1,104 @@
+"""CPU tests: pin the oracle (C++ restatement) against the reference.
+
+* golden fixtures made by the reference itself (tests/golden/make_golden.py)
+* the live reference build (oracle/_ref) when it is present in this container
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle_lib import (BODY_DTYPE, CONTACT_DTYPE, OraclePhys, PhysConfig,
+                        ReferencePhys, default_phys_config,
+                        gen_collisions_inits, ref_available)
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "collisions_ref.npz")
+
+
+def _golden():
+    return np.load(GOLDEN, allow_pickle=False)
+
+
+def _cfg_from_golden(g):
+    ci, cf = g["cfg"], g["cfg_f"]
+    return PhysConfig(int(ci[0]), int(ci[1]), float(cf[0]), float(cf[1]), int(ci[2]),
+                      float(cf[2]), float(cf[3]), float(cf[4]), float(cf[5]))
+
+
+def contacts_equal(a, b):
+    """Bit-exact equality on the meaningful part of two contact records."""
+    n = int(a["numPoints"])
+    return (a["ref"].tobytes() == b["ref"].tobytes()
+            and a["alt"].tobytes() == b["alt"].tobytes()
+            and n == int(b["numPoints"])
+            and a["normal"].tobytes() == b["normal"].tobytes()
+            and a["points"][:n].tobytes() == b["points"][:n].tobytes()
+            and a["lambdaN"][:n].tobytes() == b["lambdaN"][:n].tobytes())
+
+
+def test_init_generator_matches_golden_inputs():
+    g = _golden()
+    pos, rot = gen_collisions_inits(g["init_pos"].shape[0], 128, seed=0)
+    assert pos.tobytes() == g["init_pos"].tobytes()
+    assert rot.tobytes() == g["init_rot"].tobytes()
+
+
+def test_oracle_bit_exact_vs_golden_bodies_and_contacts():
+    g = _golden()
+    cfg = _cfg_from_golden(g)
+    W = g["init_pos"].shape[0]
+    orc = OraclePhys(cfg, g["init_pos"], g["init_rot"])
+    step = 0
+    for target in g["snap_steps"]:
+        orc.step(int(target) - step)
+        step = int(target)
+        want = g[f"bodies_{step}"].view(BODY_DTYPE).reshape(W, -1)
+        for w in range(W):
+            got = orc.bodies(w)
+            assert got.tobytes() == want[w].tobytes(), f"bodies differ at step {step} world {w}"
+        if step == 1:
+            for w in range(W):
+                _, aabbs, parents, sorted_l = orc.bvh(w)
+                assert aabbs.tobytes() == g[f"bvh_leaf_aabbs_{w}"].tobytes()
+                assert parents.tobytes() == g[f"bvh_leaf_parents_{w}"].tobytes()
+                assert sorted_l.tobytes() == g[f"bvh_sorted_{w}"].tobytes()
+        key = f"contacts_{step}_0"
+        if key in g:
+            for w in range(W):
+                want_c = g[f"contacts_{step}_{w}"].view(CONTACT_DTYPE).reshape(-1)
+                got_c = orc.contacts(w)
+                # reference prefix = last substep's contacts (longer if an
+                # earlier substep wrote more); ours is exactly the last substep
+                assert len(got_c) <= len(want_c)
+                for i in range(len(got_c)):
+                    assert contacts_equal(got_c[i], want_c[i]), (step, w, i)
+
+
+@pytest.mark.skipif(not ref_available(), reason="reference build absent (GPU box)")
+def test_oracle_bit_exact_vs_live_reference():
+    cfg = default_phys_config(num_cubes=128, max_contacts=2048)
+    pos, rot = gen_collisions_inits(2, 128, seed=7)
+    orc = OraclePhys(cfg, pos, rot)
+    ref = ReferencePhys(cfg, pos, rot)
+    for step in range(60):
+        orc.step()
+        ref.step()
+        for w in range(2):
+            assert orc.bodies(w).tobytes() == ref.bodies(w).tobytes(), (step, w)
+            n_o, a_o, p_o, s_o = orc.bvh(w)
+            n_r, a_r, p_r, s_r = ref.bvh(w)
+            assert n_o.tobytes() == n_r[:len(n_o)].tobytes()
+            assert a_o.tobytes() == a_r.tobytes()
+
+
+def test_oracle_small_world_counts_and_threads_agree():
+    """Ragged case: few bodies, 1 substep; the threaded driver must equal the
+    serial one (worlds are independent)."""
+    cfg = default_phys_config(num_cubes=5, num_substeps=1, max_contacts=256)
+    pos, rot = gen_collisions_inits(6, 5, seed=3)
+    a = OraclePhys(cfg, pos, rot)
+    b = OraclePhys(cfg, pos, rot)
+    a.step(20, threads=1)
+    b.step(20, threads=3)
+    for w in range(6):
+        assert a.bodies(w).tobytes() == b.bodies(w).tobytes()
