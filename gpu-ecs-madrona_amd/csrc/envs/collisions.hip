@@ -1,0 +1,153 @@
+// "collisions" environment: the rigid-body workload of SURVEY.md §8(d)
+// (C3/C4): per world num_cubes unit-cube hulls + one static ground plane,
+// stepped by RigidBodyPhysicsSystem.  Written against the reference's
+// registration API (registerTypes / setupTasks / world ctor, reference
+// include/madrona/mw_cpu.inl:15-69) exactly like oracle/ref_harness.cpp's
+// world, which is the same world compiled against the reference itself.
+#include <madrona/mw_gpu.hpp>
+#include <madrona/physics.hpp>
+
+#include "../runtime/env_registry.hpp"
+#include "../../../include/madrona_mw.h"
+
+#include <cfloat>
+#include <cstring>
+
+using namespace madrona;
+using namespace madrona::math;
+using namespace madrona::base;
+using namespace madrona::phys;
+
+namespace CollisionsEnv {
+
+struct PhysicsBody : Archetype<
+    Position, Rotation, Scale, Velocity, ObjectID, ResponseType,
+    solver::SubstepPrevState, solver::PreSolvePositional,
+    solver::PreSolveVelocity, ExternalForce, ExternalTorque,
+    broadphase::LeafID> {};
+
+struct Config {
+    mw_collisions_config c;
+    ObjectManager *objMgr;
+};
+
+class Engine;
+
+struct PhysWorld : public WorldBase {
+    static void registerTypes(ECSRegistry &reg, const Config &cfg)
+    {
+        base::registerTypes(reg);
+        RigidBodyPhysicsSystem::setMaxCandidatesPerWorld(reg, cfg.c.max_candidates);
+        RigidBodyPhysicsSystem::registerTypes(reg);
+        reg.registerFixedSizeArchetype<PhysicsBody>(cfg.c.num_cubes + 1);
+        reg.exportColumn<PhysicsBody, Position>(0);
+        reg.exportColumn<PhysicsBody, Rotation>(1);
+    }
+
+    static void setupTasks(TaskGraph::Builder &builder, const Config &cfg)
+    {
+        auto bp = RigidBodyPhysicsSystem::setupBroadphaseTasks(builder, {});
+        auto sub = RigidBodyPhysicsSystem::setupSubstepTasks(builder, { bp },
+                                                             cfg.c.num_substeps);
+        RigidBodyPhysicsSystem::setupCleanupTasks(builder, { sub });
+    }
+
+    PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &init);
+};
+
+class Engine : public CustomContext<Engine, PhysWorld> {
+public:
+    using CustomContext::CustomContext;
+};
+
+PhysWorld::PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &init)
+    : WorldBase(ctx)
+{
+    const mw_collisions_config &c = cfg.c;
+    RigidBodyPhysicsSystem::init(ctx, cfg.objMgr, c.delta_t, c.num_substeps,
+                                 Vector3 { 0.f, 0.f, c.gravity_z }, c.num_cubes + 1,
+                                 c.max_contacts, 16);
+
+    auto setup = [&](Entity e, Vector3 p, Quat q, int32_t obj, ResponseType rt) {
+        ctx.getUnsafe<Position>(e) = Position { p };
+        ctx.getUnsafe<Rotation>(e) = Rotation { q };
+        ctx.getUnsafe<Scale>(e) = Scale { Diag3x3 { 1.f, 1.f, 1.f } };
+        ctx.getUnsafe<Velocity>(e) = Velocity { Vector3::zero(), Vector3::zero() };
+        ctx.getUnsafe<ObjectID>(e) = ObjectID { obj };
+        ctx.getUnsafe<ResponseType>(e) = rt;
+        ctx.getUnsafe<solver::SubstepPrevState>(e) = { p, q };
+        ctx.getUnsafe<solver::PreSolvePositional>(e) = { p, q };
+        ctx.getUnsafe<solver::PreSolveVelocity>(e) = { Vector3::zero(), Vector3::zero() };
+        ctx.getUnsafe<ExternalForce>(e) = ExternalForce { Vector3::zero() };
+        ctx.getUnsafe<ExternalTorque>(e) = ExternalTorque { Vector3::zero() };
+        ctx.getUnsafe<broadphase::LeafID>(e) =
+            RigidBodyPhysicsSystem::registerEntity(ctx, e, ObjectID { obj });
+    };
+
+    for (int32_t i = 0; i < c.num_cubes; i++) {
+        Entity e = ctx.makeEntityNow<PhysicsBody>();
+        Vector3 p { init.pos[3 * i], init.pos[3 * i + 1], init.pos[3 * i + 2] };
+        Quat q { init.rot[4 * i], init.rot[4 * i + 1], init.rot[4 * i + 2], init.rot[4 * i + 3] };
+        setup(e, p, q, 0, ResponseType::Dynamic);
+    }
+    Entity plane = ctx.makeEntityNow<PhysicsBody>();
+    setup(plane, Vector3::zero(), Quat { 1.f, 0.f, 0.f, 0.f }, 1, ResponseType::Static);
+
+    ctx.getSingleton<broadphase::BVH>().rebuildOnUpdate();
+}
+
+// Object table: 0 = cube hull (half extent 1), 1 = ground plane.
+static ObjectManager *makeObjectManager(const mw_collisions_config &c)
+{
+    auto *mgr = new ObjectManager {};
+    mgr->numObjects = 2;
+    mgr->metadata = new RigidBodyMetadata[2];
+    mgr->aabbs = new AABB[2];
+    mgr->primitives = new CollisionPrimitive[2];
+
+    const Vector3 verts[8] = {
+        { -1, -1, -1 }, { 1, -1, -1 }, { 1, 1, -1 }, { -1, 1, -1 },
+        { -1, -1, 1 }, { 1, -1, 1 }, { 1, 1, 1 }, { -1, 1, 1 },
+    };
+    const uint32_t faces[6][4] = {
+        { 0, 3, 2, 1 }, { 4, 5, 6, 7 }, { 0, 1, 5, 4 },
+        { 3, 7, 6, 2 }, { 0, 4, 7, 3 }, { 1, 2, 6, 5 },
+    };
+    geometry::FastPolygonList pl {};
+    pl.allocate(6 * 5);
+    for (int f = 0; f < 6; f++) pl.addPolygon(Span<const uint32_t>(faces[f], 4));
+    mgr->primitives[0].type = CollisionPrimitive::Type::Hull;
+    mgr->primitives[0].hull.halfEdgeMesh.construct(pl, 8, verts);
+    pl.free();
+    mgr->metadata[0] = RigidBodyMetadata {
+        { c.cube_inv_inertia, c.cube_inv_inertia, c.cube_inv_inertia }, c.cube_inv_mass,
+        c.mu_s, c.mu_d };
+    mgr->aabbs[0] = AABB { { -1, -1, -1 }, { 1, 1, 1 } };
+
+    mgr->primitives[1].type = CollisionPrimitive::Type::Plane;
+    mgr->metadata[1] = RigidBodyMetadata { { 0.f, 0.f, 0.f }, 0.f, c.mu_s, c.mu_d };
+    mgr->aabbs[1] = AABB { { -FLT_MAX, -FLT_MAX, -FLT_MAX }, { FLT_MAX, FLT_MAX, 0.f } };
+    return mgr;
+}
+
+using Exec = TaskGraphExecutor<Engine, PhysWorld, Config, mw_collisions_init>;
+
+static Executor *create(const ExecConfig &ecfg, const void *user_cfg, size_t cfg_bytes,
+                        const void *inits, size_t init_stride)
+{
+    if (cfg_bytes != sizeof(mw_collisions_config)) {
+        throw std::runtime_error("collisions: user config size mismatch");
+    }
+    Config cfg;
+    memcpy(&cfg.c, user_cfg, sizeof(cfg.c));
+    cfg.objMgr = makeObjectManager(cfg.c);
+    std::vector<mw_collisions_init> init_vec(ecfg.numWorlds);
+    for (int32_t w = 0; w < ecfg.numWorlds; w++) {
+        memcpy(&init_vec[w], (const char *)inits + (size_t)w * init_stride, sizeof(mw_collisions_init));
+    }
+    return new Exec(ecfg, cfg, init_vec.data());
+}
+
+static EnvRegistration reg("collisions", &create);
+
+}

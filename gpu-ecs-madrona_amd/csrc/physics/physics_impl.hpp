@@ -1,0 +1,110 @@
+// Internal device-side data of the MI355X physics module.
+//
+// Per-world state that the reference keeps behind raw pointers inside the
+// BVH / SolverData singletons (src/physics/broadphase.cpp:11-31,
+// src/physics/physics.cpp:15-32) lives here as [world][...] slabs, so every
+// kernel indexes one contiguous array for all worlds.
+#pragma once
+
+#include <madrona/physics.hpp>
+
+namespace madrona::phys {
+
+// 4-wide BVH node, byte-identical to broadphase::BVH::Node
+// (include/madrona/physics.hpp:367-381).
+struct BVHNode {
+    float minX[4];
+    float minY[4];
+    float minZ[4];
+    float maxX[4];
+    float maxY[4];
+    float maxZ[4];
+    int32_t children[4];
+    int32_t parentID;
+};
+static_assert(sizeof(BVHNode) == 116);
+
+struct HullDev {
+    int32_t vertOffset;
+    int32_t numVerts;
+    int32_t faceOffset;     // planes and polygons (one half edge per face)
+    int32_t numFaces;
+    int32_t hedgeOffset;
+    int32_t numHedges;
+    int32_t edgeOffset;
+    int32_t numEdges;
+};
+
+struct ObjDev {
+    int32_t numObjects;
+    int32_t maxVerts;
+    int32_t maxFaces;
+    RigidBodyMetadata *metadata;
+    math::AABB *aabbs;
+    uint32_t *types;              // CollisionPrimitive::Type
+    HullDev *hulls;
+    math::Vector3 *vertices;
+    geometry::Plane *planes;
+    geometry::HalfEdge *hedges;
+    uint32_t *edges;              // half-edge index per edge
+    uint32_t *polygons;           // half-edge index per face
+};
+
+inline constexpr int32_t kMaxBodyArchetypes = 4;
+
+struct BodyArch {
+    int32_t archetype;
+    int32_t capacity;
+    int32_t slotBase;             // body slot of row 0 in the solver's LDS image
+    int32_t *numRows;
+    char *cols[13];               // Entity + Cols::Position..LeafID
+};
+
+// Everything a physics kernel needs, passed by value (< 1 KB).
+struct PhysArgs {
+    int32_t numWorlds;
+    int32_t numBodyArchs;
+    BodyArch body[kMaxBodyArchetypes];
+    int32_t maxBodiesPerWorld;    // sum of body archetype capacities
+
+    broadphase::BVH *bvh;         // singleton column, [W]
+    SolverData *solver;           // singleton column, [W]
+
+    int32_t candArchetype;
+    int32_t candCapacity;
+    int32_t *numCands;            // [W]
+    CandidateCollision *cands;    // [W][candCapacity]
+
+    IDNode *idNodes;              // entity store, [W][idsPerWorld]
+    int32_t idsPerWorld;
+    int32_t *errorFlags;          // [W]
+
+    int32_t maxLeaves;
+    int32_t maxNodes;
+    BVHNode *nodes;               // [W][maxNodes]
+    Entity *leafEntities;         // [W][maxLeaves]
+    math::AABB *leafAABBs;        // [W][maxLeaves]
+    uint32_t *leafParents;        // [W][maxLeaves]
+    int32_t *sortedLeaves;        // [W][maxLeaves]
+
+    math::Vector3 *hullVerts;     // [W][maxLeaves][maxVerts] world-space hull cache
+    geometry::Plane *hullPlanes;  // [W][maxLeaves][maxFaces]
+
+    Contact *candContacts;        // [W][candCapacity] manifold per candidate slot
+    int32_t maxContacts;          // SolverData::maxContacts (reference assert)
+    int32_t *contactOrder;        // [W][candCapacity] scratch: ordered contact list
+    int32_t *lastNumContacts;     // [W] debug: contacts of the last substep
+    int32_t *lastNumCands;        // [W] debug: candidates of the last step
+
+    ObjDev objs;
+};
+
+// Error flag bits (StateView::errorFlags)
+inline constexpr int32_t kErrIDStoreFull = 1;
+inline constexpr int32_t kErrTableFull = 2;
+inline constexpr int32_t kErrCandidateOverflow = 4;
+inline constexpr int32_t kErrContactOverflow = 8;
+inline constexpr int32_t kErrBVHStack = 16;
+inline constexpr int32_t kErrSolverBodies = 32;
+
+}

@@ -1,0 +1,242 @@
+// C ABI (include/madrona_mw.h) over the MI355X executor.
+#include "../../../include/madrona_mw.h"
+
+#include "env_registry.hpp"
+#include "../physics/physics_impl.hpp"
+
+#include <madrona/mw_gpu.hpp>
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <exception>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace madrona {
+namespace phys { PhysArgs *physicsArgs(StateManager &mgr); }
+
+static std::map<std::string, EnvFactory> &envTable()
+{
+    static std::map<std::string, EnvFactory> t;
+    return t;
+}
+
+EnvRegistration::EnvRegistration(const char *name, EnvFactory factory)
+{
+    envTable()[name] = factory;
+}
+
+EnvFactory findEnv(const char *name)
+{
+    auto it = envTable().find(name);
+    return it == envTable().end() ? nullptr : it->second;
+}
+
+}
+
+using namespace madrona;
+
+struct mw_exec {
+    Executor *exec;
+};
+
+static thread_local std::string g_last_error;
+
+static void setError(const char *what) { g_last_error = what ? what : "unknown error"; }
+
+#define MW_TRY(body, fail)                                 \
+    try {                                                  \
+        body                                               \
+    } catch (const std::exception &e) {                    \
+        setError(e.what());                                \
+        return fail;                                       \
+    } catch (...) {                                        \
+        setError("unknown exception");                     \
+        return fail;                                       \
+    }
+
+#define MW_HIP_OK(expr)                                                  \
+    do {                                                                 \
+        hipError_t e__ = (expr);                                         \
+        if (e__ != hipSuccess) throw std::runtime_error(hipGetErrorString(e__)); \
+    } while (0)
+
+extern "C" {
+
+mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
+                   size_t user_cfg_bytes, const void *inits, size_t init_stride)
+{
+    MW_TRY({
+        if (!env || !cfg) throw std::runtime_error("mw_create: null argument");
+        EnvFactory f = findEnv(env);
+        if (!f) throw std::runtime_error(std::string("mw_create: unknown environment '") + env + "'");
+        if (cfg->num_worlds <= 0) throw std::runtime_error("mw_create: num_worlds must be > 0");
+        int ndev = 0;
+        MW_HIP_OK(hipGetDeviceCount(&ndev));
+        if (cfg->gpu_id < 0 || cfg->gpu_id >= ndev) {
+            throw std::runtime_error("mw_create: no HIP device " + std::to_string(cfg->gpu_id));
+        }
+        ExecConfig ec;
+        ec.numWorlds = cfg->num_worlds;
+        ec.gpuID = cfg->gpu_id;
+        ec.defaultCapacity = cfg->default_capacity > 0 ? cfg->default_capacity : 64;
+        ec.numExportedBuffers = 0;
+        ec.useGraph = cfg->use_graph;
+        Executor *e = f(ec, user_cfg, user_cfg_bytes, inits, init_stride);
+        return new mw_exec { e };
+    }, nullptr)
+}
+
+int mw_step(mw_exec *exec, int32_t num_steps)
+{
+    MW_TRY({
+        for (int32_t i = 0; i < num_steps; i++) exec->exec->runAsync();
+        exec->exec->sync();
+        return 0;
+    }, -1)
+}
+
+int mw_step_async(mw_exec *exec, int32_t num_steps)
+{
+    MW_TRY({
+        for (int32_t i = 0; i < num_steps; i++) exec->exec->runAsync();
+        return 0;
+    }, -1)
+}
+
+int mw_sync(mw_exec *exec)
+{
+    MW_TRY({ exec->exec->sync(); return 0; }, -1)
+}
+
+void *mw_get_exported(mw_exec *exec, int32_t slot, int64_t *num_rows)
+{
+    MW_TRY({ return exec->exec->getExported(slot, num_rows); }, nullptr)
+}
+
+void *mw_stream(mw_exec *exec) { return exec ? exec->exec->stream() : nullptr; }
+
+int mw_destroy(mw_exec *exec)
+{
+    MW_TRY({
+        if (exec) {
+            delete exec->exec;
+            delete exec;
+        }
+        return 0;
+    }, -1)
+}
+
+const char *mw_last_error(void) { return g_last_error.c_str(); }
+
+int32_t mw_num_worlds(mw_exec *exec) { return exec->exec->numWorlds(); }
+
+int32_t mw_error_flags(mw_exec *exec)
+{
+    MW_TRY({ return exec->exec->errorFlags(); }, -1)
+}
+
+int32_t mw_num_archetypes(mw_exec *exec)
+{
+    return exec->exec->stateManager().numArchetypes();
+}
+
+int32_t mw_column_info(mw_exec *exec, int32_t archetype, int32_t column, int32_t *bytes,
+                       int32_t *capacity)
+{
+    uint32_t b = 0;
+    int32_t cap = 0;
+    if (!exec->exec->columnBase(archetype, column, &cap, &b)) return -1;
+    if (bytes) *bytes = (int32_t)b;
+    if (capacity) *capacity = cap;
+    return 0;
+}
+
+int32_t mw_read_column(mw_exec *exec, int32_t archetype, int32_t column, int32_t world, void *out,
+                       int32_t max_rows)
+{
+    MW_TRY({
+        int32_t cap = 0;
+        uint32_t bytes = 0;
+        char *base = (char *)exec->exec->columnBase(archetype, column, &cap, &bytes);
+        if (!base || world < 0 || world >= exec->exec->numWorlds()) return -1;
+        exec->exec->sync();
+        int32_t n = exec->exec->numRows(archetype, world);
+        int32_t copy = n < max_rows ? n : max_rows;
+        if (copy > 0) {
+            MW_HIP_OK(hipMemcpy(out, base + (size_t)world * cap * bytes, (size_t)copy * bytes,
+                                hipMemcpyDeviceToHost));
+        }
+        return n;
+    }, -1)
+}
+
+int32_t mw_phys_read_candidates(mw_exec *exec, int32_t world, void *out, int32_t cap)
+{
+    MW_TRY({
+        exec->exec->sync();
+        phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
+        if (!P) return -1;
+        int32_t n = 0;
+        MW_HIP_OK(hipMemcpy(&n, P->lastNumCands + world, 4, hipMemcpyDeviceToHost));
+        int32_t copy = n < cap ? n : cap;
+        if (copy > 0) {
+            MW_HIP_OK(hipMemcpy(out, P->cands + (size_t)world * P->candCapacity,
+                                sizeof(phys::CandidateCollision) * copy, hipMemcpyDeviceToHost));
+        }
+        return n;
+    }, -1)
+}
+
+int32_t mw_phys_read_contacts(mw_exec *exec, int32_t world, void *out, int32_t cap)
+{
+    MW_TRY({
+        exec->exec->sync();
+        phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
+        if (!P) return -1;
+        int32_t n = 0;
+        MW_HIP_OK(hipMemcpy(&n, P->lastNumContacts + world, 4, hipMemcpyDeviceToHost));
+        std::vector<int32_t> order(n);
+        if (n > 0) {
+            MW_HIP_OK(hipMemcpy(order.data(), P->contactOrder + (size_t)world * P->candCapacity,
+                                4 * n, hipMemcpyDeviceToHost));
+        }
+        std::vector<phys::Contact> slots(P->candCapacity);
+        MW_HIP_OK(hipMemcpy(slots.data(), P->candContacts + (size_t)world * P->candCapacity,
+                            sizeof(phys::Contact) * P->candCapacity, hipMemcpyDeviceToHost));
+        phys::Contact *o = (phys::Contact *)out;
+        for (int32_t i = 0; i < n && i < cap; i++) o[i] = slots[order[i]];
+        return n;
+    }, -1)
+}
+
+int32_t mw_phys_read_bvh(mw_exec *exec, int32_t world, void *nodes_out, float *leaf_aabbs_out,
+                         int32_t cap_nodes)
+{
+    MW_TRY({
+        exec->exec->sync();
+        phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
+        if (!P) return -1;
+        phys::broadphase::BVH bvh;
+        MW_HIP_OK(hipMemcpy(&bvh, P->bvh + world, sizeof(bvh), hipMemcpyDeviceToHost));
+        int32_t n = bvh.usedNodes < cap_nodes ? bvh.usedNodes : cap_nodes;
+        if (nodes_out && n > 0) {
+            MW_HIP_OK(hipMemcpy(nodes_out, P->nodes + (size_t)world * P->maxNodes,
+                                sizeof(phys::BVHNode) * n, hipMemcpyDeviceToHost));
+        }
+        if (leaf_aabbs_out && bvh.numLeaves > 0) {
+            MW_HIP_OK(hipMemcpy(leaf_aabbs_out, P->leafAABBs + (size_t)world * P->maxLeaves,
+                                sizeof(math::AABB) * bvh.numLeaves, hipMemcpyDeviceToHost));
+        }
+        return bvh.usedNodes;
+    }, -1)
+}
+
+double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps)
+{
+    MW_TRY({ return exec->exec->timeNode(node_name, num_steps); }, -1.0)
+}
+
+}

@@ -1,0 +1,373 @@
+// Executor, TaskGraph build/launch and generic launch helpers (gfx950).
+//
+// Reference: src/core/taskgraph.cpp:18-122 (Builder/build/run),
+// src/mw/cuda_exec.cpp:1519-1815 (run graph, getExported, export kernels).
+#include <madrona/mw_gpu.hpp>
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <cstdio>
+#include <stdexcept>
+#include <vector>
+
+namespace madrona {
+
+#define MW_HIP_CHECK(expr)                                                          \
+    do {                                                                            \
+        hipError_t err__ = (expr);                                                  \
+        if (err__ != hipSuccess) {                                                  \
+            fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(err__),    \
+                    __FILE__, __LINE__);                                            \
+            throw std::runtime_error(hipGetErrorString(err__));                     \
+        }                                                                           \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// TaskGraph
+// ---------------------------------------------------------------------------
+TaskGraph::Builder::Builder(Context &ctx) : ctx_(&ctx) {}
+
+StateManager &TaskGraph::Builder::stateManager()
+{
+    // The host context always carries the StateManager (WorkerInit::mgr).
+    struct Peek : Context { StateManager *mgr() { return mgr_; } };
+    return *static_cast<Peek *>(ctx_)->mgr();
+}
+
+TaskGraph::NodeID TaskGraph::Builder::registerNode(std::shared_ptr<void> data, LaunchFn fn,
+                                                   Span<const NodeID> deps, const char *name)
+{                                               // taskgraph.cpp:18-44
+    Staged s;
+    s.data = std::move(data);
+    s.fn = fn;
+    s.name = name;
+    for (const NodeID &d : deps) s.deps.push_back(d.id);
+    staged_.push_back(std::move(s));
+    return NodeID { (uint32_t)staged_.size() - 1 };
+}
+
+TaskGraph TaskGraph::Builder::build()
+{                                               // taskgraph.cpp:46-109
+    TaskGraph g;
+    const size_t n = staged_.size();
+    if (n == 0) return g;                       // the reference segfaults here
+    std::vector<bool> queued(n, false);
+    if (!staged_[0].deps.empty()) throw std::runtime_error("first node has dependencies");
+    g.nodes_.push_back(Node { staged_[0].data, staged_[0].fn, staged_[0].name });
+    queued[0] = true;
+    size_t remaining = n - 1;
+    while (remaining > 0) {
+        size_t cur;
+        for (cur = 0; queued[cur]; cur++) {}
+        bool ok = true;
+        for (uint32_t d : staged_[cur].deps) {
+            if (d >= n || !queued[d]) { ok = false; break; }
+        }
+        // The reference spins forever here; report the bad dependency instead.
+        if (!ok) throw std::runtime_error("taskgraph: node depends on a later node");
+        queued[cur] = true;
+        g.nodes_.push_back(Node { staged_[cur].data, staged_[cur].fn, staged_[cur].name });
+        remaining--;
+    }
+    return g;
+}
+
+void TaskGraph::launch(LaunchCtx &lc) const
+{
+    for (const Node &nd : nodes_) nd.fn(nd.data.get(), lc);
+}
+
+// ---------------------------------------------------------------------------
+// Generic launch helpers
+// ---------------------------------------------------------------------------
+namespace detail {
+
+void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype,
+                     const void *args, size_t)
+{
+    const int32_t cap = lc.view->arch[archetype].capacity;
+    const int64_t total = (int64_t)lc.numWorlds * cap;
+    if (total == 0) return;
+    dim3 block(256);
+    dim3 grid((unsigned)((total + 255) / 256));
+    StateView *st = lc.devState;
+    int32_t arch = archetype;
+    void *kargs[] = { &st, &arch, const_cast<void *>(args) };
+    MW_HIP_CHECK(hipLaunchKernel(kernel, grid, block, kargs, 0, (hipStream_t)lc.stream));
+}
+
+}
+
+__global__ void clearRowsKernel(int32_t *num_rows, int32_t num_worlds)
+{
+    int32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < num_worlds) num_rows[w] = 0;
+}
+
+void launchClearRows(LaunchCtx &lc, int32_t archetype)
+{
+    int32_t *rows = lc.view->arch[archetype].numRows;
+    hipLaunchKernelGGL(clearRowsKernel, dim3((lc.numWorlds + 255) / 256), dim3(256), 0,
+                       (hipStream_t)lc.stream, rows, lc.numWorlds);
+}
+
+// Packed export: world w's rows land at offset prefix(numRows)[w]
+// (reference madronaMWGPUExportCopyOut, src/mw/device/consts.cpp:190-273,
+// here a single block-wide scan per launch instead of O(blocks^2)).
+__global__ void __launch_bounds__(1024)
+exportScanKernel(const int32_t *num_rows, int32_t num_worlds, int64_t *offsets)
+{
+    __shared__ int64_t partial[1024];
+    const int32_t tid = threadIdx.x;
+    const int32_t per = (num_worlds + 1023) / 1024;
+    const int32_t beg = tid * per;
+    const int32_t end = min(beg + per, num_worlds);
+    int64_t s = 0;
+    for (int32_t w = beg; w < end; w++) s += num_rows[w];
+    partial[tid] = s;
+    __syncthreads();
+    for (int32_t off = 1; off < 1024; off <<= 1) {
+        int64_t v = tid >= off ? partial[tid - off] : 0;
+        __syncthreads();
+        partial[tid] += v;
+        __syncthreads();
+    }
+    int64_t run = partial[tid] - s;
+    for (int32_t w = beg; w < end; w++) {
+        offsets[w] = run;
+        run += num_rows[w];
+    }
+    if (tid == 1023) offsets[num_worlds] = partial[1023];
+}
+
+__global__ void exportCopyKernel(const char *col, int32_t capacity, uint32_t bytes,
+                                 const int32_t *num_rows, const int64_t *offsets,
+                                 char *out)
+{
+    const int32_t w = blockIdx.y;
+    const int32_t n = num_rows[w] * (int32_t)bytes;
+    const char *src = col + (size_t)w * capacity * bytes;
+    char *dst = out + (size_t)offsets[w] * bytes;
+    for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        dst[i] = src[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Executor
+// ---------------------------------------------------------------------------
+struct ExportBuf {
+    int32_t slot, archetype, column;
+    uint32_t bytes;
+    char *buf;
+    int64_t *offsets;
+};
+
+struct Executor::Impl {
+    ExecConfig cfg;
+    std::unique_ptr<StateManager> mgr;
+    hipStream_t stream = nullptr;
+    TaskGraph graph;
+    hipGraph_t hipGraph = nullptr;
+    hipGraphExec_t hipGraphExec = nullptr;
+    std::vector<ExportBuf> exports;
+    int64_t *hostRowsTotal = nullptr;
+};
+
+Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
+{
+    impl_->cfg = cfg;
+    MW_HIP_CHECK(hipSetDevice(cfg.gpuID));
+    MW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
+    impl_->mgr.reset(new StateManager(StateManager::Config { cfg.numWorlds, cfg.defaultCapacity }));
+}
+
+Executor::~Executor()
+{
+    if (impl_->hipGraphExec) (void)hipGraphExecDestroy(impl_->hipGraphExec);
+    if (impl_->hipGraph) (void)hipGraphDestroy(impl_->hipGraph);
+    for (auto &e : impl_->exports) {
+        (void)hipFree(e.buf);
+        (void)hipFree(e.offsets);
+    }
+    impl_->mgr.reset();
+    if (impl_->stream) (void)hipStreamDestroy(impl_->stream);
+}
+
+StateManager &Executor::stateManager() { return *impl_->mgr; }
+ECSRegistry Executor::registry() { return ECSRegistry(impl_->mgr.get(), nullptr); }
+int32_t Executor::numWorlds() const { return impl_->cfg.numWorlds; }
+void *Executor::stream() const { return impl_->stream; }
+
+void Executor::finalizeRegistration(uint32_t world_bytes, uint32_t world_align)
+{
+    impl_->mgr->finalizeLayout(world_bytes, world_align);
+}
+
+Context Executor::makeHostContext(int32_t world)
+{
+    return Context((WorldBase *)hostWorldData(world),
+                   WorkerInit { &impl_->mgr->hostView(), world, impl_->mgr.get() });
+}
+
+char *Executor::hostWorldData(int32_t world)
+{
+    StateView &v = impl_->mgr->hostView();
+    return v.worldData + (size_t)world * v.worldDataStride;
+}
+
+void Executor::uploadState()
+{
+    impl_->mgr->uploadToDevice(impl_->stream);
+
+    int32_t num_exports = 0;
+    const StateManager::ExportDesc *ex = impl_->mgr->exports(&num_exports);
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    for (int32_t i = 0; i < num_exports; i++) {
+        ExportBuf b {};
+        b.slot = ex[i].slot;
+        b.archetype = ex[i].archetype;
+        b.column = ex[i].column;
+        b.bytes = ex[i].bytes;
+        size_t bytes = (size_t)dv.numWorlds * dv.arch[b.archetype].capacity * b.bytes;
+        MW_HIP_CHECK(hipMalloc(&b.buf, std::max<size_t>(bytes, 256)));
+        MW_HIP_CHECK(hipMalloc(&b.offsets, sizeof(int64_t) * (dv.numWorlds + 1)));
+        impl_->exports.push_back(b);
+    }
+}
+
+static void launchExports(Executor::Impl &I, const StateView &dv)
+{
+    for (ExportBuf &b : I.exports) {
+        const ArchetypeView &av = dv.arch[b.archetype];
+        hipLaunchKernelGGL(exportScanKernel, dim3(1), dim3(1024), 0, I.stream,
+                           av.numRows, dv.numWorlds, b.offsets);
+        hipLaunchKernelGGL(exportCopyKernel, dim3(4, dv.numWorlds), dim3(256), 0, I.stream,
+                           av.cols[b.column], av.capacity, b.bytes, av.numRows, b.offsets,
+                           b.buf);
+    }
+}
+
+void Executor::setGraph(TaskGraph &&graph)
+{
+    impl_->graph = std::move(graph);
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
+    if (impl_->cfg.useGraph) {
+        MW_HIP_CHECK(hipStreamBeginCapture(impl_->stream, hipStreamCaptureModeThreadLocal));
+        impl_->graph.launch(lc);
+        launchExports(*impl_, dv);
+        MW_HIP_CHECK(hipStreamEndCapture(impl_->stream, &impl_->hipGraph));
+        MW_HIP_CHECK(hipGraphInstantiate(&impl_->hipGraphExec, impl_->hipGraph, nullptr, nullptr, 0));
+    }
+}
+
+void Executor::runAsync()
+{
+    if (impl_->hipGraphExec) {
+        MW_HIP_CHECK(hipGraphLaunch(impl_->hipGraphExec, impl_->stream));
+    } else {
+        const StateView &dv = impl_->mgr->deviceViewHost();
+        LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
+        impl_->graph.launch(lc);
+        launchExports(*impl_, dv);
+    }
+}
+
+void Executor::sync() { MW_HIP_CHECK(hipStreamSynchronize(impl_->stream)); }
+
+void Executor::run()
+{
+    runAsync();
+    sync();
+}
+
+void *Executor::getExported(int32_t slot, int64_t *num_rows)
+{
+    for (ExportBuf &b : impl_->exports) {
+        if (b.slot == slot) {
+            if (num_rows) {
+                int64_t total = 0;
+                MW_HIP_CHECK(hipMemcpy(&total, b.offsets + impl_->cfg.numWorlds, sizeof(int64_t),
+                                       hipMemcpyDeviceToHost));
+                *num_rows = total;
+            }
+            return b.buf;
+        }
+    }
+    return nullptr;
+}
+
+void Executor::copyOutExports() { launchExports(*impl_, impl_->mgr->deviceViewHost()); }
+
+void *Executor::columnBase(int32_t archetype, int32_t column, int32_t *capacity, uint32_t *bytes)
+{
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    if (archetype < 0 || archetype >= dv.numArchetypes) return nullptr;
+    const ArchetypeView &av = dv.arch[archetype];
+    if (column < 0 || column >= av.numColumns) return nullptr;
+    if (capacity) *capacity = av.capacity;
+    if (bytes) *bytes = av.colBytes[column];
+    return av.cols[column];
+}
+
+int32_t Executor::numRows(int32_t archetype, int32_t world)
+{
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    int32_t n = 0;
+    MW_HIP_CHECK(hipMemcpy(&n, dv.arch[archetype].numRows + world, sizeof(int32_t),
+                           hipMemcpyDeviceToHost));
+    return n;
+}
+
+double Executor::timeNode(const char *name, int32_t num_steps)
+{
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+    for (int32_t s = 0; s < num_steps; s++) {
+        for (int32_t i = 0; i < impl_->graph.numNodes(); i++) {
+            bool match = strcmp(impl_->graph.nodeName(i), name) == 0;
+            hipEvent_t a = nullptr, b = nullptr;
+            if (match) {
+                MW_HIP_CHECK(hipEventCreate(&a));
+                MW_HIP_CHECK(hipEventCreate(&b));
+                MW_HIP_CHECK(hipEventRecord(a, impl_->stream));
+            }
+            impl_->graph.launchNode(i, lc);
+            if (match) {
+                MW_HIP_CHECK(hipEventRecord(b, impl_->stream));
+                evs.push_back({ a, b });
+            }
+        }
+        launchExports(*impl_, dv);
+    }
+    MW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
+    double total = 0;
+    for (auto &e : evs) {
+        float ms = 0;
+        MW_HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
+        total += ms;
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    return evs.empty() ? -1.0 : total / (double)evs.size();
+}
+
+void Executor::downloadState() { impl_->mgr->downloadFromDevice(impl_->stream); }
+const StateView &Executor::hostView() { return impl_->mgr->hostView(); }
+
+int32_t Executor::errorFlags()
+{
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    std::vector<int32_t> f(dv.numWorlds);
+    MW_HIP_CHECK(hipMemcpy(f.data(), dv.errorFlags, sizeof(int32_t) * dv.numWorlds,
+                           hipMemcpyDeviceToHost));
+    int32_t r = 0;
+    for (int32_t v : f) r |= v;
+    return r;
+}
+
+}

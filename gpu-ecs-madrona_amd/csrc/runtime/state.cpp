@@ -1,0 +1,383 @@
+// Host-side ECS registry and arena for the MI355X framework.
+//
+// Restates the reference's registration semantics (src/core/state.cpp:363-435:
+// IDs by registration order, Entity column first, user columns from 1;
+// state.inl:171-187: one singleton entity per world from the init cache) and
+// lays every archetype out as [world][capacity] column slabs (state.hpp).
+#include <madrona/state.hpp>
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace madrona {
+
+#define MW_HIP_CHECK(expr)                                                          \
+    do {                                                                            \
+        hipError_t err__ = (expr);                                                  \
+        if (err__ != hipSuccess) {                                                  \
+            fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(err__),    \
+                    __FILE__, __LINE__);                                            \
+            throw std::runtime_error(hipGetErrorString(err__));                     \
+        }                                                                           \
+    } while (0)
+
+struct ArchetypeInfo {
+    uint64_t key;
+    std::string name;
+    std::vector<TypeDesc> cols;     // col 0 = Entity
+    int32_t capacity;
+    bool temporary;
+};
+
+struct StateManager::Impl {
+    Config cfg;
+    std::vector<TypeDesc> components;
+    std::vector<ArchetypeInfo> archetypes;
+    std::vector<uint64_t> singletons;      // archetype keys, registration order
+    std::map<uint64_t, int32_t> capacityHints;
+    std::vector<ExportDesc> exports;
+    std::vector<std::pair<std::string, std::unique_ptr<StateExtension>>> extensions;
+
+    bool finalized = false;
+    StateView host {};
+    StateView devHostCopy {};
+    StateView *devView = nullptr;
+
+    // host mirror allocations
+    std::vector<char *> hostAllocs;
+    // device allocations
+    std::vector<void *> devAllocs;
+    size_t arenaBytes = 0;
+
+    struct ColAlloc { char *host; char *dev; size_t bytes; bool temporary; };
+    std::vector<ColAlloc> colAllocs;
+
+    ~Impl()
+    {
+        for (char *p : hostAllocs) free(p);
+        for (void *p : devAllocs) (void)hipFree(p);
+        if (devView) (void)hipFree(devView);
+    }
+};
+
+static char *hostAlloc(StateManager::Impl &impl, size_t bytes)
+{
+    bytes = std::max<size_t>(bytes, 64);
+    char *p = (char *)aligned_alloc(256, (bytes + 255) & ~size_t(255));
+    if (!p) throw std::runtime_error("host allocation failed");
+    memset(p, 0, bytes);
+    impl.hostAllocs.push_back(p);
+    return p;
+}
+
+ECSRegistry::ECSRegistry(StateManager *state_mgr, void **export_ptrs)
+    : state_mgr_(state_mgr), export_ptrs_(export_ptrs)
+{}
+
+StateManager::StateManager(const Config &cfg)
+    : impl_(new Impl)
+{
+    impl_->cfg = cfg;
+    registerComponent<Entity>();                   // state.cpp:149-156
+}
+
+StateManager::~StateManager() { delete impl_; }
+
+uint32_t StateManager::registerComponentDesc(const TypeDesc &desc)
+{
+    for (size_t i = 0; i < impl_->components.size(); i++) {
+        if (impl_->components[i].key == desc.key) return (uint32_t)i;
+    }
+    impl_->components.push_back(desc);
+    return (uint32_t)impl_->components.size() - 1;
+}
+
+void StateManager::setCapacityHint(uint64_t key, int32_t capacity)
+{
+    impl_->capacityHints[key] = capacity;
+}
+
+int32_t StateManager::capacityHint(uint64_t key) const
+{
+    auto it = impl_->capacityHints.find(key);
+    return it == impl_->capacityHints.end() ? 0 : it->second;
+}
+
+void StateManager::setTemporary(uint64_t key)
+{
+    for (auto &a : impl_->archetypes) {
+        if (a.key == key) a.temporary = true;
+    }
+}
+
+uint32_t StateManager::registerArchetypeDesc(uint64_t key, const char *name,
+                                             const TypeDesc *comps, int32_t num_comps,
+                                             int32_t capacity, bool temporary)
+{
+    if (impl_->finalized) throw std::runtime_error("registerArchetype after finalize");
+    for (size_t i = 0; i < impl_->archetypes.size(); i++) {
+        if (impl_->archetypes[i].key == key) return (uint32_t)i;
+    }
+    if ((int32_t)impl_->archetypes.size() >= kMaxArchetypes) {
+        throw std::runtime_error("too many archetypes");
+    }
+    if (num_comps + 1 > kMaxColumns) throw std::runtime_error("too many columns");
+    ArchetypeInfo a;
+    a.key = key;
+    a.name = name;
+    a.cols.push_back(impl_->components[0]);        // Entity column
+    for (int32_t i = 0; i < num_comps; i++) {
+        registerComponentDesc(comps[i]);
+        a.cols.push_back(comps[i]);
+    }
+    if (capacity <= 0) capacity = capacityHint(key);
+    if (capacity <= 0) capacity = impl_->cfg.defaultCapacity;
+    a.capacity = capacity;
+    a.temporary = temporary;
+    impl_->archetypes.push_back(std::move(a));
+    return (uint32_t)impl_->archetypes.size() - 1;
+}
+
+void StateManager::registerSingletonDesc(uint64_t archetype_key)
+{
+    impl_->singletons.push_back(archetype_key);
+}
+
+int32_t StateManager::archetypeIndex(uint64_t key) const
+{
+    for (size_t i = 0; i < impl_->archetypes.size(); i++) {
+        if (impl_->archetypes[i].key == key) return (int32_t)i;
+    }
+    return -1;
+}
+
+int32_t StateManager::numArchetypes() const { return (int32_t)impl_->archetypes.size(); }
+int32_t StateManager::numWorlds() const { return impl_->cfg.numWorlds; }
+
+void StateManager::registerExport(int32_t slot, uint64_t archetype_key, uint64_t component_key)
+{
+    int32_t a = archetypeIndex(archetype_key);
+    if (a < 0) throw std::runtime_error("exportColumn: archetype not registered");
+    const ArchetypeInfo &ai = impl_->archetypes[a];
+    int32_t col = -1;
+    for (size_t c = 0; c < ai.cols.size(); c++) {
+        if (ai.cols[c].key == component_key) { col = (int32_t)c; break; }
+    }
+    if (col < 0) throw std::runtime_error("exportColumn: component not in archetype");
+    impl_->exports.push_back(ExportDesc { slot, a, col, ai.cols[col].numBytes });
+}
+
+const StateManager::ExportDesc *StateManager::exports(int32_t *num) const
+{
+    *num = (int32_t)impl_->exports.size();
+    return impl_->exports.data();
+}
+
+bool StateManager::finalized() const { return impl_->finalized; }
+StateView &StateManager::hostView() { return impl_->host; }
+const StateView &StateManager::hostViewConst() const { return impl_->host; }
+StateView *StateManager::deviceView() const { return impl_->devView; }
+const StateView &StateManager::deviceViewHost() const { return impl_->devHostCopy; }
+
+void StateManager::finalizeLayout(uint32_t world_data_bytes, uint32_t world_data_align)
+{
+    Impl &I = *impl_;
+    if (I.finalized) return;
+    const int32_t W = I.cfg.numWorlds;
+    StateView &v = I.host;
+    memset(&v, 0, sizeof(v));
+    v.numWorlds = W;
+    v.numArchetypes = (int32_t)I.archetypes.size();
+
+    int64_t ids_needed = 64;
+    for (int32_t a = 0; a < v.numArchetypes; a++) {
+        const ArchetypeInfo &ai = I.archetypes[a];
+        ArchetypeView &av = v.arch[a];
+        v.archKeys[a] = ai.key;
+        av.numColumns = (int32_t)ai.cols.size();
+        av.capacity = ai.capacity;
+        av.flags = ai.temporary ? 1u : 0u;
+        av.numRows = (int32_t *)hostAlloc(I, sizeof(int32_t) * W);
+        for (int32_t c = 0; c < av.numColumns; c++) {
+            size_t bytes = (size_t)W * ai.capacity * ai.cols[c].numBytes;
+            av.colBytes[c] = ai.cols[c].numBytes;
+            av.colKeys[c] = ai.cols[c].key;
+            // Temporaries start empty: no host mirror, the device slab is
+            // zero-filled at upload.
+            av.cols[c] = ai.temporary ? nullptr : hostAlloc(I, bytes);
+            I.colAllocs.push_back(Impl::ColAlloc { av.cols[c], nullptr, bytes, ai.temporary });
+        }
+        if (!ai.temporary) ids_needed += ai.capacity;
+    }
+
+    // Entity IDs: per world, generous slack because per-cache free lists can
+    // strand up to 2 x 64 IDs per cache (id_map_impl.inl:184-226).
+    int64_t ids = ((ids_needed * 2 + 4 * kIDsPerCache) + kIDsPerCache - 1) / kIDsPerCache * kIDsPerCache;
+    v.idsPerWorld = (int32_t)ids;
+    v.idNodes = (IDNode *)hostAlloc(I, sizeof(IDNode) * (size_t)W * ids);
+    v.idState = (IDMapState *)hostAlloc(I, sizeof(IDMapState) * W);
+    for (int32_t w = 0; w < W; w++) {
+        v.idState[w].globalHead = -1;
+        v.idState[w].numIDs = 0;
+        v.idState[w].worldCache = IDCache { -1, 0, -1, 0 };
+        v.idState[w].initCache = IDCache { -1, 0, -1, 0 };
+    }
+    uint32_t align = std::max<uint32_t>(world_data_align, 16);
+    v.worldDataStride = (std::max<uint32_t>(world_data_bytes, 16) + align - 1) / align * align;
+    v.worldData = hostAlloc(I, (size_t)v.worldDataStride * W);
+    v.errorFlags = (int32_t *)hostAlloc(I, sizeof(int32_t) * W);
+
+    // Singleton entities, per world in registration order, from the init
+    // cache (state.inl:171-187).  Single-world semantics: each world's IDs
+    // start at 0.
+    for (uint64_t skey : I.singletons) {
+        int32_t a = archetypeIndex(skey);
+        for (int32_t w = 0; w < W; w++) {
+            IDMapView idv = v.ids(w);
+            Entity e = idv.acquire(idv.st->initCache);
+            int32_t row = v.addRow(a, w);
+            v.column<Entity>(a, 0, w)[row] = e;
+            idv.nodes[e.id].val = Loc { (uint32_t)a, row };
+        }
+    }
+    I.finalized = true;
+}
+
+void StateManager::uploadToDevice(void *stream_ptr)
+{
+    Impl &I = *impl_;
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    const int32_t W = I.cfg.numWorlds;
+    StateView d = I.host;
+
+    auto devAlloc = [&](size_t bytes) -> char * {
+        void *p = nullptr;
+        MW_HIP_CHECK(hipMalloc(&p, std::max<size_t>(bytes, 256)));
+        I.devAllocs.push_back(p);
+        I.arenaBytes += bytes;
+        return (char *)p;
+    };
+    auto copy = [&](void *dst, const void *src, size_t bytes) {
+        MW_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+    };
+
+    size_t ci = 0;
+    for (int32_t a = 0; a < d.numArchetypes; a++) {
+        ArchetypeView &av = d.arch[a];
+        av.numRows = (int32_t *)devAlloc(sizeof(int32_t) * W);
+        copy(av.numRows, I.host.arch[a].numRows, sizeof(int32_t) * W);
+        for (int32_t c = 0; c < av.numColumns; c++, ci++) {
+            Impl::ColAlloc &ca = I.colAllocs[ci];
+            ca.dev = devAlloc(ca.bytes);
+            if (ca.temporary) {
+                MW_HIP_CHECK(hipMemsetAsync(ca.dev, 0, ca.bytes, stream));
+            } else {
+                copy(ca.dev, ca.host, ca.bytes);
+            }
+            av.cols[c] = ca.dev;
+        }
+    }
+    d.idNodes = (IDNode *)devAlloc(sizeof(IDNode) * (size_t)W * d.idsPerWorld);
+    copy(d.idNodes, I.host.idNodes, sizeof(IDNode) * (size_t)W * d.idsPerWorld);
+    d.idState = (IDMapState *)devAlloc(sizeof(IDMapState) * W);
+    copy(d.idState, I.host.idState, sizeof(IDMapState) * W);
+    d.worldData = devAlloc((size_t)d.worldDataStride * W);
+    copy(d.worldData, I.host.worldData, (size_t)d.worldDataStride * W);
+    d.errorFlags = (int32_t *)devAlloc(sizeof(int32_t) * W);
+    copy(d.errorFlags, I.host.errorFlags, sizeof(int32_t) * W);
+
+    MW_HIP_CHECK(hipMalloc(&I.devView, sizeof(StateView)));
+    copy(I.devView, &d, sizeof(StateView));
+    I.devHostCopy = d;
+
+    for (auto &ext : I.extensions) ext.second->upload(stream_ptr);
+    MW_HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+void StateManager::downloadFromDevice(void *stream_ptr)
+{
+    Impl &I = *impl_;
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    const int32_t W = I.cfg.numWorlds;
+    const StateView &d = I.devHostCopy;
+    StateView &h = I.host;
+    size_t ci = 0;
+    for (int32_t a = 0; a < d.numArchetypes; a++) {
+        MW_HIP_CHECK(hipMemcpyAsync(h.arch[a].numRows, d.arch[a].numRows, sizeof(int32_t) * W,
+                                    hipMemcpyDeviceToHost, stream));
+        for (int32_t c = 0; c < d.arch[a].numColumns; c++, ci++) {
+            Impl::ColAlloc &ca = I.colAllocs[ci];
+            if (!ca.host) {
+                ca.host = hostAlloc(I, ca.bytes);
+                h.arch[a].cols[c] = ca.host;
+            }
+            MW_HIP_CHECK(hipMemcpyAsync(ca.host, ca.dev, ca.bytes, hipMemcpyDeviceToHost, stream));
+        }
+    }
+    MW_HIP_CHECK(hipMemcpyAsync(h.idNodes, d.idNodes, sizeof(IDNode) * (size_t)W * d.idsPerWorld,
+                                hipMemcpyDeviceToHost, stream));
+    MW_HIP_CHECK(hipMemcpyAsync(h.idState, d.idState, sizeof(IDMapState) * W,
+                                hipMemcpyDeviceToHost, stream));
+    MW_HIP_CHECK(hipMemcpyAsync(h.errorFlags, d.errorFlags, sizeof(int32_t) * W,
+                                hipMemcpyDeviceToHost, stream));
+    MW_HIP_CHECK(hipMemcpyAsync(h.worldData, d.worldData, (size_t)d.worldDataStride * W,
+                                hipMemcpyDeviceToHost, stream));
+    MW_HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+int32_t StateManager::resolveQuery(const uint64_t *keys, int32_t num_keys,
+                                   int32_t *out_archetypes, int32_t *out_cols,
+                                   int32_t max_out) const
+{                                       // src/core/state.cpp:270-361
+    const uint64_t entity_key = typeKey<Entity>();
+    int32_t n = 0;
+    for (size_t a = 0; a < impl_->archetypes.size(); a++) {
+        const ArchetypeInfo &ai = impl_->archetypes[a];
+        int32_t cols[32];
+        bool ok = true;
+        for (int32_t k = 0; k < num_keys && ok; k++) {
+            if (keys[k] == entity_key) { cols[k] = 0; continue; }
+            int32_t found = -1;
+            for (size_t c = 1; c < ai.cols.size(); c++) {
+                if (ai.cols[c].key == keys[k]) { found = (int32_t)c; break; }
+            }
+            if (found < 0) ok = false;
+            cols[k] = found;
+        }
+        if (!ok) continue;
+        if (n >= max_out) throw std::runtime_error("query matches too many archetypes");
+        out_archetypes[n] = (int32_t)a;
+        for (int32_t k = 0; k < num_keys; k++) out_cols[n * 12 + k] = cols[k];
+        n++;
+    }
+    return n;
+}
+
+void StateManager::setExtension(const char *name, StateExtension *ext)
+{
+    for (auto &e : impl_->extensions) {
+        if (e.first == name) {
+            e.second.reset(ext);
+            return;
+        }
+    }
+    impl_->extensions.emplace_back(name, std::unique_ptr<StateExtension>(ext));
+}
+
+StateExtension *StateManager::getExtension(const char *name) const
+{
+    for (auto &e : impl_->extensions) {
+        if (e.first == name) return e.second.get();
+    }
+    return nullptr;
+}
+
+}

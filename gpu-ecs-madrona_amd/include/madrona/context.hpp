@@ -1,0 +1,255 @@
+// Per-world context (reference include/madrona/context.hpp:17-159,
+// context.inl, custom_context.hpp).  One Context type serves both sides:
+//   * host, while WorldT constructors build the initial state into the
+//     arena's host mirror (IDs are computed exactly as the reference's
+//     single-world executor would, SURVEY.md §8c entity-ID rule);
+//   * device, inside every kernel, one Context per (world, lane).
+// Structural mutation on the device (makeEntityNow / destroyEntityNow /
+// clear) is only legal from a node that owns the world serially (see
+// taskgraph.hpp SerialWorldNode); row-parallel nodes use makeTemporary's
+// ordered append instead.
+#pragma once
+
+#include <madrona/state.hpp>
+
+#include <new>
+
+namespace madrona {
+
+struct WorkerInit {
+    StateView *state;
+    int32_t worldIdx;
+    StateManager *mgr;     // host only (query resolution); null on device
+};
+
+template <typename T>
+class ResultRef {
+public:
+    MW_INLINE ResultRef(T *ptr) : ptr_(ptr) {}
+    MW_INLINE T &value() { return *ptr_; }
+    MW_INLINE bool valid() const { return ptr_ != nullptr; }
+private:
+    T *ptr_;
+};
+
+inline constexpr int32_t kMaxQueryArchetypes = 8;
+inline constexpr int32_t kMaxQueryComponents = 12;
+
+// A resolved query: matching archetypes and the column of each component.
+// Plain data, so a Query built on the host (e.g. stored in world data) is
+// valid inside kernels.
+template <typename... ComponentTs>
+struct Query {
+    int32_t numArchetypes = 0;
+    int32_t archetypes[kMaxQueryArchetypes];
+    int32_t cols[kMaxQueryArchetypes][sizeof...(ComponentTs) > 0 ? sizeof...(ComponentTs) : 1];
+
+    static Query resolve(const StateManager &mgr);
+};
+
+class Context {
+public:
+    MW_INLINE Context(WorldBase *world_data, const WorkerInit &init)
+        : data_(world_data), state_(init.state), world_(init.worldIdx), mgr_(init.mgr)
+    {}
+
+    template <typename ArchetypeT, typename... Args>
+    MW_INLINE Entity makeEntityNow(Args &&...args);
+    MW_INLINE void destroyEntityNow(Entity e);
+    template <typename ArchetypeT>
+    MW_INLINE Loc makeTemporary();
+
+    MW_INLINE Loc getLoc(Entity e) const { return state_->ids(world_).lookup(e); }
+
+    template <typename ComponentT> MW_INLINE ResultRef<ComponentT> get(Entity e);
+    template <typename ComponentT> MW_INLINE ResultRef<ComponentT> get(Loc l);
+    template <typename ComponentT> MW_INLINE ComponentT &getUnsafe(Entity e) { return getUnsafe<ComponentT>(e.id); }
+    template <typename ComponentT> MW_INLINE ComponentT &getUnsafe(int32_t e_id);
+    template <typename ComponentT> MW_INLINE ComponentT &getUnsafe(Loc l);
+    template <typename ComponentT>
+    MW_INLINE ComponentT &getDirect(int32_t column_idx, Loc loc)
+    {
+        return state_->column<ComponentT>(loc.archetype, column_idx, world_)[loc.row];
+    }
+    template <typename SingletonT> MW_INLINE SingletonT &getSingleton();
+
+    template <typename ArchetypeT> MW_INLINE void clearArchetype() { clear(state_->findArchetype(typeKey<ArchetypeT>()), false); }
+    template <typename ArchetypeT> MW_INLINE void clearTemporaries() { clear(state_->findArchetype(typeKey<ArchetypeT>()), true); }
+
+    template <typename... ComponentTs> Query<ComponentTs...> query();
+    template <typename... ComponentTs, typename Fn>
+    MW_INLINE void forEach(const Query<ComponentTs...> &q, Fn &&fn);
+    template <typename... ComponentTs>
+    MW_INLINE uint32_t numMatches(const Query<ComponentTs...> &q);
+
+    template <typename ArchetypeT> MW_INLINE int32_t numRows()
+    {
+        return state_->arch[state_->findArchetype(typeKey<ArchetypeT>())].numRows[world_];
+    }
+
+    MW_INLINE void *tmpAlloc(uint64_t) { return nullptr; }
+    MW_INLINE void resetTmpAlloc() {}
+
+    MW_INLINE WorldID worldID() const { return WorldID { world_ }; }
+    MW_INLINE WorldBase &data() { return *data_; }
+    MW_INLINE StateView &state() { return *state_; }
+
+    // registration forwarding used by some reference examples' ctors
+    template <typename ComponentT> void registerComponent() {}
+    template <typename ArchetypeT> void registerArchetype() {}
+
+protected:
+    MW_INLINE void clear(int32_t archetype, bool is_temporary);
+
+    WorldBase *data_;
+    StateView *state_;
+    int32_t world_;
+    StateManager *mgr_;
+};
+
+template <typename ContextT, typename DataT>
+class CustomContext : public Context {
+public:
+    MW_INLINE CustomContext(DataT *world_data, const WorkerInit &init)
+        : Context(world_data, init)
+    {}
+    MW_INLINE DataT &data() const { return *static_cast<DataT *>(data_); }
+
+    using WorldDataT = DataT;
+};
+
+// ---------------------------------------------------------------------------
+template <typename ArchetypeT, typename... Args>
+MW_INLINE Entity Context::makeEntityNow(Args &&...args)
+{                                              // state.inl:398-449
+    int32_t arch = state_->findArchetype(typeKey<ArchetypeT>());
+    IDMapView ids = state_->ids(world_);
+    Entity e = ids.acquire(ids.st->worldCache);
+    int32_t row = state_->addRow(arch, world_);
+    if (row < 0 || e.id < 0) return Entity::none();
+    state_->column<Entity>(arch, 0, world_)[row] = e;
+    int32_t col = 1;
+    auto construct = [&](auto &&arg) {
+        using T = std::remove_cv_t<std::remove_reference_t<decltype(arg)>>;
+        new (&state_->column<T>(arch, col, world_)[row]) T(std::forward<decltype(arg)>(arg));
+        col++;
+    };
+    (construct(std::forward<Args>(args)), ...);
+    ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
+    return e;
+}
+
+MW_INLINE void Context::destroyEntityNow(Entity e)
+{                                              // src/core/state.cpp:181-202
+    IDMapView ids = state_->ids(world_);
+    Loc loc = ids.lookup(e);
+    if (!loc.valid()) return;
+    bool moved = state_->removeRow(loc.archetype, world_, loc.row);
+    if (moved) {
+        Entity m = state_->column<Entity>(loc.archetype, 0, world_)[loc.row];
+        ids.nodes[m.id].val.row = loc.row;
+    }
+    ids.release(ids.st->worldCache, e.id);
+}
+
+template <typename ArchetypeT>
+MW_INLINE Loc Context::makeTemporary()
+{                                              // state.inl:451-463
+    int32_t arch = state_->findArchetype(typeKey<ArchetypeT>());
+    int32_t row = state_->addRow(arch, world_);
+    return Loc { (uint32_t)arch, row };
+}
+
+MW_INLINE void Context::clear(int32_t arch, bool is_temporary)
+{                                              // src/core/state.cpp:565-581
+    if (!is_temporary) {
+        IDMapView ids = state_->ids(world_);
+        ids.bulkRelease(ids.st->worldCache, state_->column<Entity>(arch, 0, world_),
+                        state_->arch[arch].numRows[world_]);
+    }
+    state_->arch[arch].numRows[world_] = 0;
+}
+
+template <typename ComponentT>
+MW_INLINE ResultRef<ComponentT> Context::get(Loc loc)
+{
+    int32_t col = state_->findColumn(loc.archetype, typeKey<ComponentT>());
+    if (col < 0) return ResultRef<ComponentT>(nullptr);
+    return ResultRef<ComponentT>(&state_->column<ComponentT>(loc.archetype, col, world_)[loc.row]);
+}
+
+template <typename ComponentT>
+MW_INLINE ResultRef<ComponentT> Context::get(Entity e)
+{
+    Loc loc = getLoc(e);
+    if (!loc.valid()) return ResultRef<ComponentT>(nullptr);
+    return get<ComponentT>(loc);
+}
+
+template <typename ComponentT>
+MW_INLINE ComponentT &Context::getUnsafe(int32_t e_id)
+{
+    Loc loc = state_->ids(world_).nodes[e_id].val;
+    return getUnsafe<ComponentT>(loc);
+}
+
+template <typename ComponentT>
+MW_INLINE ComponentT &Context::getUnsafe(Loc loc)
+{
+    int32_t col = state_->findColumn(loc.archetype, typeKey<ComponentT>());
+    return state_->column<ComponentT>(loc.archetype, col, world_)[loc.row];
+}
+
+template <typename SingletonT>
+MW_INLINE SingletonT &Context::getSingleton()
+{
+    int32_t arch = state_->findArchetype(typeKey<SingletonArchetype<SingletonT>>());
+    return state_->column<SingletonT>(arch, 1, world_)[0];
+}
+
+template <typename... ComponentTs, typename Fn>
+MW_INLINE void Context::forEach(const Query<ComponentTs...> &q, Fn &&fn)
+{                                              // state.inl:358-396
+    for (int32_t a = 0; a < q.numArchetypes; a++) {
+        int32_t arch = q.archetypes[a];
+        int32_t n = state_->arch[arch].numRows[world_];
+        int32_t ci = 0;
+        auto ptrs = std::make_tuple(
+            state_->column<std::remove_const_t<ComponentTs>>(arch, q.cols[a][ci++], world_)...);
+        for (int32_t r = 0; r < n; r++) {
+            std::apply([&](auto *...p) { fn(p[r]...); }, ptrs);
+        }
+    }
+}
+
+template <typename... ComponentTs>
+MW_INLINE uint32_t Context::numMatches(const Query<ComponentTs...> &q)
+{
+    uint32_t n = 0;
+    for (int32_t a = 0; a < q.numArchetypes; a++) n += state_->arch[q.archetypes[a]].numRows[world_];
+    return n;
+}
+
+template <typename... ComponentTs>
+Query<ComponentTs...> Query<ComponentTs...>::resolve(const StateManager &mgr)
+{
+    Query<ComponentTs...> q;
+    constexpr int32_t nc = sizeof...(ComponentTs);
+    uint64_t keys[nc > 0 ? nc : 1] = { typeKey<std::remove_const_t<ComponentTs>>()... };
+    int32_t archs[kMaxQueryArchetypes];
+    int32_t cols[kMaxQueryArchetypes * kMaxQueryComponents];
+    q.numArchetypes = mgr.resolveQuery(keys, nc, archs, cols, kMaxQueryArchetypes);
+    for (int32_t a = 0; a < q.numArchetypes; a++) {
+        q.archetypes[a] = archs[a];
+        for (int32_t c = 0; c < nc; c++) q.cols[a][c] = cols[a * kMaxQueryComponents + c];
+    }
+    return q;
+}
+
+template <typename... ComponentTs>
+Query<ComponentTs...> Context::query()
+{
+    return Query<ComponentTs...>::resolve(*mgr_);
+}
+
+}

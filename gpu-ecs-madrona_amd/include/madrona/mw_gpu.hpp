@@ -1,0 +1,104 @@
+// MI355X multi-world executor.
+//
+// Reference interfaces: MWCudaExecutor (include/madrona/mw_gpu.hpp:20-76,
+// src/mw/cuda_exec.cpp:1692-1815) and TaskGraphExecutor (include/madrona/
+// mw_cpu.hpp:53-81, mw_cpu.inl).  The reference JIT-compiles user sources
+// with NVRTC at executor construction; here the environment is compiled ahead
+// of time by hipcc for gfx950 and the executor is a template over the world
+// type, exactly like TaskGraphExecutor<ContextT, WorldT, ConfigT, InitT>.
+//
+// Construction (host):  registerTypes -> finalize arena -> per-world WorldT
+// ctor into the host mirror (IDs as the reference computes them) -> upload ->
+// setupTasks / build -> capture the step into a hipGraph.
+// run():  one hipGraphLaunch on the executor's stream (+ sync unless async).
+#pragma once
+
+#include <madrona/taskgraph.hpp>
+
+#include <functional>
+#include <memory>
+#include <new>
+#include <vector>
+
+namespace madrona {
+
+struct ExecConfig {
+    int32_t numWorlds;
+    int32_t gpuID;
+    int32_t defaultCapacity;        // rows per world per archetype
+    int32_t numExportedBuffers;
+    int32_t useGraph;               // capture the step into a hipGraph
+};
+
+// Non-template core (csrc/runtime/executor.cpp).
+class Executor {
+public:
+    explicit Executor(const ExecConfig &cfg);
+    ~Executor();
+
+    StateManager &stateManager();
+    ECSRegistry registry();
+
+    // Phase hooks used by the TaskGraphExecutor template below.
+    void finalizeRegistration(uint32_t world_bytes, uint32_t world_align);
+    Context makeHostContext(int32_t world);
+    char *hostWorldData(int32_t world);
+    void uploadState();
+    void setGraph(TaskGraph &&graph);
+
+    void run();                               // step + sync
+    void runAsync();                          // step, no sync
+    void sync();
+    void *stream() const;
+
+    // Packed export (reference getExported contract: rows of all worlds,
+    // world-major).  Valid after run().
+    void *getExported(int32_t slot, int64_t *num_rows = nullptr);
+    void copyOutExports();
+
+    // Raw column access (device pointer of a [world][capacity] slab).
+    void *columnBase(int32_t archetype, int32_t column, int32_t *capacity, uint32_t *bytes);
+    int32_t numRows(int32_t archetype, int32_t world);
+    void downloadState();
+    const StateView &hostView();
+    int32_t numWorlds() const;
+    int32_t errorFlags();                     // OR of per-world error flags
+
+    // Eagerly run num_steps steps with HIP events around every launch of the
+    // node kind `name` (on the executor stream); mean ms per launch.
+    double timeNode(const char *name, int32_t num_steps);
+
+    struct Impl;
+private:
+    std::unique_ptr<Impl> impl_;
+};
+
+template <typename ContextT, typename WorldT, typename ConfigT, typename InitT>
+class TaskGraphExecutor : public Executor {
+public:
+    TaskGraphExecutor(const ExecConfig &cfg, const ConfigT &user_cfg, const InitT *user_inits)
+        : Executor(cfg)
+    {
+        ECSRegistry reg = registry();
+        WorldT::registerTypes(reg, user_cfg);
+        finalizeRegistration((uint32_t)sizeof(WorldT), (uint32_t)alignof(WorldT));
+
+        for (int32_t w = 0; w < cfg.numWorlds; w++) {
+            Context base = makeHostContext(w);
+            WorldT *world = (WorldT *)hostWorldData(w);
+            ContextT ctx(world, WorkerInit { &stateManager().hostView(), w, &stateManager() });
+            new (world) WorldT(ctx, user_cfg, user_inits[w]);
+            (void)base;
+        }
+
+        uploadState();
+
+        WorldT *world0 = (WorldT *)hostWorldData(0);
+        ContextT ctx0(world0, WorkerInit { &stateManager().hostView(), 0, &stateManager() });
+        TaskGraph::Builder builder(ctx0);
+        WorldT::setupTasks(builder, user_cfg);
+        setGraph(builder.build());
+    }
+};
+
+}

@@ -1,0 +1,254 @@
+"""Python host mirror of the MI355X world-stepper (ctypes over the C ABI in
+include/madrona_mw.h).
+
+Mirrors the reference executor surface (TaskGraphExecutor / MWCudaExecutor:
+construct with per-world inits, ``step()`` = ``run()``, ``exported(slot)`` =
+``getExported(slot)``).  The HIP library is REQUIRED: importing this package
+without ``gpu-ecs-madrona_amd/build/libmadrona_mw.so`` raises, and creating an
+executor without a HIP device raises -- there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "build", "libmadrona_mw.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"madrona_mi355x: HIP library missing at {LIB_PATH}; "
+        "build it with `make -C gpu-ecs-madrona_amd` (or __graft_entry__.build())")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+
+class MwConfig(ctypes.Structure):
+    _fields_ = [("num_worlds", ctypes.c_int32), ("gpu_id", ctypes.c_int32),
+                ("default_capacity", ctypes.c_int32), ("use_graph", ctypes.c_int32)]
+
+
+class CollisionsConfig(ctypes.Structure):
+    _fields_ = [("num_cubes", ctypes.c_int32), ("num_substeps", ctypes.c_int32),
+                ("delta_t", ctypes.c_float), ("gravity_z", ctypes.c_float),
+                ("max_contacts", ctypes.c_int32), ("max_candidates", ctypes.c_int32),
+                ("cube_inv_mass", ctypes.c_float), ("cube_inv_inertia", ctypes.c_float),
+                ("mu_s", ctypes.c_float), ("mu_d", ctypes.c_float)]
+
+
+class CollisionsInit(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_void_p), ("rot", ctypes.c_void_p)]
+
+
+_lib.mw_create.restype = ctypes.c_void_p
+_lib.mw_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(MwConfig), ctypes.c_void_p,
+                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+_lib.mw_step.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_step_async.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_sync.argtypes = [ctypes.c_void_p]
+_lib.mw_get_exported.restype = ctypes.c_void_p
+_lib.mw_get_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
+_lib.mw_stream.restype = ctypes.c_void_p
+_lib.mw_stream.argtypes = [ctypes.c_void_p]
+_lib.mw_destroy.argtypes = [ctypes.c_void_p]
+_lib.mw_last_error.restype = ctypes.c_char_p
+_lib.mw_num_worlds.argtypes = [ctypes.c_void_p]
+_lib.mw_error_flags.argtypes = [ctypes.c_void_p]
+_lib.mw_num_archetypes.argtypes = [ctypes.c_void_p]
+_lib.mw_read_column.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_column_info.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+_lib.mw_phys_read_candidates.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_phys_read_contacts.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_phys_time_node.restype = ctypes.c_double
+_lib.mw_phys_time_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
+
+# The symbols include/madrona_mw.h declares (checked by tests/test_capi_symbols.py).
+C_ABI_SYMBOLS = (
+    "mw_create", "mw_step", "mw_step_async", "mw_sync", "mw_get_exported", "mw_stream",
+    "mw_destroy", "mw_last_error", "mw_num_worlds", "mw_error_flags", "mw_num_archetypes",
+    "mw_read_column", "mw_column_info", "mw_phys_read_candidates", "mw_phys_read_contacts",
+    "mw_phys_read_bvh", "mw_phys_time_node",
+)
+
+ERR_BITS = {1: "id store full", 2: "table full", 4: "candidate overflow",
+            8: "contact overflow", 16: "BVH stack overflow"}
+
+
+class MadronaError(RuntimeError):
+    pass
+
+
+def _err():
+    return MadronaError(_lib.mw_last_error().decode())
+
+
+def library():
+    return _lib
+
+
+CONTACT_DTYPE = np.dtype([
+    ("ref", np.uint32, 2), ("alt", np.uint32, 2), ("points", np.float32, (4, 4)),
+    ("numPoints", np.int32), ("normal", np.float32, 3), ("lambdaN", np.float32, 4),
+])
+BVH_NODE_DTYPE = np.dtype([
+    ("minX", np.float32, 4), ("minY", np.float32, 4), ("minZ", np.float32, 4),
+    ("maxX", np.float32, 4), ("maxY", np.float32, 4), ("maxZ", np.float32, 4),
+    ("children", np.int32, 4), ("parentID", np.int32),
+])
+
+# Same record layout the oracle libraries return, for 1:1 comparisons.
+BODY_DTYPE = np.dtype([
+    ("gen", np.uint32), ("id", np.int32),
+    ("pos", np.float32, 3), ("rot", np.float32, 4), ("vel", np.float32, 6),
+    ("prevPos", np.float32, 3), ("prevRot", np.float32, 4),
+    ("presolvePos", np.float32, 3), ("presolveRot", np.float32, 4),
+    ("presolveVel", np.float32, 6),
+    ("leafID", np.int32), ("objID", np.int32), ("responseType", np.uint32),
+])
+
+# physics body archetype id = registration order.
+BODY_ARCHETYPE = 6
+BODY_COLUMNS = {  # column index -> (BODY_DTYPE field(s), float/int words)
+    0: ("entity", 2), 1: ("pos", 3), 2: ("rot", 4), 4: ("vel", 6), 5: ("objID", 1),
+    6: ("responseType", 1), 7: ("prev", 7), 8: ("presolve", 7), 9: ("presolveVel", 6),
+    12: ("leafID", 1),
+}
+
+
+class Executor:
+    """A batch of worlds of one environment on one GPU."""
+
+    def __init__(self, env, num_worlds, user_cfg, inits, init_stride, gpu_id=0,
+                 default_capacity=64, use_graph=True):
+        cfg = MwConfig(num_worlds, gpu_id, default_capacity, 1 if use_graph else 0)
+        self._keep = (user_cfg, inits)
+        self.h = _lib.mw_create(env.encode(), ctypes.byref(cfg), ctypes.byref(user_cfg),
+                                ctypes.sizeof(user_cfg), ctypes.cast(inits, ctypes.c_void_p),
+                                init_stride)
+        if not self.h:
+            raise _err()
+        self.num_worlds = num_worlds
+
+    def step(self, n=1):
+        if _lib.mw_step(self.h, n) != 0:
+            raise _err()
+
+    def step_async(self, n=1):
+        if _lib.mw_step_async(self.h, n) != 0:
+            raise _err()
+
+    def sync(self):
+        if _lib.mw_sync(self.h) != 0:
+            raise _err()
+
+    @property
+    def stream(self):
+        return _lib.mw_stream(self.h)
+
+    def exported(self, slot):
+        rows = ctypes.c_int64(0)
+        ptr = _lib.mw_get_exported(self.h, slot, ctypes.byref(rows))
+        return ptr, rows.value
+
+    def error_flags(self):
+        return _lib.mw_error_flags(self.h)
+
+    def read_column(self, archetype, column, world, dtype, max_rows=4096):
+        b = ctypes.c_int32()
+        cap = ctypes.c_int32()
+        if _lib.mw_column_info(self.h, archetype, column, ctypes.byref(b), ctypes.byref(cap)) != 0:
+            raise MadronaError(f"no column {archetype}:{column}")
+        buf = np.zeros(max(cap.value, 1) * b.value, np.uint8)
+        n = _lib.mw_read_column(self.h, archetype, column, world,
+                                buf.ctypes.data_as(ctypes.c_void_p), cap.value)
+        if n < 0:
+            raise _err()
+        return buf[: n * b.value].view(dtype)
+
+    def time_node(self, name, steps):
+        return _lib.mw_phys_time_node(self.h, name.encode(), steps)
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.mw_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def default_collisions_config(num_cubes=128, num_substeps=4, max_contacts=4096,
+                              max_candidates=4096):
+    """dt 1/60, S=4, g=-9.8, unit mass cubes."""
+    return CollisionsConfig(num_cubes, num_substeps, 1.0 / 60.0, -9.8, max_contacts,
+                            max_candidates, 1.0, 1.5, 0.5, 0.5)
+
+
+class CollisionsSim(Executor):
+    """The `collisions` rigid-body environment (RigidBodyPhysicsSystem)."""
+
+    def __init__(self, num_worlds, pos, rot, cfg=None, gpu_id=0, use_graph=True):
+        cfg = cfg or default_collisions_config(num_cubes=pos.shape[1])
+        self._pos = np.ascontiguousarray(pos, np.float32)
+        self._rot = np.ascontiguousarray(rot, np.float32)
+        assert self._pos.shape == (num_worlds, cfg.num_cubes, 3)
+        assert self._rot.shape == (num_worlds, cfg.num_cubes, 4)
+        inits = (CollisionsInit * num_worlds)()
+        pbase = self._pos.ctypes.data
+        rbase = self._rot.ctypes.data
+        for w in range(num_worlds):
+            inits[w].pos = pbase + w * cfg.num_cubes * 12
+            inits[w].rot = rbase + w * cfg.num_cubes * 16
+        self.cfg = cfg
+        self.num_bodies = cfg.num_cubes + 1
+        super().__init__("collisions", num_worlds, cfg, inits, ctypes.sizeof(CollisionsInit),
+                         gpu_id=gpu_id, default_capacity=64, use_graph=use_graph)
+
+    def bodies(self, w):
+        """Per-body state of world w in the oracle's record layout."""
+        A = BODY_ARCHETYPE
+        out = np.zeros(self.num_bodies, BODY_DTYPE)
+        ent = self.read_column(A, 0, w, np.uint32).reshape(-1, 2)
+        n = len(ent)
+        out = out[:n]
+        out["gen"] = ent[:, 0]
+        out["id"] = ent[:, 1].view(np.int32)
+        out["pos"] = self.read_column(A, 1, w, np.float32).reshape(n, 3)
+        out["rot"] = self.read_column(A, 2, w, np.float32).reshape(n, 4)
+        out["vel"] = self.read_column(A, 4, w, np.float32).reshape(n, 6)
+        out["objID"] = self.read_column(A, 5, w, np.int32)
+        out["responseType"] = self.read_column(A, 6, w, np.uint32)
+        prev = self.read_column(A, 7, w, np.float32).reshape(n, 7)
+        out["prevPos"], out["prevRot"] = prev[:, :3], prev[:, 3:]
+        ps = self.read_column(A, 8, w, np.float32).reshape(n, 7)
+        out["presolvePos"], out["presolveRot"] = ps[:, :3], ps[:, 3:]
+        out["presolveVel"] = self.read_column(A, 9, w, np.float32).reshape(n, 6)
+        out["leafID"] = self.read_column(A, 12, w, np.int32)
+        return out
+
+    def candidates(self, w, cap=1 << 15):
+        out = np.zeros((cap, 4), np.int32)
+        n = _lib.mw_phys_read_candidates(self.h, w, out.ctypes.data_as(ctypes.c_void_p), cap)
+        if n < 0:
+            raise _err()
+        return out[:n]
+
+    def contacts(self, w, cap=1 << 14):
+        out = np.zeros(cap, CONTACT_DTYPE)
+        n = _lib.mw_phys_read_contacts(self.h, w, out.ctypes.data_as(ctypes.c_void_p), cap)
+        if n < 0:
+            raise _err()
+        return out[:n]
+
+    def bvh(self, w, cap=4096):
+        nodes = np.zeros(cap, BVH_NODE_DTYPE)
+        aabbs = np.zeros((self.num_bodies, 6), np.float32)
+        n = _lib.mw_phys_read_bvh(self.h, w, nodes.ctypes.data_as(ctypes.c_void_p),
+                                  aabbs.ctypes.data_as(ctypes.c_void_p), cap)
+        if n < 0:
+            raise _err()
+        return nodes[:n], aabbs

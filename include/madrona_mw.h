@@ -1,0 +1,125 @@
+/*
+ * C ABI of the MI355X-native batched ECS world-stepper.
+ *
+ * This is the drop-in boundary for the reference's executor surface:
+ *
+ *   mw_create        <- madrona::MWCudaExecutor::MWCudaExecutor(StateConfig,
+ *                       CompileConfig)  (reference include/madrona/mw_gpu.hpp:55-59,
+ *                       src/mw/cuda_exec.cpp:1692-1763) and
+ *                       TaskGraphExecutor::TaskGraphExecutor(cfg, user_cfg, inits)
+ *                       (include/madrona/mw_cpu.hpp:53-60, mw_cpu.inl:8-44)
+ *   mw_step          <- MWCudaExecutor::run()   (src/mw/cuda_exec.cpp:1777-1794),
+ *                       TaskGraphExecutor::run() (include/madrona/mw_cpu.inl:46-50)
+ *   mw_get_exported  <- getExported(slot)       (src/mw/cuda_exec.cpp:1796-1800,
+ *                       include/madrona/mw_cpu.hpp:38); adds the packed row count
+ *   mw_destroy       <- ~MWCudaExecutor()
+ *
+ * The reference reports errors by aborting (FATAL / REQ_CUDA,
+ * include/madrona/cuda_utils.hpp:46-54); here every entry point returns a
+ * status (0 = ok) or NULL and mw_last_error() describes the failure.
+ * Environments are compiled ahead of time into the library and selected by
+ * name (the reference JIT-compiles them with NVRTC instead).
+ *
+ * All pointers are plain host pointers except those documented as device
+ * pointers (mw_get_exported, mw_stream).  No torch types cross this boundary.
+ */
+#ifndef MADRONA_MW_H
+#define MADRONA_MW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mw_exec mw_exec;
+
+/* Executor configuration (reference StateConfig, mw_gpu.hpp:20-32). */
+typedef struct mw_config {
+    int32_t num_worlds;        /* worlds stepped by this executor (this GPU) */
+    int32_t gpu_id;            /* HIP device ordinal                         */
+    int32_t default_capacity;  /* rows per world for archetypes w/o a size   */
+    int32_t use_graph;         /* 1: replay the step as one hipGraph         */
+} mw_config;
+
+/* "collisions": rigid-body workload of SURVEY.md §8(d) C3/C4 (128 unit cube
+ * hulls + one static plane per world, src/physics).                        */
+typedef struct mw_collisions_config {
+    int32_t num_cubes;
+    int32_t num_substeps;
+    float delta_t;
+    float gravity_z;
+    int32_t max_contacts;      /* SolverData::maxContacts per world          */
+    int32_t max_candidates;    /* CandidateTemporary rows per world          */
+    float cube_inv_mass;
+    float cube_inv_inertia;
+    float mu_s;
+    float mu_d;
+} mw_collisions_config;
+
+/* Per-world init (reference InitT): host pointers to num_cubes x 3 positions
+ * and num_cubes x 4 quaternions (w, x, y, z).                              */
+typedef struct mw_collisions_init {
+    const float *pos;
+    const float *rot;
+} mw_collisions_init;
+
+/* Create an executor for environment `env`.  `inits` points at num_worlds
+ * records of `init_stride` bytes each (reference: const InitT *user_inits). */
+mw_exec *mw_create(const char *env, const mw_config *cfg,
+                   const void *user_cfg, size_t user_cfg_bytes,
+                   const void *inits, size_t init_stride);
+
+/* Step every world `num_steps` times; blocks until done. */
+int mw_step(mw_exec *exec, int32_t num_steps);
+
+/* Enqueue `num_steps` steps on the executor stream without waiting. */
+int mw_step_async(mw_exec *exec, int32_t num_steps);
+
+/* Wait for enqueued steps. */
+int mw_sync(mw_exec *exec);
+
+/* Device pointer of export slot `slot`: rows of all worlds packed
+ * world-major (reference getExported).  *num_rows receives the row count. */
+void *mw_get_exported(mw_exec *exec, int32_t slot, int64_t *num_rows);
+
+/* hipStream_t of the executor (device work ordering for callers). */
+void *mw_stream(mw_exec *exec);
+
+int mw_destroy(mw_exec *exec);
+const char *mw_last_error(void);
+
+/* ---- introspection (tests, tooling) ------------------------------------ */
+int32_t mw_num_worlds(mw_exec *exec);
+/* OR of per-world error flags (1 id store full, 2 table full, 4 candidate
+ * overflow, 8 contact overflow, 16 BVH stack overflow).                    */
+int32_t mw_error_flags(mw_exec *exec);
+int32_t mw_num_archetypes(mw_exec *exec);
+/* Copy rows of (archetype, column) of one world to host `out` (capacity
+ * max_rows); returns the world's row count or -1. */
+int32_t mw_read_column(mw_exec *exec, int32_t archetype, int32_t column,
+                       int32_t world, void *out, int32_t max_rows);
+/* Column byte width and rows-per-world capacity. */
+int32_t mw_column_info(mw_exec *exec, int32_t archetype, int32_t column,
+                       int32_t *bytes, int32_t *capacity);
+
+/* physics (collisions env): the last step's candidate pairs (4 x int32:
+ * a.archetype, a.row, b.archetype, b.row), the last substep's contacts in
+ * solver order (112-byte reference Contact records), the BVH (116-byte
+ * nodes, used prefix) and leaf AABBs.  Each returns the element count.    */
+int32_t mw_phys_read_candidates(mw_exec *exec, int32_t world, void *out, int32_t cap);
+int32_t mw_phys_read_contacts(mw_exec *exec, int32_t world, void *out, int32_t cap);
+int32_t mw_phys_read_bvh(mw_exec *exec, int32_t world, void *nodes_out,
+                         float *leaf_aabbs_out, int32_t cap_nodes);
+
+/* physics kernel timing hook for the bench: records HIP events around each
+ * launch of the named node kind on the executor stream ("SolverNode", ...).
+ * Returns the mean duration in ms over `num_steps` fresh steps.            */
+double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif
