@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of the `collisions` rigid-body workload
+(BASELINE.json configs[2]: 8192 worlds x 128 cube hulls + ground plane, S=4,
+dt=1/60) on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+
+A "step" = one taskgraph step of every world (broadphase, 4 XPBD substeps of
+integrate / narrowphase / solve, cleanup, episode-return node) replayed as one
+hipGraph, followed by the training hand-off: the per-world episode returns are
+copied into a torch tensor and, for N > 1, all-gathered over RCCL (xGMI).
+Worlds are sharded contiguously across ranks (weak scaling: 8192 per GPU;
+N = 8 is BASELINE.json configs[3], 65 536 worlds).
+
+Prints ONE JSON line on rank 0 (metric / value / roofline / cpu_baseline; see
+DESIGN.md §6 for the byte model behind `roofline`).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E 8.0 TB/s spec
+
+# Bytes each node moves per unit (SURVEY.md §8d column sizes).
+# body = one physics body row, cand = one candidate pair, contact = one
+# contact manifold.
+BYTES = {
+    "SubstepRigidBodiesNode": {"body": 108 + 108 + 192 + 192},
+    "NarrowphaseNode": {"cand": 16 + 2 * 52 + 2 * 28 + 2 * 192 + 4, "contact": 112},
+    "SolverNode": {"body": 156 + 52, "cand": 4, "contact": 4 + 112 + 16 + 112 + 8},
+    "FindOverlappingNode": {"body": 52 + 116 * 8, "cand": 16 + 20},
+    "UpdateLeafPositionsNode": {"body": 96 + 28},
+    "RefitNode": {"body": 80},
+    "UpdateBVHNode": {"body": 0},
+}
+NODE_KINDS = list(BYTES.keys()) + ["ParallelForNode"]
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--worlds", type=int, default=8192, help="worlds per GPU")
+    p.add_argument("--cubes", type=int, default=128)
+    p.add_argument("--substeps", type=int, default=4)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-worlds", type=int, default=256)
+    p.add_argument("--cpu-steps", type=int, default=40)
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--no-handoff", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(args, cfg):
+    """Reference CPU executor (oracle/_ref, the reference's own src/core +
+    src/physics) on a bounded sample of the same workload; falls back to the
+    parity-pinned restatement (oracle/) when the reference build is absent."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as ol
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    pos, rot = ol.gen_collisions_inits(args.cpu_worlds, args.cubes, seed=0)
+    ocfg = ol.PhysConfig(args.cubes, args.substeps, cfg.delta_t, cfg.gravity_z,
+                         cfg.max_contacts, cfg.cube_inv_mass, cfg.cube_inv_inertia,
+                         cfg.mu_s, cfg.mu_d)
+    if ol.ref_available():
+        lib = ol.load_ref()
+        lib.ref_phys_step_mt.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+        sim = ol.ReferencePhys(ocfg, pos, rot)
+        kind = "reference"
+        t0 = time.perf_counter()
+        lib.ref_phys_step_mt(sim.h, args.cpu_steps, threads)
+        dt = time.perf_counter() - t0
+    else:
+        sim = ol.OraclePhys(ocfg, pos, rot)
+        kind = "port"
+        t0 = time.perf_counter()
+        sim.step(args.cpu_steps, threads)
+        dt = time.perf_counter() - t0
+    value = args.cpu_worlds * args.cpu_steps / dt
+    return {
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": f"collisions {args.cpu_worlds} worlds x {args.cubes} cubes, S={args.substeps}, "
+                  f"steps 1-{args.cpu_steps} from init, {threads} host threads, {dt:.2f} s wall",
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus and world_size > 1:
+        print(f"warning: WORLD_SIZE={world_size} != --gpus {args.gpus}", file=sys.stderr)
+
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world_size > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+
+    import madrona_mi355x as mw
+
+    W = args.worlds
+    cfg = mw.default_collisions_config(args.cubes, args.substeps, max_contacts=4096,
+                                       max_candidates=4096)
+    pos, rot = mw.gen_collisions_inits(W, args.cubes, seed=0, first_world=rank * W)
+    sim = mw.CollisionsSim(W, pos, rot, cfg, gpu_id=local_rank)
+    del pos, rot
+
+    returns = torch.empty(W, dtype=torch.float32, device="cuda")
+    gathered = (torch.empty(W * world_size, dtype=torch.float32, device="cuda")
+                if world_size > 1 else None)
+
+    def step():
+        sim.step(1)
+        if args.no_handoff:
+            return
+        sim.copy_exported(2, returns.data_ptr(), W * 4)
+        if dist is not None:
+            dist.all_gather_into_tensor(gathered, returns)
+
+    for _ in range(args.warmup):
+        step()
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    flags = sim.error_flags()
+    total_worlds = W * world_size
+    value = total_worlds * args.steps / elapsed
+
+    roofline = None
+    node_table = {}
+    if not args.no_roofline:
+        cands, contacts = sim.counts()
+        units = {"body": W * (args.cubes + 1), "cand": float(cands.sum()),
+                 "contact": float(contacts.sum())}
+        launches = {"SubstepRigidBodiesNode": args.substeps, "NarrowphaseNode": args.substeps,
+                    "SolverNode": args.substeps, "FindOverlappingNode": 1,
+                    "UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
+                    "ParallelForNode": 1}
+        for name in NODE_KINDS:
+            ms = sim.time_node(name, 2)
+            if ms > 0:
+                node_table[name] = {"ms_per_launch": round(ms, 4),
+                                    "ms_per_step": round(ms * launches[name], 4)}
+        dom = max((n for n in node_table if n in BYTES),
+                  key=lambda n: node_table[n]["ms_per_step"])
+        nbytes = sum(BYTES[dom].get(u, 0) * units[u] for u in units)
+        ms = node_table[dom]["ms_per_launch"]
+        achieved = nbytes / (ms * 1e-3) / 1e9
+        roofline = {
+            "bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": None, "bytes_per_launch": int(nbytes), "ms_per_launch": ms,
+            "mean_candidates_per_world": round(float(cands.mean()), 1),
+            "mean_contacts_per_world": round(float(contacts.mean()), 1),
+        }
+
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, cfg)
+
+    if rank == 0:
+        out = {
+            "metric": "env-steps/sec (summed worlds)",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (reference example init: mt19937 seed 0 positions/rotations)",
+            "config": {
+                "workload": f"examples/collisions physics: {W} worlds/GPU x {args.cubes} cube hulls "
+                            f"+ ground plane, S={args.substeps}, dt=1/60",
+                "worlds_per_gpu": W, "total_worlds": total_worlds,
+                "parallelism": f"world-sharded x{world_size}" +
+                               ("" if args.no_handoff else ", per-step return hand-off"
+                                + (" (RCCL all-gather)" if world_size > 1 else "")),
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "error_flags": flags,
+            "nodes": node_table,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+    sim.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -12,6 +12,7 @@
 
 #include <cfloat>
 #include <cstring>
+#include <random>
 
 using namespace madrona;
 using namespace madrona::math;
@@ -31,6 +32,13 @@ struct Config {
     ObjectManager *objMgr;
 };
 
+// Per-world episode return handed to a learner: the running
+// sum over steps of the mean height of the dynamic bodies.  Exported as a
+// singleton column, all-gathered across GPUs by bench.py / the trainer.
+struct EpisodeReturn {
+    float value;
+};
+
 class Engine;
 
 struct PhysWorld : public WorldBase {
@@ -40,8 +48,10 @@ struct PhysWorld : public WorldBase {
         RigidBodyPhysicsSystem::setMaxCandidatesPerWorld(reg, cfg.c.max_candidates);
         RigidBodyPhysicsSystem::registerTypes(reg);
         reg.registerFixedSizeArchetype<PhysicsBody>(cfg.c.num_cubes + 1);
+        reg.registerSingleton<EpisodeReturn>();
         reg.exportColumn<PhysicsBody, Position>(0);
         reg.exportColumn<PhysicsBody, Rotation>(1);
+        reg.exportSingleton<EpisodeReturn>(2);
     }
 
     static void setupTasks(TaskGraph::Builder &builder, const Config &cfg)
@@ -49,16 +59,36 @@ struct PhysWorld : public WorldBase {
         auto bp = RigidBodyPhysicsSystem::setupBroadphaseTasks(builder, {});
         auto sub = RigidBodyPhysicsSystem::setupSubstepTasks(builder, { bp },
                                                              cfg.c.num_substeps);
-        RigidBodyPhysicsSystem::setupCleanupTasks(builder, { sub });
+        auto cleanup = RigidBodyPhysicsSystem::setupCleanupTasks(builder, { sub });
+        builder.addToGraph<ParallelForNode<Engine, accumulateReturn, EpisodeReturn>>({ cleanup });
     }
 
     PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &init);
+
+    static MW_HD void accumulateReturn(Engine &ctx, EpisodeReturn &ret);
+
+    Query<Position, ResponseType> bodyQuery;
 };
 
 class Engine : public CustomContext<Engine, PhysWorld> {
 public:
     using CustomContext::CustomContext;
 };
+
+// Generic ParallelForNode over the EpisodeReturn singleton: one lane per
+// world walks that world's bodies in row order (deterministic sum).
+MW_HD void PhysWorld::accumulateReturn(Engine &ctx, EpisodeReturn &ret)
+{
+    float sum = 0.f;
+    int32_t n = 0;
+    ctx.forEach(ctx.data().bodyQuery, [&](const Position &p, const ResponseType &rt) {
+        if (rt == ResponseType::Dynamic) {
+            sum += p.z;
+            n++;
+        }
+    });
+    ret.value += n > 0 ? sum / (float)n : 0.f;
+}
 
 PhysWorld::PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &init)
     : WorldBase(ctx)
@@ -94,6 +124,8 @@ PhysWorld::PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &i
     setup(plane, Vector3::zero(), Quat { 1.f, 0.f, 0.f, 0.f }, 1, ResponseType::Static);
 
     ctx.getSingleton<broadphase::BVH>().rebuildOnUpdate();
+    ctx.getSingleton<EpisodeReturn>().value = 0.f;
+    bodyQuery = ctx.query<Position, ResponseType>();
 }
 
 // Object table: 0 = cube hull (half extent 1), 1 = ground plane.
@@ -150,4 +182,33 @@ static Executor *create(const ExecConfig &ecfg, const void *user_cfg, size_t cfg
 
 static EnvRegistration reg("collisions", &create);
 
+}
+
+// Deterministic synthetic inputs (examples/collisions/collisions.cpp:20-39,
+// 48-51, 76-80): one mt19937 drawn serially over worlds; per body x, y, z
+// then the rotation angle about +Y.  first_world lets a rank draw only its
+// shard while staying identical to the serial sequence.
+extern "C" void mw_gen_collisions_inits(int32_t first_world, int32_t num_worlds,
+                                        int32_t num_cubes, uint32_t seed,
+                                        float *pos_out, float *rot_out)
+{
+    std::mt19937 gen(seed);
+    std::uniform_real_distribution<float> xd(-10.f, 10.f), yd(-10.f, 10.f), zd(0.f, 10.f);
+    std::uniform_real_distribution<float> ad(0.f, madrona::math::pi);
+    for (int64_t w = 0; w < (int64_t)first_world + num_worlds; w++) {
+        for (int64_t i = 0; i < num_cubes; i++) {
+            float x = xd(gen), y = yd(gen), z = zd(gen);
+            float angle = ad(gen);
+            if (w < first_world) continue;
+            int64_t k = (w - first_world) * num_cubes + i;
+            pos_out[3 * k] = x;
+            pos_out[3 * k + 1] = y;
+            pos_out[3 * k + 2] = z;
+            Quat q = Quat::angleAxis(angle, Vector3 { 0, 1, 0 });
+            rot_out[4 * k] = q.w;
+            rot_out[4 * k + 1] = q.x;
+            rot_out[4 * k + 2] = q.y;
+            rot_out[4 * k + 3] = q.z;
+        }
+    }
 }

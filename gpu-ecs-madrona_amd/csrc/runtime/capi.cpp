@@ -116,6 +116,22 @@ void *mw_get_exported(mw_exec *exec, int32_t slot, int64_t *num_rows)
     MW_TRY({ return exec->exec->getExported(slot, num_rows); }, nullptr)
 }
 
+int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_bytes)
+{
+    MW_TRY({
+        int64_t rows = 0;
+        void *src = exec->exec->getExported(slot, &rows);
+        if (!src) throw std::runtime_error("mw_copy_exported: no such export slot");
+        int32_t bytes_per_row = exec->exec->exportRowBytes(slot);
+        int64_t n = rows * bytes_per_row;
+        if (n > max_bytes) n = max_bytes;
+        MW_HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice,
+                                 (hipStream_t)exec->exec->stream()));
+        exec->exec->sync();
+        return n;
+    }, (int64_t)-1)
+}
+
 void *mw_stream(mw_exec *exec) { return exec ? exec->exec->stream() : nullptr; }
 
 int mw_destroy(mw_exec *exec)
@@ -239,4 +255,21 @@ double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps
     MW_TRY({ return exec->exec->timeNode(node_name, num_steps); }, -1.0)
 }
 
+}
+
+extern "C" int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *contacts_out)
+{
+    MW_TRY({
+        exec->exec->sync();
+        phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
+        if (!P) return -1;
+        if (cands_out) {
+            MW_HIP_OK(hipMemcpy(cands_out, P->lastNumCands, 4 * P->numWorlds, hipMemcpyDeviceToHost));
+        }
+        if (contacts_out) {
+            MW_HIP_OK(hipMemcpy(contacts_out, P->lastNumContacts, 4 * P->numWorlds,
+                                hipMemcpyDeviceToHost));
+        }
+        return P->numWorlds;
+    }, -1)
 }

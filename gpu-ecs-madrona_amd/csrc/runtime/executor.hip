@@ -300,6 +300,14 @@ void *Executor::getExported(int32_t slot, int64_t *num_rows)
     return nullptr;
 }
 
+int32_t Executor::exportRowBytes(int32_t slot)
+{
+    for (ExportBuf &b : impl_->exports) {
+        if (b.slot == slot) return (int32_t)b.bytes;
+    }
+    return 0;
+}
+
 void Executor::copyOutExports() { launchExports(*impl_, impl_->mgr->deviceViewHost()); }
 
 void *Executor::columnBase(int32_t archetype, int32_t column, int32_t *capacity, uint32_t *bytes)

@@ -55,6 +55,7 @@ public:
     // world-major).  Valid after run().
     void *getExported(int32_t slot, int64_t *num_rows = nullptr);
     void copyOutExports();
+    int32_t exportRowBytes(int32_t slot);
 
     // Raw column access (device pointer of a [world][capacity] slab).
     void *columnBase(int32_t archetype, int32_t column, int32_t *capacity, uint32_t *bytes);

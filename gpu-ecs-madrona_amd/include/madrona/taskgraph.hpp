@@ -121,6 +121,15 @@ private:
 // ---------------------------------------------------------------------------
 namespace detail {
 
+template <typename C, typename = void>
+struct WorldOf {
+    using type = WorldBase;
+};
+template <typename C>
+struct WorldOf<C, std::void_t<typename C::WorldDataT>> {
+    using type = typename C::WorldDataT;
+};
+
 template <int32_t N>
 struct ColArgs {
     int32_t c[N > 0 ? N : 1];
@@ -147,7 +156,7 @@ parallelForKernel(StateView *st, int32_t arch, ColArgs<sizeof...(ComponentTs)> c
     const int32_t w = (int32_t)(t / cap);
     const int32_t r = (int32_t)(t - (int64_t)w * cap);
     if (w >= st->numWorlds || r >= st->arch[arch].numRows[w]) return;
-    using WorldT = typename std::remove_reference_t<decltype(std::declval<ContextT>().data())>;
+    using WorldT = typename WorldOf<ContextT>::type;
     ContextT ctx((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
                  WorkerInit { st, w, nullptr });
     invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, r,

@@ -63,6 +63,11 @@ _lib.mw_phys_read_candidates.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes
 _lib.mw_phys_read_contacts.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
 _lib.mw_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_phys_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+_lib.mw_copy_exported.restype = ctypes.c_int64
+_lib.mw_copy_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
+_lib.mw_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 _lib.mw_phys_time_node.restype = ctypes.c_double
 _lib.mw_phys_time_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
 
@@ -71,8 +76,20 @@ C_ABI_SYMBOLS = (
     "mw_create", "mw_step", "mw_step_async", "mw_sync", "mw_get_exported", "mw_stream",
     "mw_destroy", "mw_last_error", "mw_num_worlds", "mw_error_flags", "mw_num_archetypes",
     "mw_read_column", "mw_column_info", "mw_phys_read_candidates", "mw_phys_read_contacts",
-    "mw_phys_read_bvh", "mw_phys_time_node",
+    "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_copy_exported",
+    "mw_gen_collisions_inits",
 )
+
+
+def gen_collisions_inits(num_worlds, num_cubes=128, seed=0, first_world=0):
+    """Product-side synthetic inputs (same serial mt19937 draw as the
+    reference example; first_world selects a shard)."""
+    pos = np.zeros((num_worlds, num_cubes, 3), np.float32)
+    rot = np.zeros((num_worlds, num_cubes, 4), np.float32)
+    _lib.mw_gen_collisions_inits(first_world, num_worlds, num_cubes, seed,
+                                 pos.ctypes.data_as(ctypes.c_void_p),
+                                 rot.ctypes.data_as(ctypes.c_void_p))
+    return pos, rot
 
 ERR_BITS = {1: "id store full", 2: "table full", 4: "candidate overflow",
             8: "contact overflow", 16: "BVH stack overflow"}
@@ -169,6 +186,12 @@ class Executor:
             raise _err()
         return buf[: n * b.value].view(dtype)
 
+    def copy_exported(self, slot, dst_ptr, max_bytes):
+        n = _lib.mw_copy_exported(self.h, slot, ctypes.c_void_p(dst_ptr), max_bytes)
+        if n < 0:
+            raise _err()
+        return n
+
     def time_node(self, name, steps):
         return _lib.mw_phys_time_node(self.h, name.encode(), steps)
 
@@ -243,6 +266,14 @@ class CollisionsSim(Executor):
         if n < 0:
             raise _err()
         return out[:n]
+
+    def counts(self):
+        c = np.zeros(self.num_worlds, np.int32)
+        k = np.zeros(self.num_worlds, np.int32)
+        if _lib.mw_phys_counts(self.h, c.ctypes.data_as(ctypes.c_void_p),
+                               k.ctypes.data_as(ctypes.c_void_p)) < 0:
+            raise _err()
+        return c, k
 
     def bvh(self, w, cap=4096):
         nodes = np.zeros(cap, BVH_NODE_DTYPE)

@@ -65,6 +65,12 @@ typedef struct mw_collisions_init {
     const float *rot;
 } mw_collisions_init;
 
+/* Synthetic inputs for worlds [first_world, first_world + num_worlds) of the
+ * reference's serial mt19937(seed) draw (examples/collisions/collisions.cpp). */
+void mw_gen_collisions_inits(int32_t first_world, int32_t num_worlds,
+                             int32_t num_cubes, uint32_t seed,
+                             float *pos_out, float *rot_out);
+
 /* Create an executor for environment `env`.  `inits` points at num_worlds
  * records of `init_stride` bytes each (reference: const InitT *user_inits). */
 mw_exec *mw_create(const char *env, const mw_config *cfg,
@@ -83,6 +89,10 @@ int mw_sync(mw_exec *exec);
 /* Device pointer of export slot `slot`: rows of all worlds packed
  * world-major (reference getExported).  *num_rows receives the row count. */
 void *mw_get_exported(mw_exec *exec, int32_t slot, int64_t *num_rows);
+
+/* Copy up to max_bytes of export slot `slot` into device buffer `dst`
+ * (ordered on the executor stream, then synchronised).  Returns bytes copied. */
+int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_bytes);
 
 /* hipStream_t of the executor (device work ordering for callers). */
 void *mw_stream(mw_exec *exec);
@@ -112,6 +122,9 @@ int32_t mw_phys_read_candidates(mw_exec *exec, int32_t world, void *out, int32_t
 int32_t mw_phys_read_contacts(mw_exec *exec, int32_t world, void *out, int32_t cap);
 int32_t mw_phys_read_bvh(mw_exec *exec, int32_t world, void *nodes_out,
                          float *leaf_aabbs_out, int32_t cap_nodes);
+
+/* per-world candidate / contact counts of the last step / substep. */
+int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *contacts_out);
 
 /* physics kernel timing hook for the bench: records HIP events around each
  * launch of the named node kind on the executor stream ("SolverNode", ...).

@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 using namespace madrona;
@@ -276,6 +277,28 @@ MADRONA_EXPORT void ref_phys_step(void *handle, int32_t num_steps)
             rw->graph->run(rw->ctx);
         }
     }
+}
+
+// Worlds are independent (one StateManager each), so a world-parallel loop
+// over host threads is the reference ThreadPoolExecutor's job model
+// (src/mw/cpu_exec.cpp:244-284) without its (unbuildable) render plumbing.
+MADRONA_EXPORT void ref_phys_step_mt(void *handle, int32_t num_steps,
+                                     int32_t num_threads)
+{
+    auto *h = (RefPhys *)handle;
+    int32_t W = (int32_t)h->worlds.size();
+    std::vector<std::thread> pool;
+    for (int32_t t = 0; t < num_threads; t++) {
+        pool.emplace_back([=]() {
+            for (int32_t w = t; w < W; w += num_threads) {
+                RefWorld *rw = h->worlds[w];
+                for (int32_t s = 0; s < num_steps; s++) {
+                    rw->graph->run(rw->ctx);
+                }
+            }
+        });
+    }
+    for (auto &th : pool) th.join();
 }
 
 MADRONA_EXPORT int32_t ref_phys_num_bodies(void *handle)
