@@ -53,52 +53,90 @@ def parse():
     p.add_argument("--cubes", type=int, default=128)
     p.add_argument("--substeps", type=int, default=4)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-worlds", type=int, default=256)
-    p.add_argument("--cpu-steps", type=int, default=40)
+    p.add_argument("--cpu-worlds", type=int, default=256, help="worlds per CPU batch")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-target-s", type=float, default=10.0)
+    p.add_argument("--cpu-max-batches", type=int, default=64)
+    p.add_argument("--cpu-port", action="store_true", help="time oracle/ instead of oracle/_ref")
+    p.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--cpu-first-world", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--no-roofline", action="store_true")
     p.add_argument("--no-handoff", action="store_true")
     return p.parse_args()
 
 
-def cpu_baseline(args, cfg):
-    """Reference CPU executor (oracle/_ref, the reference's own src/core +
-    src/physics) on a bounded sample of the same workload; falls back to the
-    parity-pinned restatement (oracle/) when the reference build is absent."""
+def _cpu_child(args):
+    """One bounded CPU sample in a fresh process: the reference executor
+    reserves virtual address space per world that it never releases, so each
+    batch of worlds lives in its own short-lived child."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as ol
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    pos, rot = ol.gen_collisions_inits(args.cpu_worlds, args.cubes, seed=0)
-    ocfg = ol.PhysConfig(args.cubes, args.substeps, cfg.delta_t, cfg.gravity_z,
-                         cfg.max_contacts, cfg.cube_inv_mass, cfg.cube_inv_inertia,
-                         cfg.mu_s, cfg.mu_d)
-    if ol.ref_available():
+    threads = max(1, args.cpu_threads)
+    W, first = args.cpu_worlds, args.cpu_first_world
+    pos, rot = ol.gen_collisions_inits(first + W, args.cubes, seed=0)
+    pos, rot = pos[first:], rot[first:]
+    ocfg = ol.default_phys_config(args.cubes, args.substeps, max_contacts=4096)
+    if ol.ref_available() and not args.cpu_port:
         lib = ol.load_ref()
         lib.ref_phys_step_mt.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         sim = ol.ReferencePhys(ocfg, pos, rot)
         kind = "reference"
+        lib.ref_phys_step_mt(sim.h, args.warmup, threads)
         t0 = time.perf_counter()
-        lib.ref_phys_step_mt(sim.h, args.cpu_steps, threads)
+        lib.ref_phys_step_mt(sim.h, args.steps, threads)
         dt = time.perf_counter() - t0
     else:
         sim = ol.OraclePhys(ocfg, pos, rot)
         kind = "port"
+        sim.step(args.warmup, threads)
         t0 = time.perf_counter()
-        sim.step(args.cpu_steps, threads)
+        sim.step(args.steps, threads)
         dt = time.perf_counter() - t0
-    value = args.cpu_worlds * args.cpu_steps / dt
+    print(json.dumps({"kind": kind, "seconds": dt, "env_steps": W * args.steps}))
+
+
+def cpu_baseline(args):
+    """Reference CPU executor (oracle/_ref, built from the reference's own
+    src/core + src/physics) on a bounded sample of the same workload and the
+    same step window as the timed GPU region (steps warmup+1 .. warmup+K of
+    consecutive world batches); falls back to the parity-pinned restatement
+    (oracle/) when the reference build is absent."""
+    import subprocess
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    total_s, total_steps, kind, batches = 0.0, 0, None, 0
+    t_wall = time.perf_counter()
+    while batches < args.cpu_max_batches and total_s < args.cpu_target_s:
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child",
+               "--cpu-worlds", str(args.cpu_worlds),
+               "--cpu-first-world", str(batches * args.cpu_worlds),
+               "--cpu-threads", str(threads), "--cubes", str(args.cubes),
+               "--substeps", str(args.substeps), "--steps", str(args.steps),
+               "--warmup", str(args.warmup)] + (["--cpu-port"] if args.cpu_port else [])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"cpu baseline child failed: {r.stderr[-2000:]}")
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        kind = res["kind"]
+        total_s += res["seconds"]
+        total_steps += res["env_steps"]
+        batches += 1
+    wall = time.perf_counter() - t_wall
     return {
-        "value": round(value, 1),
+        "value": round(total_steps / total_s, 1),
         "unit": "env-steps/s",
         "cores": threads,
         "kind": kind,
-        "sample": f"collisions {args.cpu_worlds} worlds x {args.cubes} cubes, S={args.substeps}, "
-                  f"steps 1-{args.cpu_steps} from init, {threads} host threads, {dt:.2f} s wall",
+        "sample": f"collisions {batches} batches x {args.cpu_worlds} worlds (worlds 0-"
+                  f"{batches * args.cpu_worlds - 1}) x {args.cubes} cubes, S={args.substeps}; "
+                  f"timed steps {args.warmup + 1}-{args.warmup + args.steps} (same window as "
+                  f"the GPU), {threads} host threads, {total_s:.2f} s timed / {wall:.1f} s wall",
     }
 
 
 def main():
     args = parse()
+    if args.cpu_child:
+        return _cpu_child(args)
     rank = int(os.environ.get("RANK", "0"))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -185,7 +223,7 @@ def main():
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, cfg)
+        cpu = cpu_baseline(args)
 
     if rank == 0:
         out = {

@@ -1,0 +1,136 @@
+// Device-side helpers shared by the physics kernels (broadphase.hip,
+// narrowphase.hip, solver.hip) and the kernel entry points the host module
+// (physics.hip) launches.
+#pragma once
+
+#include <madrona/physics.hpp>
+
+#include "physics_impl.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace madrona::phys {
+
+using namespace math;
+using namespace base;
+
+__host__ __device__ inline int32_t numInternalNodes(int32_t num_leaves)   // broadphase.cpp:33-40
+{
+    int32_t a = (num_leaves - 1 + 2) / 3;
+    return (a > 1 ? a : 1) + num_leaves;
+}
+
+template <typename T>
+__device__ __forceinline__ T &bcol(const BodyArch &B, int col, int32_t w, int32_t r)
+{
+    return ((T *)B.cols[col])[(size_t)w * B.capacity + r];
+}
+
+__device__ __forceinline__ int bodyArchIndex(const PhysArgs &P, uint32_t archetype)
+{
+    for (int i = 0; i < P.numBodyArchs; i++) {
+        if ((uint32_t)P.body[i].archetype == archetype) return i;
+    }
+    return 0;
+}
+
+__device__ __forceinline__ Loc entityLoc(const PhysArgs &P, int32_t w, Entity e)
+{
+    const IDNode &n = P.idNodes[(size_t)w * P.idsPerWorld + e.id];
+    if (n.gen != e.gen) return Loc::none();
+    return n.val;
+}
+
+// Float min/max updates with the reference's "v < old" rule; CAS loop so
+// concurrent leaves of one world compose like the reference's atomicMinF
+// (broadphase.cpp:494-543).  Values only shrink (min) / grow (max), so a
+// stale first read is safe.
+__device__ __forceinline__ float atomicMinRef(float *addr, float v)
+{
+    uint32_t *p = (uint32_t *)addr;
+    uint32_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+        float of = __uint_as_float(old);
+        if (!(v < of)) return of;
+        uint32_t prev = atomicCAS(p, old, __float_as_uint(v));
+        if (prev == old) return of;
+        old = prev;
+    }
+}
+
+__device__ __forceinline__ float atomicMaxRef(float *addr, float v)
+{
+    uint32_t *p = (uint32_t *)addr;
+    uint32_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+        float of = __uint_as_float(old);
+        if (!(v > of)) return of;
+        uint32_t prev = atomicCAS(p, old, __float_as_uint(v));
+        if (prev == old) return of;
+        old = prev;
+    }
+}
+
+// Grid helper: lanes over (world, row) of body archetype blockIdx.y.
+struct RowIdx {
+    int32_t w, r;
+    bool valid;
+};
+
+__device__ __forceinline__ RowIdx rowIndex(const PhysArgs &P, const BodyArch &B)
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    RowIdx ri;
+    ri.w = (int32_t)(t / B.capacity);
+    ri.r = (int32_t)(t - (int64_t)ri.w * B.capacity);
+    ri.valid = ri.w < P.numWorlds && ri.r < B.numRows[ri.w];
+    return ri;
+}
+
+__device__ __forceinline__ int32_t blockExclusiveScan(int32_t v, int32_t *scratch, int32_t *total)
+{
+    // Wave-level inclusive scan with DPP-friendly shuffles, then across waves.
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    int32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) scratch[wave] = x;
+    __syncthreads();
+    const int nwaves = blockDim.x >> 6;
+    int32_t wave_base = 0, sum = 0;
+    for (int i = 0; i < nwaves; i++) {
+        int32_t s = scratch[i];
+        if (i < wave) wave_base += s;
+        sum += s;
+    }
+    __syncthreads();
+    *total = sum;
+    return wave_base + x - v;
+}
+
+__device__ __forceinline__ Vector3 multDiag(Vector3 d, Vector3 v)
+{
+    return Vector3 { d.x * v.x, d.y * v.y, d.z * v.z };
+}
+
+// Kernel entry points (one launch processes every world).
+__global__ void leafUpdateKernel(PhysArgs P);
+__global__ void bvhRebuildKernel(PhysArgs P);
+__global__ void refitKernel(PhysArgs P);
+__global__ void findOverlapsKernel(PhysArgs P);
+__global__ void integrateKernel(PhysArgs P);
+__global__ void narrowphaseKernel(PhysArgs P);
+__global__ void solverKernel(PhysArgs P);
+
+size_t findOverlapsSharedBytes(const PhysArgs &P);
+size_t solverSharedBytes(const PhysArgs &P);
+
+constexpr int32_t kOverlapBlock = 192;
+constexpr int32_t kNarrowBlock = 256;
+constexpr int32_t kSolverBlock = 64;
+
+}

@@ -90,7 +90,9 @@ struct PhysArgs {
     math::Vector3 *hullVerts;     // [W][maxLeaves][maxVerts] world-space hull cache
     geometry::Plane *hullPlanes;  // [W][maxLeaves][maxFaces]
 
-    Contact *candContacts;        // [W][candCapacity] manifold per candidate slot
+    math::AABB *bodyAABBs;        // [W][maxLeaves] world AABB of each body (substep)
+    int32_t *survivors;           // [W][candCapacity] candidates passing the AABB recheck
+    Contact *candContacts;        // [W][candCapacity] manifold per survivor slot
     int32_t maxContacts;          // SolverData::maxContacts (reference assert)
     int32_t *contactOrder;        // [W][candCapacity] scratch: ordered contact list
     int32_t *lastNumContacts;     // [W] debug: contacts of the last substep

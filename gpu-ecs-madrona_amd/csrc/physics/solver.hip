@@ -1,0 +1,398 @@
+// XPBD solver kernel (reference src/physics/physics.cpp:166-1008).
+#include "physics_device.hpp"
+
+#include <cfloat>
+
+namespace madrona::phys {
+
+// ===========================================================================
+// XPBD solver: solvePositions + setVelocities + solveVelocities
+// (physics.cpp:166-1008), one wave per world, body state in LDS,
+// level-scheduled contacts.
+// ===========================================================================
+struct SBody {
+    Vector3 x;
+    Quat q;
+    Vector3 v;
+    Vector3 omega;
+    Vector3 prevX;
+    Quat prevQ;
+    Vector3 psX;
+    Quat psQ;
+    Vector3 psV;
+    Vector3 psOmega;
+    Vector3 invI;
+    float invMass;
+    float muS;
+    float muD;
+    uint32_t resp;
+};
+
+
+
+__device__ __forceinline__ int32_t bodySlot(const PhysArgs &P, Loc l)
+{
+    return P.body[bodyArchIndex(P, l.archetype)].slotBase + l.row;
+}
+
+__device__ __forceinline__ float computePositionalLambda(Vector3 ta1, Vector3 ta2, Vector3 ra1,
+                                                         Vector3 ra2, float im1, float im2,
+                                                         float c, float alpha)
+{                                                          // physics.cpp:166-183
+    float w1 = im1 + dot(ta1, ra1);
+    float w2 = im2 + dot(ta2, ra2);
+    return -c / (w1 + w2 + alpha);
+}
+
+__device__ __forceinline__ void applyPositionalUpdate(Vector3 &x1, Vector3 &x2, Quat &q1, Quat &q2,
+                                                      Vector3 ral1, Vector3 ral2, float im1,
+                                                      float im2, Vector3 n, float dl)
+{                                                          // physics.cpp:185-211
+    x1 += dl * im1 * n;
+    x2 -= dl * im2 * n;
+    float half = 0.5f * dl;
+    Vector3 q1u = q1.rotateVec(half * ral1);
+    Vector3 q2u = q2.rotateVec(half * ral2);
+    q1 += Quat::fromAngularVec(q1u) * q1;
+    q2 -= Quat::fromAngularVec(q2u) * q2;
+    q1 = q1.normalize();
+    q2 = q2.normalize();
+}
+
+__device__ void solveContactPositions(SBody &b1, SBody &b2, Contact &c)
+{                                                          // physics.cpp:281-476
+    Vector3 x1 = b1.x, x2 = b2.x;
+    Quat q1 = b1.q, q2 = b2.q;
+    float im1 = b1.invMass, im2 = b2.invMass;
+    Vector3 iI1 = b1.invI, iI2 = b2.invI;
+    if (b1.resp == (uint32_t)ResponseType::Static) { im1 = 0.f; iI1 = Vector3::zero(); }
+    if (b2.resp == (uint32_t)ResponseType::Static) { im2 = 0.f; iI2 = Vector3::zero(); }
+    const float avg_mu_s = 0.5f * (b1.muS + b2.muS);
+    const Vector3 n = c.normal;
+    for (int i = 0; i < 4; i++) {
+        if (i >= c.numPoints) continue;
+        Vector3 c1 = c.points[i].xyz();
+        float depth = c.points[i].w;
+        Vector3 c2 = c1 - n * depth;
+        Vector3 r1 = b1.psQ.inv().rotateVec(c1 - b1.psX);
+        Vector3 r2 = b2.psQ.inv().rotateVec(c2 - b2.psX);
+        float lambda_n = 0.f;
+        Vector3 p1 = q1.rotateVec(r1) + x1;
+        Vector3 p2 = q2.rotateVec(r2) + x2;
+        float d = dot(p1 - p2, n);
+        if (d > 0) {
+            Vector3 nl1 = q1.inv().rotateVec(n);
+            Vector3 nl2 = q2.inv().rotateVec(n);
+            Vector3 ta1 = cross(r1, nl1);
+            Vector3 ta2 = cross(r2, nl2);
+            Vector3 ra1 = multDiag(iI1, ta1);
+            Vector3 ra2 = multDiag(iI2, ta2);
+            lambda_n = computePositionalLambda(ta1, ta2, ra1, ra2, im1, im2, d, 0);
+            applyPositionalUpdate(x1, x2, q1, q2, ra1, ra2, im1, im2, n, lambda_n);
+
+            Vector3 p1_hat = b1.prevQ.rotateVec(r1) + b1.prevX;
+            Vector3 p2_hat = b2.prevQ.rotateVec(r2) + b2.prevX;
+            p1 = q1.rotateVec(r1) + x1;
+            p2 = q2.rotateVec(r2) + x2;
+            Vector3 dp = (p1 - p1_hat) - (p2 - p2_hat);
+            Vector3 dpt = dp - dot(dp, n) * n;
+            float tmag = dpt.length();
+            if (tmag > 0.f) {
+                Vector3 tw = dpt / tmag;
+                Vector3 tl1 = q1.inv().rotateVec(tw);
+                Vector3 tl2 = q2.inv().rotateVec(tw);
+                Vector3 fta1 = cross(r1, tl1);
+                Vector3 fta2 = cross(r2, tl2);
+                Vector3 fra1 = multDiag(iI1, fta1);
+                Vector3 fra2 = multDiag(iI2, fta2);
+                float lambda_t = computePositionalLambda(fta1, fta2, fra1, fra2, im1, im2, tmag, 0);
+                float thresh = lambda_n * avg_mu_s;
+                if (lambda_t > thresh) {
+                    applyPositionalUpdate(x1, x2, q1, q2, fra1, fra2, im1, im2, tw, lambda_t);
+                }
+            }
+        }
+        c.lambdaN[i] = lambda_n;
+    }
+    b1.x = x1; b2.x = x2;
+    b1.q = q1; b2.q = q2;
+}
+
+__device__ __forceinline__ Vector3 relVel(Vector3 v1, Vector3 v2, Vector3 o1, Vector3 o2,
+                                          Vector3 d1, Vector3 d2)
+{
+    return (v1 + cross(o1, d1)) - (v2 + cross(o2, d2));
+}
+
+__device__ __forceinline__ void applyVelocityUpdate(Vector3 &v1, Vector3 &v2, Vector3 &o1,
+                                                    Vector3 &o2, Quat q1, Quat q2, Vector3 ta1,
+                                                    Vector3 ta2, float im1, float im2,
+                                                    Vector3 iI1, Vector3 iI2, Vector3 dv,
+                                                    float mag)
+{                                                          // physics.cpp:724-750
+    Vector3 ra1 = multDiag(iI1, ta1);
+    Vector3 ra2 = multDiag(iI2, ta2);
+    float w1 = im1 + dot(ta1, ra1);
+    float w2 = im2 + dot(ta2, ra2);
+    mag *= 1.f / (w1 + w2);
+    v1 += mag * im1 * dv;
+    v2 -= mag * im2 * dv;
+    Vector3 o1u = mag * ra1;
+    Vector3 o2u = mag * ra2;
+    o1 += q1.rotateVec(o1u);
+    o2 -= q2.rotateVec(o2u);
+}
+
+__device__ void solveContactVelocities(SBody &b1, SBody &b2, const Contact &c, float h,
+                                       float rest_thresh)
+{                                                          // physics.cpp:865-993
+    const Quat q1 = b1.q, q2 = b2.q;
+    Vector3 v1 = b1.v, o1 = b1.omega, v2 = b2.v, o2 = b2.omega;
+    float im1 = b1.invMass, im2 = b2.invMass;
+    Vector3 iI1 = b1.invI, iI2 = b2.invI;
+    if (b1.resp == (uint32_t)ResponseType::Static) { im1 = 0.f; iI1 = Vector3::zero(); }
+    if (b2.resp == (uint32_t)ResponseType::Static) { im2 = 0.f; iI2 = Vector3::zero(); }
+    const float mu_d = 0.5f * (b1.muD + b2.muD);
+    const Vector3 n = c.normal;
+
+    Vector3 r1l[4], r2l[4], r1w[4], r2w[4], rt1[4], rt2[4];
+    float vn_bars[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if (i >= c.numPoints) continue;
+        Vector3 c1 = c.points[i].xyz();
+        float depth = c.points[i].w;
+        Vector3 c2 = c1 - n * depth;
+        Vector3 r1 = b1.psQ.inv().rotateVec(c1 - b1.psX);
+        Vector3 r2 = b2.psQ.inv().rotateVec(c2 - b2.psX);
+        Vector3 r1p = b1.psQ.rotateVec(r1);
+        Vector3 r2p = b2.psQ.rotateVec(r2);
+        Vector3 vbar = relVel(b1.psV, b2.psV, b1.psOmega, b2.psOmega, r1p, r2p);
+        vn_bars[i] = dot(n, vbar);
+        r1l[i] = r1;
+        r2l[i] = r2;
+        r1w[i] = q1.rotateVec(r1);
+        r2w[i] = q2.rotateVec(r2);
+        rt1[i] = cross(r1, q1.inv().rotateVec(n));
+        rt2[i] = cross(r2, q2.inv().rotateVec(n));
+    }
+    for (int it = 0; it < 2; it++) {                       // :813-863
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            if (i >= c.numPoints) continue;
+            Vector3 v = relVel(v1, v2, o1, o2, r1w[i], r2w[i]);
+            float vn = dot(n, v);
+            float vn_bar = vn_bars[i];
+            float e = 0.3f;
+            if (fabsf(vn_bar) <= rest_thresh) e = 0.f;
+            float mag = fminRef(-e * vn_bar, 0) - vn;
+            applyVelocityUpdate(v1, v2, o1, o2, q1, q2, rt1[i], rt2[i], im1, im2, iI1, iI2, n, mag);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {                          // :752-811
+        if (i >= c.numPoints) continue;
+        Vector3 v = relVel(v1, v2, o1, o2, r1w[i], r2w[i]);
+        float dfm = mu_d * fabsf(c.lambdaN[i]) / h;
+        float vn = dot(n, v);
+        Vector3 vt = v - n * vn;
+        float vt_len = vt.length();
+        if (vt_len != 0 && dfm != 0.f) {
+            float corrected = -fminRef(dfm, vt_len);
+            Vector3 dw = vt / vt_len;
+            Vector3 d1l = q1.inv().rotateVec(dw);
+            Vector3 d2l = q2.inv().rotateVec(dw);
+            Vector3 fta1 = cross(r1l[i], d1l);
+            Vector3 fta2 = cross(r2l[i], d2l);
+            applyVelocityUpdate(v1, v2, o1, o2, q1, q2, fta1, fta2, im1, im2, iI1, iI2, dw,
+                                corrected);
+        }
+    }
+    b1.v = v1; b1.omega = o1;
+    b2.v = v2; b2.omega = o2;
+}
+
+__device__ __forceinline__ bool isNegZero(float f) { return __float_as_uint(f) == 0x80000000u; }
+
+// A static body is never written through if every solver write to it is an
+// exact no-op: x +- (+-0) and q +- (+-0) keep bits when no component is -0,
+// and normalize() must be idempotent on its rotation (static velocities are
+// always +0 after setVelocities).  Such bodies add no ordering edge.
+__device__ __forceinline__ bool staticInvariant(const SBody &b)
+{
+    if (b.resp != (uint32_t)ResponseType::Static) return false;
+    if (isNegZero(b.x.x) || isNegZero(b.x.y) || isNegZero(b.x.z)) return false;
+    if (isNegZero(b.q.w) || isNegZero(b.q.x) || isNegZero(b.q.y) || isNegZero(b.q.z)) return false;
+    Quat nq = b.q.normalize();
+    return __float_as_uint(nq.w) == __float_as_uint(b.q.w) &&
+           __float_as_uint(nq.x) == __float_as_uint(b.q.x) &&
+           __float_as_uint(nq.y) == __float_as_uint(b.q.y) &&
+           __float_as_uint(nq.z) == __float_as_uint(b.q.z);
+}
+
+struct SolverLDS {
+    SBody *bodies;        // [nb]
+    int16_t *lastLevel;   // [nb]
+    int16_t *lvl;         // [maxContacts]
+    int16_t *slot1;       // [maxContacts]
+    int16_t *slot2;       // [maxContacts]
+};
+
+__host__ __device__ inline size_t solverLDSBytes(int32_t nb, int32_t max_contacts)
+{
+    auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+    return a16(sizeof(SBody) * nb) + a16(sizeof(int16_t) * nb) + 3 * a16(sizeof(int16_t) * max_contacts);
+}
+
+__device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb, int32_t max_contacts)
+{
+    auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+    SolverLDS L;
+    L.bodies = (SBody *)smem;
+    char *p = smem + a16(sizeof(SBody) * nb);
+    L.lastLevel = (int16_t *)p;
+    p += a16(sizeof(int16_t) * nb);
+    L.lvl = (int16_t *)p;
+    p += a16(sizeof(int16_t) * max_contacts);
+    L.slot1 = (int16_t *)p;
+    p += a16(sizeof(int16_t) * max_contacts);
+    L.slot2 = (int16_t *)p;
+    return L;
+}
+
+__global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int32_t w = blockIdx.x;
+    const int32_t nb = P.maxBodiesPerWorld;
+    SolverLDS L = solverLDS(smem, nb, P.maxContacts);
+    SBody *bodies = L.bodies;
+    __shared__ int32_t s_num_contacts, s_max_level, s_scan[kSolverBlock / 64];
+
+    // 1. load bodies into LDS
+    for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
+        const BodyArch &B = P.body[ba];
+        const int32_t rows = B.numRows[w];
+        for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
+            SBody &s = bodies[B.slotBase + r];
+            s.x = bcol<Vector3>(B, Cols::Position, w, r);
+            s.q = bcol<Quat>(B, Cols::Rotation, w, r);
+            const Velocity vel = bcol<Velocity>(B, Cols::Velocity, w, r);
+            s.v = vel.linear;
+            s.omega = vel.angular;
+            const auto prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
+            s.prevX = prev.prevPosition;
+            s.prevQ = prev.prevRotation;
+            const auto psp = bcol<solver::PreSolvePositional>(B, Cols::PreSolvePositional, w, r);
+            s.psX = psp.x;
+            s.psQ = psp.q;
+            const auto psv = bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
+            s.psV = psv.v;
+            s.psOmega = psv.omega;
+            const int32_t obj = bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
+            const RigidBodyMetadata md = P.objs.metadata[obj];
+            s.invI = md.invInertiaTensor;
+            s.invMass = md.invMass;
+            s.muS = md.muS;
+            s.muD = md.muD;
+            s.resp = (uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r);
+            L.lastLevel[B.slotBase + r] = staticInvariant(s) ? (int16_t)-1 : (int16_t)0;
+        }
+    }
+
+    // 2. ordered contact list (built by the narrowphase kernel)
+    const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
+    const int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
+    const int32_t K = P.solver[w].numContacts;
+    (void)s_scan;
+    for (int32_t k = threadIdx.x; k < K; k += kSolverBlock) {
+        const Contact &c = cslots[order[k]];
+        L.slot1[k] = (int16_t)bodySlot(P, c.ref);
+        L.slot2[k] = (int16_t)bodySlot(P, c.alt);
+    }
+    __syncthreads();
+
+    // 3. levels (serial, one lane, LDS only)
+    if (threadIdx.x == 0) {
+        int32_t max_level = 0;
+        for (int32_t k = 0; k < K; k++) {
+            const int32_t s1 = L.slot1[k], s2 = L.slot2[k];
+            const int32_t l1 = L.lastLevel[s1], l2 = L.lastLevel[s2];
+            const int32_t l = max(max(l1, l2), 0) + 1;
+            L.lvl[k] = (int16_t)l;
+            if (l1 >= 0) L.lastLevel[s1] = (int16_t)l;
+            if (l2 >= 0) L.lastLevel[s2] = (int16_t)l;
+            max_level = max(max_level, l);
+        }
+        s_num_contacts = K;
+        s_max_level = max_level;
+        P.lastNumContacts[w] = K;
+    }
+    __syncthreads();
+    const int32_t max_level = s_max_level;
+    const SolverData &sd = P.solver[w];
+    int16_t *lvl = L.lvl;
+    (void)s_num_contacts;
+
+    // 4. solvePositions, level by level
+    for (int32_t l = 1; l <= max_level; l++) {
+        for (int32_t k = threadIdx.x; k < K; k += kSolverBlock) {
+            if (lvl[k] != l) continue;
+            Contact &c = P.candContacts[(size_t)w * P.candCapacity + order[k]];
+            solveContactPositions(bodies[L.slot1[k]], bodies[L.slot2[k]], c);
+        }
+        __syncthreads();
+    }
+
+    // 5. setVelocities (physics.cpp:673-714)
+    const float h = sd.h;
+    for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
+        const BodyArch &B = P.body[ba];
+        const int32_t rows = B.numRows[w];
+        for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
+            SBody &s = bodies[B.slotBase + r];
+            const Quat q = s.q, qp = s.prevQ;
+            Quat dq;
+            if (q.w != qp.w || q.x != qp.x || q.y != qp.y || q.z != qp.z) {
+                dq = q * qp.inv();
+            } else {
+                dq = Quat { 1, 0, 0, 0 };
+            }
+            Vector3 new_omega = 2.f / h * Vector3 { dq.x, dq.y, dq.z };
+            s.v = (s.x - s.prevX) / h;
+            s.omega = dq.w > 0.f ? new_omega : -new_omega;
+        }
+    }
+    __syncthreads();
+
+    // 6. solveVelocities, same levels
+    for (int32_t l = 1; l <= max_level; l++) {
+        for (int32_t k = threadIdx.x; k < K; k += kSolverBlock) {
+            if (lvl[k] != l) continue;
+            const Contact &c = P.candContacts[(size_t)w * P.candCapacity + order[k]];
+            solveContactVelocities(bodies[L.slot1[k]], bodies[L.slot2[k]], c, h,
+                                   sd.restitutionThreshold);
+        }
+        __syncthreads();
+    }
+
+    // 7. write back
+    for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
+        const BodyArch &B = P.body[ba];
+        const int32_t rows = B.numRows[w];
+        for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
+            const SBody &s = bodies[B.slotBase + r];
+            bcol<Vector3>(B, Cols::Position, w, r) = s.x;
+            bcol<Quat>(B, Cols::Rotation, w, r) = s.q;
+            bcol<Velocity>(B, Cols::Velocity, w, r) = Velocity { s.v, s.omega };
+        }
+    }
+    if (threadIdx.x == 0) P.solver[w].numContacts = 0;     // physics.cpp:1007
+}
+
+size_t solverSharedBytes(const PhysArgs &P)
+{
+    return solverLDSBytes(P.maxBodiesPerWorld, P.maxContacts);
+}
+
+}
