@@ -50,13 +50,17 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--worlds", type=int, default=8192, help="worlds per GPU")
+    p.add_argument("--settle", type=int, default=120,
+                   help="untimed pre-roll steps so the timed window is the settled, "
+                        "contact-heavy regime (cubes fall from z<=10 for ~85 steps)")
     p.add_argument("--cubes", type=int, default=128)
     p.add_argument("--substeps", type=int, default=4)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-worlds", type=int, default=256, help="worlds per CPU batch")
     p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-steps", type=int, default=80, help="timed steps per CPU batch")
     p.add_argument("--cpu-target-s", type=float, default=10.0)
-    p.add_argument("--cpu-max-batches", type=int, default=64)
+    p.add_argument("--cpu-max-batches", type=int, default=12)
     p.add_argument("--cpu-port", action="store_true", help="time oracle/ instead of oracle/_ref")
     p.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--cpu-first-world", type=int, default=0, help=argparse.SUPPRESS)
@@ -81,18 +85,18 @@ def _cpu_child(args):
         lib.ref_phys_step_mt.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         sim = ol.ReferencePhys(ocfg, pos, rot)
         kind = "reference"
-        lib.ref_phys_step_mt(sim.h, args.warmup, threads)
+        lib.ref_phys_step_mt(sim.h, args.settle + args.warmup, threads)
         t0 = time.perf_counter()
-        lib.ref_phys_step_mt(sim.h, args.steps, threads)
+        lib.ref_phys_step_mt(sim.h, args.cpu_steps, threads)
         dt = time.perf_counter() - t0
     else:
         sim = ol.OraclePhys(ocfg, pos, rot)
         kind = "port"
-        sim.step(args.warmup, threads)
+        sim.step(args.settle + args.warmup, threads)
         t0 = time.perf_counter()
-        sim.step(args.steps, threads)
+        sim.step(args.cpu_steps, threads)
         dt = time.perf_counter() - t0
-    print(json.dumps({"kind": kind, "seconds": dt, "env_steps": W * args.steps}))
+    print(json.dumps({"kind": kind, "seconds": dt, "env_steps": W * args.cpu_steps}))
 
 
 def cpu_baseline(args):
@@ -110,8 +114,8 @@ def cpu_baseline(args):
                "--cpu-worlds", str(args.cpu_worlds),
                "--cpu-first-world", str(batches * args.cpu_worlds),
                "--cpu-threads", str(threads), "--cubes", str(args.cubes),
-               "--substeps", str(args.substeps), "--steps", str(args.steps),
-               "--warmup", str(args.warmup)] + (["--cpu-port"] if args.cpu_port else [])
+               "--substeps", str(args.substeps), "--cpu-steps", str(args.cpu_steps),
+               "--settle", str(args.settle), "--warmup", str(args.warmup)] + (["--cpu-port"] if args.cpu_port else [])
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             raise RuntimeError(f"cpu baseline child failed: {r.stderr[-2000:]}")
@@ -128,8 +132,9 @@ def cpu_baseline(args):
         "kind": kind,
         "sample": f"collisions {batches} batches x {args.cpu_worlds} worlds (worlds 0-"
                   f"{batches * args.cpu_worlds - 1}) x {args.cubes} cubes, S={args.substeps}; "
-                  f"timed steps {args.warmup + 1}-{args.warmup + args.steps} (same window as "
-                  f"the GPU), {threads} host threads, {total_s:.2f} s timed / {wall:.1f} s wall",
+                  f"timed steps {args.settle + args.warmup + 1}-"
+                  f"{args.settle + args.warmup + args.cpu_steps} (settled regime, GPU window starts "
+                  f"at the same step), {threads} host threads, {total_s:.2f} s timed / {wall:.1f} s wall",
     }
 
 
@@ -171,6 +176,8 @@ def main():
         if dist is not None:
             dist.all_gather_into_tensor(gathered, returns)
 
+    if args.settle:
+        sim.step(args.settle)
     for _ in range(args.warmup):
         step()
 
@@ -243,6 +250,7 @@ def main():
                 "workload": f"examples/collisions physics: {W} worlds/GPU x {args.cubes} cube hulls "
                             f"+ ground plane, S={args.substeps}, dt=1/60",
                 "worlds_per_gpu": W, "total_worlds": total_worlds,
+                "timed_steps": f"{args.settle + args.warmup + 1}-{args.settle + args.warmup + args.steps}",
                 "parallelism": f"world-sharded x{world_size}" +
                                ("" if args.no_handoff else ", per-step return hand-off"
                                 + (" (RCCL all-gather)" if world_size > 1 else "")),

@@ -99,14 +99,96 @@ __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
 }
 
 // ===========================================================================
-// Narrowphase (narrowphase.cpp, CPU branch), one lane per candidate
+// Narrowphase (narrowphase.cpp, CPU branch).
+//
+// A 16-lane group owns one candidate pair at a time: the SAT queries
+// (face directions A->B and B->A, all edge pairs) are spread over the
+// group's lanes and combined with (value, index) reductions whose tie-break
+// reproduces the reference's serial strict-'>' scan exactly (first
+// occurrence wins, NaN never wins); the clip / manifold tail runs on the
+// group's leader lane with its scratch polygons in LDS.
 // ===========================================================================
+constexpr int32_t kGroup = 16;
+constexpr int32_t kGroupsPerBlock = kNarrowBlock / kGroup;
+constexpr int32_t kMaxClip = 32;
+
 struct HullRef {
     const Vector3 *verts;          // world space
     const geometry::Plane *planes; // world space
     HullDev hd;
     Vector3 center;
 };
+
+// Per-edge SAT inputs gathered once per pair (edgeDistance's operands,
+// narrowphase.cpp:433-472 via queryEdgeDirections :474-540).
+struct EdgeRec {
+    Vector3 n1, n2;                // normals of the two faces sharing the edge
+    Vector3 p1, p2;                // root vertex, root vertex of next
+};
+
+struct GroupScratch {
+    EdgeRec *edgesA;               // [maxEdges]
+    EdgeRec *edgesB;               // [maxEdges]
+    Vector3 *clip0;                // [kMaxClip]
+    Vector3 *clip1;                // [kMaxClip]
+    float *depths;                 // [kMaxClip]
+};
+
+__host__ __device__ inline size_t groupScratchBytes(int32_t max_edges)
+{
+    return (size_t)2 * max_edges * sizeof(EdgeRec) + 2 * kMaxClip * sizeof(Vector3) +
+           kMaxClip * sizeof(float);
+}
+
+size_t narrowphaseSharedBytes(const PhysArgs &P)
+{
+    return kGroupsPerBlock * groupScratchBytes(P.objs.maxEdges);
+}
+
+__device__ __forceinline__ GroupScratch groupScratch(char *smem, int32_t group, int32_t max_edges)
+{
+    char *p = smem + (size_t)group * groupScratchBytes(max_edges);
+    GroupScratch g;
+    g.edgesA = (EdgeRec *)p;
+    p += max_edges * sizeof(EdgeRec);
+    g.edgesB = (EdgeRec *)p;
+    p += max_edges * sizeof(EdgeRec);
+    g.clip0 = (Vector3 *)p;
+    p += kMaxClip * sizeof(Vector3);
+    g.clip1 = (Vector3 *)p;
+    p += kMaxClip * sizeof(Vector3);
+    g.depths = (float *)p;
+    return g;
+}
+
+// LDS writes of one lane are visible to the other lanes of its wave once the
+// wave's LDS queue drains; this keeps the compiler from moving accesses
+// across that point.
+__device__ __forceinline__ void groupSync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Would (v1, k1) replace (v2, k2) in a serial `if (v > best)` scan visiting
+// indices in increasing order?  NaN never wins; ties go to the lower index.
+__device__ __forceinline__ bool scanWins(float v1, int32_t k1, float v2, int32_t k2)
+{
+    if (v1 != v1) return false;
+    if (v2 != v2) return true;
+    return v1 > v2 || (v1 == v2 && k1 < k2);
+}
+
+__device__ __forceinline__ void groupArgMax(float &v, int32_t &k)
+{
+#pragma unroll
+    for (int32_t off = kGroup / 2; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(v, off, kGroup);
+        const int32_t ok = __shfl_xor(k, off, kGroup);
+        if (scanWins(ov, ok, v, k)) { v = ov; k = ok; }
+    }
+}
 
 __device__ __forceinline__ float distFromPlane(const geometry::Plane &p, const Vector3 &a)
 {
@@ -137,22 +219,21 @@ struct FaceQuery {
     geometry::Plane plane;
 };
 
-__device__ FaceQuery queryFaceDirections(const HullRef &a, const HullRef &b)
+// queryFaceDirections (narrowphase.cpp:395-431).  The reference stops at the
+// first face with positive distance; any positive result rejects the pair,
+// so the group evaluates every face and only the non-positive case needs the
+// serial argmax, which groupArgMax reproduces.
+__device__ FaceQuery groupFaceQuery(const HullRef &a, const HullRef &b, int32_t lane)
 {
-    geometry::Plane max_plane { { 0, 0, 0 }, 0 };
-    int32_t max_face = -1;
-    float max_dist = -FLT_MAX;
-    for (int32_t f = 0; f < a.hd.numFaces; f++) {
-        geometry::Plane p = a.planes[f];
-        float d = hullDistFromPlane(p, b);
-        if (d > max_dist) {
-            max_dist = d;
-            max_face = f;
-            max_plane = p;
-            if (max_dist > 0) break;
-        }
+    float v = __builtin_nanf("");
+    int32_t k = INT32_MAX;
+    for (int32_t f = lane; f < a.hd.numFaces; f += kGroup) {
+        const float d = hullDistFromPlane(a.planes[f], b);
+        if (scanWins(d, f, v, k)) { v = d; k = f; }
     }
-    return { max_dist, max_face, max_plane };
+    groupArgMax(v, k);
+    if (v > -FLT_MAX) return { v, k, a.planes[k] };
+    return { -FLT_MAX, -1, geometry::Plane { { 0, 0, 0 }, 0 } };
 }
 
 __device__ __forceinline__ bool isMinkowskiFace(const Vector3 &a, const Vector3 &b,
@@ -167,57 +248,72 @@ __device__ __forceinline__ bool isMinkowskiFace(const Vector3 &a, const Vector3 
     return cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f;
 }
 
+// edgeDistance (narrowphase.cpp:433-472) for one edge pair: separation along
+// the edges' cross product, or -FLT_MAX when the edges do not form a face of
+// the Minkowski difference or are parallel.
+__device__ __forceinline__ float edgePairSeparation(const EdgeRec &ea, const EdgeRec &eb,
+                                                    const Vector3 &a_center, Vector3 *normal_out)
+{
+    float sep = -FLT_MAX;
+    Vector3 n { 0, 0, 0 };
+    if (isMinkowskiFace(ea.n1, ea.n2, -eb.n1, -eb.n2)) {
+        Vector3 da = ea.p2 - ea.p1, db = eb.p2 - eb.p1;
+        Vector3 uc = da.cross(db);
+        float l2 = uc.length2();
+        if (l2 != 0) {
+            float inv = 1.f / sqrtf(l2);
+            n = uc * inv;
+            if (n.dot(ea.p1 - a_center) < 0.0f) n = -n;
+            sep = n.dot(eb.p1 - ea.p1);
+        }
+    }
+    if (normal_out) *normal_out = n;
+    return sep;
+}
+
+__device__ __forceinline__ void stageEdges(const ObjDev &O, const HullRef &h, EdgeRec *dst,
+                                           int32_t lane)
+{
+    const geometry::HalfEdge *he = O.hedges + h.hd.hedgeOffset;
+    for (int32_t i = lane; i < h.hd.numEdges; i += kGroup) {
+        const geometry::HalfEdge e = he[O.edges[h.hd.edgeOffset + i]];
+        EdgeRec r;
+        r.n1 = h.planes[e.polygon].normal;
+        r.n2 = h.planes[he[e.twin].polygon].normal;
+        r.p1 = h.verts[e.rootVertex];
+        r.p2 = h.verts[he[e.next].rootVertex];
+        dst[i] = r;
+    }
+}
+
 struct EdgeQuery {
     float separation;
     Vector3 normal;
-    int32_t edgeA;
+    int32_t edgeA;                 // half-edge indices (queryEdgeDirections' result)
     int32_t edgeB;
 };
 
-__device__ EdgeQuery queryEdgeDirections(const ObjDev &O, const HullRef &a, const HullRef &b)
+// queryEdgeDirections (narrowphase.cpp:474-540) over the staged edge records.
+// Pair index k = i * nB + j is the reference's loop order.
+__device__ EdgeQuery groupEdgeQuery(const ObjDev &O, const HullRef &a, const HullRef &b,
+                                    const GroupScratch &g, int32_t lane)
 {
-    Vector3 normal { 0, 0, 0 };
-    int32_t ea_max = 0, eb_max = 0;
-    float max_d = -FLT_MAX;
-    const geometry::HalfEdge *ha = O.hedges + a.hd.hedgeOffset;
-    const geometry::HalfEdge *hb = O.hedges + b.hd.hedgeOffset;
-    for (int32_t i = 0; i < a.hd.numEdges; i++) {
-        const int32_t he_a = (int32_t)O.edges[a.hd.edgeOffset + i];
-        const geometry::HalfEdge ea = ha[he_a];
-        const Vector3 an1 = a.planes[ea.polygon].normal;
-        const Vector3 an2 = a.planes[ha[ea.twin].polygon].normal;
-        const Vector3 pa1 = a.verts[ea.rootVertex];
-        const Vector3 pa2 = a.verts[ha[ea.next].rootVertex];
-        for (int32_t j = 0; j < b.hd.numEdges; j++) {
-            const int32_t he_b = (int32_t)O.edges[b.hd.edgeOffset + j];
-            const geometry::HalfEdge eb = hb[he_b];
-            const Vector3 bn1 = b.planes[eb.polygon].normal;
-            const Vector3 bn2 = b.planes[hb[eb.twin].polygon].normal;
-            float sep = -FLT_MAX;
-            Vector3 n { 0, 0, 0 };
-            if (isMinkowskiFace(an1, an2, -bn1, -bn2)) {      // edgeDistance :433-472
-                const Vector3 pb1 = b.verts[eb.rootVertex];
-                const Vector3 pb2 = b.verts[hb[eb.next].rootVertex];
-                Vector3 da = pa2 - pa1, db = pb2 - pb1;
-                Vector3 uc = da.cross(db);
-                float l2 = uc.length2();
-                if (l2 != 0) {
-                    float inv = 1.f / sqrtf(l2);
-                    n = uc * inv;
-                    if (n.dot(pa1 - a.center) < 0.0f) n = -n;
-                    sep = n.dot(pb1 - pa1);
-                }
-            }
-            if (sep > max_d) {
-                max_d = sep;
-                normal = n;
-                ea_max = he_a;
-                eb_max = he_b;
-                if (max_d > 0) return { max_d, normal, ea_max, eb_max };
-            }
-        }
+    const int32_t nA = a.hd.numEdges, nB = b.hd.numEdges;
+    float v = __builtin_nanf("");
+    int32_t k = INT32_MAX;
+    for (int32_t p = lane; p < nA * nB; p += kGroup) {
+        const int32_t i = p / nB, j = p - i * nB;
+        const float sep = edgePairSeparation(g.edgesA[i], g.edgesB[j], a.center, nullptr);
+        if (scanWins(sep, p, v, k)) { v = sep; k = p; }
     }
-    return { max_d, normal, ea_max, eb_max };
+    groupArgMax(v, k);
+    if (!(v > -FLT_MAX)) return { -FLT_MAX, { 0, 0, 0 }, 0, 0 };
+    const int32_t i = k / nB, j = k - i * nB;
+    EdgeQuery q;
+    q.separation = edgePairSeparation(g.edgesA[i], g.edgesB[j], a.center, &q.normal);
+    q.edgeA = (int32_t)O.edges[a.hd.edgeOffset + i];
+    q.edgeB = (int32_t)O.edges[b.hd.edgeOffset + j];
+    return q;
 }
 
 __device__ __forceinline__ int32_t findIncidentFace(const HullRef &h, Vector3 ref_normal)
@@ -230,8 +326,6 @@ __device__ __forceinline__ int32_t findIncidentFace(const HullRef &h, Vector3 re
     }
     return face;
 }
-
-constexpr int32_t kMaxClip = 32;
 
 __device__ __forceinline__ int32_t clipPolygon(Vector3 *dst, geometry::Plane cp,
                                                const Vector3 *in, int32_t n)
@@ -257,67 +351,71 @@ __device__ __forceinline__ int32_t clipPolygon(Vector3 *dst, geometry::Plane cp,
     return out;
 }
 
-struct Manifold {
+// buildFaceContactManifold (narrowphase.cpp:790-864) written straight into
+// the contact slot.
+__device__ void storeFaceManifold(Contact &c, Vector3 n, Vector3 *contacts, const float *depths,
+                                  int32_t num, Loc ref, Loc alt)
+{
     Vector3 cp[4];
     float depth[4];
-    int32_t num;
-    Vector3 normal;
-};
-
-__device__ Manifold buildFaceContactManifold(Vector3 n, Vector3 *contacts, float *depths,
-                                             int32_t num)
-{                                                          // narrowphase.cpp:790-864
-    Manifold m;
-    for (int i = 0; i < 4; i++) { m.cp[i] = Vector3::zero(); m.depth[i] = 0.f; }
+    for (int i = 0; i < 4; i++) { cp[i] = Vector3::zero(); depth[i] = 0.f; }
+    int32_t m;
     if (num <= 4) {
-        m.num = num;
-        for (int32_t i = 0; i < num; i++) { m.cp[i] = contacts[i]; m.depth[i] = depths[i]; }
+        m = num;
+        for (int32_t i = 0; i < num; i++) { cp[i] = contacts[i]; depth[i] = depths[i]; }
     } else {
-        m.num = 4;
-        m.cp[0] = contacts[0];
-        m.depth[0] = depths[0];
-        Vector3 p0 = m.cp[0];
+        m = 4;
+        cp[0] = contacts[0];
+        depth[0] = depths[0];
+        Vector3 p0 = cp[0];
         float largest_d2 = 0.0f;
         int32_t largest_d2_idx = 0;
         for (int32_t i = 1; i < num; i++) {
-            Vector3 c = contacts[i];
-            float d2 = p0.distance2(c);
+            Vector3 c2 = contacts[i];
+            float d2 = p0.distance2(c2);
             if (d2 > largest_d2) {
                 largest_d2 = d2;
-                m.cp[1] = c;
-                m.depth[1] = depths[i];
+                cp[1] = c2;
+                depth[1] = depths[i];
                 largest_d2_idx = i;
             }
         }
-        contacts[largest_d2_idx] = m.cp[0];
-        Vector3 diff0 = m.cp[1] - p0;
+        contacts[largest_d2_idx] = cp[0];
+        Vector3 diff0 = cp[1] - p0;
         const float largest_area = 0.0f;        // never updated in the reference
         int32_t largest_area_idx = 0;
         for (int32_t i = 1; i < num; i++) {
-            Vector3 c = contacts[i];
-            Vector3 diff1 = c - p0;
+            Vector3 c2 = contacts[i];
+            Vector3 diff1 = c2 - p0;
             float area = n.dot(diff0.cross(diff1));
             if (area > largest_area) {
-                m.cp[2] = c;
-                m.depth[2] = depths[i];
+                cp[2] = c2;
+                depth[2] = depths[i];
                 largest_area_idx = i;
             }
         }
-        contacts[largest_area_idx] = m.cp[0];
+        contacts[largest_area_idx] = cp[0];
         for (int32_t i = 1; i < num; i++) {
-            Vector3 c = contacts[i];
-            Vector3 diff1 = c - p0;
+            Vector3 c2 = contacts[i];
+            Vector3 diff1 = c2 - p0;
             float area = n.dot(diff0.cross(diff1));
             if (area < largest_area) {
-                m.cp[3] = c;
-                m.depth[3] = depths[i];
+                cp[3] = c2;
+                depth[3] = depths[i];
             }
         }
     }
+    if (m == 0) return;
     const Quat ident { 1, 0, 0, 0 };
-    for (int32_t i = 0; i < m.num; i++) m.cp[i] = ident.rotateVec(m.cp[i]) + Vector3::zero();
-    m.normal = ident.rotateVec(n);
-    return m;
+    c.ref = ref;
+    c.alt = alt;
+    for (int i = 0; i < 4; i++) {
+        Vector3 p = (i < m) ? ident.rotateVec(cp[i]) + Vector3::zero() : cp[i];
+        c.points[i] = Vector4::fromVector3(p, depth[i]);
+    }
+    c.numPoints = m;
+    c.normal = ident.rotateVec(n);
+    for (int i = 0; i < 4; i++) c.lambdaN[i] = 0.f;
 }
 
 __device__ __forceinline__ geometry::Segment shortestSegmentBetween(const geometry::Segment &s1,
@@ -345,20 +443,7 @@ __device__ __forceinline__ geometry::Segment shortestSegmentBetween(const geomet
     return { s1.p1 + s * v1, s2.p1 + t * v2 };
 }
 
-__device__ __forceinline__ void storeManifold(Contact &c, const Manifold &m, Loc ref, Loc alt)
-{
-    c.ref = ref;
-    c.alt = alt;
-    for (int i = 0; i < 4; i++) c.points[i] = Vector4::fromVector3(m.cp[i], m.depth[i]);
-    c.numPoints = m.num;
-    c.normal = m.normal;
-    for (int i = 0; i < 4; i++) c.lambdaN[i] = 0.f;
-}
-
-
-
-// Candidate order helper shared by the filter and the SAT phase:
-// runNarrowphase's type swap (narrowphase.cpp:1574-1580).
+// Candidate order: runNarrowphase's type swap (narrowphase.cpp:1574-1580).
 struct CandBodies {
     Loc a_loc, b_loc;
     const BodyArch *BA, *BB;
@@ -402,157 +487,148 @@ __device__ __forceinline__ bool candidateOverlaps(const PhysArgs &P, int32_t w,
     return a.overlaps(b);
 }
 
-// SAT + contact generation for one candidate that passed the AABB recheck;
-// writes out.numPoints (0 = no contact) and, on contact, the manifold.
-__device__ void narrowphaseCandidate(const PhysArgs &P, int32_t w,
-                                     const CandidateCollision &cand, Contact &out)
+__device__ __forceinline__ HullRef hullOf(const PhysArgs &P, int32_t w, const BodyArch &B,
+                                          Loc loc, int32_t obj)
+{
+    const int32_t leaf = bcol<broadphase::LeafID>(B, Cols::LeafID, w, loc.row).id;
+    HullRef h;
+    h.hd = P.objs.hulls[obj];
+    h.verts = P.hullVerts + ((size_t)w * P.maxLeaves + leaf) * P.objs.maxVerts;
+    h.planes = P.hullPlanes + ((size_t)w * P.maxLeaves + leaf) * P.objs.maxFaces;
+    h.center = bcol<Vector3>(B, Cols::Position, w, loc.row);
+    return h;
+}
+
+// Hull-hull: doSAT (narrowphase.cpp:678-758) on the group, then
+// createFaceContact (:866-972) or createEdgeContact (:1053-1121) on the
+// leader lane.  All group lanes must enter.
+__device__ void hullHullPair(const PhysArgs &P, int32_t w, const CandBodies &cb,
+                             const GroupScratch &g, int32_t lane, Contact &out)
 {
     const ObjDev &O = P.objs;
-    out.numPoints = 0;
-    do {
-        const CandBodies cb = orderCandidate(P, w, cand);
-        const Loc a_loc = cb.a_loc, b_loc = cb.b_loc;
-        const BodyArch *BA = cb.BA, *BB = cb.BB;
-        const int32_t a_obj = cb.a_obj, b_obj = cb.b_obj;
-        const uint32_t ta = cb.ta, tb = cb.tb;
-        const Vector3 a_pos = bcol<Vector3>(*BA, Cols::Position, w, a_loc.row);
-        const Vector3 b_pos = bcol<Vector3>(*BB, Cols::Position, w, b_loc.row);
-        const Quat b_rot = bcol<Quat>(*BB, Cols::Rotation, w, b_loc.row);
-        const uint32_t test = ta | tb;
-        const int32_t a_leaf = bcol<broadphase::LeafID>(*BA, Cols::LeafID, w, a_loc.row).id;
-        HullRef ha;
-        ha.hd = O.hulls[a_obj];
-        ha.verts = P.hullVerts + ((size_t)w * P.maxLeaves + a_leaf) * O.maxVerts;
-        ha.planes = P.hullPlanes + ((size_t)w * P.maxLeaves + a_leaf) * O.maxFaces;
-        ha.center = a_pos;
-        Vector3 tmp1[kMaxClip], tmp2[kMaxClip];
-        float depths[kMaxClip];
+    const HullRef ha = hullOf(P, w, *cb.BA, cb.a_loc, cb.a_obj);
+    const HullRef hb = hullOf(P, w, *cb.BB, cb.b_loc, cb.b_obj);
 
-        if (test == (uint32_t)CollisionPrimitive::Type::Hull) {
-            const int32_t b_leaf = bcol<broadphase::LeafID>(*BB, Cols::LeafID, w, b_loc.row).id;
-            HullRef hb;
-            hb.hd = O.hulls[b_obj];
-            hb.verts = P.hullVerts + ((size_t)w * P.maxLeaves + b_leaf) * O.maxVerts;
-            hb.planes = P.hullPlanes + ((size_t)w * P.maxLeaves + b_leaf) * O.maxFaces;
-            hb.center = b_pos;
+    const FaceQuery fa = groupFaceQuery(ha, hb, lane);
+    if (fa.separation > 0.0f) return;
+    const FaceQuery fb = groupFaceQuery(hb, ha, lane);
+    if (fb.separation > 0.0f) return;
+    stageEdges(O, ha, g.edgesA, lane);
+    stageEdges(O, hb, g.edgesB, lane);
+    groupSync();
+    const EdgeQuery eq = groupEdgeQuery(O, ha, hb, g, lane);
+    groupSync();
+    if (eq.separation > 0.0f) return;
+    if (lane != 0) return;
 
-            // doSAT (narrowphase.cpp:678-758)
-            FaceQuery fa = queryFaceDirections(ha, hb);
-            if (fa.separation > 0.0f) continue;
-            FaceQuery fb = queryFaceDirections(hb, ha);
-            if (fb.separation > 0.0f) continue;
-            EdgeQuery eq = queryEdgeDirections(O, ha, hb);
-            if (eq.separation > 0.0f) continue;
+    if (fa.separation > eq.separation || fb.separation > eq.separation) {
+        const bool a_is_ref = fa.separation >= fb.separation;
+        const geometry::Plane ref_plane = a_is_ref ? fa.plane : fb.plane;
+        const int32_t ref_face = a_is_ref ? fa.faceIdx : fb.faceIdx;
+        const HullRef &ref = a_is_ref ? ha : hb;
+        const HullRef &inc = a_is_ref ? hb : ha;
+        const int32_t inc_face = findIncidentFace(inc, ref_plane.normal);
 
-            Manifold m;
-            Loc ref_loc, other_loc;
-            if (fa.separation > eq.separation || fb.separation > eq.separation) {
-                const bool a_is_ref = fa.separation >= fb.separation;
-                const geometry::Plane ref_plane = a_is_ref ? fa.plane : fb.plane;
-                const int32_t ref_face = a_is_ref ? fa.faceIdx : fb.faceIdx;
-                const HullRef &ref = a_is_ref ? ha : hb;
-                const HullRef &inc = a_is_ref ? hb : ha;
-                const int32_t inc_face = findIncidentFace(inc, ref_plane.normal);
-                ref_loc = a_is_ref ? a_loc : b_loc;
-                other_loc = a_is_ref ? b_loc : a_loc;
-
-                // createFaceContact (narrowphase.cpp:866-972)
-                const geometry::HalfEdge *rh = O.hedges + ref.hd.hedgeOffset;
-                const geometry::HalfEdge *oh = O.hedges + inc.hd.hedgeOffset;
-                int32_t n_in = 0;
-                {
-                    uint32_t hidx = O.polygons[inc.hd.faceOffset + inc_face], start = hidx;
-                    do {
-                        const geometry::HalfEdge he = oh[hidx];
-                        hidx = he.next;
-                        if (n_in < kMaxClip) tmp1[n_in++] = inc.verts[he.rootVertex];
-                    } while (hidx != start);
-                }
-                Vector3 *cin = tmp1, *cdst = tmp2;
-                int32_t n_clip = n_in;
-                {
-                    uint32_t hidx = O.polygons[ref.hd.faceOffset + ref_face], start = hidx;
-                    geometry::HalfEdge che = rh[hidx];
-                    Vector3 cur = ref.verts[che.rootVertex];
-                    do {
-                        hidx = che.next;
-                        che = rh[hidx];
-                        Vector3 next = ref.verts[che.rootVertex];
-                        Vector3 edge = next - cur;
-                        Vector3 pn = cross(edge, ref_plane.normal);
-                        float d = dot(pn, cur);
-                        cur = next;
-                        n_clip = clipPolygon(cdst, geometry::Plane { pn, d }, cin, n_clip);
-                        Vector3 *t = cdst; cdst = cin; cin = t;
-                    } while (hidx != start);
-                }
-                int32_t n_below = 0;
-                for (int32_t i = 0; i < n_clip; i++) {
-                    Vector3 v = cin[i];
-                    float d = distFromPlane(ref_plane, v);
-                    if (d < 0.0f) {
-                        cin[n_below] = v - d * ref_plane.normal;
-                        depths[n_below] = -d;
-                        n_below++;
-                    }
-                }
-                m = buildFaceContactManifold(ref_plane.normal, cin, depths, n_below);
-            } else {
-                // createEdgeContact (narrowphase.cpp:1053-1121)
-                ref_loc = a_loc;
-                other_loc = b_loc;
-                const geometry::HalfEdge *ha_e = O.hedges + ha.hd.hedgeOffset;
-                const geometry::HalfEdge *hb_e = O.hedges + hb.hd.hedgeOffset;
-                const geometry::HalfEdge ea = ha_e[eq.edgeA];
-                const geometry::HalfEdge eb = hb_e[eq.edgeB];
-                geometry::Segment sa { ha.verts[ea.rootVertex], ha.verts[ha_e[ea.next].rootVertex] };
-                geometry::Segment sb { hb.verts[eb.rootVertex], hb.verts[hb_e[eb.next].rootVertex] };
-                geometry::Segment s = shortestSegmentBetween(sa, sb);
-                const Quat ident { 1, 0, 0, 0 };
-                for (int i = 0; i < 4; i++) { m.cp[i] = Vector3::zero(); m.depth[i] = 0.f; }
-                m.cp[0] = ident.rotateVec(s.p1) + Vector3::zero();
-                m.depth[0] = -eq.separation;
-                m.num = 1;
-                m.normal = ident.rotateVec(eq.normal);
-            }
-            if (m.num > 0) storeManifold(out, m, ref_loc, other_loc);
-        } else if (test == ((uint32_t)CollisionPrimitive::Type::Hull |
-                            (uint32_t)CollisionPrimitive::Type::Plane)) {
-            Vector3 pn = b_rot.rotateVec(Vector3 { 0, 0, 1 });
-            geometry::Plane plane { pn, dot(pn, b_pos) };
-            // doSATPlane (narrowphase.cpp:760-788)
-            float sep = hullDistFromPlane(plane, ha);
-            if (sep > 0.0f) continue;
-            int32_t inc_face = findIncidentFace(ha, plane.normal);
-            // createFacePlaneContact (narrowphase.cpp:974-1017)
-            const geometry::HalfEdge *hh = O.hedges + ha.hd.hedgeOffset;
-            int32_t n = 0;
-            uint32_t hidx = O.polygons[ha.hd.faceOffset + inc_face], start = hidx;
+        const geometry::HalfEdge *rh = O.hedges + ref.hd.hedgeOffset;
+        const geometry::HalfEdge *oh = O.hedges + inc.hd.hedgeOffset;
+        int32_t n_in = 0;
+        {
+            uint32_t hidx = O.polygons[inc.hd.faceOffset + inc_face], start = hidx;
             do {
-                const geometry::HalfEdge he = hh[hidx];
+                const geometry::HalfEdge he = oh[hidx];
                 hidx = he.next;
-                Vector3 v = ha.verts[he.rootVertex];
-                float d = distFromPlane(plane, v);
-                if (d < 0.0f && n < kMaxClip) {
-                    tmp1[n] = v - d * plane.normal;
-                    depths[n] = -d;
-                    n++;
-                }
+                if (n_in < kMaxClip) g.clip0[n_in++] = inc.verts[he.rootVertex];
             } while (hidx != start);
-            Manifold m = buildFaceContactManifold(plane.normal, tmp1, depths, n);
-            if (m.num > 0) storeManifold(out, m, b_loc, a_loc);
         }
-        // sphere / plane-plane: the reference asserts (narrowphase.cpp:1197-1313)
-    } while (0);
+        Vector3 *cin = g.clip0, *cdst = g.clip1;
+        int32_t n_clip = n_in;
+        {
+            uint32_t hidx = O.polygons[ref.hd.faceOffset + ref_face], start = hidx;
+            geometry::HalfEdge che = rh[hidx];
+            Vector3 cur = ref.verts[che.rootVertex];
+            do {
+                hidx = che.next;
+                che = rh[hidx];
+                Vector3 next = ref.verts[che.rootVertex];
+                Vector3 edge = next - cur;
+                Vector3 pn = cross(edge, ref_plane.normal);
+                float d = dot(pn, cur);
+                cur = next;
+                n_clip = clipPolygon(cdst, geometry::Plane { pn, d }, cin, n_clip);
+                Vector3 *t = cdst; cdst = cin; cin = t;
+            } while (hidx != start);
+        }
+        int32_t n_below = 0;
+        for (int32_t i = 0; i < n_clip; i++) {
+            Vector3 v = cin[i];
+            float d = distFromPlane(ref_plane, v);
+            if (d < 0.0f) {
+                cin[n_below] = v - d * ref_plane.normal;
+                g.depths[n_below] = -d;
+                n_below++;
+            }
+        }
+        storeFaceManifold(out, ref_plane.normal, cin, g.depths, n_below,
+                          a_is_ref ? cb.a_loc : cb.b_loc, a_is_ref ? cb.b_loc : cb.a_loc);
+    } else {
+        const geometry::HalfEdge *ha_e = O.hedges + ha.hd.hedgeOffset;
+        const geometry::HalfEdge *hb_e = O.hedges + hb.hd.hedgeOffset;
+        const geometry::HalfEdge ea = ha_e[eq.edgeA];
+        const geometry::HalfEdge eb = hb_e[eq.edgeB];
+        geometry::Segment sa { ha.verts[ea.rootVertex], ha.verts[ha_e[ea.next].rootVertex] };
+        geometry::Segment sb { hb.verts[eb.rootVertex], hb.verts[hb_e[eb.next].rootVertex] };
+        geometry::Segment s = shortestSegmentBetween(sa, sb);
+        const Quat ident { 1, 0, 0, 0 };
+        out.ref = cb.a_loc;
+        out.alt = cb.b_loc;
+        out.points[0] = Vector4::fromVector3(ident.rotateVec(s.p1) + Vector3::zero(),
+                                             -eq.separation);
+        for (int i = 1; i < 4; i++) out.points[i] = Vector4::fromVector3(Vector3::zero(), 0.f);
+        out.numPoints = 1;
+        out.normal = ident.rotateVec(eq.normal);
+        for (int i = 0; i < 4; i++) out.lambdaN[i] = 0.f;
+    }
+}
+
+// Hull-plane: doSATPlane (narrowphase.cpp:760-788) + createFacePlaneContact
+// (:974-1017) on the leader lane.
+__device__ void hullPlanePair(const PhysArgs &P, int32_t w, const CandBodies &cb,
+                              const GroupScratch &g, Contact &out)
+{
+    const ObjDev &O = P.objs;
+    const HullRef ha = hullOf(P, w, *cb.BA, cb.a_loc, cb.a_obj);
+    const Vector3 b_pos = bcol<Vector3>(*cb.BB, Cols::Position, w, cb.b_loc.row);
+    const Quat b_rot = bcol<Quat>(*cb.BB, Cols::Rotation, w, cb.b_loc.row);
+    Vector3 pn = b_rot.rotateVec(Vector3 { 0, 0, 1 });
+    geometry::Plane plane { pn, dot(pn, b_pos) };
+    float sep = hullDistFromPlane(plane, ha);
+    if (sep > 0.0f) return;
+    int32_t inc_face = findIncidentFace(ha, plane.normal);
+    const geometry::HalfEdge *hh = O.hedges + ha.hd.hedgeOffset;
+    int32_t n = 0;
+    uint32_t hidx = O.polygons[ha.hd.faceOffset + inc_face], start = hidx;
+    do {
+        const geometry::HalfEdge he = hh[hidx];
+        hidx = he.next;
+        Vector3 v = ha.verts[he.rootVertex];
+        float d = distFromPlane(plane, v);
+        if (d < 0.0f && n < kMaxClip) {
+            g.clip0[n] = v - d * plane.normal;
+            g.depths[n] = -d;
+            n++;
+        }
+    } while (hidx != start);
+    storeFaceManifold(out, plane.normal, g.clip0, g.depths, n, cb.b_loc, cb.a_loc);
 }
 
 // runNarrowphaseSystem over every candidate of a world (one block per world):
 //   A. lane-per-candidate AABB recheck, block scan -> survivor list (order kept)
-//   B. lane-per-survivor SAT + contact generation into survivor slots
+//   B. group-per-survivor SAT + contact generation into survivor slots
 //   C. block scan of survivors with a manifold -> the solver's contact order
 //      (== the reference's addManifoldToSolver append order).
 __global__ void __launch_bounds__(kNarrowBlock) narrowphaseKernel(PhysArgs P)
 {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int32_t s_scan[kNarrowBlock / 64];
     const int32_t w = blockIdx.x;
     const int32_t num = min(P.numCands[w], P.candCapacity);
@@ -571,8 +647,22 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowphaseKernel(PhysArgs P)
     }
     __syncthreads();
 
-    for (int32_t s = threadIdx.x; s < S; s += kNarrowBlock) {
-        narrowphaseCandidate(P, w, cands[surv[s]], slots[s]);
+    const int32_t group = threadIdx.x / kGroup;
+    const int32_t lane = threadIdx.x % kGroup;
+    const GroupScratch g = groupScratch(smem, group, P.objs.maxEdges);
+    for (int32_t s = group; s < S; s += kGroupsPerBlock) {
+        const CandBodies cb = orderCandidate(P, w, cands[surv[s]]);
+        Contact &out = slots[s];
+        if (lane == 0) out.numPoints = 0;
+        const uint32_t test = cb.ta | cb.tb;
+        if (test == (uint32_t)CollisionPrimitive::Type::Hull) {
+            hullHullPair(P, w, cb, g, lane, out);
+        } else if (test == ((uint32_t)CollisionPrimitive::Type::Hull |
+                            (uint32_t)CollisionPrimitive::Type::Plane)) {
+            if (lane == 0) hullPlanePair(P, w, cb, g, out);
+        }
+        // sphere / plane-plane: the reference asserts (narrowphase.cpp:1197-1313)
+        groupSync();
     }
     __syncthreads();
 

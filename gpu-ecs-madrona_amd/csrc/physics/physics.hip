@@ -289,9 +289,11 @@ void PhysicsModule::upload(void *stream_ptr)
     O.numObjects = (int32_t)metadata.size();
     O.maxVerts = 0;
     O.maxFaces = 0;
+    O.maxEdges = 0;
     for (const HullDev &h : hulls) {
         O.maxVerts = std::max(O.maxVerts, h.numVerts);
         O.maxFaces = std::max(O.maxFaces, h.numFaces);
+        O.maxEdges = std::max(O.maxEdges, h.numEdges);
     }
     O.metadata = devUpload(metadata, stream);
     O.aabbs = devUpload(aabbs, stream);
@@ -369,7 +371,8 @@ MW_PHYS_NODE(SubstepRigidBodiesNode,
         hipLaunchKernelGGL(integrateKernel, rowGrid(P), dim3(256), 0, stream, P);)
 
 MW_PHYS_NODE(NarrowphaseNode,
-    hipLaunchKernelGGL(narrowphaseKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);)
+    hipLaunchKernelGGL(narrowphaseKernel, dim3(P.numWorlds), dim3(kNarrowBlock),
+                       narrowphaseSharedBytes(P), stream, P);)
 
 MW_PHYS_NODE(SolverNode,
     hipLaunchKernelGGL(solverKernel, dim3(P.numWorlds), dim3(kSolverBlock),

@@ -128,6 +128,7 @@ __global__ void solverKernel(PhysArgs P);
 
 size_t findOverlapsSharedBytes(const PhysArgs &P);
 size_t solverSharedBytes(const PhysArgs &P);
+size_t narrowphaseSharedBytes(const PhysArgs &P);
 
 constexpr int32_t kOverlapBlock = 192;
 constexpr int32_t kNarrowBlock = 256;

@@ -39,6 +39,7 @@ struct ObjDev {
     int32_t numObjects;
     int32_t maxVerts;
     int32_t maxFaces;
+    int32_t maxEdges;
     RigidBodyMetadata *metadata;
     math::AABB *aabbs;
     uint32_t *types;              // CollisionPrimitive::Type

@@ -105,3 +105,50 @@ def test_collisions_bvh_matches_oracle_after_first_step():
             assert len(na) == len(nb)
             assert na.tobytes() == nb.tobytes()
             assert aa.tobytes() == ab.tobytes()
+
+
+def test_collisions_bit_exact_long_horizon_contacts():
+    # 300 steps: every cube lands (z <= 10 falls for ~85 steps), stacks and
+    # settles, so cube-cube face / edge manifolds and cube-plane contacts
+    # dominate the tail of the run.
+    mw = _mw()
+    gcfg, ocfg = _cfg_pair()
+    W, steps = 8, 300
+    pos, rot = gen_collisions_inits(W, 128, seed=3)
+    sim = mw.CollisionsSim(W, pos, rot, gcfg)
+    orc = OraclePhys(ocfg, pos, rot)
+    seen_contacts = 0
+    for s in range(steps):
+        sim.step()
+        orc.step(1, 8)
+        _, contacts = sim.counts()
+        seen_contacts += int(contacts.sum())
+        if (s + 1) % 25:
+            continue
+        assert sim.error_flags() == 0, mw.ERR_BITS
+        for w in range(W):
+            d = _diff(sim.bodies(w), orc.bodies(w))
+            assert d is None, f"step {s} world {w}: {d}"
+            ka, kb = sim.contacts(w), orc.contacts(w)
+            assert len(ka) == len(kb)
+            for i in range(len(ka)):
+                assert _contacts_equal(ka[i], kb[i]), f"step {s} world {w}: contact {i} differs"
+    assert seen_contacts > W * steps * 10, seen_contacts
+
+
+def test_collisions_full_size_sampled_worlds():
+    # BASELINE.json configs[2] size (8192 worlds); the oracle replays a sample
+    # of worlds (first, middle, last) from the same per-world seeds.
+    mw = _mw()
+    gcfg, ocfg = _cfg_pair(max_contacts=4096)
+    W, steps = 8192, 40
+    pos, rot = mw.gen_collisions_inits(W, 128, seed=0)
+    sim = mw.CollisionsSim(W, pos, rot, gcfg)
+    sample = [0, 1, W // 2, W - 1]
+    orc = OraclePhys(ocfg, np.ascontiguousarray(pos[sample]), np.ascontiguousarray(rot[sample]))
+    sim.step(steps)
+    orc.step(steps, 4)
+    assert sim.error_flags() == 0, mw.ERR_BITS
+    for i, w in enumerate(sample):
+        d = _diff(sim.bodies(w), orc.bodies(i))
+        assert d is None, f"world {w}: {d}"
