@@ -29,19 +29,38 @@ sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E 8.0 TB/s spec
 
-# Bytes each node moves per unit (SURVEY.md §8d column sizes).
-# body = one physics body row, cand = one candidate pair, contact = one
-# contact manifold.
+# Algorithmic bytes each node moves per unit, per launch (SURVEY.md §8(d),
+# DESIGN.md §6): body = one physics body row, cand = one candidate pair,
+# contact = one contact manifold.  The solver node fuses solvePositions,
+# setVelocities and solveVelocities.  The overlap query's 116 B per visited
+# BVH node is not counted (lower bound).
 BYTES = {
-    "SubstepRigidBodiesNode": {"body": 108 + 108 + 192 + 192},
-    "NarrowphaseNode": {"cand": 16 + 2 * 52 + 2 * 28 + 2 * 192 + 4, "contact": 112},
-    "SolverNode": {"body": 156 + 52, "cand": 4, "contact": 4 + 112 + 16 + 112 + 8},
-    "FindOverlappingNode": {"body": 52 + 116 * 8, "cand": 16 + 20},
-    "UpdateLeafPositionsNode": {"body": 96 + 28},
-    "RefitNode": {"body": 80},
+    "UpdateLeafPositionsNode": {"body": 96 + 68},
+    "RefitNode": {"body": 32 + 2 * 24},
     "UpdateBVHNode": {"body": 0},
+    "FindOverlappingNode": {"body": 8 + 4 + 4 + 12, "cand": 16},
+    "SubstepRigidBodiesNode": {"body": 84 + 108},
+    "NarrowphaseNode": {"cand": 16 + 2 * 44, "contact": 112},
+    "SolverNode": {"body": 56 + 24, "contact": (112 + 2 * 92 + 2 * 28 + 16) + (112 + 2 * 100 + 2 * 24)},
 }
 NODE_KINDS = list(BYTES.keys()) + ["ParallelForNode"]
+
+
+def pmc_traffic(kernel_node):
+    """HBM bytes per launch of the node's kernel from the committed rocprofv3
+    PMC passes (profiles/*_traffic.json, written by profiles/pmc_traffic.py:
+    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            data = json.load(f)
+        entry = data.get("nodes", {}).get(kernel_node)
+        return None if entry is None else entry["bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def parse():
@@ -178,8 +197,28 @@ def main():
 
     if args.settle:
         sim.step(args.settle)
+
+    # Per-node breakdown (eager, untimed pre-roll): picks the dominant kernel,
+    # whose launches are then timed live inside the replayed graph.
+    launches = {"SubstepRigidBodiesNode": args.substeps, "NarrowphaseNode": args.substeps,
+                "SolverNode": args.substeps, "FindOverlappingNode": 1,
+                "UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
+                "ParallelForNode": 1}
+    node_table = {}
+    dom = None
+    if not args.no_roofline:
+        for name in NODE_KINDS:
+            ms = sim.time_node(name, 2)
+            if ms > 0:
+                node_table[name] = {"ms_per_launch": round(ms, 4),
+                                    "ms_per_step": round(ms * launches[name], 4)}
+        dom = max((n for n in node_table if n in BYTES),
+                  key=lambda n: node_table[n]["ms_per_step"])
+        sim.set_timed_node(dom)
+
     for _ in range(args.warmup):
         step()
+    ev_ms0, ev_n0 = sim.timed_node() if dom else (0.0, 0)
 
     if dist is not None:
         dist.barrier()
@@ -201,29 +240,25 @@ def main():
     value = total_worlds * args.steps / elapsed
 
     roofline = None
-    node_table = {}
-    if not args.no_roofline:
+    if dom:
+        ev_ms1, ev_n1 = sim.timed_node()
+        ms = (ev_ms1 - ev_ms0) / max(1, ev_n1 - ev_n0)
         cands, contacts = sim.counts()
         units = {"body": W * (args.cubes + 1), "cand": float(cands.sum()),
                  "contact": float(contacts.sum())}
-        launches = {"SubstepRigidBodiesNode": args.substeps, "NarrowphaseNode": args.substeps,
-                    "SolverNode": args.substeps, "FindOverlappingNode": 1,
-                    "UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
-                    "ParallelForNode": 1}
-        for name in NODE_KINDS:
-            ms = sim.time_node(name, 2)
-            if ms > 0:
-                node_table[name] = {"ms_per_launch": round(ms, 4),
-                                    "ms_per_step": round(ms * launches[name], 4)}
-        dom = max((n for n in node_table if n in BYTES),
-                  key=lambda n: node_table[n]["ms_per_step"])
         nbytes = sum(BYTES[dom].get(u, 0) * units[u] for u in units)
-        ms = node_table[dom]["ms_per_launch"]
         achieved = nbytes / (ms * 1e-3) / 1e9
+        step_bytes = sum(launches[n] * sum(BYTES[n].get(u, 0) * units[u] for u in units)
+                         for n in BYTES)
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": None, "bytes_per_launch": int(nbytes), "ms_per_launch": ms,
+            "traffic": pmc_traffic(dom),
+            "bytes_per_launch": int(nbytes), "ms_per_launch": round(ms, 4),
+            "timed_launches": int(ev_n1 - ev_n0),
+            "timing": "HIP events on the executor stream around every launch of the kernel during the timed steps (step graph split at that node)",
+            "step_algorithmic_bytes": int(step_bytes),
+            "step_achieved_gbs": round(step_bytes / (elapsed / args.steps) / 1e9, 2),
             "mean_candidates_per_world": round(float(cands.mean()), 1),
             "mean_contacts_per_world": round(float(contacts.mean()), 1),
         }

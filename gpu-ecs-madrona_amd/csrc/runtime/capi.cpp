@@ -255,6 +255,19 @@ double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps
     MW_TRY({ return exec->exec->timeNode(node_name, num_steps); }, -1.0)
 }
 
+int32_t mw_set_timed_node(mw_exec *exec, const char *node_name)
+{
+    MW_TRY({
+        exec->exec->setTimedNode(node_name);
+        return 0;
+    }, -1)
+}
+
+double mw_timed_node_ms(mw_exec *exec, int64_t *launches)
+{
+    MW_TRY({ return exec->exec->timedNodeMs(launches); }, -1.0)
+}
+
 }
 
 extern "C" int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *contacts_out)

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <cstdio>
 #include <stdexcept>
+#include <string>
 #include <vector>
 
 namespace madrona {
@@ -170,10 +171,26 @@ struct Executor::Impl {
     std::unique_ptr<StateManager> mgr;
     hipStream_t stream = nullptr;
     TaskGraph graph;
-    hipGraph_t hipGraph = nullptr;
-    hipGraphExec_t hipGraphExec = nullptr;
+    // The step as replayable hipGraph segments.  Normally one segment holds
+    // every node plus the export gathers; with live node timing enabled the
+    // step is split at each timed node, which is launched directly on the
+    // stream between its segments, bracketed by HIP events.
+    struct Segment {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        int32_t timedNode = -1;   // node launched (timed) after this segment
+    };
+    std::vector<Segment> segs;
     std::vector<ExportBuf> exports;
     int64_t *hostRowsTotal = nullptr;
+
+    // Live per-node timing: HIP events recorded around every launch of one
+    // node kind inside each step, accumulated at each sync.
+    std::string timedName;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timedEvents;
+    double timedMs = 0.0;
+    int64_t timedLaunches = 0;
+    bool timedPending = false;
 };
 
 Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
@@ -186,8 +203,14 @@ Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
 
 Executor::~Executor()
 {
-    if (impl_->hipGraphExec) (void)hipGraphExecDestroy(impl_->hipGraphExec);
-    if (impl_->hipGraph) (void)hipGraphDestroy(impl_->hipGraph);
+    for (auto &e : impl_->timedEvents) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    for (auto &sg : impl_->segs) {
+        if (sg.exec) (void)hipGraphExecDestroy(sg.exec);
+        if (sg.graph) (void)hipGraphDestroy(sg.graph);
+    }
     for (auto &e : impl_->exports) {
         (void)hipFree(e.buf);
         (void)hipFree(e.offsets);
@@ -250,38 +273,133 @@ static void launchExports(Executor::Impl &I, const StateView &dv)
     }
 }
 
+static bool isTimed(const Executor::Impl &I, int32_t node)
+{
+    return !I.timedName.empty() && I.timedName == I.graph.nodeName(node);
+}
+
+// One step's launch sequence: every node in sorted order, then the export
+// gathers.  Nodes of the timed kind are bracketed by their own event pair.
+static void launchStep(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
+{
+    size_t ev = 0;
+    for (int32_t i = 0; i < I.graph.numNodes(); i++) {
+        const bool timed = isTimed(I, i);
+        if (timed) MW_HIP_CHECK(hipEventRecord(I.timedEvents[ev].first, I.stream));
+        I.graph.launchNode(i, lc);
+        if (timed) MW_HIP_CHECK(hipEventRecord(I.timedEvents[ev++].second, I.stream));
+    }
+    launchExports(I, dv);
+}
+
+static void captureGraph(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
+{
+    for (auto &sg : I.segs) {
+        if (sg.exec) MW_HIP_CHECK(hipGraphExecDestroy(sg.exec));
+        if (sg.graph) MW_HIP_CHECK(hipGraphDestroy(sg.graph));
+    }
+    I.segs.clear();
+    const int32_t n = I.graph.numNodes();
+    int32_t start = 0;
+    for (int32_t i = 0; i <= n; i++) {
+        const bool last = i == n;
+        if (!last && !isTimed(I, i)) continue;
+        Executor::Impl::Segment sg;
+        sg.timedNode = last ? -1 : i;
+        if (i > start || last) {
+            MW_HIP_CHECK(hipStreamBeginCapture(I.stream, hipStreamCaptureModeThreadLocal));
+            for (int32_t k = start; k < i; k++) I.graph.launchNode(k, lc);
+            if (last) launchExports(I, dv);
+            MW_HIP_CHECK(hipStreamEndCapture(I.stream, &sg.graph));
+            MW_HIP_CHECK(hipGraphInstantiate(&sg.exec, sg.graph, nullptr, nullptr, 0));
+        }
+        I.segs.push_back(sg);
+        start = i + 1;
+    }
+}
+
 void Executor::setGraph(TaskGraph &&graph)
 {
     impl_->graph = std::move(graph);
     const StateView &dv = impl_->mgr->deviceViewHost();
     LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
-    if (impl_->cfg.useGraph) {
-        MW_HIP_CHECK(hipStreamBeginCapture(impl_->stream, hipStreamCaptureModeThreadLocal));
-        impl_->graph.launch(lc);
-        launchExports(*impl_, dv);
-        MW_HIP_CHECK(hipStreamEndCapture(impl_->stream, &impl_->hipGraph));
-        MW_HIP_CHECK(hipGraphInstantiate(&impl_->hipGraphExec, impl_->hipGraph, nullptr, nullptr, 0));
-    }
+    if (impl_->cfg.useGraph) captureGraph(*impl_, lc, dv);
 }
 
 void Executor::runAsync()
 {
-    if (impl_->hipGraphExec) {
-        MW_HIP_CHECK(hipGraphLaunch(impl_->hipGraphExec, impl_->stream));
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
+    if (!impl_->segs.empty()) {
+        size_t ev = 0;
+        for (auto &sg : impl_->segs) {
+            if (sg.exec) MW_HIP_CHECK(hipGraphLaunch(sg.exec, impl_->stream));
+            if (sg.timedNode >= 0) {
+                MW_HIP_CHECK(hipEventRecord(impl_->timedEvents[ev].first, impl_->stream));
+                impl_->graph.launchNode(sg.timedNode, lc);
+                MW_HIP_CHECK(hipEventRecord(impl_->timedEvents[ev].second, impl_->stream));
+                ev++;
+            }
+        }
     } else {
-        const StateView &dv = impl_->mgr->deviceViewHost();
-        LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
-        impl_->graph.launch(lc);
-        launchExports(*impl_, dv);
+        launchStep(*impl_, lc, dv);
     }
+    impl_->timedPending = !impl_->timedEvents.empty();
 }
 
-void Executor::sync() { MW_HIP_CHECK(hipStreamSynchronize(impl_->stream)); }
+void Executor::sync()
+{
+    MW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
+    if (impl_->timedPending) {
+        // Events hold the most recent step's launches (earlier unsynced steps
+        // of a runAsync burst are not double counted).
+        for (auto &e : impl_->timedEvents) {
+            float ms = 0;
+            MW_HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
+            impl_->timedMs += ms;
+            impl_->timedLaunches++;
+        }
+        impl_->timedPending = false;
+    }
+}
 
 void Executor::run()
 {
     runAsync();
     sync();
+}
+
+void Executor::setTimedNode(const char *name)
+{
+    sync();
+    impl_->timedName = name ? name : "";
+    for (auto &e : impl_->timedEvents) {
+        MW_HIP_CHECK(hipEventDestroy(e.first));
+        MW_HIP_CHECK(hipEventDestroy(e.second));
+    }
+    impl_->timedEvents.clear();
+    impl_->timedMs = 0.0;
+    impl_->timedLaunches = 0;
+    if (!impl_->timedName.empty()) {
+        for (int32_t i = 0; i < impl_->graph.numNodes(); i++) {
+            if (impl_->timedName == impl_->graph.nodeName(i)) {
+                hipEvent_t a, b;
+                MW_HIP_CHECK(hipEventCreate(&a));
+                MW_HIP_CHECK(hipEventCreate(&b));
+                impl_->timedEvents.push_back({ a, b });
+            }
+        }
+    }
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
+    if (impl_->cfg.useGraph) captureGraph(*impl_, lc, dv);
+}
+
+double Executor::timedNodeMs(int64_t *launches)
+{
+    sync();
+    if (launches) *launches = impl_->timedLaunches;
+    return impl_->timedMs;
 }
 
 void *Executor::getExported(int32_t slot, int64_t *num_rows)

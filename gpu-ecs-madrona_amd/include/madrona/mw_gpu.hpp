@@ -68,6 +68,10 @@ public:
     // Eagerly run num_steps steps with HIP events around every launch of the
     // node kind `name` (on the executor stream); mean ms per launch.
     double timeNode(const char *name, int32_t num_steps);
+    // Live timing of one node kind inside the replayed step (HIP events on
+    // the executor stream); setTimedNode re-captures the graph and resets.
+    void setTimedNode(const char *name);
+    double timedNodeMs(int64_t *launches);
 
     struct Impl;
 private:

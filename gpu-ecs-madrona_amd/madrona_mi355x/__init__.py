@@ -70,6 +70,10 @@ _lib.mw_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.
                                          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 _lib.mw_phys_time_node.restype = ctypes.c_double
 _lib.mw_phys_time_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
+_lib.mw_set_timed_node.restype = ctypes.c_int32
+_lib.mw_set_timed_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+_lib.mw_timed_node_ms.restype = ctypes.c_double
+_lib.mw_timed_node_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
 
 # The symbols include/madrona_mw.h declares (checked by tests/test_capi_symbols.py).
 C_ABI_SYMBOLS = (
@@ -77,7 +81,7 @@ C_ABI_SYMBOLS = (
     "mw_destroy", "mw_last_error", "mw_num_worlds", "mw_error_flags", "mw_num_archetypes",
     "mw_read_column", "mw_column_info", "mw_phys_read_candidates", "mw_phys_read_contacts",
     "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_copy_exported",
-    "mw_gen_collisions_inits",
+    "mw_gen_collisions_inits", "mw_set_timed_node", "mw_timed_node_ms",
 )
 
 
@@ -193,7 +197,20 @@ class Executor:
         return n
 
     def time_node(self, name, steps):
+        """Eager timing of `steps` extra steps (advances the simulation)."""
         return _lib.mw_phys_time_node(self.h, name.encode(), steps)
+
+    def set_timed_node(self, name):
+        """Bracket every launch of node kind `name` with HIP events inside the
+        replayed step (None disables); resets the accumulators."""
+        if _lib.mw_set_timed_node(self.h, name.encode() if name else None) != 0:
+            raise _err()
+
+    def timed_node(self):
+        """(total ms, launches) accumulated since set_timed_node."""
+        n = ctypes.c_int64(0)
+        ms = _lib.mw_timed_node_ms(self.h, ctypes.byref(n))
+        return ms, n.value
 
     def close(self):
         if getattr(self, "h", None):

@@ -131,6 +131,14 @@ int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *contacts_out)
  * Returns the mean duration in ms over `num_steps` fresh steps.            */
 double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps);
 
+/* live timing inside the replayed step: the step graph is split at every
+ * launch of the named node kind, which then runs directly on the executor
+ * stream between graph segments, bracketed by HIP events; mw_timed_node_ms
+ * returns the accumulated ms and the number of timed launches since the
+ * last mw_set_timed_node (NULL/"" disables and restores the single graph). */
+int32_t mw_set_timed_node(mw_exec *exec, const char *node_name);
+double mw_timed_node_ms(mw_exec *exec, int64_t *launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -152,3 +152,25 @@ def test_collisions_full_size_sampled_worlds():
     for i, w in enumerate(sample):
         d = _diff(sim.bodies(w), orc.bodies(i))
         assert d is None, f"world {w}: {d}"
+
+
+def test_live_node_timing_does_not_perturb_state():
+    # set_timed_node splits the step graph at the named node kind and times
+    # its launches with HIP events; state must stay bit-identical to an
+    # untimed run.
+    mw = _mw()
+    gcfg, _ = _cfg_pair()
+    pos, rot = gen_collisions_inits(16, 128, seed=2)
+    a = mw.CollisionsSim(16, pos, rot, gcfg)
+    b = mw.CollisionsSim(16, pos, rot, gcfg)
+    a.set_timed_node("NarrowphaseNode")
+    for _ in range(10):
+        a.step()           # synchronous steps: each one's launches are counted
+    b.step(10)
+    ms, n = a.timed_node()
+    assert n == 10 * gcfg.num_substeps and ms > 0
+    for w in range(16):
+        assert a.bodies(w).tobytes() == b.bodies(w).tobytes()
+    a.set_timed_node(None)
+    a.step(1)
+    assert a.timed_node() == (0.0, 0)
