@@ -113,50 +113,51 @@ constexpr int32_t kGroupsPerBlock = kNarrowBlock / kGroup;
 constexpr int32_t kMaxClip = 32;
 
 struct HullRef {
-    const Vector3 *verts;          // world space
-    const geometry::Plane *planes; // world space
+    const Vector3 *verts;          // world space (LDS copy)
+    const geometry::Plane *planes; // world space (LDS copy)
+    const EdgeQuad *quads;         // edge topology (LDS copy)
     HullDev hd;
     Vector3 center;
 };
 
-// Per-edge SAT inputs gathered once per pair (edgeDistance's operands,
-// narrowphase.cpp:433-472 via queryEdgeDirections :474-540).
-struct EdgeRec {
-    Vector3 n1, n2;                // normals of the two faces sharing the edge
-    Vector3 p1, p2;                // root vertex, root vertex of next
+// Per-group LDS: both hulls of the pair (world-space vertices, face planes,
+// edge topology) and the leader lane's clipping polygons.
+struct GroupLDS {
+    Vector3 *vA, *vB;
+    geometry::Plane *pA, *pB;
+    EdgeQuad *qA, *qB;
+    Vector3 *clip0, *clip1;
+    float *depths;
 };
 
-struct GroupScratch {
-    EdgeRec *edgesA;               // [maxEdges]
-    EdgeRec *edgesB;               // [maxEdges]
-    Vector3 *clip0;                // [kMaxClip]
-    Vector3 *clip1;                // [kMaxClip]
-    float *depths;                 // [kMaxClip]
-};
+__host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
 
-__host__ __device__ inline size_t groupScratchBytes(int32_t max_edges)
+__host__ __device__ inline size_t groupLDSBytes(int32_t max_verts, int32_t max_faces,
+                                                int32_t max_edges)
 {
-    return (size_t)2 * max_edges * sizeof(EdgeRec) + 2 * kMaxClip * sizeof(Vector3) +
-           kMaxClip * sizeof(float);
+    return 2 * a16(sizeof(Vector3) * max_verts) + 2 * a16(sizeof(geometry::Plane) * max_faces) +
+           2 * a16(sizeof(EdgeQuad) * max_edges) + 2 * a16(sizeof(Vector3) * kMaxClip) +
+           a16(sizeof(float) * kMaxClip);
 }
 
 size_t narrowphaseSharedBytes(const PhysArgs &P)
 {
-    return kGroupsPerBlock * groupScratchBytes(P.objs.maxEdges);
+    const ObjDev &O = P.objs;
+    return kGroupsPerBlock * groupLDSBytes(O.maxVerts, O.maxFaces, O.maxEdges);
 }
 
-__device__ __forceinline__ GroupScratch groupScratch(char *smem, int32_t group, int32_t max_edges)
+__device__ __forceinline__ GroupLDS groupLDS(char *smem, int32_t group, const ObjDev &O)
 {
-    char *p = smem + (size_t)group * groupScratchBytes(max_edges);
-    GroupScratch g;
-    g.edgesA = (EdgeRec *)p;
-    p += max_edges * sizeof(EdgeRec);
-    g.edgesB = (EdgeRec *)p;
-    p += max_edges * sizeof(EdgeRec);
-    g.clip0 = (Vector3 *)p;
-    p += kMaxClip * sizeof(Vector3);
-    g.clip1 = (Vector3 *)p;
-    p += kMaxClip * sizeof(Vector3);
+    char *p = smem + (size_t)group * groupLDSBytes(O.maxVerts, O.maxFaces, O.maxEdges);
+    GroupLDS g;
+    g.vA = (Vector3 *)p; p += a16(sizeof(Vector3) * O.maxVerts);
+    g.vB = (Vector3 *)p; p += a16(sizeof(Vector3) * O.maxVerts);
+    g.pA = (geometry::Plane *)p; p += a16(sizeof(geometry::Plane) * O.maxFaces);
+    g.pB = (geometry::Plane *)p; p += a16(sizeof(geometry::Plane) * O.maxFaces);
+    g.qA = (EdgeQuad *)p; p += a16(sizeof(EdgeQuad) * O.maxEdges);
+    g.qB = (EdgeQuad *)p; p += a16(sizeof(EdgeQuad) * O.maxEdges);
+    g.clip0 = (Vector3 *)p; p += a16(sizeof(Vector3) * kMaxClip);
+    g.clip1 = (Vector3 *)p; p += a16(sizeof(Vector3) * kMaxClip);
     g.depths = (float *)p;
     return g;
 }
@@ -188,6 +189,23 @@ __device__ __forceinline__ void groupArgMax(float &v, int32_t &k)
         const int32_t ok = __shfl_xor(k, off, kGroup);
         if (scanWins(ov, ok, v, k)) { v = ov; k = ok; }
     }
+}
+
+// Copy one body's world-space hull (written by the integrate kernel) and its
+// edge topology into the group's LDS.
+__device__ __forceinline__ void stageHull(const PhysArgs &P, int32_t w, int32_t leaf,
+                                          const HullDev &hd, Vector3 *v, geometry::Plane *pl,
+                                          EdgeQuad *q, int32_t lane)
+{
+    const size_t body = (size_t)w * P.maxLeaves + leaf;
+    const float *gv = (const float *)(P.hullVerts + body * P.objs.maxVerts);
+    float *lv = (float *)v;
+    for (int32_t i = lane; i < hd.numVerts * 3; i += kGroup) lv[i] = gv[i];
+    const float4 *gp = (const float4 *)(P.hullPlanes + body * P.objs.maxFaces);
+    float4 *lp = (float4 *)pl;
+    for (int32_t i = lane; i < hd.numFaces; i += kGroup) lp[i] = gp[i];
+    const EdgeQuad *gq = P.objs.edgeQuads + hd.edgeOffset;
+    for (int32_t i = lane; i < hd.numEdges; i += kGroup) q[i] = gq[i];
 }
 
 __device__ __forceinline__ float distFromPlane(const geometry::Plane &p, const Vector3 &a)
@@ -248,71 +266,58 @@ __device__ __forceinline__ bool isMinkowskiFace(const Vector3 &a, const Vector3 
     return cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f;
 }
 
-// edgeDistance (narrowphase.cpp:433-472) for one edge pair: separation along
-// the edges' cross product, or -FLT_MAX when the edges do not form a face of
-// the Minkowski difference or are parallel.
-__device__ __forceinline__ float edgePairSeparation(const EdgeRec &ea, const EdgeRec &eb,
-                                                    const Vector3 &a_center, Vector3 *normal_out)
+// edgeDistance (narrowphase.cpp:433-472) for edge i of a against edge j of
+// b: separation along the edges' cross product, or -FLT_MAX when the edges
+// do not form a face of the Minkowski difference or are parallel.
+__device__ __forceinline__ float edgePairSeparation(const HullRef &a, const HullRef &b,
+                                                    int32_t i, int32_t j, Vector3 *normal_out)
 {
+    const EdgeQuad ea = a.quads[i], eb = b.quads[j];
     float sep = -FLT_MAX;
     Vector3 n { 0, 0, 0 };
-    if (isMinkowskiFace(ea.n1, ea.n2, -eb.n1, -eb.n2)) {
-        Vector3 da = ea.p2 - ea.p1, db = eb.p2 - eb.p1;
+    if (isMinkowskiFace(a.planes[ea.face1].normal, a.planes[ea.face2].normal,
+                        -b.planes[eb.face1].normal, -b.planes[eb.face2].normal)) {
+        const Vector3 pa1 = a.verts[ea.v1], pb1 = b.verts[eb.v1];
+        Vector3 da = a.verts[ea.v2] - pa1, db = b.verts[eb.v2] - pb1;
         Vector3 uc = da.cross(db);
         float l2 = uc.length2();
         if (l2 != 0) {
             float inv = 1.f / sqrtf(l2);
             n = uc * inv;
-            if (n.dot(ea.p1 - a_center) < 0.0f) n = -n;
-            sep = n.dot(eb.p1 - ea.p1);
+            if (n.dot(pa1 - a.center) < 0.0f) n = -n;
+            sep = n.dot(pb1 - pa1);
         }
     }
     if (normal_out) *normal_out = n;
     return sep;
 }
 
-__device__ __forceinline__ void stageEdges(const ObjDev &O, const HullRef &h, EdgeRec *dst,
-                                           int32_t lane)
-{
-    const geometry::HalfEdge *he = O.hedges + h.hd.hedgeOffset;
-    for (int32_t i = lane; i < h.hd.numEdges; i += kGroup) {
-        const geometry::HalfEdge e = he[O.edges[h.hd.edgeOffset + i]];
-        EdgeRec r;
-        r.n1 = h.planes[e.polygon].normal;
-        r.n2 = h.planes[he[e.twin].polygon].normal;
-        r.p1 = h.verts[e.rootVertex];
-        r.p2 = h.verts[he[e.next].rootVertex];
-        dst[i] = r;
-    }
-}
-
 struct EdgeQuery {
     float separation;
     Vector3 normal;
-    int32_t edgeA;                 // half-edge indices (queryEdgeDirections' result)
+    int32_t edgeA;                 // edge indices (into the hull's edge list)
     int32_t edgeB;
 };
 
-// queryEdgeDirections (narrowphase.cpp:474-540) over the staged edge records.
-// Pair index k = i * nB + j is the reference's loop order.
-__device__ EdgeQuery groupEdgeQuery(const ObjDev &O, const HullRef &a, const HullRef &b,
-                                    const GroupScratch &g, int32_t lane)
+// queryEdgeDirections (narrowphase.cpp:474-540).  Pair index p = i * nB + j
+// is the reference's loop order; the early return on a positive separation
+// only ever rejects the pair.
+__device__ EdgeQuery groupEdgeQuery(const HullRef &a, const HullRef &b, int32_t lane)
 {
     const int32_t nA = a.hd.numEdges, nB = b.hd.numEdges;
     float v = __builtin_nanf("");
     int32_t k = INT32_MAX;
     for (int32_t p = lane; p < nA * nB; p += kGroup) {
         const int32_t i = p / nB, j = p - i * nB;
-        const float sep = edgePairSeparation(g.edgesA[i], g.edgesB[j], a.center, nullptr);
+        const float sep = edgePairSeparation(a, b, i, j, nullptr);
         if (scanWins(sep, p, v, k)) { v = sep; k = p; }
     }
     groupArgMax(v, k);
     if (!(v > -FLT_MAX)) return { -FLT_MAX, { 0, 0, 0 }, 0, 0 };
-    const int32_t i = k / nB, j = k - i * nB;
     EdgeQuery q;
-    q.separation = edgePairSeparation(g.edgesA[i], g.edgesB[j], a.center, &q.normal);
-    q.edgeA = (int32_t)O.edges[a.hd.edgeOffset + i];
-    q.edgeB = (int32_t)O.edges[b.hd.edgeOffset + j];
+    q.edgeA = k / nB;
+    q.edgeB = k - q.edgeA * nB;
+    q.separation = edgePairSeparation(a, b, q.edgeA, q.edgeB, &q.normal);
     return q;
 }
 
@@ -443,40 +448,11 @@ __device__ __forceinline__ geometry::Segment shortestSegmentBetween(const geomet
     return { s1.p1 + s * v1, s2.p1 + t * v2 };
 }
 
-// Candidate order: runNarrowphase's type swap (narrowphase.cpp:1574-1580).
-struct CandBodies {
-    Loc a_loc, b_loc;
-    const BodyArch *BA, *BB;
-    int32_t a_obj, b_obj;
-    uint32_t ta, tb;
-};
-
-__device__ __forceinline__ CandBodies orderCandidate(const PhysArgs &P, int32_t w,
-                                                     const CandidateCollision &cand)
-{
-    const ObjDev &O = P.objs;
-    CandBodies c;
-    c.a_loc = cand.a;
-    c.b_loc = cand.b;
-    c.BA = &P.body[bodyArchIndex(P, c.a_loc.archetype)];
-    c.BB = &P.body[bodyArchIndex(P, c.b_loc.archetype)];
-    c.a_obj = bcol<ObjectID>(*c.BA, Cols::ObjectID, w, c.a_loc.row).idx;
-    c.b_obj = bcol<ObjectID>(*c.BB, Cols::ObjectID, w, c.b_loc.row).idx;
-    c.ta = O.types[c.a_obj];
-    c.tb = O.types[c.b_obj];
-    if (c.ta > c.tb) {
-        Loc tl = c.a_loc; c.a_loc = c.b_loc; c.b_loc = tl;
-        const BodyArch *tB = c.BA; c.BA = c.BB; c.BB = tB;
-        int32_t to = c.a_obj; c.a_obj = c.b_obj; c.b_obj = to;
-        uint32_t tt = c.ta; c.ta = c.tb; c.tb = tt;
-    }
-    return c;
-}
-
 // World-space AABB recheck (narrowphase.cpp:1589-1603) against the per-body
-// AABBs the integrate kernel cached (same applyTRS, same inputs).
-__device__ __forceinline__ bool candidateOverlaps(const PhysArgs &P, int32_t w,
-                                                  const CandidateCollision &cand)
+// AABBs the integrate kernel cached (same applyTRS, same inputs), then the
+// type ordering of runNarrowphase (:1574-1580) for pairs that survive.
+__device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
+                                            const CandidateCollision &cand, SatWork &out)
 {
     const BodyArch &BA = P.body[bodyArchIndex(P, cand.a.archetype)];
     const BodyArch &BB = P.body[bodyArchIndex(P, cand.b.archetype)];
@@ -484,40 +460,50 @@ __device__ __forceinline__ bool candidateOverlaps(const PhysArgs &P, int32_t w,
     const int32_t lb = bcol<broadphase::LeafID>(BB, Cols::LeafID, w, cand.b.row).id;
     const AABB a = P.bodyAABBs[(size_t)w * P.maxLeaves + la];
     const AABB b = P.bodyAABBs[(size_t)w * P.maxLeaves + lb];
-    return a.overlaps(b);
-}
-
-__device__ __forceinline__ HullRef hullOf(const PhysArgs &P, int32_t w, const BodyArch &B,
-                                          Loc loc, int32_t obj)
-{
-    const int32_t leaf = bcol<broadphase::LeafID>(B, Cols::LeafID, w, loc.row).id;
-    HullRef h;
-    h.hd = P.objs.hulls[obj];
-    h.verts = P.hullVerts + ((size_t)w * P.maxLeaves + leaf) * P.objs.maxVerts;
-    h.planes = P.hullPlanes + ((size_t)w * P.maxLeaves + leaf) * P.objs.maxFaces;
-    h.center = bcol<Vector3>(B, Cols::Position, w, loc.row);
-    return h;
+    if (!a.overlaps(b)) return false;
+    const int32_t oa = bcol<ObjectID>(BA, Cols::ObjectID, w, cand.a.row).idx;
+    const int32_t ob = bcol<ObjectID>(BB, Cols::ObjectID, w, cand.b.row).idx;
+    const uint32_t ta = P.objs.types[oa], tb = P.objs.types[ob];
+    out.world = w;
+    out.test = ta | tb;
+    out.pad = 0;
+    if (ta > tb) {
+        out.a = cand.b; out.b = cand.a;
+        out.aLeaf = lb; out.bLeaf = la;
+        out.aObj = ob; out.bObj = oa;
+    } else {
+        out.a = cand.a; out.b = cand.b;
+        out.aLeaf = la; out.bLeaf = lb;
+        out.aObj = oa; out.bObj = ob;
+    }
+    return true;
 }
 
 // Hull-hull: doSAT (narrowphase.cpp:678-758) on the group, then
 // createFaceContact (:866-972) or createEdgeContact (:1053-1121) on the
-// leader lane.  All group lanes must enter.
-__device__ void hullHullPair(const PhysArgs &P, int32_t w, const CandBodies &cb,
-                             const GroupScratch &g, int32_t lane, Contact &out)
+// leader lane.  All group lanes must enter; both hulls are staged in LDS.
+__device__ void hullHullPair(const PhysArgs &P, const SatWork &wk, const GroupLDS &g,
+                             int32_t lane, Contact &out)
 {
     const ObjDev &O = P.objs;
-    const HullRef ha = hullOf(P, w, *cb.BA, cb.a_loc, cb.a_obj);
-    const HullRef hb = hullOf(P, w, *cb.BB, cb.b_loc, cb.b_obj);
+    const int32_t w = wk.world;
+    HullRef ha, hb;
+    ha.hd = O.hulls[wk.aObj];
+    hb.hd = O.hulls[wk.bObj];
+    ha.verts = g.vA; ha.planes = g.pA; ha.quads = g.qA;
+    hb.verts = g.vB; hb.planes = g.pB; hb.quads = g.qB;
+    const BodyArch &BA = P.body[bodyArchIndex(P, wk.a.archetype)];
+    ha.center = bcol<Vector3>(BA, Cols::Position, w, wk.a.row);
+    hb.center = Vector3::zero();            // unused by the hull-hull path
+    stageHull(P, w, wk.aLeaf, ha.hd, g.vA, g.pA, g.qA, lane);
+    stageHull(P, w, wk.bLeaf, hb.hd, g.vB, g.pB, g.qB, lane);
+    groupSync();
 
     const FaceQuery fa = groupFaceQuery(ha, hb, lane);
     if (fa.separation > 0.0f) return;
     const FaceQuery fb = groupFaceQuery(hb, ha, lane);
     if (fb.separation > 0.0f) return;
-    stageEdges(O, ha, g.edgesA, lane);
-    stageEdges(O, hb, g.edgesB, lane);
-    groupSync();
-    const EdgeQuery eq = groupEdgeQuery(O, ha, hb, g, lane);
-    groupSync();
+    const EdgeQuery eq = groupEdgeQuery(ha, hb, lane);
     if (eq.separation > 0.0f) return;
     if (lane != 0) return;
 
@@ -569,18 +555,15 @@ __device__ void hullHullPair(const PhysArgs &P, int32_t w, const CandBodies &cb,
             }
         }
         storeFaceManifold(out, ref_plane.normal, cin, g.depths, n_below,
-                          a_is_ref ? cb.a_loc : cb.b_loc, a_is_ref ? cb.b_loc : cb.a_loc);
+                          a_is_ref ? wk.a : wk.b, a_is_ref ? wk.b : wk.a);
     } else {
-        const geometry::HalfEdge *ha_e = O.hedges + ha.hd.hedgeOffset;
-        const geometry::HalfEdge *hb_e = O.hedges + hb.hd.hedgeOffset;
-        const geometry::HalfEdge ea = ha_e[eq.edgeA];
-        const geometry::HalfEdge eb = hb_e[eq.edgeB];
-        geometry::Segment sa { ha.verts[ea.rootVertex], ha.verts[ha_e[ea.next].rootVertex] };
-        geometry::Segment sb { hb.verts[eb.rootVertex], hb.verts[hb_e[eb.next].rootVertex] };
+        const EdgeQuad ea = ha.quads[eq.edgeA], eb = hb.quads[eq.edgeB];
+        geometry::Segment sa { ha.verts[ea.v1], ha.verts[ea.v2] };
+        geometry::Segment sb { hb.verts[eb.v1], hb.verts[eb.v2] };
         geometry::Segment s = shortestSegmentBetween(sa, sb);
         const Quat ident { 1, 0, 0, 0 };
-        out.ref = cb.a_loc;
-        out.alt = cb.b_loc;
+        out.ref = wk.a;
+        out.alt = wk.b;
         out.points[0] = Vector4::fromVector3(ident.rotateVec(s.p1) + Vector3::zero(),
                                              -eq.separation);
         for (int i = 1; i < 4; i++) out.points[i] = Vector4::fromVector3(Vector3::zero(), 0.f);
@@ -591,14 +574,22 @@ __device__ void hullHullPair(const PhysArgs &P, int32_t w, const CandBodies &cb,
 }
 
 // Hull-plane: doSATPlane (narrowphase.cpp:760-788) + createFacePlaneContact
-// (:974-1017) on the leader lane.
-__device__ void hullPlanePair(const PhysArgs &P, int32_t w, const CandBodies &cb,
-                              const GroupScratch &g, Contact &out)
+// (:974-1017) on the leader lane after the group stages the hull.
+__device__ void hullPlanePair(const PhysArgs &P, const SatWork &wk, const GroupLDS &g,
+                              int32_t lane, Contact &out)
 {
     const ObjDev &O = P.objs;
-    const HullRef ha = hullOf(P, w, *cb.BA, cb.a_loc, cb.a_obj);
-    const Vector3 b_pos = bcol<Vector3>(*cb.BB, Cols::Position, w, cb.b_loc.row);
-    const Quat b_rot = bcol<Quat>(*cb.BB, Cols::Rotation, w, cb.b_loc.row);
+    const int32_t w = wk.world;
+    HullRef ha;
+    ha.hd = O.hulls[wk.aObj];
+    ha.verts = g.vA; ha.planes = g.pA; ha.quads = g.qA;
+    ha.center = Vector3::zero();
+    stageHull(P, w, wk.aLeaf, ha.hd, g.vA, g.pA, g.qA, lane);
+    groupSync();
+    if (lane != 0) return;
+    const BodyArch &BB = P.body[bodyArchIndex(P, wk.b.archetype)];
+    const Vector3 b_pos = bcol<Vector3>(BB, Cols::Position, w, wk.b.row);
+    const Quat b_rot = bcol<Quat>(BB, Cols::Rotation, w, wk.b.row);
     Vector3 pn = b_rot.rotateVec(Vector3 { 0, 0, 1 });
     geometry::Plane plane { pn, dot(pn, b_pos) };
     float sep = hullDistFromPlane(plane, ha);
@@ -618,72 +609,64 @@ __device__ void hullPlanePair(const PhysArgs &P, int32_t w, const CandBodies &cb
             n++;
         }
     } while (hidx != start);
-    storeFaceManifold(out, plane.normal, g.clip0, g.depths, n, cb.b_loc, cb.a_loc);
+    storeFaceManifold(out, plane.normal, g.clip0, g.depths, n, wk.b, wk.a);
 }
 
-// runNarrowphaseSystem over every candidate of a world (one block per world):
-//   A. lane-per-candidate AABB recheck, block scan -> survivor list (order kept)
-//   B. group-per-survivor SAT + contact generation into survivor slots
-//   C. block scan of survivors with a manifold -> the solver's contact order
-//      (== the reference's addManifoldToSolver append order).
-__global__ void __launch_bounds__(kNarrowBlock) narrowphaseKernel(PhysArgs P)
+// runNarrowphaseSystem (narrowphase.cpp:1515-1728), stage 1, one block per
+// world: lane-per-candidate AABB recheck and type ordering; a block scan
+// numbers the survivors in the reference's candidate order (their slot ==
+// contact slot) and appends them to the device-wide SAT work list.
+__global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
 {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int32_t s_scan[kNarrowBlock / 64];
+    __shared__ int32_t s_base;
     const int32_t w = blockIdx.x;
     const int32_t num = min(P.numCands[w], P.candCapacity);
     const CandidateCollision *cands = P.cands + (size_t)w * P.candCapacity;
-    int32_t *surv = P.survivors + (size_t)w * P.candCapacity;
-    Contact *slots = P.candContacts + (size_t)w * P.candCapacity;
 
     int32_t S = 0;
     for (int32_t chunk = 0; chunk < num; chunk += kNarrowBlock) {
         const int32_t ci = chunk + threadIdx.x;
-        const int32_t keep = (ci < num && candidateOverlaps(P, w, cands[ci])) ? 1 : 0;
+        SatWork wk;
+        const int32_t keep = (ci < num && resolvePair(P, w, cands[ci], wk)) ? 1 : 0;
         int32_t total;
         const int32_t off = blockExclusiveScan(keep, s_scan, &total);
-        if (keep) surv[S + off] = ci;
+        if (threadIdx.x == 0 && total > 0) s_base = atomicAdd(P.satWorkCount, total);
+        __syncthreads();
+        if (keep) {
+            wk.slot = S + off;
+            P.satWork[s_base + off] = wk;
+        }
         S += total;
+        __syncthreads();
     }
-    __syncthreads();
+    if (threadIdx.x == 0) P.survCount[w] = S;
+}
 
+// Stage 2, persistent: each 16-lane group takes pairs off the work list and
+// writes the pair's manifold (numPoints 0 = no contact) into its world's
+// survivor slot.  The grid is sized to what is resident at once, so every
+// group reaches the end of the list and exits.
+__global__ void __launch_bounds__(kNarrowBlock) narrowSATKernel(PhysArgs P)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
     const int32_t group = threadIdx.x / kGroup;
     const int32_t lane = threadIdx.x % kGroup;
-    const GroupScratch g = groupScratch(smem, group, P.objs.maxEdges);
-    for (int32_t s = group; s < S; s += kGroupsPerBlock) {
-        const CandBodies cb = orderCandidate(P, w, cands[surv[s]]);
-        Contact &out = slots[s];
+    const GroupLDS g = groupLDS(smem, group, P.objs);
+    const int32_t total = *(volatile int32_t *)P.satWorkCount;
+    const int32_t stride = gridDim.x * kGroupsPerBlock;
+    for (int32_t idx = blockIdx.x * kGroupsPerBlock + group; idx < total; idx += stride) {
+        const SatWork wk = P.satWork[idx];
+        Contact &out = P.candContacts[(size_t)wk.world * P.candCapacity + wk.slot];
         if (lane == 0) out.numPoints = 0;
-        const uint32_t test = cb.ta | cb.tb;
-        if (test == (uint32_t)CollisionPrimitive::Type::Hull) {
-            hullHullPair(P, w, cb, g, lane, out);
-        } else if (test == ((uint32_t)CollisionPrimitive::Type::Hull |
-                            (uint32_t)CollisionPrimitive::Type::Plane)) {
-            if (lane == 0) hullPlanePair(P, w, cb, g, out);
+        if (wk.test == (uint32_t)CollisionPrimitive::Type::Hull) {
+            hullHullPair(P, wk, g, lane, out);
+        } else if (wk.test == ((uint32_t)CollisionPrimitive::Type::Hull |
+                               (uint32_t)CollisionPrimitive::Type::Plane)) {
+            hullPlanePair(P, wk, g, lane, out);
         }
         // sphere / plane-plane: the reference asserts (narrowphase.cpp:1197-1313)
         groupSync();
-    }
-    __syncthreads();
-
-    int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
-    int32_t K = 0;
-    for (int32_t chunk = 0; chunk < S; chunk += kNarrowBlock) {
-        const int32_t s = chunk + threadIdx.x;
-        const int32_t has = (s < S && slots[s].numPoints > 0) ? 1 : 0;
-        int32_t total;
-        const int32_t off = blockExclusiveScan(has, s_scan, &total);
-        if (has) order[K + off] = s;
-        K += total;
-    }
-    if (threadIdx.x == 0) {
-        if (K > P.maxContacts) {
-            // The reference asserts here (narrowphase.cpp:1130); flag, truncate.
-            atomicOr(P.errorFlags + w, kErrContactOverflow);
-            K = P.maxContacts;
-        }
-        P.solver[w].numContacts = K;
-        P.lastNumContacts[w] = K;
     }
 }
 

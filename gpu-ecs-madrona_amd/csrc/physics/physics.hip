@@ -167,6 +167,7 @@ struct PhysicsModule : StateExtension {
     std::vector<geometry::HalfEdge> hedges;
     std::vector<uint32_t> edges;
     std::vector<uint32_t> polygons;
+    std::vector<EdgeQuad> edgeQuads;
 
     PhysArgs args {};
     std::vector<void *> devAllocs;
@@ -271,6 +272,10 @@ void PhysicsModule::upload(void *stream_ptr)
     P.solver = (SolverData *)dv.arch[solver_arch].cols[1];
     P.candArchetype = mgr->archetypeIndex(typeKey<CandidateTemporary>());
     P.candCapacity = dv.arch[P.candArchetype].capacity;
+    if (P.candCapacity > 32767 || P.maxBodiesPerWorld > 32767) {
+        // solver contact records hold survivor slots and body slots as int16
+        throw std::runtime_error("physics: max candidates / bodies per world must be <= 32767");
+    }
     P.numCands = dv.arch[P.candArchetype].numRows;
     P.cands = (CandidateCollision *)dv.arch[P.candArchetype].cols[1];
     P.idNodes = dv.idNodes;
@@ -303,17 +308,30 @@ void PhysicsModule::upload(void *stream_ptr)
     O.planes = devUpload(planes, stream);
     O.hedges = devUpload(hedges, stream);
     O.edges = devUpload(edges, stream);
+    O.edgeQuads = devUpload(edgeQuads, stream);
     O.polygons = devUpload(polygons, stream);
 
     P.hullVerts = devAlloc<Vector3>((size_t)W * maxLeaves * std::max(O.maxVerts, 1), stream);
     P.hullPlanes = devAlloc<geometry::Plane>((size_t)W * maxLeaves * std::max(O.maxFaces, 1), stream);
     P.bodyAABBs = devAlloc<AABB>((size_t)W * maxLeaves, stream);
     P.survivors = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
+    P.survCount = devAlloc<int32_t>(W, stream);
+    P.satWork = devAlloc<SatWork>((size_t)W * P.candCapacity, stream);
+    P.satWorkCount = devAlloc<int32_t>(1, stream);
     P.candContacts = devAlloc<Contact>((size_t)W * P.candCapacity, stream);
     P.maxContacts = maxContacts;
     P.contactOrder = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
+    P.solverRecs = devAlloc<uint64_t>((size_t)W * P.candCapacity, stream);
     P.lastNumContacts = devAlloc<int32_t>(W, stream);
     P.lastNumCands = devAlloc<int32_t>(W, stream);
+
+    // Persistent SAT grid: exactly the blocks that can be resident at once.
+    int dev = 0, cus = 0, per_cu = 0;
+    MW_HIP_CHECK(hipGetDevice(&dev));
+    MW_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, narrowSATKernel, kNarrowBlock, narrowphaseSharedBytes(P)));
+    P.satGrid = std::max(1, cus * std::max(per_cu, 1));
     uploaded = true;
 }
 
@@ -370,8 +388,14 @@ MW_PHYS_NODE(SubstepRigidBodiesNode,
     if (P.numBodyArchs > 0)
         hipLaunchKernelGGL(integrateKernel, rowGrid(P), dim3(256), 0, stream, P);)
 
+// Narrowphase = AABB recheck + per-world survivor compaction (block per
+// world) feeding one device-wide work list, then a persistent SAT kernel
+// whose 16-lane groups drain that list.  The solver turns the per-survivor
+// manifolds into the ordered contact list.
 MW_PHYS_NODE(NarrowphaseNode,
-    hipLaunchKernelGGL(narrowphaseKernel, dim3(P.numWorlds), dim3(kNarrowBlock),
+    MW_HIP_CHECK(hipMemsetAsync(P.satWorkCount, 0, sizeof(int32_t), stream));
+    hipLaunchKernelGGL(narrowFilterKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
+    hipLaunchKernelGGL(narrowSATKernel, dim3(P.satGrid), dim3(kNarrowBlock),
                        narrowphaseSharedBytes(P), stream, P);)
 
 MW_PHYS_NODE(SolverNode,
@@ -461,6 +485,15 @@ void RigidBodyPhysicsSystem::init(Context &ctx, ObjectManager *obj_mgr, float de
                 m.polygons.insert(m.polygons.end(), he.mPolygons, he.mPolygons + he.mPolygonCount);
                 m.hedges.insert(m.hedges.end(), he.mHalfEdges, he.mHalfEdges + he.mHalfEdgeCount);
                 m.edges.insert(m.edges.end(), he.mEdges, he.mEdges + he.mEdgeCount);
+                if (he.mVertexCount > 65535 || he.mPolygonCount > 65535) {
+                    throw std::runtime_error("hull too large (edge topology is 16-bit)");
+                }
+                for (uint32_t e = 0; e < he.mEdgeCount; e++) {
+                    const geometry::HalfEdge &h = he.mHalfEdges[he.mEdges[e]];
+                    m.edgeQuads.push_back(EdgeQuad {
+                        (uint16_t)h.polygon, (uint16_t)he.mHalfEdges[h.twin].polygon,
+                        (uint16_t)h.rootVertex, (uint16_t)he.mHalfEdges[h.next].rootVertex });
+                }
             } else if (prim.type == CollisionPrimitive::Type::Sphere) {
                 throw std::runtime_error("sphere primitives are unsupported (the reference asserts, "
                                          "narrowphase.cpp:1197-1313)");

@@ -123,7 +123,8 @@ __global__ void bvhRebuildKernel(PhysArgs P);
 __global__ void refitKernel(PhysArgs P);
 __global__ void findOverlapsKernel(PhysArgs P);
 __global__ void integrateKernel(PhysArgs P);
-__global__ void narrowphaseKernel(PhysArgs P);
+__global__ void narrowFilterKernel(PhysArgs P);
+__global__ void narrowSATKernel(PhysArgs P);
 __global__ void solverKernel(PhysArgs P);
 
 size_t findOverlapsSharedBytes(const PhysArgs &P);

@@ -35,6 +35,13 @@ struct HullDev {
     int32_t numEdges;
 };
 
+// Per-edge topology of a hull, precomputed on the host from the half-edge
+// mesh (the operands queryEdgeDirections gathers, narrowphase.cpp:474-540):
+// the two faces sharing the edge and its two end vertices.
+struct EdgeQuad {
+    uint16_t face1, face2, v1, v2;
+};
+
 struct ObjDev {
     int32_t numObjects;
     int32_t maxVerts;
@@ -49,6 +56,7 @@ struct ObjDev {
     geometry::HalfEdge *hedges;
     uint32_t *edges;              // half-edge index per edge
     uint32_t *polygons;           // half-edge index per face
+    EdgeQuad *edgeQuads;          // per edge (same offsets as edges)
 };
 
 inline constexpr int32_t kMaxBodyArchetypes = 4;
@@ -60,6 +68,19 @@ struct BodyArch {
     int32_t *numRows;
     char *cols[13];               // Entity + Cols::Position..LeafID
 };
+
+// One narrowphase pair that passed the AABB recheck, fully resolved by the
+// filter kernel so the SAT kernel starts from a single load.
+struct SatWork {
+    int32_t world;
+    int32_t slot;                 // survivor slot (== contact slot) in the world
+    Loc a, b;                     // after runNarrowphase's type ordering
+    int32_t aLeaf, bLeaf;
+    int32_t aObj, bObj;
+    uint32_t test;                // type(a) | type(b)
+    int32_t pad;
+};
+static_assert(sizeof(SatWork) == 48);
 
 // Everything a physics kernel needs, passed by value (< 1 KB).
 struct PhysArgs {
@@ -93,9 +114,15 @@ struct PhysArgs {
 
     math::AABB *bodyAABBs;        // [W][maxLeaves] world AABB of each body (substep)
     int32_t *survivors;           // [W][candCapacity] candidates passing the AABB recheck
+    int32_t *survCount;           // [W] survivors per world
+    struct SatWork *satWork;      // [W * candCapacity] SAT work list (one per survivor)
+    int32_t *satWorkCount;        // [1] entries in satWork this substep
+    int32_t satGrid;              // persistent SAT grid (blocks)
     Contact *candContacts;        // [W][candCapacity] manifold per survivor slot
     int32_t maxContacts;          // SolverData::maxContacts (reference assert)
     int32_t *contactOrder;        // [W][candCapacity] scratch: ordered contact list
+    uint64_t *solverRecs;         // [W][candCapacity] solver contact records when K
+                                  // exceeds the LDS-resident budget
     int32_t *lastNumContacts;     // [W] debug: contacts of the last substep
     int32_t *lastNumCands;        // [W] debug: candidates of the last step
 

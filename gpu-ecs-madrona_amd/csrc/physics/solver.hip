@@ -230,21 +230,31 @@ __device__ __forceinline__ bool staticInvariant(const SBody &b)
            __float_as_uint(nq.z) == __float_as_uint(b.q.z);
 }
 
+// Per-contact solver record: body slots of ref / alt and the contact's
+// level (1 + max level of earlier contacts sharing a non-invariant body).
+struct CRec {
+    int16_t s1, s2, lvl, slot;   // slot: survivor slot holding the manifold
+};
+static_assert(sizeof(CRec) == 8);
+
+// Contacts whose records stay in LDS; worlds with more contacts keep them
+// in a global slab instead, so the LDS footprint (and with it the number of
+// worlds resident per CU) does not scale with SolverData::maxContacts.
+constexpr int32_t kSolverLDSContacts = 512;
+
 struct SolverLDS {
     SBody *bodies;        // [nb]
     int16_t *lastLevel;   // [nb]
-    int16_t *lvl;         // [maxContacts]
-    int16_t *slot1;       // [maxContacts]
-    int16_t *slot2;       // [maxContacts]
+    CRec *recs;           // [kSolverLDSContacts]
 };
 
-__host__ __device__ inline size_t solverLDSBytes(int32_t nb, int32_t max_contacts)
+__host__ __device__ inline size_t solverLDSBytes(int32_t nb)
 {
     auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-    return a16(sizeof(SBody) * nb) + a16(sizeof(int16_t) * nb) + 3 * a16(sizeof(int16_t) * max_contacts);
+    return a16(sizeof(SBody) * nb) + a16(sizeof(int16_t) * nb) + sizeof(CRec) * kSolverLDSContacts;
 }
 
-__device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb, int32_t max_contacts)
+__device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb)
 {
     auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
     SolverLDS L;
@@ -252,11 +262,7 @@ __device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb, int32_t m
     char *p = smem + a16(sizeof(SBody) * nb);
     L.lastLevel = (int16_t *)p;
     p += a16(sizeof(int16_t) * nb);
-    L.lvl = (int16_t *)p;
-    p += a16(sizeof(int16_t) * max_contacts);
-    L.slot1 = (int16_t *)p;
-    p += a16(sizeof(int16_t) * max_contacts);
-    L.slot2 = (int16_t *)p;
+    L.recs = (CRec *)p;
     return L;
 }
 
@@ -265,9 +271,9 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int32_t w = blockIdx.x;
     const int32_t nb = P.maxBodiesPerWorld;
-    SolverLDS L = solverLDS(smem, nb, P.maxContacts);
+    SolverLDS L = solverLDS(smem, nb);
     SBody *bodies = L.bodies;
-    __shared__ int32_t s_num_contacts, s_max_level, s_scan[kSolverBlock / 64];
+    __shared__ int32_t s_max_level;
 
     // 1. load bodies into LDS
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
@@ -300,46 +306,68 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
         }
     }
 
-    // 2. ordered contact list (built by the narrowphase kernel)
+    // 2. ordered contact list: survivors with a manifold, in survivor order
+    //    (== the reference's addManifoldToSolver append order,
+    //    narrowphase.cpp:1123-1162).  Pass 1 counts, pass 2 writes.
     const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
-    const int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
-    const int32_t K = P.solver[w].numContacts;
-    (void)s_scan;
-    for (int32_t k = threadIdx.x; k < K; k += kSolverBlock) {
-        const Contact &c = cslots[order[k]];
-        L.slot1[k] = (int16_t)bodySlot(P, c.ref);
-        L.slot2[k] = (int16_t)bodySlot(P, c.alt);
+    int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
+    const int32_t S = P.survCount[w];
+    const int32_t lane = threadIdx.x;
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    int32_t K = 0;
+    for (int32_t chunk = 0; chunk < S; chunk += kSolverBlock) {
+        const int32_t s = chunk + lane;
+        K += __popcll(__ballot(s < S && cslots[s].numPoints > 0));
+    }
+    if (K > P.maxContacts) {
+        // The reference asserts here (narrowphase.cpp:1130); flag, truncate.
+        if (lane == 0) atomicOr(P.errorFlags + w, kErrContactOverflow);
+        K = P.maxContacts;
+    }
+    CRec *recs = K <= kSolverLDSContacts ? L.recs : (CRec *)(P.solverRecs + (size_t)w * P.candCapacity);
+    int32_t k0 = 0;
+    for (int32_t chunk = 0; chunk < S && k0 < K; chunk += kSolverBlock) {
+        const int32_t s = chunk + lane;
+        const bool has = s < S && cslots[s].numPoints > 0;
+        const uint64_t mask = __ballot(has);
+        const int32_t k = k0 + __popcll(mask & lt_mask);
+        if (has && k < K) {
+            const Contact &c = cslots[s];
+            recs[k] = CRec { (int16_t)bodySlot(P, c.ref), (int16_t)bodySlot(P, c.alt), 0,
+                             (int16_t)s };
+            order[k] = s;
+        }
+        k0 += __popcll(mask);
     }
     __syncthreads();
 
-    // 3. levels (serial, one lane, LDS only)
+    // 3. levels (serial, one lane)
     if (threadIdx.x == 0) {
         int32_t max_level = 0;
         for (int32_t k = 0; k < K; k++) {
-            const int32_t s1 = L.slot1[k], s2 = L.slot2[k];
-            const int32_t l1 = L.lastLevel[s1], l2 = L.lastLevel[s2];
+            CRec r = recs[k];
+            const int32_t l1 = L.lastLevel[r.s1], l2 = L.lastLevel[r.s2];
             const int32_t l = max(max(l1, l2), 0) + 1;
-            L.lvl[k] = (int16_t)l;
-            if (l1 >= 0) L.lastLevel[s1] = (int16_t)l;
-            if (l2 >= 0) L.lastLevel[s2] = (int16_t)l;
+            r.lvl = (int16_t)l;
+            recs[k] = r;
+            if (l1 >= 0) L.lastLevel[r.s1] = (int16_t)l;
+            if (l2 >= 0) L.lastLevel[r.s2] = (int16_t)l;
             max_level = max(max_level, l);
         }
-        s_num_contacts = K;
         s_max_level = max_level;
         P.lastNumContacts[w] = K;
     }
     __syncthreads();
     const int32_t max_level = s_max_level;
     const SolverData &sd = P.solver[w];
-    int16_t *lvl = L.lvl;
-    (void)s_num_contacts;
 
     // 4. solvePositions, level by level
     for (int32_t l = 1; l <= max_level; l++) {
         for (int32_t k = threadIdx.x; k < K; k += kSolverBlock) {
-            if (lvl[k] != l) continue;
-            Contact &c = P.candContacts[(size_t)w * P.candCapacity + order[k]];
-            solveContactPositions(bodies[L.slot1[k]], bodies[L.slot2[k]], c);
+            const CRec r = recs[k];
+            if (r.lvl != l) continue;
+            Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
+            solveContactPositions(bodies[r.s1], bodies[r.s2], c);
         }
         __syncthreads();
     }
@@ -368,10 +396,10 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
     // 6. solveVelocities, same levels
     for (int32_t l = 1; l <= max_level; l++) {
         for (int32_t k = threadIdx.x; k < K; k += kSolverBlock) {
-            if (lvl[k] != l) continue;
-            const Contact &c = P.candContacts[(size_t)w * P.candCapacity + order[k]];
-            solveContactVelocities(bodies[L.slot1[k]], bodies[L.slot2[k]], c, h,
-                                   sd.restitutionThreshold);
+            const CRec r = recs[k];
+            if (r.lvl != l) continue;
+            const Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
+            solveContactVelocities(bodies[r.s1], bodies[r.s2], c, h, sd.restitutionThreshold);
         }
         __syncthreads();
     }
@@ -392,7 +420,7 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
 
 size_t solverSharedBytes(const PhysArgs &P)
 {
-    return solverLDSBytes(P.maxBodiesPerWorld, P.maxContacts);
+    return solverLDSBytes(P.maxBodiesPerWorld);
 }
 
 }

@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "build", "libmadrona_mw.so")
+LIB_PATH = os.environ.get("MADRONA_MW_LIB") or os.path.join(os.path.dirname(PKG_DIR), "build", "libmadrona_mw.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
