@@ -179,7 +179,9 @@ def main():
     W = args.worlds
     cfg = mw.default_collisions_config(args.cubes, args.substeps, max_contacts=4096,
                                        max_candidates=4096)
-    pos, rot = mw.gen_collisions_inits(W, args.cubes, seed=0, first_world=rank * W)
+    from madrona_mi355x.sharding import gather_world_returns, world_shard
+    first_world, W = world_shard(rank, W)
+    pos, rot = mw.gen_collisions_inits(W, args.cubes, seed=0, first_world=first_world)
     sim = mw.CollisionsSim(W, pos, rot, cfg, gpu_id=local_rank)
     del pos, rot
 
@@ -193,7 +195,7 @@ def main():
             return
         sim.copy_exported(2, returns.data_ptr(), W * 4)
         if dist is not None:
-            dist.all_gather_into_tensor(gathered, returns)
+            gather_world_returns(returns, out=gathered)
 
     if args.settle:
         sim.step(args.settle)

@@ -96,7 +96,7 @@ def gen_collisions_inits(num_worlds, num_cubes=128, seed=0, first_world=0):
     return pos, rot
 
 ERR_BITS = {1: "id store full", 2: "table full", 4: "candidate overflow",
-            8: "contact overflow", 16: "BVH stack overflow"}
+            8: "contact overflow", 16: "BVH stack overflow", 32: "solver body overflow"}
 
 
 class MadronaError(RuntimeError):
