@@ -8,7 +8,8 @@ dt=1/60) on MI355X.
 A "step" = one taskgraph step of every world (broadphase, 4 XPBD substeps of
 integrate / narrowphase / solve, cleanup, episode-return node) replayed as one
 hipGraph, followed by the training hand-off: the per-world episode returns are
-copied into a torch tensor and, for N > 1, all-gathered over RCCL (xGMI).
+copied into a device buffer and, for N > 1, all-gathered over RCCL (xGMI) by
+the framework on its step stream.
 Worlds are sharded contiguously across ranks (weak scaling: 8192 per GPU;
 N = 8 is BASELINE.json configs[3], 65 536 worlds).
 
@@ -167,35 +168,44 @@ def main():
     if world_size != args.gpus and world_size > 1:
         print(f"warning: WORLD_SIZE={world_size} != --gpus {args.gpus}", file=sys.stderr)
 
-    import torch
-    torch.cuda.set_device(local_rank)
+    # The framework owns the GPU in this process: device memory, the step
+    # stream, and the hand-off collective (RCCL over xGMI from the C ABI).
+    # torch is used on the CPU only (gloo rendezvous, barrier, max-reduce):
+    # initialising torch's own HIP context next to the framework's mixes two
+    # HIP runtime builds in one process (madrona_mi355x/__init__.py).
+    import madrona_mi355x as mw
+    from madrona_mi355x.sharding import bootstrap_rccl, world_shard
     dist = None
     if world_size > 1:
         import torch.distributed as dist
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group(backend="gloo")
 
-    import madrona_mi355x as mw
-
-    W = args.worlds
     cfg = mw.default_collisions_config(args.cubes, args.substeps, max_contacts=4096,
                                        max_candidates=4096)
-    from madrona_mi355x.sharding import gather_world_returns, world_shard
-    first_world, W = world_shard(rank, W)
+    first_world, W = world_shard(rank, args.worlds)
     pos, rot = mw.gen_collisions_inits(W, args.cubes, seed=0, first_world=first_world)
     sim = mw.CollisionsSim(W, pos, rot, cfg, gpu_id=local_rank)
     del pos, rot
 
-    returns = torch.empty(W, dtype=torch.float32, device="cuda")
-    gathered = (torch.empty(W * world_size, dtype=torch.float32, device="cuda")
-                if world_size > 1 else None)
+    if dist is not None:
+        bootstrap_rccl(sim, rank, world_size)
+    # per-world returns of every rank, in world order (device memory)
+    handoff = sim.device_alloc(4 * W * world_size)
 
     def step():
-        sim.step(1)
         if args.no_handoff:
+            sim.step(1)
             return
-        sim.copy_exported(2, returns.data_ptr(), W * 4)
+        sim.step_async(1)
         if dist is not None:
-            gather_world_returns(returns, out=gathered)
+            sim.allgather_exported(2, handoff, 4 * W)
+            sim.sync()
+        else:
+            sim.copy_exported(2, handoff, 4 * W)     # D2D on the step stream + sync
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
 
     if args.settle:
         sim.step(args.settle)
@@ -222,18 +232,19 @@ def main():
         step()
     ev_ms0, ev_n0 = sim.timed_node() if dom else (0.0, 0)
 
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
+    # timed region: barrier + device sync on both sides (the framework's
+    # stream is the only GPU work in this process), max over ranks
+    barrier()
+    sim.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
+    sim.sync()
+    barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -290,7 +301,7 @@ def main():
                 "timed_steps": f"{args.settle + args.warmup + 1}-{args.settle + args.warmup + args.steps}",
                 "parallelism": f"world-sharded x{world_size}" +
                                ("" if args.no_handoff else ", per-step return hand-off"
-                                + (" (RCCL all-gather)" if world_size > 1 else "")),
+                                + (" (RCCL all-gather over xGMI)" if world_size > 1 else "")),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -298,9 +309,10 @@ def main():
             "nodes": node_table,
         }
         print(json.dumps(out))
+    sim.device_free(handoff)
+    sim.close()
     if dist is not None:
         dist.destroy_process_group()
-    sim.close()
 
 
 if __name__ == "__main__":

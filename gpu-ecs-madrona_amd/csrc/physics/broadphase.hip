@@ -29,7 +29,8 @@ __global__ void __launch_bounds__(256) leafUpdateKernel(PhysArgs P)
     RowIdx ri = rowIndex(P, B);
     if (!ri.valid) return;
     const int32_t w = ri.w, r = ri.r;
-    const int32_t leaf = bcol<broadphase::LeafID>(B, Cols::LeafID, w, r).id;
+    const int32_t leaf = guardIndex(bcol<broadphase::LeafID>(B, Cols::LeafID, w, r).id,
+                                    P.maxLeaves, P.errorFlags + w, kGuardLeaf);
     const Vector3 pos = bcol<Vector3>(B, Cols::Position, w, r);
     const Quat rot = bcol<Quat>(B, Cols::Rotation, w, r);
     const Diag3x3 scale = bcol<Diag3x3>(B, Cols::Scale, w, r);
@@ -171,12 +172,13 @@ __global__ void __launch_bounds__(256) refitKernel(PhysArgs P)
     RowIdx ri = rowIndex(P, B);
     if (!ri.valid) return;
     const int32_t w = ri.w;
-    const int32_t leaf = bcol<broadphase::LeafID>(B, Cols::LeafID, w, ri.r).id;
+    const int32_t leaf = guardIndex(bcol<broadphase::LeafID>(B, Cols::LeafID, w, ri.r).id,
+                                    P.maxLeaves, P.errorFlags + w, kGuardLeaf);
     const size_t li = (size_t)w * P.maxLeaves + leaf;
     const AABB a = P.leafAABBs[li];
     const uint32_t lp = P.leafParents[li];
     BVHNode *nodes = P.nodes + (size_t)w * P.maxNodes;
-    int32_t node_idx = (int32_t)(lp >> 2);
+    int32_t node_idx = guardIndex((int32_t)(lp >> 2), P.maxNodes, P.errorFlags + w, kGuardNode);
     const int sub = (int)(lp & 3);
 
     {   // leaf slot: owned by this leaf alone -> plain read-modify-write
@@ -196,6 +198,10 @@ __global__ void __launch_bounds__(256) refitKernel(PhysArgs P)
     int32_t child_idx = node_idx;
     node_idx = nodes[node_idx].parentID;
     while (node_idx != -1) {
+        if ((uint32_t)node_idx >= (uint32_t)P.maxNodes) {
+            atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardNode << 8));
+            return;
+        }
         BVHNode &n = nodes[node_idx];
         int c = -1;
         for (int j = 0; j < 4; j++) {
@@ -221,39 +227,53 @@ __global__ void __launch_bounds__(256) refitKernel(PhysArgs P)
 // each row's candidates, a block scan gives the reference's append order,
 // pass 2 writes them.
 
-constexpr int32_t kOverlapStack = 32;
+constexpr int32_t kOverlapStack = 24;   // int16 entries; 4-wide tree depth <= 7 at 4096 leaves
+constexpr int32_t kOverlapBuf = 12;     // candidates kept per body before a re-walk
 
-// LDS image of one world's BVH plus per-leaf (entity id, Loc, static flag),
-// so the traversal's dependent loads hit LDS instead of L2 / MALL.
+// LDS image of one world's BVH (nodes padded to 128 B so a node is eight
+// 16-byte LDS reads) plus per-leaf (entity id, Loc, static flag), per-lane
+// traversal stacks and per-lane candidate buffers.
+struct alignas(16) LNode {
+    float minX[4], minY[4], minZ[4];
+    float maxX[4], maxY[4], maxZ[4];
+    int32_t children[4];
+    int32_t pad[4];
+};
+static_assert(sizeof(LNode) == 128);
+
 struct OverlapLDS {
-    BVHNode *nodes;
+    LNode *nodes;
     int32_t *leafId;
     Loc *leafLoc;
-    int32_t *leafStatic;
-    int32_t *stacks;
+    int8_t *leafStatic;
+    int16_t *stacks;
+    uint16_t *bufs;
 };
+
+__host__ __device__ inline size_t a16b(size_t b) { return (b + 15) & ~size_t(15); }
 
 __host__ __device__ inline size_t overlapLDSBytes(int32_t max_nodes, int32_t max_leaves)
 {
-    auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-    return a16(sizeof(BVHNode) * max_nodes) + a16(4 * max_leaves) + a16(8 * max_leaves) +
-           a16(4 * max_leaves) + (size_t)4 * kOverlapBlock * kOverlapStack;
+    return a16b(sizeof(LNode) * max_nodes) + a16b(4 * max_leaves) + a16b(8 * max_leaves) +
+           a16b(max_leaves) + a16b(2 * kOverlapBlock * kOverlapStack) +
+           a16b(2 * kOverlapBlock * kOverlapBuf);
 }
 
 __device__ __forceinline__ OverlapLDS overlapLDS(char *smem, int32_t max_nodes, int32_t max_leaves)
 {
-    auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
     OverlapLDS L;
     char *p = smem;
-    L.nodes = (BVHNode *)p;
-    p += a16(sizeof(BVHNode) * max_nodes);
+    L.nodes = (LNode *)p;
+    p += a16b(sizeof(LNode) * max_nodes);
     L.leafId = (int32_t *)p;
-    p += a16(4 * max_leaves);
+    p += a16b(4 * max_leaves);
     L.leafLoc = (Loc *)p;
-    p += a16(8 * max_leaves);
-    L.leafStatic = (int32_t *)p;
-    p += a16(4 * max_leaves);
-    L.stacks = (int32_t *)p;
+    p += a16b(8 * max_leaves);
+    L.leafStatic = (int8_t *)p;
+    p += a16b(max_leaves);
+    L.stacks = (int16_t *)p;
+    p += a16b(2 * kOverlapBlock * kOverlapStack);
+    L.bufs = (uint16_t *)p;
     return L;
 }
 
@@ -262,12 +282,15 @@ size_t findOverlapsSharedBytes(const PhysArgs &P)
     return overlapLDSBytes(P.maxNodes, P.maxLeaves);
 }
 
+// BVH::findOverlaps for one body (physics.inl:61-100): DFS with the
+// reference's push order; a hit is a leaf whose entity id is larger than the
+// body's and that is not static-static.  kWrite = false: count hits and keep
+// the first kOverlapBuf other-leaf indices; kWrite = true: write every hit.
 template <bool kWrite>
 __device__ __forceinline__ int32_t traverseOverlaps(const PhysArgs &P, const OverlapLDS &L,
-                                                    int32_t w, const BodyArch &B, int32_t row,
-                                                    int32_t *stack, int32_t out_base)
+                                                    int32_t w, int32_t leaf, int16_t *stack,
+                                                    uint16_t *buf, int32_t out_base)
 {
-    const int32_t leaf = bcol<broadphase::LeafID>(B, Cols::LeafID, w, row).id;
     const int32_t e_id = L.leafId[leaf];
     const Loc a_loc = L.leafLoc[leaf];
     const bool a_static = L.leafStatic[leaf] != 0;
@@ -277,7 +300,7 @@ __device__ __forceinline__ int32_t traverseOverlaps(const PhysArgs &P, const Ove
     stack[0] = 0;
     int32_t ss = 1;
     while (ss > 0) {
-        const BVHNode &n = L.nodes[stack[--ss]];
+        const LNode &n = L.nodes[stack[--ss]];
         for (int i = 0; i < 4; i++) {
             const int32_t child = n.children[i];
             if (child == -1) continue;
@@ -288,17 +311,19 @@ __device__ __forceinline__ int32_t traverseOverlaps(const PhysArgs &P, const Ove
                 if (e_id < L.leafId[ol]) {
                     if (a_static && L.leafStatic[ol]) continue;
                     if (kWrite) {
-                        int32_t slot = out_base + count;
+                        const int32_t slot = out_base + count;
                         if (slot < P.candCapacity) {
                             P.cands[(size_t)w * P.candCapacity + slot] =
                                 CandidateCollision { a_loc, L.leafLoc[ol] };
                         }
+                    } else if (count < kOverlapBuf) {
+                        buf[count] = (uint16_t)ol;
                     }
                     count++;
                 }
             } else {
                 if (ss < kOverlapStack) {
-                    stack[ss++] = child;
+                    stack[ss++] = (int16_t)child;
                 } else {
                     atomicOr(P.errorFlags + w, kErrBVHStack);
                 }
@@ -308,6 +333,10 @@ __device__ __forceinline__ int32_t traverseOverlaps(const PhysArgs &P, const Ove
     return count;
 }
 
+// findOverlappingEntry (broadphase.cpp:897-932): one block per world, lanes
+// own body rows.  One walk per body fills a small LDS buffer; a block scan of
+// the counts gives the reference's append order (row order, DFS order within
+// a row); bodies with more hits than the buffer holds walk again to write.
 __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -315,12 +344,15 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
     const int32_t w = blockIdx.x;
     OverlapLDS L = overlapLDS(smem, P.maxNodes, P.maxLeaves);
 
-    // stage nodes (29 dwords each) and leaf info
+    // stage nodes (29 dwords each -> 32-dword LDS slots) and leaf info
     const broadphase::BVH &bvh = P.bvh[w];
-    const int32_t used = bvh.usedNodes;
+    const int32_t used = min(bvh.usedNodes, P.maxNodes);
     const uint32_t *gnodes = (const uint32_t *)(P.nodes + (size_t)w * P.maxNodes);
     uint32_t *lnodes = (uint32_t *)L.nodes;
-    for (int32_t i = threadIdx.x; i < used * 29; i += kOverlapBlock) lnodes[i] = gnodes[i];
+    for (int32_t i = threadIdx.x; i < used * 32; i += kOverlapBlock) {
+        const int32_t node = i >> 5, d = i & 31;
+        lnodes[i] = d < 29 ? gnodes[node * 29 + d] : 0u;
+    }
     const int32_t nleaves = bvh.numLeaves;
     for (int32_t l = threadIdx.x; l < nleaves; l += kOverlapBlock) {
         const Entity e = P.leafEntities[(size_t)w * P.maxLeaves + l];
@@ -328,23 +360,38 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
         L.leafId[l] = e.id;
         L.leafLoc[l] = loc;
         const BodyArch &OB = P.body[bodyArchIndex(P, loc.archetype)];
+        const int32_t row = guardIndex(loc.row, OB.capacity, P.errorFlags + w, kGuardLeaf);
         L.leafStatic[l] =
-            bcol<ResponseType>(OB, Cols::ResponseType, w, loc.row) == ResponseType::Static ? 1 : 0;
+            bcol<ResponseType>(OB, Cols::ResponseType, w, row) == ResponseType::Static ? 1 : 0;
     }
     __syncthreads();
 
-    int32_t *stack = L.stacks + threadIdx.x * kOverlapStack;
+    int16_t *stack = L.stacks + threadIdx.x * kOverlapStack;
+    uint16_t *buf = L.bufs + threadIdx.x * kOverlapBuf;
     int32_t base = 0;
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
         for (int32_t chunk = 0; chunk < rows; chunk += kOverlapBlock) {
             const int32_t row = chunk + threadIdx.x;
-            int32_t cnt = 0;
-            if (row < rows) cnt = traverseOverlaps<false>(P, L, w, B, row, stack, 0);
+            int32_t cnt = 0, leaf = 0;
+            if (row < rows) {
+                leaf = guardIndex(bcol<broadphase::LeafID>(B, Cols::LeafID, w, row).id,
+                                  P.maxLeaves, P.errorFlags + w, kGuardLeaf);
+                cnt = traverseOverlaps<false>(P, L, w, leaf, stack, buf, 0);
+            }
             int32_t total;
-            int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
-            if (row < rows && cnt > 0) traverseOverlaps<true>(P, L, w, B, row, stack, base + off);
+            const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
+            if (cnt > kOverlapBuf) {
+                traverseOverlaps<true>(P, L, w, leaf, stack, buf, base + off);
+            } else if (cnt > 0) {
+                const Loc a_loc = L.leafLoc[leaf];
+                CandidateCollision *out = P.cands + (size_t)w * P.candCapacity;
+                for (int32_t i = 0; i < cnt; i++) {
+                    const int32_t slot = base + off + i;
+                    if (slot < P.candCapacity) out[slot] = CandidateCollision { a_loc, L.leafLoc[buf[i]] };
+                }
+            }
             base += total;
         }
     }

@@ -7,8 +7,8 @@
 namespace madrona::phys {
 
 // ===========================================================================
-// Substep integration (physics.cpp:79-164) fused with the world-space hull
-// transform the narrowphase needs (narrowphase.cpp:139-212, CPU branch).
+// Substep integration (physics.cpp:79-164) plus the world AABB of every body
+// for the narrowphase's recheck.
 // ===========================================================================
 
 __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
@@ -73,29 +73,11 @@ __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
         ps_vel.omega = omega;
     }
 
+    // World AABB the narrowphase recheck uses (narrowphase.cpp:1590-1594),
+    // indexed by body slot so the filter reaches it straight from a Loc.
     const Diag3x3 scale = bcol<Diag3x3>(B, Cols::Scale, w, r);
-    const int32_t leaf = bcol<broadphase::LeafID>(B, Cols::LeafID, w, r).id;
-    // World AABB the narrowphase recheck uses (narrowphase.cpp:1590-1594).
-    P.bodyAABBs[(size_t)w * P.maxLeaves + leaf] = P.objs.aabbs[obj].applyTRS(x, q, scale);
-
-    // World-space hull for this body (makeHullState with dst buffers).
-    if (P.objs.types[obj] == (uint32_t)CollisionPrimitive::Type::Hull) {
-        const HullDev hd = P.objs.hulls[obj];
-        Mat3x3 unscaled_rot = Mat3x3::fromQuat(q);
-        Mat3x3 vertex_txfm = unscaled_rot * scale;
-        Mat3x3 normal_txfm = unscaled_rot * scale.inv();
-        Vector3 *dv = P.hullVerts + ((size_t)w * P.maxLeaves + leaf) * P.objs.maxVerts;
-        geometry::Plane *dp = P.hullPlanes + ((size_t)w * P.maxLeaves + leaf) * P.objs.maxFaces;
-        for (int32_t i = 0; i < hd.numVerts; i++) {
-            dv[i] = vertex_txfm * P.objs.vertices[hd.vertOffset + i] + x;
-        }
-        for (int32_t i = 0; i < hd.numFaces; i++) {
-            geometry::Plane op = P.objs.planes[hd.faceOffset + i];
-            Vector3 origin = vertex_txfm * (op.normal * op.d) + x;
-            Vector3 n = (normal_txfm * op.normal).normalize();
-            dp[i] = geometry::Plane { n, dot(n, origin) };
-        }
-    }
+    P.bodyAABBs[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r] =
+        P.objs.aabbs[obj].applyTRS(x, q, scale);
 }
 
 // ===========================================================================
@@ -191,21 +173,35 @@ __device__ __forceinline__ void groupArgMax(float &v, int32_t &k)
     }
 }
 
-// Copy one body's world-space hull (written by the integrate kernel) and its
-// edge topology into the group's LDS.
-__device__ __forceinline__ void stageHull(const PhysArgs &P, int32_t w, int32_t leaf,
-                                          const HullDev &hd, Vector3 *v, geometry::Plane *pl,
-                                          EdgeQuad *q, int32_t lane)
+// Transform one body's hull to world space straight into the group's LDS
+// (makeHullState, narrowphase.cpp:139-212: vertex_txfm = R * S, normals by
+// R * S^-1, renormalised) and copy its edge topology.  Returns the body
+// position (the hull's center for the edge query).
+__device__ __forceinline__ Vector3 stageHull(const PhysArgs &P, int32_t w, const BodyArch &B,
+                                             int32_t row, const HullDev &hd, Vector3 *v,
+                                             geometry::Plane *pl, EdgeQuad *q, int32_t lane)
 {
-    const size_t body = (size_t)w * P.maxLeaves + leaf;
-    const float *gv = (const float *)(P.hullVerts + body * P.objs.maxVerts);
-    float *lv = (float *)v;
-    for (int32_t i = lane; i < hd.numVerts * 3; i += kGroup) lv[i] = gv[i];
-    const float4 *gp = (const float4 *)(P.hullPlanes + body * P.objs.maxFaces);
-    float4 *lp = (float4 *)pl;
-    for (int32_t i = lane; i < hd.numFaces; i += kGroup) lp[i] = gp[i];
-    const EdgeQuad *gq = P.objs.edgeQuads + hd.edgeOffset;
+    const ObjDev &O = P.objs;
+    const Vector3 x = bcol<Vector3>(B, Cols::Position, w, row);
+    const Quat rot = bcol<Quat>(B, Cols::Rotation, w, row);
+    const Diag3x3 scale = bcol<Diag3x3>(B, Cols::Scale, w, row);
+    const Mat3x3 unscaled_rot = Mat3x3::fromQuat(rot);
+    const Mat3x3 vertex_txfm = unscaled_rot * scale;
+    for (int32_t i = lane; i < hd.numVerts; i += kGroup) {
+        v[i] = vertex_txfm * O.vertices[hd.vertOffset + i] + x;
+    }
+    if (lane < hd.numFaces) {
+        const Mat3x3 normal_txfm = unscaled_rot * scale.inv();
+        for (int32_t i = lane; i < hd.numFaces; i += kGroup) {
+            const geometry::Plane op = O.planes[hd.faceOffset + i];
+            const Vector3 origin = vertex_txfm * (op.normal * op.d) + x;
+            const Vector3 n = (normal_txfm * op.normal).normalize();
+            pl[i] = geometry::Plane { n, dot(n, origin) };
+        }
+    }
+    const EdgeQuad *gq = O.edgeQuads + hd.edgeOffset;
     for (int32_t i = lane; i < hd.numEdges; i += kGroup) q[i] = gq[i];
+    return x;
 }
 
 __device__ __forceinline__ float distFromPlane(const geometry::Plane &p, const Vector3 &a)
@@ -454,12 +450,18 @@ __device__ __forceinline__ geometry::Segment shortestSegmentBetween(const geomet
 __device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
                                             const CandidateCollision &cand, SatWork &out)
 {
-    const BodyArch &BA = P.body[bodyArchIndex(P, cand.a.archetype)];
-    const BodyArch &BB = P.body[bodyArchIndex(P, cand.b.archetype)];
-    const int32_t la = bcol<broadphase::LeafID>(BA, Cols::LeafID, w, cand.a.row).id;
-    const int32_t lb = bcol<broadphase::LeafID>(BB, Cols::LeafID, w, cand.b.row).id;
-    const AABB a = P.bodyAABBs[(size_t)w * P.maxLeaves + la];
-    const AABB b = P.bodyAABBs[(size_t)w * P.maxLeaves + lb];
+    const int32_t ia = bodyArchIndex(P, cand.a.archetype);
+    const int32_t ib = bodyArchIndex(P, cand.b.archetype);
+    const BodyArch &BA = P.body[ia];
+    const BodyArch &BB = P.body[ib];
+    if ((uint32_t)cand.a.row >= (uint32_t)BA.capacity ||
+        (uint32_t)cand.b.row >= (uint32_t)BB.capacity) {
+        atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardWork << 8));
+        return false;
+    }
+    const AABB *aabbs = P.bodyAABBs + (size_t)w * P.maxBodiesPerWorld;
+    const AABB a = aabbs[BA.slotBase + cand.a.row];
+    const AABB b = aabbs[BB.slotBase + cand.b.row];
     if (!a.overlaps(b)) return false;
     const int32_t oa = bcol<ObjectID>(BA, Cols::ObjectID, w, cand.a.row).idx;
     const int32_t ob = bcol<ObjectID>(BB, Cols::ObjectID, w, cand.b.row).idx;
@@ -469,11 +471,11 @@ __device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
     out.pad = 0;
     if (ta > tb) {
         out.a = cand.b; out.b = cand.a;
-        out.aLeaf = lb; out.bLeaf = la;
+        out.aArch = ib; out.bArch = ia;
         out.aObj = ob; out.bObj = oa;
     } else {
         out.a = cand.a; out.b = cand.b;
-        out.aLeaf = la; out.bLeaf = lb;
+        out.aArch = ia; out.bArch = ib;
         out.aObj = oa; out.bObj = ob;
     }
     return true;
@@ -492,11 +494,8 @@ __device__ void hullHullPair(const PhysArgs &P, const SatWork &wk, const GroupLD
     hb.hd = O.hulls[wk.bObj];
     ha.verts = g.vA; ha.planes = g.pA; ha.quads = g.qA;
     hb.verts = g.vB; hb.planes = g.pB; hb.quads = g.qB;
-    const BodyArch &BA = P.body[bodyArchIndex(P, wk.a.archetype)];
-    ha.center = bcol<Vector3>(BA, Cols::Position, w, wk.a.row);
-    hb.center = Vector3::zero();            // unused by the hull-hull path
-    stageHull(P, w, wk.aLeaf, ha.hd, g.vA, g.pA, g.qA, lane);
-    stageHull(P, w, wk.bLeaf, hb.hd, g.vB, g.pB, g.qB, lane);
+    ha.center = stageHull(P, w, P.body[wk.aArch], wk.a.row, ha.hd, g.vA, g.pA, g.qA, lane);
+    hb.center = stageHull(P, w, P.body[wk.bArch], wk.b.row, hb.hd, g.vB, g.pB, g.qB, lane);
     groupSync();
 
     const FaceQuery fa = groupFaceQuery(ha, hb, lane);
@@ -513,36 +512,47 @@ __device__ void hullHullPair(const PhysArgs &P, const SatWork &wk, const GroupLD
         const int32_t ref_face = a_is_ref ? fa.faceIdx : fb.faceIdx;
         const HullRef &ref = a_is_ref ? ha : hb;
         const HullRef &inc = a_is_ref ? hb : ha;
-        const int32_t inc_face = findIncidentFace(inc, ref_plane.normal);
+        int32_t *flags = P.errorFlags + w;
+        const int32_t inc_face = guardIndex(findIncidentFace(inc, ref_plane.normal),
+                                            inc.hd.numFaces, flags, kGuardIncFace);
+        const int32_t ref_face_g = guardIndex(ref_face, ref.hd.numFaces, flags, kGuardRefFace);
 
         const geometry::HalfEdge *rh = O.hedges + ref.hd.hedgeOffset;
         const geometry::HalfEdge *oh = O.hedges + inc.hd.hedgeOffset;
         int32_t n_in = 0;
         {
             uint32_t hidx = O.polygons[inc.hd.faceOffset + inc_face], start = hidx;
+            int32_t steps = 0;
             do {
+                hidx = guardIndex(hidx, inc.hd.numHedges, flags, kGuardIncWalk);
                 const geometry::HalfEdge he = oh[hidx];
                 hidx = he.next;
-                if (n_in < kMaxClip) g.clip0[n_in++] = inc.verts[he.rootVertex];
-            } while (hidx != start);
+                if (n_in < kMaxClip)
+                    g.clip0[n_in++] = inc.verts[guardIndex(he.rootVertex, inc.hd.numVerts, flags,
+                                                           kGuardVertex)];
+            } while (hidx != start && ++steps <= inc.hd.numHedges);
         }
         Vector3 *cin = g.clip0, *cdst = g.clip1;
         int32_t n_clip = n_in;
         {
-            uint32_t hidx = O.polygons[ref.hd.faceOffset + ref_face], start = hidx;
+            uint32_t hidx = O.polygons[ref.hd.faceOffset + ref_face_g], start = hidx;
+            hidx = guardIndex(hidx, ref.hd.numHedges, flags, kGuardRefWalk);
             geometry::HalfEdge che = rh[hidx];
-            Vector3 cur = ref.verts[che.rootVertex];
+            Vector3 cur = ref.verts[guardIndex(che.rootVertex, ref.hd.numVerts, flags,
+                                               kGuardVertex)];
+            int32_t steps = 0;
             do {
-                hidx = che.next;
+                hidx = guardIndex(che.next, ref.hd.numHedges, flags, kGuardRefWalk);
                 che = rh[hidx];
-                Vector3 next = ref.verts[che.rootVertex];
+                Vector3 next = ref.verts[guardIndex(che.rootVertex, ref.hd.numVerts, flags,
+                                                    kGuardVertex)];
                 Vector3 edge = next - cur;
                 Vector3 pn = cross(edge, ref_plane.normal);
                 float d = dot(pn, cur);
                 cur = next;
                 n_clip = clipPolygon(cdst, geometry::Plane { pn, d }, cin, n_clip);
                 Vector3 *t = cdst; cdst = cin; cin = t;
-            } while (hidx != start);
+            } while (hidx != start && ++steps <= ref.hd.numHedges);
         }
         int32_t n_below = 0;
         for (int32_t i = 0; i < n_clip; i++) {
@@ -583,32 +593,35 @@ __device__ void hullPlanePair(const PhysArgs &P, const SatWork &wk, const GroupL
     HullRef ha;
     ha.hd = O.hulls[wk.aObj];
     ha.verts = g.vA; ha.planes = g.pA; ha.quads = g.qA;
-    ha.center = Vector3::zero();
-    stageHull(P, w, wk.aLeaf, ha.hd, g.vA, g.pA, g.qA, lane);
+    ha.center = stageHull(P, w, P.body[wk.aArch], wk.a.row, ha.hd, g.vA, g.pA, g.qA, lane);
     groupSync();
     if (lane != 0) return;
-    const BodyArch &BB = P.body[bodyArchIndex(P, wk.b.archetype)];
+    const BodyArch &BB = P.body[wk.bArch];
     const Vector3 b_pos = bcol<Vector3>(BB, Cols::Position, w, wk.b.row);
     const Quat b_rot = bcol<Quat>(BB, Cols::Rotation, w, wk.b.row);
     Vector3 pn = b_rot.rotateVec(Vector3 { 0, 0, 1 });
     geometry::Plane plane { pn, dot(pn, b_pos) };
     float sep = hullDistFromPlane(plane, ha);
     if (sep > 0.0f) return;
-    int32_t inc_face = findIncidentFace(ha, plane.normal);
+    int32_t *flags = P.errorFlags + w;
+    const int32_t inc_face = guardIndex(findIncidentFace(ha, plane.normal), ha.hd.numFaces,
+                                        flags, kGuardPlaneFace);
     const geometry::HalfEdge *hh = O.hedges + ha.hd.hedgeOffset;
     int32_t n = 0;
     uint32_t hidx = O.polygons[ha.hd.faceOffset + inc_face], start = hidx;
+    int32_t steps = 0;
     do {
+        hidx = guardIndex(hidx, ha.hd.numHedges, flags, kGuardPlaneWalk);
         const geometry::HalfEdge he = hh[hidx];
         hidx = he.next;
-        Vector3 v = ha.verts[he.rootVertex];
+        Vector3 v = ha.verts[guardIndex(he.rootVertex, ha.hd.numVerts, flags, kGuardVertex)];
         float d = distFromPlane(plane, v);
         if (d < 0.0f && n < kMaxClip) {
             g.clip0[n] = v - d * plane.normal;
             g.depths[n] = -d;
             n++;
         }
-    } while (hidx != start);
+    } while (hidx != start && ++steps <= ha.hd.numHedges);
     storeFaceManifold(out, plane.normal, g.clip0, g.depths, n, wk.b, wk.a);
 }
 
@@ -656,7 +669,18 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowSATKernel(PhysArgs P)
     const int32_t total = *(volatile int32_t *)P.satWorkCount;
     const int32_t stride = gridDim.x * kGroupsPerBlock;
     for (int32_t idx = blockIdx.x * kGroupsPerBlock + group; idx < total; idx += stride) {
-        const SatWork wk = P.satWork[idx];
+        SatWork wk = P.satWork[idx];
+        if ((uint32_t)wk.world >= (uint32_t)P.numWorlds ||
+            (uint32_t)wk.slot >= (uint32_t)P.candCapacity ||
+            (uint32_t)wk.aObj >= (uint32_t)P.objs.numObjects ||
+            (uint32_t)wk.bObj >= (uint32_t)P.objs.numObjects ||
+            (uint32_t)wk.aArch >= (uint32_t)P.numBodyArchs ||
+            (uint32_t)wk.bArch >= (uint32_t)P.numBodyArchs ||
+            (uint32_t)wk.a.row >= (uint32_t)P.body[wk.aArch].capacity ||
+            (uint32_t)wk.b.row >= (uint32_t)P.body[wk.bArch].capacity) {
+            if (lane == 0) atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
+            continue;
+        }
         Contact &out = P.candContacts[(size_t)wk.world * P.candCapacity + wk.slot];
         if (lane == 0) out.numPoints = 0;
         if (wk.test == (uint32_t)CollisionPrimitive::Type::Hull) {

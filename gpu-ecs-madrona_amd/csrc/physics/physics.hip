@@ -311,9 +311,7 @@ void PhysicsModule::upload(void *stream_ptr)
     O.edgeQuads = devUpload(edgeQuads, stream);
     O.polygons = devUpload(polygons, stream);
 
-    P.hullVerts = devAlloc<Vector3>((size_t)W * maxLeaves * std::max(O.maxVerts, 1), stream);
-    P.hullPlanes = devAlloc<geometry::Plane>((size_t)W * maxLeaves * std::max(O.maxFaces, 1), stream);
-    P.bodyAABBs = devAlloc<AABB>((size_t)W * maxLeaves, stream);
+    P.bodyAABBs = devAlloc<AABB>((size_t)W * std::max(P.maxBodiesPerWorld, 1), stream);
     P.survivors = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
     P.survCount = devAlloc<int32_t>(W, stream);
     P.satWork = devAlloc<SatWork>((size_t)W * P.candCapacity, stream);

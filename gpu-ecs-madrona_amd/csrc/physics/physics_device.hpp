@@ -34,9 +34,26 @@ __device__ __forceinline__ int bodyArchIndex(const PhysArgs &P, uint32_t archety
     return 0;
 }
 
+// Clamp a data-derived index into [0, n): a miss raises kErrIndexGuard (with
+// the site in bits 8..15) on the world instead of faulting the device.
+enum GuardSite : int32_t {
+    kGuardRefFace = 1, kGuardIncFace, kGuardIncWalk, kGuardRefWalk, kGuardVertex,
+    kGuardPlaneFace, kGuardPlaneWalk, kGuardSolverBody, kGuardSolverSlot, kGuardEntity,
+    kGuardLeaf, kGuardNode, kGuardWork,
+};
+
+__device__ __forceinline__ int32_t guardIndex(int32_t i, int32_t n, int32_t *flags,
+                                              int32_t site)
+{
+    if ((uint32_t)i < (uint32_t)n) return i;
+    atomicOr(flags, kErrIndexGuard | (site << 8));
+    return 0;
+}
+
 __device__ __forceinline__ Loc entityLoc(const PhysArgs &P, int32_t w, Entity e)
 {
-    const IDNode &n = P.idNodes[(size_t)w * P.idsPerWorld + e.id];
+    const int32_t id = guardIndex(e.id, P.idsPerWorld, P.errorFlags + w, kGuardEntity);
+    const IDNode &n = P.idNodes[(size_t)w * P.idsPerWorld + id];
     if (n.gen != e.gen) return Loc::none();
     return n.val;
 }

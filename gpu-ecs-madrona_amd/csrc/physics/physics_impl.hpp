@@ -75,7 +75,7 @@ struct SatWork {
     int32_t world;
     int32_t slot;                 // survivor slot (== contact slot) in the world
     Loc a, b;                     // after runNarrowphase's type ordering
-    int32_t aLeaf, bLeaf;
+    int32_t aArch, bArch;         // body archetype index (PhysArgs::body)
     int32_t aObj, bObj;
     uint32_t test;                // type(a) | type(b)
     int32_t pad;
@@ -109,10 +109,8 @@ struct PhysArgs {
     uint32_t *leafParents;        // [W][maxLeaves]
     int32_t *sortedLeaves;        // [W][maxLeaves]
 
-    math::Vector3 *hullVerts;     // [W][maxLeaves][maxVerts] world-space hull cache
-    geometry::Plane *hullPlanes;  // [W][maxLeaves][maxFaces]
 
-    math::AABB *bodyAABBs;        // [W][maxLeaves] world AABB of each body (substep)
+    math::AABB *bodyAABBs;        // [W][maxBodiesPerWorld] world AABB per body slot (substep)
     int32_t *survivors;           // [W][candCapacity] candidates passing the AABB recheck
     int32_t *survCount;           // [W] survivors per world
     struct SatWork *satWork;      // [W * candCapacity] SAT work list (one per survivor)
@@ -136,5 +134,8 @@ inline constexpr int32_t kErrCandidateOverflow = 4;
 inline constexpr int32_t kErrContactOverflow = 8;
 inline constexpr int32_t kErrBVHStack = 16;
 inline constexpr int32_t kErrSolverBodies = 32;
+// A data-derived index left its range (only reachable through corrupted
+// state); bits 8..15 carry the site (physics_device.hpp guardIndex).
+inline constexpr int32_t kErrIndexGuard = 64;
 
 }

@@ -333,8 +333,10 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
         const int32_t k = k0 + __popcll(mask & lt_mask);
         if (has && k < K) {
             const Contact &c = cslots[s];
-            recs[k] = CRec { (int16_t)bodySlot(P, c.ref), (int16_t)bodySlot(P, c.alt), 0,
-                             (int16_t)s };
+            int32_t *flags = P.errorFlags + w;
+            recs[k] = CRec { (int16_t)guardIndex(bodySlot(P, c.ref), nb, flags, kGuardSolverBody),
+                             (int16_t)guardIndex(bodySlot(P, c.alt), nb, flags, kGuardSolverBody),
+                             0, (int16_t)s };
             order[k] = s;
         }
         k0 += __popcll(mask);

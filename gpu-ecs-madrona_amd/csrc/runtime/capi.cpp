@@ -7,7 +7,9 @@
 #include <madrona/mw_gpu.hpp>
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <exception>
 #include <map>
@@ -40,6 +42,7 @@ using namespace madrona;
 
 struct mw_exec {
     Executor *exec;
+    ncclComm_t comm = nullptr;    // RCCL communicator for the world-shard hand-off
 };
 
 static thread_local std::string g_last_error;
@@ -138,6 +141,7 @@ int mw_destroy(mw_exec *exec)
 {
     MW_TRY({
         if (exec) {
+            if (exec->comm) (void)ncclCommDestroy(exec->comm);
             delete exec->exec;
             delete exec;
         }
@@ -146,6 +150,70 @@ int mw_destroy(mw_exec *exec)
 }
 
 const char *mw_last_error(void) { return g_last_error.c_str(); }
+
+// ---------------------------------------------------------------------------
+// Training hand-off across world shards: RCCL over xGMI, issued on the
+// executor's stream right behind the step that produced the export.
+// ---------------------------------------------------------------------------
+#define MW_NCCL_OK(expr)                                                     \
+    do {                                                                     \
+        ncclResult_t r__ = (expr);                                           \
+        if (r__ != ncclSuccess) throw std::runtime_error(ncclGetErrorString(r__)); \
+    } while (0)
+
+static_assert(sizeof(ncclUniqueId) == MW_RCCL_ID_BYTES, "RCCL unique id size");
+
+int mw_rccl_get_unique_id(void *id_out)
+{
+    MW_TRY({
+        ncclUniqueId id;
+        MW_NCCL_OK(ncclGetUniqueId(&id));
+        memcpy(id_out, &id, sizeof(id));
+        return 0;
+    }, -1)
+}
+
+int mw_rccl_init(mw_exec *exec, const void *id, int32_t nranks, int32_t rank)
+{
+    MW_TRY({
+        if (exec->comm) throw std::runtime_error("mw_rccl_init: communicator already set");
+        ncclUniqueId uid;
+        memcpy(&uid, id, sizeof(uid));
+        MW_NCCL_OK(ncclCommInitRank(&exec->comm, nranks, uid, rank));
+        return 0;
+    }, -1)
+}
+
+int mw_allgather_exported(mw_exec *exec, int32_t slot, void *dst, int64_t bytes_per_rank)
+{
+    MW_TRY({
+        if (!exec->comm) throw std::runtime_error("mw_allgather_exported: call mw_rccl_init first");
+        void *src = exec->exec->getExported(slot, nullptr);
+        if (!src) throw std::runtime_error("mw_allgather_exported: no such export slot");
+        MW_NCCL_OK(ncclAllGather(src, dst, (size_t)bytes_per_rank, ncclChar, exec->comm,
+                                 (hipStream_t)exec->exec->stream()));
+        return 0;
+    }, -1)
+}
+
+void *mw_device_alloc(mw_exec *exec, int64_t bytes)
+{
+    MW_TRY({
+        (void)exec;
+        void *p = nullptr;
+        MW_HIP_OK(hipMalloc(&p, (size_t)std::max<int64_t>(bytes, 256)));
+        return p;
+    }, nullptr)
+}
+
+int mw_device_free(mw_exec *exec, void *ptr)
+{
+    MW_TRY({
+        (void)exec;
+        MW_HIP_OK(hipFree(ptr));
+        return 0;
+    }, -1)
+}
 
 int32_t mw_num_worlds(mw_exec *exec) { return exec->exec->numWorlds(); }
 

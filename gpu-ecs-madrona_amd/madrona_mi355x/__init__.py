@@ -20,6 +20,29 @@ if not os.path.exists(LIB_PATH):
         f"madrona_mi355x: HIP library missing at {LIB_PATH}; "
         "build it with `make -C gpu-ecs-madrona_amd` (or __graft_entry__.build())")
 
+
+def _mapped_hip_runtimes():
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({l.split()[-1] for l in f if "libamdhip64" in l and "/" in l})
+    except OSError:
+        return []
+
+
+# The library is built by the system ROCm compiler and must run on the
+# matching HIP runtime.  PyTorch wheels bundle an older libamdhip64 with the
+# same soname: if torch was imported first, the dynamic linker binds this
+# library to torch's runtime, whose loader mis-handles these code objects
+# (device memory faults).  Import madrona_mi355x before torch; torch then
+# binds to the system runtime, which is backward compatible.
+_preloaded = [p for p in _mapped_hip_runtimes()
+              if not os.path.realpath(p).startswith(os.path.realpath(
+                  os.environ.get("ROCM_PATH", "/opt/rocm")))]
+if _preloaded and not os.environ.get("MADRONA_MW_ALLOW_FOREIGN_HIP"):
+    raise ImportError(
+        "madrona_mi355x: a different HIP runtime is already loaded "
+        f"({_preloaded[0]}); import madrona_mi355x before torch")
+
 _lib = ctypes.CDLL(LIB_PATH)
 
 
@@ -70,6 +93,14 @@ _lib.mw_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.
                                          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 _lib.mw_phys_time_node.restype = ctypes.c_double
 _lib.mw_phys_time_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
+_lib.mw_rccl_get_unique_id.argtypes = [ctypes.c_void_p]
+_lib.mw_rccl_init.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+_lib.mw_allgather_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                       ctypes.c_int64]
+_lib.mw_device_alloc.restype = ctypes.c_void_p
+_lib.mw_device_alloc.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+_lib.mw_device_free.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+RCCL_ID_BYTES = 128
 _lib.mw_set_timed_node.restype = ctypes.c_int32
 _lib.mw_set_timed_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
 _lib.mw_timed_node_ms.restype = ctypes.c_double
@@ -82,7 +113,17 @@ C_ABI_SYMBOLS = (
     "mw_read_column", "mw_column_info", "mw_phys_read_candidates", "mw_phys_read_contacts",
     "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_copy_exported",
     "mw_gen_collisions_inits", "mw_set_timed_node", "mw_timed_node_ms",
+    "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
+    "mw_device_free",
 )
+
+
+def rccl_unique_id():
+    """128-byte RCCL id (rank 0 creates it; the launcher distributes it)."""
+    buf = ctypes.create_string_buffer(RCCL_ID_BYTES)
+    if _lib.mw_rccl_get_unique_id(buf) != 0:
+        raise _err()
+    return buf.raw
 
 
 def gen_collisions_inits(num_worlds, num_cubes=128, seed=0, first_world=0):
@@ -96,7 +137,8 @@ def gen_collisions_inits(num_worlds, num_cubes=128, seed=0, first_world=0):
     return pos, rot
 
 ERR_BITS = {1: "id store full", 2: "table full", 4: "candidate overflow",
-            8: "contact overflow", 16: "BVH stack overflow", 32: "solver body overflow"}
+            8: "contact overflow", 16: "BVH stack overflow", 32: "solver body overflow",
+            64: "index guard (site in bits 8..15)"}
 
 
 class MadronaError(RuntimeError):
@@ -195,6 +237,28 @@ class Executor:
         if n < 0:
             raise _err()
         return n
+
+    def rccl_init(self, uid, nranks, rank):
+        """Join the world-shard communicator (RCCL over xGMI)."""
+        buf = ctypes.create_string_buffer(bytes(uid), RCCL_ID_BYTES)
+        if _lib.mw_rccl_init(self.h, buf, nranks, rank) != 0:
+            raise _err()
+
+    def allgather_exported(self, slot, dst_ptr, bytes_per_rank):
+        """Enqueue an all-gather of export `slot` into device memory dst_ptr
+        (nranks * bytes_per_rank bytes, rank order) on the executor stream."""
+        if _lib.mw_allgather_exported(self.h, slot, ctypes.c_void_p(dst_ptr), bytes_per_rank) != 0:
+            raise _err()
+
+    def device_alloc(self, nbytes):
+        p = _lib.mw_device_alloc(self.h, nbytes)
+        if not p:
+            raise _err()
+        return p
+
+    def device_free(self, ptr):
+        if _lib.mw_device_free(self.h, ctypes.c_void_p(ptr)) != 0:
+            raise _err()
 
     def time_node(self, name, steps):
         """Eager timing of `steps` extra steps (advances the simulation)."""

@@ -5,8 +5,10 @@ reference include/madrona/context.hpp:152-156), so N GPUs hold contiguous
 world ranges: rank r owns worlds [r * W, (r + 1) * W) and steps them with no
 cross-GPU traffic.  The only collective is the training hand-off: the
 per-world episode returns (an exported singleton column, state.hpp:128-129)
-are all-gathered into world order -- RCCL over xGMI on the GPU path, gloo in
-the CPU tests.
+are all-gathered into world order -- RCCL over xGMI issued by the framework
+on its step stream (bootstrap_rccl + Executor.allgather_exported) on the GPU
+path; gather_world_returns is the same gather over any torch.distributed
+backend (gloo in the CPU tests).
 """
 
 
@@ -37,3 +39,15 @@ def gather_world_returns(local, out=None, group=None):
         dist.all_gather(parts, local, group=group)
         torch.cat(parts, out=out)
     return out
+
+
+def bootstrap_rccl(sim, rank, world_size, group=None):
+    """Create the world-shard RCCL communicator of `sim` (an Executor): rank 0
+    draws the 128-byte id, torch.distributed (any backend, e.g. gloo over the
+    launcher's TCP store) broadcasts it, every rank joins."""
+    import torch.distributed as dist
+    import madrona_mi355x as mw
+
+    uid = [mw.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0, group=group)
+    sim.rccl_init(uid[0], world_size, rank)

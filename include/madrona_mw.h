@@ -139,6 +139,21 @@ double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps
 int32_t mw_set_timed_node(mw_exec *exec, const char *node_name);
 double mw_timed_node_ms(mw_exec *exec, int64_t *launches);
 
+/* ---- training hand-off across world shards (RCCL over xGMI) -------------
+ * One process per GPU; rank 0 creates the id, the launcher distributes the
+ * 128 bytes (e.g. over the torch.distributed TCP store), every rank calls
+ * mw_rccl_init.  mw_allgather_exported enqueues an all-gather of the slot's
+ * packed export buffer on the executor stream (after the step that wrote
+ * it): dst receives nranks * bytes_per_rank bytes in rank order.  Replaces
+ * the reference's host-side getExported gather for multi-GPU learners
+ * (include/madrona/mw_gpu.hpp:71).                                         */
+#define MW_RCCL_ID_BYTES 128
+int mw_rccl_get_unique_id(void *id_out);
+int mw_rccl_init(mw_exec *exec, const void *id, int32_t nranks, int32_t rank);
+int mw_allgather_exported(mw_exec *exec, int32_t slot, void *dst, int64_t bytes_per_rank);
+void *mw_device_alloc(mw_exec *exec, int64_t bytes);
+int mw_device_free(mw_exec *exec, void *ptr);
+
 #ifdef __cplusplus
 }
 #endif

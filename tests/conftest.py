@@ -7,6 +7,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
 
+# Bind the framework to the system HIP runtime before any test module
+# imports torch (madrona_mi355x/__init__.py explains why).
+try:
+    import madrona_mi355x  # noqa: F401,E402
+except ImportError:
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")

@@ -8,6 +8,8 @@ import socket
 
 import numpy as np
 import pytest
+
+import madrona_mi355x  # noqa: F401  (before torch, see madrona_mi355x/__init__.py)
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as tmp
