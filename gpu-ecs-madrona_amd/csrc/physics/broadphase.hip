@@ -163,6 +163,29 @@ __global__ void __launch_bounds__(64) bvhRebuildKernel(PhysArgs P)
         parent.maxY[c] = combined.pMax.y; parent.maxZ[c] = combined.pMax.z;
     }
     bvh.usedNodes = cur_node_offset;
+
+    // Leaf emission order of BVH::findOverlaps (physics.inl:61-100) with no
+    // pruning: pop a node, emit its leaf children in slot order, push its
+    // inner children.  Pruning a subtree only deletes its leaves from this
+    // sequence, so every query's candidates come out in this order.
+    int32_t *order = P.leafOrder + (size_t)w * P.maxLeaves;
+    int32_t ostack[128];
+    int32_t os = 0, emitted = 0;
+    if (bvh.numLeaves > 0) ostack[os++] = 0;
+    while (os > 0) {
+        const BVHNode &n = nodes[ostack[--os]];
+        for (int i = 0; i < 4; i++) {
+            const int32_t child = n.children[i];
+            if (child == -1) continue;
+            if (child & 0x80000000) {
+                if (emitted < P.maxLeaves) order[emitted++] = child & ~0x80000000;
+            } else if (os < 128) {
+                ostack[os++] = child;
+            } else {
+                atomicOr(P.errorFlags + w, kErrBVHStack);
+            }
+        }
+    }
 }
 
 // refitEntry -> BVH::refitLeaf (broadphase.cpp:545-642, 891-895)
@@ -227,169 +250,133 @@ __global__ void __launch_bounds__(256) refitKernel(PhysArgs P)
 // each row's candidates, a block scan gives the reference's append order,
 // pass 2 writes them.
 
-constexpr int32_t kOverlapStack = 24;   // int16 entries; 4-wide tree depth <= 7 at 4096 leaves
-constexpr int32_t kOverlapBuf = 12;     // candidates kept per body before a re-walk
+constexpr int32_t kOverlapBuf = 12;     // candidates kept per body before a second sweep
 
-// LDS image of one world's BVH (nodes padded to 128 B so a node is eight
-// 16-byte LDS reads) plus per-leaf (entity id, Loc, static flag), per-lane
-// traversal stacks and per-lane candidate buffers.
-struct alignas(16) LNode {
-    float minX[4], minY[4], minZ[4];
-    float maxX[4], maxY[4], maxZ[4];
-    int32_t children[4];
-    int32_t pad[4];
+// findOverlappingEntry + BVH::findOverlaps (broadphase.cpp:897-932,
+// physics.inl:61-100) without a per-lane tree walk.  Every ancestor slot of
+// a leaf contains the leaf's slot AABB (rebuild merges children, refit only
+// grows slots and propagates growth upward), so a query overlaps a leaf slot
+// exactly when the walk would reach and emit it; and the walk emits leaves in
+// a fixed order (BVH leafOrder, computed at rebuild) with pruned subtrees
+// simply missing.  So each body sweeps the world's leaves in that order and
+// tests the leaf slots: same candidates, same order, no divergent stacks.
+struct alignas(16) OrderedLeaf {
+    float minX, minY, minZ;
+    float maxX, maxY, maxZ;
+    int32_t id;                   // entity id (the e.id < other.id rule)
+    int32_t isStatic;
+    Loc loc;
 };
-static_assert(sizeof(LNode) == 128);
+static_assert(sizeof(OrderedLeaf) == 48);
 
-struct OverlapLDS {
-    LNode *nodes;
-    int32_t *leafId;
-    Loc *leafLoc;
-    int8_t *leafStatic;
-    int16_t *stacks;
-    uint16_t *bufs;
-};
+// AABB::overlaps (math.hpp) of the query against a leaf slot.
+__device__ __forceinline__ bool slotOverlaps(const AABB &q, const OrderedLeaf &o)
+{
+    return q.pMin.x < o.maxX && o.minX < q.pMax.x &&
+           q.pMin.y < o.maxY && o.minY < q.pMax.y &&
+           q.pMin.z < o.maxZ && o.minZ < q.pMax.z;
+}
 
 __host__ __device__ inline size_t a16b(size_t b) { return (b + 15) & ~size_t(15); }
 
-__host__ __device__ inline size_t overlapLDSBytes(int32_t max_nodes, int32_t max_leaves)
+__host__ __device__ inline size_t overlapLDSBytes(int32_t max_leaves)
 {
-    return a16b(sizeof(LNode) * max_nodes) + a16b(4 * max_leaves) + a16b(8 * max_leaves) +
-           a16b(max_leaves) + a16b(2 * kOverlapBlock * kOverlapStack) +
+    return a16b(sizeof(OrderedLeaf) * max_leaves) + a16b(4 * max_leaves) +
            a16b(2 * kOverlapBlock * kOverlapBuf);
-}
-
-__device__ __forceinline__ OverlapLDS overlapLDS(char *smem, int32_t max_nodes, int32_t max_leaves)
-{
-    OverlapLDS L;
-    char *p = smem;
-    L.nodes = (LNode *)p;
-    p += a16b(sizeof(LNode) * max_nodes);
-    L.leafId = (int32_t *)p;
-    p += a16b(4 * max_leaves);
-    L.leafLoc = (Loc *)p;
-    p += a16b(8 * max_leaves);
-    L.leafStatic = (int8_t *)p;
-    p += a16b(max_leaves);
-    L.stacks = (int16_t *)p;
-    p += a16b(2 * kOverlapBlock * kOverlapStack);
-    L.bufs = (uint16_t *)p;
-    return L;
 }
 
 size_t findOverlapsSharedBytes(const PhysArgs &P)
 {
-    return overlapLDSBytes(P.maxNodes, P.maxLeaves);
+    return overlapLDSBytes(P.maxLeaves);
 }
 
-// BVH::findOverlaps for one body (physics.inl:61-100): DFS with the
-// reference's push order; a hit is a leaf whose entity id is larger than the
-// body's and that is not static-static.  kWrite = false: count hits and keep
-// the first kOverlapBuf other-leaf indices; kWrite = true: write every hit.
-template <bool kWrite>
-__device__ __forceinline__ int32_t traverseOverlaps(const PhysArgs &P, const OverlapLDS &L,
-                                                    int32_t w, int32_t leaf, int16_t *stack,
-                                                    uint16_t *buf, int32_t out_base)
-{
-    const int32_t e_id = L.leafId[leaf];
-    const Loc a_loc = L.leafLoc[leaf];
-    const bool a_static = L.leafStatic[leaf] != 0;
-    const AABB q = P.leafAABBs[(size_t)w * P.maxLeaves + leaf];
-
-    int32_t count = 0;
-    stack[0] = 0;
-    int32_t ss = 1;
-    while (ss > 0) {
-        const LNode &n = L.nodes[stack[--ss]];
-        for (int i = 0; i < 4; i++) {
-            const int32_t child = n.children[i];
-            if (child == -1) continue;
-            AABB c { { n.minX[i], n.minY[i], n.minZ[i] }, { n.maxX[i], n.maxY[i], n.maxZ[i] } };
-            if (!q.overlaps(c)) continue;
-            if (child & 0x80000000) {
-                const int32_t ol = child & ~0x80000000;
-                if (e_id < L.leafId[ol]) {
-                    if (a_static && L.leafStatic[ol]) continue;
-                    if (kWrite) {
-                        const int32_t slot = out_base + count;
-                        if (slot < P.candCapacity) {
-                            P.cands[(size_t)w * P.candCapacity + slot] =
-                                CandidateCollision { a_loc, L.leafLoc[ol] };
-                        }
-                    } else if (count < kOverlapBuf) {
-                        buf[count] = (uint16_t)ol;
-                    }
-                    count++;
-                }
-            } else {
-                if (ss < kOverlapStack) {
-                    stack[ss++] = (int16_t)child;
-                } else {
-                    atomicOr(P.errorFlags + w, kErrBVHStack);
-                }
-            }
-        }
-    }
-    return count;
-}
-
-// findOverlappingEntry (broadphase.cpp:897-932): one block per world, lanes
-// own body rows.  One walk per body fills a small LDS buffer; a block scan of
-// the counts gives the reference's append order (row order, DFS order within
-// a row); bodies with more hits than the buffer holds walk again to write.
 __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int32_t scan_scratch[kOverlapBlock / 64];
     const int32_t w = blockIdx.x;
-    OverlapLDS L = overlapLDS(smem, P.maxNodes, P.maxLeaves);
+    OrderedLeaf *leaves = (OrderedLeaf *)smem;
+    int32_t *rank_of = (int32_t *)(smem + a16b(sizeof(OrderedLeaf) * P.maxLeaves));
+    uint16_t *bufs = (uint16_t *)((char *)rank_of + a16b(4 * P.maxLeaves));
 
-    // stage nodes (29 dwords each -> 32-dword LDS slots) and leaf info
+    // Stage leaf slots (from the refit tree) + identity in emission order.
     const broadphase::BVH &bvh = P.bvh[w];
-    const int32_t used = min(bvh.usedNodes, P.maxNodes);
-    const uint32_t *gnodes = (const uint32_t *)(P.nodes + (size_t)w * P.maxNodes);
-    uint32_t *lnodes = (uint32_t *)L.nodes;
-    for (int32_t i = threadIdx.x; i < used * 32; i += kOverlapBlock) {
-        const int32_t node = i >> 5, d = i & 31;
-        lnodes[i] = d < 29 ? gnodes[node * 29 + d] : 0u;
-    }
-    const int32_t nleaves = bvh.numLeaves;
-    for (int32_t l = threadIdx.x; l < nleaves; l += kOverlapBlock) {
-        const Entity e = P.leafEntities[(size_t)w * P.maxLeaves + l];
+    const int32_t nleaves = min(bvh.numLeaves, P.maxLeaves);
+    const BVHNode *nodes = P.nodes + (size_t)w * P.maxNodes;
+    const int32_t *order = P.leafOrder + (size_t)w * P.maxLeaves;
+    int32_t *flags = P.errorFlags + w;
+    for (int32_t k = threadIdx.x; k < nleaves; k += kOverlapBlock) {
+        const int32_t leaf = guardIndex(order[k], P.maxLeaves, flags, kGuardLeaf);
+        const uint32_t lp = P.leafParents[(size_t)w * P.maxLeaves + leaf];
+        const BVHNode &n = nodes[guardIndex((int32_t)(lp >> 2), P.maxNodes, flags, kGuardNode)];
+        const int sub = (int)(lp & 3);
+        const Entity e = P.leafEntities[(size_t)w * P.maxLeaves + leaf];
         const Loc loc = entityLoc(P, w, e);
-        L.leafId[l] = e.id;
-        L.leafLoc[l] = loc;
         const BodyArch &OB = P.body[bodyArchIndex(P, loc.archetype)];
-        const int32_t row = guardIndex(loc.row, OB.capacity, P.errorFlags + w, kGuardLeaf);
-        L.leafStatic[l] =
+        const int32_t row = guardIndex(loc.row, OB.capacity, flags, kGuardLeaf);
+        OrderedLeaf ol;
+        ol.minX = n.minX[sub]; ol.minY = n.minY[sub]; ol.minZ = n.minZ[sub];
+        ol.maxX = n.maxX[sub]; ol.maxY = n.maxY[sub]; ol.maxZ = n.maxZ[sub];
+        ol.id = e.id;
+        ol.isStatic =
             bcol<ResponseType>(OB, Cols::ResponseType, w, row) == ResponseType::Static ? 1 : 0;
+        ol.loc = loc;
+        leaves[k] = ol;
+        rank_of[leaf] = k;
     }
     __syncthreads();
 
-    int16_t *stack = L.stacks + threadIdx.x * kOverlapStack;
-    uint16_t *buf = L.bufs + threadIdx.x * kOverlapBuf;
+    uint16_t *buf = bufs + threadIdx.x * kOverlapBuf;
     int32_t base = 0;
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
         for (int32_t chunk = 0; chunk < rows; chunk += kOverlapBlock) {
             const int32_t row = chunk + threadIdx.x;
-            int32_t cnt = 0, leaf = 0;
+            int32_t cnt = 0;
+            AABB q = AABB::invalid();
+            int32_t self = 0;
             if (row < rows) {
-                leaf = guardIndex(bcol<broadphase::LeafID>(B, Cols::LeafID, w, row).id,
-                                  P.maxLeaves, P.errorFlags + w, kGuardLeaf);
-                cnt = traverseOverlaps<false>(P, L, w, leaf, stack, buf, 0);
+                const int32_t leaf = guardIndex(bcol<broadphase::LeafID>(B, Cols::LeafID, w, row).id,
+                                                P.maxLeaves, flags, kGuardLeaf);
+                q = P.leafAABBs[(size_t)w * P.maxLeaves + leaf];
+                self = rank_of[leaf];
+            }
+            const OrderedLeaf &me = leaves[self];
+            const int32_t e_id = me.id;
+            const bool a_static = me.isStatic != 0;
+            const bool active = row < rows;
+            // sweep 1: count hits, keep the first kOverlapBuf ranks
+            for (int32_t k = 0; k < nleaves; k++) {
+                const OrderedLeaf &o = leaves[k];            // LDS broadcast
+                const bool hit = active && e_id < o.id && !(a_static && o.isStatic) &&
+                                 slotOverlaps(q, o);
+                if (hit) {
+                    if (cnt < kOverlapBuf) buf[cnt] = (uint16_t)k;
+                    cnt++;
+                }
             }
             int32_t total;
             const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
-            if (cnt > kOverlapBuf) {
-                traverseOverlaps<true>(P, L, w, leaf, stack, buf, base + off);
-            } else if (cnt > 0) {
-                const Loc a_loc = L.leafLoc[leaf];
-                CandidateCollision *out = P.cands + (size_t)w * P.candCapacity;
-                for (int32_t i = 0; i < cnt; i++) {
-                    const int32_t slot = base + off + i;
-                    if (slot < P.candCapacity) out[slot] = CandidateCollision { a_loc, L.leafLoc[buf[i]] };
+            CandidateCollision *out = P.cands + (size_t)w * P.candCapacity;
+            if (cnt > 0) {
+                const Loc a_loc = me.loc;
+                if (cnt <= kOverlapBuf) {
+                    for (int32_t i = 0; i < cnt; i++) {
+                        const int32_t slot = base + off + i;
+                        if (slot < P.candCapacity) out[slot] = CandidateCollision { a_loc, leaves[buf[i]].loc };
+                    }
+                } else {
+                    int32_t i = 0;
+                    for (int32_t k = 0; k < nleaves; k++) {
+                        const OrderedLeaf &o = leaves[k];
+                        const bool hit = e_id < o.id && !(a_static && o.isStatic) &&
+                                         slotOverlaps(q, o);
+                        if (hit) {
+                            const int32_t slot = base + off + i++;
+                            if (slot < P.candCapacity) out[slot] = CandidateCollision { a_loc, o.loc };
+                        }
+                    }
                 }
             }
             base += total;

@@ -289,6 +289,7 @@ void PhysicsModule::upload(void *stream_ptr)
     P.leafAABBs = devAlloc<AABB>((size_t)W * maxLeaves, stream);
     P.leafParents = devAlloc<uint32_t>((size_t)W * maxLeaves, stream);
     P.sortedLeaves = devAlloc<int32_t>((size_t)W * maxLeaves, stream);
+    P.leafOrder = devAlloc<int32_t>((size_t)W * maxLeaves, stream);
 
     ObjDev &O = P.objs;
     O.numObjects = (int32_t)metadata.size();

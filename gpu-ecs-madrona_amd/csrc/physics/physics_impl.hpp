@@ -108,6 +108,7 @@ struct PhysArgs {
     math::AABB *leafAABBs;        // [W][maxLeaves]
     uint32_t *leafParents;        // [W][maxLeaves]
     int32_t *sortedLeaves;        // [W][maxLeaves]
+    int32_t *leafOrder;           // [W][maxLeaves] leaves in BVH traversal (emission) order
 
 
     math::AABB *bodyAABBs;        // [W][maxBodiesPerWorld] world AABB per body slot (substep)

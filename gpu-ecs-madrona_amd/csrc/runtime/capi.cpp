@@ -128,7 +128,8 @@ int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_byt
         int32_t bytes_per_row = exec->exec->exportRowBytes(slot);
         int64_t n = rows * bytes_per_row;
         if (n > max_bytes) n = max_bytes;
-        MW_HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice,
+        // dst may be device or host memory (unified addressing)
+        MW_HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDefault,
                                  (hipStream_t)exec->exec->stream()));
         exec->exec->sync();
         return n;

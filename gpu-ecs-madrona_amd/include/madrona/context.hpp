@@ -13,6 +13,8 @@
 #include <madrona/state.hpp>
 
 #include <new>
+#include <tuple>
+#include <utility>
 
 namespace madrona {
 
@@ -79,6 +81,9 @@ public:
     template <typename... ComponentTs> Query<ComponentTs...> query();
     template <typename... ComponentTs, typename Fn>
     MW_INLINE void forEach(const Query<ComponentTs...> &q, Fn &&fn);
+    template <typename Fn, size_t... Is, typename... Ts>
+    MW_INLINE void forEachRows(int32_t arch, const int32_t *cols, int32_t n, Fn &fn,
+                               std::index_sequence<Is...>, Ts *...);
     template <typename... ComponentTs>
     MW_INLINE uint32_t numMatches(const Query<ComponentTs...> &q);
 
@@ -211,14 +216,24 @@ template <typename... ComponentTs, typename Fn>
 MW_INLINE void Context::forEach(const Query<ComponentTs...> &q, Fn &&fn)
 {                                              // state.inl:358-396
     for (int32_t a = 0; a < q.numArchetypes; a++) {
-        int32_t arch = q.archetypes[a];
-        int32_t n = state_->arch[arch].numRows[world_];
-        int32_t ci = 0;
-        auto ptrs = std::make_tuple(
-            state_->column<std::remove_const_t<ComponentTs>>(arch, q.cols[a][ci++], world_)...);
-        for (int32_t r = 0; r < n; r++) {
-            std::apply([&](auto *...p) { fn(p[r]...); }, ptrs);
-        }
+        const int32_t arch = q.archetypes[a];
+        const int32_t n = state_->arch[arch].numRows[world_];
+        forEachRows(arch, q.cols[a], n, fn, std::index_sequence_for<ComponentTs...> {},
+                    (std::remove_const_t<ComponentTs> *)nullptr...);
+    }
+}
+
+template <typename Fn, size_t... Is, typename... Ts>
+MW_INLINE void Context::forEachRows(int32_t arch, const int32_t *cols, int32_t n, Fn &fn,
+                                    std::index_sequence<Is...>, Ts *...)
+{
+    // column i of the query is cols[i] (the pack is expanded by index, so the
+    // column binding does not depend on argument evaluation order)
+    auto ptrs = std::make_tuple(state_->column<Ts>(arch, cols[Is], world_)...);
+    // unrolled so a device lane keeps several rows' loads in flight
+#pragma unroll 4
+    for (int32_t r = 0; r < n; r++) {
+        fn(std::get<Is>(ptrs)[r]...);
     }
 }
 

@@ -217,6 +217,14 @@ class Executor:
         ptr = _lib.mw_get_exported(self.h, slot, ctypes.byref(rows))
         return ptr, rows.value
 
+    def exported_array(self, slot, dtype):
+        """Host copy of export `slot` (packed [world-major, row] rows)."""
+        dtype = np.dtype(dtype)
+        _, rows = self.exported(slot)
+        out = np.empty(max(rows, 1) * 256, np.uint8)       # >= rows * row bytes
+        n = self.copy_exported(slot, out.ctypes.data, out.nbytes)
+        return out[:n].view(dtype)
+
     def error_flags(self):
         return _lib.mw_error_flags(self.h)
 

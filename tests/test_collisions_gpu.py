@@ -174,3 +174,25 @@ def test_live_node_timing_does_not_perturb_state():
     a.set_timed_node(None)
     a.step(1)
     assert a.timed_node() == (0.0, 0)
+
+
+def test_episode_return_export_matches_oracle():
+    # ParallelForNode over the EpisodeReturn singleton (Context::forEach over
+    # a two-component query) + the packed export buffer (getExported slot 2).
+    mw = _mw()
+    gcfg, ocfg = _cfg_pair()
+    W, steps = 5, 12
+    pos, rot = gen_collisions_inits(W, 128, seed=4)
+    sim = mw.CollisionsSim(W, pos, rot, gcfg)
+    orc = OraclePhys(ocfg, pos, rot)
+    ret = np.zeros(W, np.float32)
+    for _ in range(steps):
+        sim.step()
+        orc.step()
+        for w in range(W):
+            b = orc.bodies(w)
+            z = b["pos"][b["responseType"] == 0][:, 2].astype(np.float32)
+            ret[w] = np.float32(ret[w] + np.cumsum(z, dtype=np.float32)[-1] / np.float32(len(z)))
+    got = sim.exported_array(2, np.float32)
+    assert got.shape == (W,)
+    assert got.tobytes() == ret.tobytes()
