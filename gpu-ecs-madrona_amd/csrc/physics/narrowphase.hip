@@ -81,19 +81,77 @@ __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
 }
 
 // ===========================================================================
-// Narrowphase (narrowphase.cpp, CPU branch).
-//
-// A 16-lane group owns one candidate pair at a time: the SAT queries
-// (face directions A->B and B->A, all edge pairs) are spread over the
-// group's lanes and combined with (value, index) reductions whose tie-break
-// reproduces the reference's serial strict-'>' scan exactly (first
-// occurrence wins, NaN never wins); the clip / manifold tail runs on the
-// group's leader lane with its scratch polygons in LDS.
+// Narrowphase (narrowphase.cpp, CPU branch), three kernels per substep:
+//   1. narrowFilterKernel, block per world: AABB recheck + type ordering of
+//      every candidate; a block scan numbers the survivors in candidate order
+//      (survivor slot == contact slot); hull-hull survivors go to the SAT
+//      work list, hull-plane survivors straight to the contact job list.
+//   2. narrowSATKernel, persistent, one 16-lane group per hull-hull pair:
+//      both hulls are transformed into LDS and the SAT queries are spread
+//      over the group with (value, index) reductions that reproduce the
+//      reference's serial strict-'>' scans (first occurrence wins, NaN never
+//      wins).  A non-separated pair becomes a contact job carrying the
+//      chosen feature (reference / incident face or edge pair).
+//   3. narrowContactKernel, persistent, one lane per contact job: clipping
+//      and manifold reduction (all lanes busy, clip polygons in LDS).
 // ===========================================================================
 constexpr int32_t kGroup = 16;
 constexpr int32_t kGroupsPerBlock = kNarrowBlock / kGroup;
-constexpr int32_t kMaxClip = 32;
 
+__host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
+
+// World transform of a body's hull (makeHullState, narrowphase.cpp:139-212:
+// vertices by R * S, plane normals by R * S^-1 then renormalised).  Every
+// kernel derives world-space hull data through these helpers, so the SAT
+// kernel's LDS copies and the contact kernel's on-the-fly values agree bit
+// for bit.
+struct HullXform {
+    Mat3x3 vtx;
+    Mat3x3 nrm;
+    Vector3 x;
+};
+
+__device__ __forceinline__ HullXform hullXform(const PhysArgs &P, int32_t w, const BodyArch &B,
+                                               int32_t row)
+{
+    const Vector3 x = bcol<Vector3>(B, Cols::Position, w, row);
+    const Quat rot = bcol<Quat>(B, Cols::Rotation, w, row);
+    const Diag3x3 scale = bcol<Diag3x3>(B, Cols::Scale, w, row);
+    const Mat3x3 unscaled_rot = Mat3x3::fromQuat(rot);
+    return HullXform { unscaled_rot * scale, unscaled_rot * scale.inv(), x };
+}
+
+__device__ __forceinline__ Vector3 worldVertex(const ObjDev &O, const HullDev &hd,
+                                               const HullXform &xf, int32_t i)
+{
+    return xf.vtx * O.vertices[hd.vertOffset + i] + xf.x;
+}
+
+__device__ __forceinline__ geometry::Plane worldPlane(const ObjDev &O, const HullDev &hd,
+                                                      const HullXform &xf, int32_t i)
+{
+    const geometry::Plane op = O.planes[hd.faceOffset + i];
+    const Vector3 origin = xf.vtx * (op.normal * op.d) + xf.x;
+    const Vector3 n = (xf.nrm * op.normal).normalize();
+    return geometry::Plane { n, dot(n, origin) };
+}
+
+__device__ __forceinline__ float distFromPlane(const geometry::Plane &p, const Vector3 &a)
+{
+    float adotn = a.dot(p.normal);
+    return adotn - p.d;
+}
+
+__device__ __forceinline__ Vector3 planeIntersection(const geometry::Plane &p, const Vector3 &p1,
+                                                     const Vector3 &p2)
+{
+    float distance = distFromPlane(p, p1);
+    return p1 + (p2 - p1) * (-distance / p.normal.dot(p2 - p1));
+}
+
+// ---------------------------------------------------------------------------
+// SAT kernel helpers (group of 16 lanes, hulls staged in LDS)
+// ---------------------------------------------------------------------------
 struct HullRef {
     const Vector3 *verts;          // world space (LDS copy)
     const geometry::Plane *planes; // world space (LDS copy)
@@ -102,45 +160,33 @@ struct HullRef {
     Vector3 center;
 };
 
-// Per-group LDS: both hulls of the pair (world-space vertices, face planes,
-// edge topology) and the leader lane's clipping polygons.
 struct GroupLDS {
     Vector3 *vA, *vB;
     geometry::Plane *pA, *pB;
     EdgeQuad *qA, *qB;
-    Vector3 *clip0, *clip1;
-    float *depths;
 };
 
-__host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
-
-__host__ __device__ inline size_t groupLDSBytes(int32_t max_verts, int32_t max_faces,
-                                                int32_t max_edges)
+__host__ __device__ inline size_t groupLDSBytes(const ObjDev &O)
 {
-    return 2 * a16(sizeof(Vector3) * max_verts) + 2 * a16(sizeof(geometry::Plane) * max_faces) +
-           2 * a16(sizeof(EdgeQuad) * max_edges) + 2 * a16(sizeof(Vector3) * kMaxClip) +
-           a16(sizeof(float) * kMaxClip);
+    return 2 * a16(sizeof(Vector3) * O.maxVerts) + 2 * a16(sizeof(geometry::Plane) * O.maxFaces) +
+           2 * a16(sizeof(EdgeQuad) * O.maxEdges);
 }
 
 size_t narrowphaseSharedBytes(const PhysArgs &P)
 {
-    const ObjDev &O = P.objs;
-    return kGroupsPerBlock * groupLDSBytes(O.maxVerts, O.maxFaces, O.maxEdges);
+    return kGroupsPerBlock * groupLDSBytes(P.objs);
 }
 
 __device__ __forceinline__ GroupLDS groupLDS(char *smem, int32_t group, const ObjDev &O)
 {
-    char *p = smem + (size_t)group * groupLDSBytes(O.maxVerts, O.maxFaces, O.maxEdges);
+    char *p = smem + (size_t)group * groupLDSBytes(O);
     GroupLDS g;
     g.vA = (Vector3 *)p; p += a16(sizeof(Vector3) * O.maxVerts);
     g.vB = (Vector3 *)p; p += a16(sizeof(Vector3) * O.maxVerts);
     g.pA = (geometry::Plane *)p; p += a16(sizeof(geometry::Plane) * O.maxFaces);
     g.pB = (geometry::Plane *)p; p += a16(sizeof(geometry::Plane) * O.maxFaces);
     g.qA = (EdgeQuad *)p; p += a16(sizeof(EdgeQuad) * O.maxEdges);
-    g.qB = (EdgeQuad *)p; p += a16(sizeof(EdgeQuad) * O.maxEdges);
-    g.clip0 = (Vector3 *)p; p += a16(sizeof(Vector3) * kMaxClip);
-    g.clip1 = (Vector3 *)p; p += a16(sizeof(Vector3) * kMaxClip);
-    g.depths = (float *)p;
+    g.qB = (EdgeQuad *)p;
     return g;
 }
 
@@ -173,48 +219,18 @@ __device__ __forceinline__ void groupArgMax(float &v, int32_t &k)
     }
 }
 
-// Transform one body's hull to world space straight into the group's LDS
-// (makeHullState, narrowphase.cpp:139-212: vertex_txfm = R * S, normals by
-// R * S^-1, renormalised) and copy its edge topology.  Returns the body
-// position (the hull's center for the edge query).
+// Transform one body's hull into the group's LDS and copy its edge topology.
 __device__ __forceinline__ Vector3 stageHull(const PhysArgs &P, int32_t w, const BodyArch &B,
                                              int32_t row, const HullDev &hd, Vector3 *v,
                                              geometry::Plane *pl, EdgeQuad *q, int32_t lane)
 {
     const ObjDev &O = P.objs;
-    const Vector3 x = bcol<Vector3>(B, Cols::Position, w, row);
-    const Quat rot = bcol<Quat>(B, Cols::Rotation, w, row);
-    const Diag3x3 scale = bcol<Diag3x3>(B, Cols::Scale, w, row);
-    const Mat3x3 unscaled_rot = Mat3x3::fromQuat(rot);
-    const Mat3x3 vertex_txfm = unscaled_rot * scale;
-    for (int32_t i = lane; i < hd.numVerts; i += kGroup) {
-        v[i] = vertex_txfm * O.vertices[hd.vertOffset + i] + x;
-    }
-    if (lane < hd.numFaces) {
-        const Mat3x3 normal_txfm = unscaled_rot * scale.inv();
-        for (int32_t i = lane; i < hd.numFaces; i += kGroup) {
-            const geometry::Plane op = O.planes[hd.faceOffset + i];
-            const Vector3 origin = vertex_txfm * (op.normal * op.d) + x;
-            const Vector3 n = (normal_txfm * op.normal).normalize();
-            pl[i] = geometry::Plane { n, dot(n, origin) };
-        }
-    }
+    const HullXform xf = hullXform(P, w, B, row);
+    for (int32_t i = lane; i < hd.numVerts; i += kGroup) v[i] = worldVertex(O, hd, xf, i);
+    for (int32_t i = lane; i < hd.numFaces; i += kGroup) pl[i] = worldPlane(O, hd, xf, i);
     const EdgeQuad *gq = O.edgeQuads + hd.edgeOffset;
     for (int32_t i = lane; i < hd.numEdges; i += kGroup) q[i] = gq[i];
-    return x;
-}
-
-__device__ __forceinline__ float distFromPlane(const geometry::Plane &p, const Vector3 &a)
-{
-    float adotn = a.dot(p.normal);
-    return adotn - p.d;
-}
-
-__device__ __forceinline__ Vector3 planeIntersection(const geometry::Plane &p, const Vector3 &p1,
-                                                     const Vector3 &p2)
-{
-    float distance = distFromPlane(p, p1);
-    return p1 + (p2 - p1) * (-distance / p.normal.dot(p2 - p1));
+    return xf.x;
 }
 
 __device__ __forceinline__ float hullDistFromPlane(const geometry::Plane &p, const HullRef &h)
@@ -328,8 +344,12 @@ __device__ __forceinline__ int32_t findIncidentFace(const HullRef &h, Vector3 re
     return face;
 }
 
+// ---------------------------------------------------------------------------
+// Contact generation helpers (one lane per job)
+// ---------------------------------------------------------------------------
 __device__ __forceinline__ int32_t clipPolygon(Vector3 *dst, geometry::Plane cp,
-                                               const Vector3 *in, int32_t n)
+                                               const Vector3 *in, int32_t n,
+                                               int32_t cap)
 {                                                          // narrowphase.cpp:626-661
     if (n == 0) return 0;
     int32_t out = 0;
@@ -339,12 +359,12 @@ __device__ __forceinline__ int32_t clipPolygon(Vector3 *dst, geometry::Plane cp,
         Vector3 v2 = in[i];
         float d2 = distFromPlane(cp, v2);
         if (d1 <= 0.0f && d2 <= 0.0f) {
-            if (out < kMaxClip) dst[out++] = v2;
+            if (out < cap) dst[out++] = v2;
         } else if (d1 <= 0.0f && d2 > 0.0f) {
-            if (out < kMaxClip) dst[out++] = planeIntersection(cp, v1, v2);
+            if (out < cap) dst[out++] = planeIntersection(cp, v1, v2);
         } else if (d2 <= 0.0f && d1 > 0.0f) {
-            if (out < kMaxClip) dst[out++] = planeIntersection(cp, v1, v2);
-            if (out < kMaxClip) dst[out++] = v2;
+            if (out < cap) dst[out++] = planeIntersection(cp, v1, v2);
+            if (out < cap) dst[out++] = v2;
         }
         v1 = v2;
         d1 = d2;
@@ -481,11 +501,107 @@ __device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
     return true;
 }
 
-// Hull-hull: doSAT (narrowphase.cpp:678-758) on the group, then
-// createFaceContact (:866-972) or createEdgeContact (:1053-1121) on the
-// leader lane.  All group lanes must enter; both hulls are staged in LDS.
-__device__ void hullHullPair(const PhysArgs &P, const SatWork &wk, const GroupLDS &g,
-                             int32_t lane, Contact &out)
+// Stage 1, block per world: AABB recheck + type ordering of every candidate.
+// One block scan numbers the survivors in candidate order (survivor slot ==
+// contact slot) and, packed in the same scan, numbers the hull-hull and
+// hull-plane survivors separately; both go to the world's staging row
+// (hull-hull from the front, hull-plane from the back).  No global atomics.
+__global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
+{
+    __shared__ int32_t s_scan[kNarrowBlock / 64];
+    const int32_t w = blockIdx.x;
+    const int32_t cap = P.candCapacity;
+    const int32_t num = min(P.numCands[w], cap);
+    const CandidateCollision *cands = P.cands + (size_t)w * cap;
+    Contact *slots = P.candContacts + (size_t)w * cap;
+    SatWork *stage = P.satStage + (size_t)w * cap;
+    constexpr uint32_t kHull = (uint32_t)CollisionPrimitive::Type::Hull;
+    constexpr uint32_t kHullPlane = kHull | (uint32_t)CollisionPrimitive::Type::Plane;
+
+    int32_t S = 0, nhh = 0, npl = 0;
+    for (int32_t chunk = 0; chunk < num; chunk += kNarrowBlock) {
+        const int32_t ci = chunk + threadIdx.x;
+        SatWork wk;
+        const bool keep = ci < num && resolvePair(P, w, cands[ci], wk);
+        const bool hh = keep && wk.test == kHull;
+        const bool pl = keep && wk.test == kHullPlane;
+        // sphere / plane-plane survivors get a slot but no manifold: the
+        // reference asserts on them (narrowphase.cpp:1197-1313)
+        const int32_t packed = (keep ? 1 : 0) | (hh ? 1 << 10 : 0) | (pl ? 1 << 20 : 0);
+        int32_t total;
+        const int32_t off = blockExclusiveScan(packed, s_scan, &total);
+        if (keep) {
+            wk.slot = S + (off & 1023);
+            slots[wk.slot].numPoints = 0;
+            if (hh) stage[nhh + ((off >> 10) & 1023)] = wk;
+            if (pl) stage[cap - 1 - (npl + (off >> 20))] = wk;
+        }
+        S += total & 1023;
+        nhh += (total >> 10) & 1023;
+        npl += total >> 20;
+    }
+    if (threadIdx.x == 0) {
+        P.survCount[w] = S;
+        P.hhCount[w] = nhh;
+        P.planeCount[w] = npl;
+    }
+}
+
+// Stage 2, one block: exclusive scans of the per-world hull-hull and
+// hull-plane counts -> each world's offset in the flat lists, and totals.
+__global__ void __launch_bounds__(1024) narrowScanKernel(PhysArgs P)
+{
+    __shared__ int32_t s_scan[1024 / 64];
+    int32_t base_hh = 0, base_pl = 0;
+    for (int32_t chunk = 0; chunk < P.numWorlds; chunk += 1024) {
+        const int32_t w = chunk + threadIdx.x;
+        const int32_t hh = w < P.numWorlds ? P.hhCount[w] : 0;
+        const int32_t pl = w < P.numWorlds ? P.planeCount[w] : 0;
+        int32_t total_hh, total_pl;
+        const int32_t off_hh = blockExclusiveScan(hh, s_scan, &total_hh);
+        const int32_t off_pl = blockExclusiveScan(pl, s_scan, &total_pl);
+        if (w < P.numWorlds) {
+            P.hhOffset[w] = base_hh + off_hh;
+            P.planeOffset[w] = base_pl + off_pl;
+        }
+        base_hh += total_hh;
+        base_pl += total_pl;
+    }
+    if (threadIdx.x == 0) {
+        *P.satWorkCount = base_hh;
+        *P.jobCount = base_pl;
+    }
+}
+
+// Stage 3, block per world: move the world's staged pairs to their flat
+// positions (hull-plane pairs become contact jobs directly).
+__global__ void __launch_bounds__(kNarrowBlock) narrowCompactKernel(PhysArgs P)
+{
+    const int32_t w = blockIdx.x;
+    const int32_t cap = P.candCapacity;
+    const SatWork *stage = P.satStage + (size_t)w * cap;
+    const int32_t nhh = P.hhCount[w], npl = P.planeCount[w];
+    SatWork *hh_out = P.satWork + P.hhOffset[w];
+    ContactJob *pl_out = P.planeJobs + P.planeOffset[w];
+    for (int32_t i = threadIdx.x; i < nhh; i += kNarrowBlock) hh_out[i] = stage[i];
+    for (int32_t i = threadIdx.x; i < npl; i += kNarrowBlock) {
+        ContactJob job;
+        job.pair = stage[cap - 1 - i];
+        job.kind = kJobPlane;
+        job.refIsA = 0;
+        job.feature0 = 0;
+        job.feature1 = 0;
+        job.plane = geometry::Plane { { 0, 0, 0 }, 0 };
+        pl_out[i] = job;
+    }
+}
+
+// Hull-hull SAT (doSAT, narrowphase.cpp:678-758) for one pair on one group.
+// Returns true (on every lane of the group) if the pair is not separated;
+// the leader's `job` then holds createFaceContact's / createEdgeContact's
+// inputs.
+__device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS &g,
+                            int32_t lane, ContactJob &job)
 {
     const ObjDev &O = P.objs;
     const int32_t w = wk.world;
@@ -499,167 +615,34 @@ __device__ void hullHullPair(const PhysArgs &P, const SatWork &wk, const GroupLD
     groupSync();
 
     const FaceQuery fa = groupFaceQuery(ha, hb, lane);
-    if (fa.separation > 0.0f) return;
+    if (fa.separation > 0.0f) return false;
     const FaceQuery fb = groupFaceQuery(hb, ha, lane);
-    if (fb.separation > 0.0f) return;
+    if (fb.separation > 0.0f) return false;
     const EdgeQuery eq = groupEdgeQuery(ha, hb, lane);
-    if (eq.separation > 0.0f) return;
-    if (lane != 0) return;
+    if (eq.separation > 0.0f) return false;
 
+    job.pair = wk;
     if (fa.separation > eq.separation || fb.separation > eq.separation) {
         const bool a_is_ref = fa.separation >= fb.separation;
-        const geometry::Plane ref_plane = a_is_ref ? fa.plane : fb.plane;
-        const int32_t ref_face = a_is_ref ? fa.faceIdx : fb.faceIdx;
-        const HullRef &ref = a_is_ref ? ha : hb;
-        const HullRef &inc = a_is_ref ? hb : ha;
-        int32_t *flags = P.errorFlags + w;
-        const int32_t inc_face = guardIndex(findIncidentFace(inc, ref_plane.normal),
-                                            inc.hd.numFaces, flags, kGuardIncFace);
-        const int32_t ref_face_g = guardIndex(ref_face, ref.hd.numFaces, flags, kGuardRefFace);
-
-        const geometry::HalfEdge *rh = O.hedges + ref.hd.hedgeOffset;
-        const geometry::HalfEdge *oh = O.hedges + inc.hd.hedgeOffset;
-        int32_t n_in = 0;
-        {
-            uint32_t hidx = O.polygons[inc.hd.faceOffset + inc_face], start = hidx;
-            int32_t steps = 0;
-            do {
-                hidx = guardIndex(hidx, inc.hd.numHedges, flags, kGuardIncWalk);
-                const geometry::HalfEdge he = oh[hidx];
-                hidx = he.next;
-                if (n_in < kMaxClip)
-                    g.clip0[n_in++] = inc.verts[guardIndex(he.rootVertex, inc.hd.numVerts, flags,
-                                                           kGuardVertex)];
-            } while (hidx != start && ++steps <= inc.hd.numHedges);
-        }
-        Vector3 *cin = g.clip0, *cdst = g.clip1;
-        int32_t n_clip = n_in;
-        {
-            uint32_t hidx = O.polygons[ref.hd.faceOffset + ref_face_g], start = hidx;
-            hidx = guardIndex(hidx, ref.hd.numHedges, flags, kGuardRefWalk);
-            geometry::HalfEdge che = rh[hidx];
-            Vector3 cur = ref.verts[guardIndex(che.rootVertex, ref.hd.numVerts, flags,
-                                               kGuardVertex)];
-            int32_t steps = 0;
-            do {
-                hidx = guardIndex(che.next, ref.hd.numHedges, flags, kGuardRefWalk);
-                che = rh[hidx];
-                Vector3 next = ref.verts[guardIndex(che.rootVertex, ref.hd.numVerts, flags,
-                                                    kGuardVertex)];
-                Vector3 edge = next - cur;
-                Vector3 pn = cross(edge, ref_plane.normal);
-                float d = dot(pn, cur);
-                cur = next;
-                n_clip = clipPolygon(cdst, geometry::Plane { pn, d }, cin, n_clip);
-                Vector3 *t = cdst; cdst = cin; cin = t;
-            } while (hidx != start && ++steps <= ref.hd.numHedges);
-        }
-        int32_t n_below = 0;
-        for (int32_t i = 0; i < n_clip; i++) {
-            Vector3 v = cin[i];
-            float d = distFromPlane(ref_plane, v);
-            if (d < 0.0f) {
-                cin[n_below] = v - d * ref_plane.normal;
-                g.depths[n_below] = -d;
-                n_below++;
-            }
-        }
-        storeFaceManifold(out, ref_plane.normal, cin, g.depths, n_below,
-                          a_is_ref ? wk.a : wk.b, a_is_ref ? wk.b : wk.a);
+        job.kind = kJobFace;
+        job.refIsA = a_is_ref ? 1 : 0;
+        job.plane = a_is_ref ? fa.plane : fb.plane;
+        job.feature0 = a_is_ref ? fa.faceIdx : fb.faceIdx;
+        job.feature1 = findIncidentFace(a_is_ref ? hb : ha, job.plane.normal);
     } else {
-        const EdgeQuad ea = ha.quads[eq.edgeA], eb = hb.quads[eq.edgeB];
-        geometry::Segment sa { ha.verts[ea.v1], ha.verts[ea.v2] };
-        geometry::Segment sb { hb.verts[eb.v1], hb.verts[eb.v2] };
-        geometry::Segment s = shortestSegmentBetween(sa, sb);
-        const Quat ident { 1, 0, 0, 0 };
-        out.ref = wk.a;
-        out.alt = wk.b;
-        out.points[0] = Vector4::fromVector3(ident.rotateVec(s.p1) + Vector3::zero(),
-                                             -eq.separation);
-        for (int i = 1; i < 4; i++) out.points[i] = Vector4::fromVector3(Vector3::zero(), 0.f);
-        out.numPoints = 1;
-        out.normal = ident.rotateVec(eq.normal);
-        for (int i = 0; i < 4; i++) out.lambdaN[i] = 0.f;
+        job.kind = kJobEdge;
+        job.refIsA = 1;
+        job.feature0 = eq.edgeA;
+        job.feature1 = eq.edgeB;
+        job.plane = geometry::Plane { eq.normal, eq.separation };
     }
+    return true;
 }
 
-// Hull-plane: doSATPlane (narrowphase.cpp:760-788) + createFacePlaneContact
-// (:974-1017) on the leader lane after the group stages the hull.
-__device__ void hullPlanePair(const PhysArgs &P, const SatWork &wk, const GroupLDS &g,
-                              int32_t lane, Contact &out)
-{
-    const ObjDev &O = P.objs;
-    const int32_t w = wk.world;
-    HullRef ha;
-    ha.hd = O.hulls[wk.aObj];
-    ha.verts = g.vA; ha.planes = g.pA; ha.quads = g.qA;
-    ha.center = stageHull(P, w, P.body[wk.aArch], wk.a.row, ha.hd, g.vA, g.pA, g.qA, lane);
-    groupSync();
-    if (lane != 0) return;
-    const BodyArch &BB = P.body[wk.bArch];
-    const Vector3 b_pos = bcol<Vector3>(BB, Cols::Position, w, wk.b.row);
-    const Quat b_rot = bcol<Quat>(BB, Cols::Rotation, w, wk.b.row);
-    Vector3 pn = b_rot.rotateVec(Vector3 { 0, 0, 1 });
-    geometry::Plane plane { pn, dot(pn, b_pos) };
-    float sep = hullDistFromPlane(plane, ha);
-    if (sep > 0.0f) return;
-    int32_t *flags = P.errorFlags + w;
-    const int32_t inc_face = guardIndex(findIncidentFace(ha, plane.normal), ha.hd.numFaces,
-                                        flags, kGuardPlaneFace);
-    const geometry::HalfEdge *hh = O.hedges + ha.hd.hedgeOffset;
-    int32_t n = 0;
-    uint32_t hidx = O.polygons[ha.hd.faceOffset + inc_face], start = hidx;
-    int32_t steps = 0;
-    do {
-        hidx = guardIndex(hidx, ha.hd.numHedges, flags, kGuardPlaneWalk);
-        const geometry::HalfEdge he = hh[hidx];
-        hidx = he.next;
-        Vector3 v = ha.verts[guardIndex(he.rootVertex, ha.hd.numVerts, flags, kGuardVertex)];
-        float d = distFromPlane(plane, v);
-        if (d < 0.0f && n < kMaxClip) {
-            g.clip0[n] = v - d * plane.normal;
-            g.depths[n] = -d;
-            n++;
-        }
-    } while (hidx != start && ++steps <= ha.hd.numHedges);
-    storeFaceManifold(out, plane.normal, g.clip0, g.depths, n, wk.b, wk.a);
-}
-
-// runNarrowphaseSystem (narrowphase.cpp:1515-1728), stage 1, one block per
-// world: lane-per-candidate AABB recheck and type ordering; a block scan
-// numbers the survivors in the reference's candidate order (their slot ==
-// contact slot) and appends them to the device-wide SAT work list.
-__global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
-{
-    __shared__ int32_t s_scan[kNarrowBlock / 64];
-    __shared__ int32_t s_base;
-    const int32_t w = blockIdx.x;
-    const int32_t num = min(P.numCands[w], P.candCapacity);
-    const CandidateCollision *cands = P.cands + (size_t)w * P.candCapacity;
-
-    int32_t S = 0;
-    for (int32_t chunk = 0; chunk < num; chunk += kNarrowBlock) {
-        const int32_t ci = chunk + threadIdx.x;
-        SatWork wk;
-        const int32_t keep = (ci < num && resolvePair(P, w, cands[ci], wk)) ? 1 : 0;
-        int32_t total;
-        const int32_t off = blockExclusiveScan(keep, s_scan, &total);
-        if (threadIdx.x == 0 && total > 0) s_base = atomicAdd(P.satWorkCount, total);
-        __syncthreads();
-        if (keep) {
-            wk.slot = S + off;
-            P.satWork[s_base + off] = wk;
-        }
-        S += total;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) P.survCount[w] = S;
-}
-
-// Stage 2, persistent: each 16-lane group takes pairs off the work list and
-// writes the pair's manifold (numPoints 0 = no contact) into its world's
-// survivor slot.  The grid is sized to what is resident at once, so every
-// group reaches the end of the list and exits.
+// Stage 4, persistent: each group takes hull-hull pairs off the flat list
+// and leaves its verdict in the job at the same index (kind kJobNone when
+// separated).  The grid is what is resident at once; every group reaches
+// the end of the list and exits.
 __global__ void __launch_bounds__(kNarrowBlock) narrowSATKernel(PhysArgs P)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -669,28 +652,187 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowSATKernel(PhysArgs P)
     const int32_t total = *(volatile int32_t *)P.satWorkCount;
     const int32_t stride = gridDim.x * kGroupsPerBlock;
     for (int32_t idx = blockIdx.x * kGroupsPerBlock + group; idx < total; idx += stride) {
-        SatWork wk = P.satWork[idx];
-        if ((uint32_t)wk.world >= (uint32_t)P.numWorlds ||
-            (uint32_t)wk.slot >= (uint32_t)P.candCapacity ||
-            (uint32_t)wk.aObj >= (uint32_t)P.objs.numObjects ||
-            (uint32_t)wk.bObj >= (uint32_t)P.objs.numObjects ||
-            (uint32_t)wk.aArch >= (uint32_t)P.numBodyArchs ||
-            (uint32_t)wk.bArch >= (uint32_t)P.numBodyArchs ||
-            (uint32_t)wk.a.row >= (uint32_t)P.body[wk.aArch].capacity ||
-            (uint32_t)wk.b.row >= (uint32_t)P.body[wk.bArch].capacity) {
-            if (lane == 0) atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
-            continue;
+        const SatWork wk = P.satWork[idx];
+        const bool ok = (uint32_t)wk.world < (uint32_t)P.numWorlds &&
+                        (uint32_t)wk.slot < (uint32_t)P.candCapacity &&
+                        (uint32_t)wk.aObj < (uint32_t)P.objs.numObjects &&
+                        (uint32_t)wk.bObj < (uint32_t)P.objs.numObjects &&
+                        (uint32_t)wk.aArch < (uint32_t)P.numBodyArchs &&
+                        (uint32_t)wk.bArch < (uint32_t)P.numBodyArchs &&
+                        (uint32_t)wk.a.row < (uint32_t)P.body[wk.aArch].capacity &&
+                        (uint32_t)wk.b.row < (uint32_t)P.body[wk.bArch].capacity;
+        ContactJob job;
+        job.kind = kJobNone;
+        if (ok) {
+            hullHullSAT(P, wk, g, lane, job);
+        } else if (lane == 0) {
+            atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
         }
-        Contact &out = P.candContacts[(size_t)wk.world * P.candCapacity + wk.slot];
-        if (lane == 0) out.numPoints = 0;
-        if (wk.test == (uint32_t)CollisionPrimitive::Type::Hull) {
-            hullHullPair(P, wk, g, lane, out);
-        } else if (wk.test == ((uint32_t)CollisionPrimitive::Type::Hull |
-                               (uint32_t)CollisionPrimitive::Type::Plane)) {
-            hullPlanePair(P, wk, g, lane, out);
-        }
-        // sphere / plane-plane: the reference asserts (narrowphase.cpp:1197-1313)
+        if (lane == 0) P.hhJobs[idx] = job;
         groupSync();
+    }
+}
+
+__host__ __device__ inline size_t contactLDSBytes(int32_t clip_cap)
+{
+    return (size_t)kContactBlock * (2 * a16(sizeof(Vector3) * clip_cap) + a16(4 * clip_cap));
+}
+
+size_t contactSharedBytes(const PhysArgs &P)
+{
+    return contactLDSBytes(P.clipCap);
+}
+
+// createFaceContact / createFacePlaneContact / createEdgeContact
+// (narrowphase.cpp:866-1121) for one job per lane.
+__global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const ObjDev &O = P.objs;
+    const int32_t cap = P.clipCap;
+    char *mine = smem + (size_t)threadIdx.x * (2 * a16(sizeof(Vector3) * cap) + a16(4 * cap));
+    Vector3 *clip0 = (Vector3 *)mine;
+    Vector3 *clip1 = (Vector3 *)(mine + a16(sizeof(Vector3) * cap));
+    float *depths = (float *)(mine + 2 * a16(sizeof(Vector3) * cap));
+    const Quat ident { 1, 0, 0, 0 };
+
+    const int32_t n_plane = *(volatile int32_t *)P.jobCount;
+    const int32_t total = n_plane + *(volatile int32_t *)P.satWorkCount;
+    for (int32_t i = blockIdx.x * kContactBlock + threadIdx.x; i < total;
+         i += gridDim.x * kContactBlock) {
+        const ContactJob job = i < n_plane ? P.planeJobs[i] : P.hhJobs[i - n_plane];
+        if (job.kind == kJobNone) continue;
+        const SatWork &wk = job.pair;
+        const int32_t w = wk.world;
+        int32_t *flags = P.errorFlags + w;
+        Contact &out = P.candContacts[(size_t)w * P.candCapacity + wk.slot];
+        const HullDev ha = O.hulls[wk.aObj];
+
+        if (job.kind == kJobPlane) {
+            // doSATPlane (:760-788) + createFacePlaneContact (:974-1017);
+            // hull a against the plane of body b
+            const HullXform xa = hullXform(P, w, P.body[wk.aArch], wk.a.row);
+            const BodyArch &BB = P.body[wk.bArch];
+            const Vector3 b_pos = bcol<Vector3>(BB, Cols::Position, w, wk.b.row);
+            const Quat b_rot = bcol<Quat>(BB, Cols::Rotation, w, wk.b.row);
+            const Vector3 pn = b_rot.rotateVec(Vector3 { 0, 0, 1 });
+            const geometry::Plane plane { pn, dot(pn, b_pos) };
+            float min_dot = FLT_MAX;
+            for (int32_t v = 0; v < ha.numVerts; v++) {
+                const float d = plane.normal.dot(worldVertex(O, ha, xa, v));
+                if (d < min_dot) min_dot = d;
+            }
+            if (min_dot - plane.d > 0.0f) continue;
+            float min_fd = FLT_MAX;
+            int32_t inc_face = -1;
+            for (int32_t f = 0; f < ha.numFaces; f++) {
+                const float d = dot(worldPlane(O, ha, xa, f).normal, plane.normal);
+                if (d < min_fd) { min_fd = d; inc_face = f; }
+            }
+            inc_face = guardIndex(inc_face, ha.numFaces, flags, kGuardPlaneFace);
+            const geometry::HalfEdge *hh = O.hedges + ha.hedgeOffset;
+            int32_t n = 0, steps = 0;
+            uint32_t hidx = O.polygons[ha.faceOffset + inc_face], start = hidx;
+            do {
+                hidx = guardIndex(hidx, ha.numHedges, flags, kGuardPlaneWalk);
+                const geometry::HalfEdge he = hh[hidx];
+                hidx = he.next;
+                const Vector3 v = worldVertex(O, ha, xa,
+                                              guardIndex(he.rootVertex, ha.numVerts, flags,
+                                                         kGuardVertex));
+                const float d = distFromPlane(plane, v);
+                if (d < 0.0f && n < cap) {
+                    clip0[n] = v - d * plane.normal;
+                    depths[n] = -d;
+                    n++;
+                }
+            } while (hidx != start && ++steps <= ha.numHedges);
+            storeFaceManifold(out, plane.normal, clip0, depths, n, wk.b, wk.a);
+        } else if (job.kind == kJobFace) {
+            const bool a_is_ref = job.refIsA != 0;
+            const HullDev hb = O.hulls[wk.bObj];
+            const HullDev ref = a_is_ref ? ha : hb;
+            const HullDev inc = a_is_ref ? hb : ha;
+            const HullXform xref = a_is_ref ? hullXform(P, w, P.body[wk.aArch], wk.a.row)
+                                            : hullXform(P, w, P.body[wk.bArch], wk.b.row);
+            const HullXform xinc = a_is_ref ? hullXform(P, w, P.body[wk.bArch], wk.b.row)
+                                            : hullXform(P, w, P.body[wk.aArch], wk.a.row);
+            const geometry::Plane ref_plane = job.plane;
+            const int32_t ref_face = guardIndex(job.feature0, ref.numFaces, flags, kGuardRefFace);
+            const int32_t inc_face = guardIndex(job.feature1, inc.numFaces, flags, kGuardIncFace);
+            const geometry::HalfEdge *rh = O.hedges + ref.hedgeOffset;
+            const geometry::HalfEdge *oh = O.hedges + inc.hedgeOffset;
+            int32_t n_in = 0;
+            {
+                uint32_t hidx = O.polygons[inc.faceOffset + inc_face], start = hidx;
+                int32_t steps = 0;
+                do {
+                    hidx = guardIndex(hidx, inc.numHedges, flags, kGuardIncWalk);
+                    const geometry::HalfEdge he = oh[hidx];
+                    hidx = he.next;
+                    if (n_in < cap)
+                        clip0[n_in++] = worldVertex(O, inc, xinc,
+                                                    guardIndex(he.rootVertex, inc.numVerts, flags,
+                                                               kGuardVertex));
+                } while (hidx != start && ++steps <= inc.numHedges);
+            }
+            Vector3 *cin = clip0, *cdst = clip1;
+            int32_t n_clip = n_in;
+            {
+                uint32_t hidx = guardIndex(O.polygons[ref.faceOffset + ref_face], ref.numHedges,
+                                           flags, kGuardRefWalk);
+                const uint32_t start = hidx;
+                geometry::HalfEdge che = rh[hidx];
+                Vector3 cur = worldVertex(O, ref, xref,
+                                          guardIndex(che.rootVertex, ref.numVerts, flags,
+                                                     kGuardVertex));
+                int32_t steps = 0;
+                do {
+                    hidx = guardIndex(che.next, ref.numHedges, flags, kGuardRefWalk);
+                    che = rh[hidx];
+                    const Vector3 next = worldVertex(O, ref, xref,
+                                                     guardIndex(che.rootVertex, ref.numVerts,
+                                                                flags, kGuardVertex));
+                    const Vector3 edge = next - cur;
+                    const Vector3 pn = cross(edge, ref_plane.normal);
+                    const float d = dot(pn, cur);
+                    cur = next;
+                    n_clip = clipPolygon(cdst, geometry::Plane { pn, d }, cin, n_clip, cap);
+                    Vector3 *t = cdst; cdst = cin; cin = t;
+                } while (hidx != start && ++steps <= ref.numHedges);
+            }
+            int32_t n_below = 0;
+            for (int32_t k = 0; k < n_clip; k++) {
+                const Vector3 v = cin[k];
+                const float d = distFromPlane(ref_plane, v);
+                if (d < 0.0f) {
+                    cin[n_below] = v - d * ref_plane.normal;
+                    depths[n_below] = -d;
+                    n_below++;
+                }
+            }
+            storeFaceManifold(out, ref_plane.normal, cin, depths, n_below,
+                              a_is_ref ? wk.a : wk.b, a_is_ref ? wk.b : wk.a);
+        } else {
+            const HullDev hb = O.hulls[wk.bObj];
+            const HullXform xa = hullXform(P, w, P.body[wk.aArch], wk.a.row);
+            const HullXform xb = hullXform(P, w, P.body[wk.bArch], wk.b.row);
+            const EdgeQuad ea = O.edgeQuads[ha.edgeOffset +
+                                            guardIndex(job.feature0, ha.numEdges, flags, kGuardVertex)];
+            const EdgeQuad eb = O.edgeQuads[hb.edgeOffset +
+                                            guardIndex(job.feature1, hb.numEdges, flags, kGuardVertex)];
+            const geometry::Segment sa { worldVertex(O, ha, xa, ea.v1), worldVertex(O, ha, xa, ea.v2) };
+            const geometry::Segment sb { worldVertex(O, hb, xb, eb.v1), worldVertex(O, hb, xb, eb.v2) };
+            const geometry::Segment sg = shortestSegmentBetween(sa, sb);
+            out.ref = wk.a;
+            out.alt = wk.b;
+            out.points[0] = Vector4::fromVector3(ident.rotateVec(sg.p1) + Vector3::zero(),
+                                                 -job.plane.d);
+            for (int k = 1; k < 4; k++) out.points[k] = Vector4::fromVector3(Vector3::zero(), 0.f);
+            out.numPoints = 1;
+            out.normal = ident.rotateVec(job.plane.normal);
+            for (int k = 0; k < 4; k++) out.lambdaN[k] = 0.f;
+        }
     }
 }
 

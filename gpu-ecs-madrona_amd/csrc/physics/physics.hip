@@ -316,7 +316,15 @@ void PhysicsModule::upload(void *stream_ptr)
     P.survivors = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
     P.survCount = devAlloc<int32_t>(W, stream);
     P.satWork = devAlloc<SatWork>((size_t)W * P.candCapacity, stream);
-    P.satWorkCount = devAlloc<int32_t>(1, stream);
+    P.satWorkCount = devAlloc<int32_t>(2, stream);
+    P.jobCount = P.satWorkCount + 1;
+    P.satStage = devAlloc<SatWork>((size_t)W * P.candCapacity, stream);
+    P.hhCount = devAlloc<int32_t>(W, stream);
+    P.planeCount = devAlloc<int32_t>(W, stream);
+    P.hhOffset = devAlloc<int32_t>(W, stream);
+    P.planeOffset = devAlloc<int32_t>(W, stream);
+    P.planeJobs = devAlloc<ContactJob>((size_t)W * P.candCapacity, stream);
+    P.hhJobs = devAlloc<ContactJob>((size_t)W * P.candCapacity, stream);
     P.candContacts = devAlloc<Contact>((size_t)W * P.candCapacity, stream);
     P.maxContacts = maxContacts;
     P.contactOrder = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
@@ -331,6 +339,24 @@ void PhysicsModule::upload(void *stream_ptr)
     MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, narrowSATKernel, kNarrowBlock, narrowphaseSharedBytes(P)));
     P.satGrid = std::max(1, cus * std::max(per_cu, 1));
+    int32_t max_face_verts = 1;
+    for (const HullDev &h : hulls) {
+        for (int32_t f = 0; f < h.numFaces; f++) {
+            int32_t n = 0;
+            uint32_t e = polygons[h.faceOffset + f], start = e;
+            do {
+                e = hedges[h.hedgeOffset + e].next;
+                n++;
+            } while (e != start && n <= h.numHedges);
+            max_face_verts = std::max(max_face_verts, n);
+        }
+    }
+    // clipping an incident face against a reference face's side planes
+    // yields at most |incident| + |reference| vertices
+    P.clipCap = 2 * max_face_verts;
+    MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, narrowContactKernel, kContactBlock, contactSharedBytes(P)));
+    P.contactGrid = std::max(1, cus * std::max(per_cu, 1));
     uploaded = true;
 }
 
@@ -387,15 +413,19 @@ MW_PHYS_NODE(SubstepRigidBodiesNode,
     if (P.numBodyArchs > 0)
         hipLaunchKernelGGL(integrateKernel, rowGrid(P), dim3(256), 0, stream, P);)
 
-// Narrowphase = AABB recheck + per-world survivor compaction (block per
-// world) feeding one device-wide work list, then a persistent SAT kernel
-// whose 16-lane groups drain that list.  The solver turns the per-survivor
-// manifolds into the ordered contact list.
+// Narrowphase = AABB recheck + survivor numbering (block per world), a
+// one-block scan and a per-world compaction into flat lists, a persistent
+// SAT kernel (16-lane group per hull-hull pair) and a persistent contact
+// kernel (lane per manifold); see narrowphase.hip.  The solver turns
+// the per-survivor manifolds into the ordered contact list.
 MW_PHYS_NODE(NarrowphaseNode,
-    MW_HIP_CHECK(hipMemsetAsync(P.satWorkCount, 0, sizeof(int32_t), stream));
     hipLaunchKernelGGL(narrowFilterKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
+    hipLaunchKernelGGL(narrowScanKernel, dim3(1), dim3(1024), 0, stream, P);
+    hipLaunchKernelGGL(narrowCompactKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
     hipLaunchKernelGGL(narrowSATKernel, dim3(P.satGrid), dim3(kNarrowBlock),
-                       narrowphaseSharedBytes(P), stream, P);)
+                       narrowphaseSharedBytes(P), stream, P);
+    hipLaunchKernelGGL(narrowContactKernel, dim3(P.contactGrid), dim3(kContactBlock),
+                       contactSharedBytes(P), stream, P);)
 
 MW_PHYS_NODE(SolverNode,
     hipLaunchKernelGGL(solverKernel, dim3(P.numWorlds), dim3(kSolverBlock),

@@ -141,15 +141,20 @@ __global__ void refitKernel(PhysArgs P);
 __global__ void findOverlapsKernel(PhysArgs P);
 __global__ void integrateKernel(PhysArgs P);
 __global__ void narrowFilterKernel(PhysArgs P);
+__global__ void narrowScanKernel(PhysArgs P);
+__global__ void narrowCompactKernel(PhysArgs P);
 __global__ void narrowSATKernel(PhysArgs P);
+__global__ void narrowContactKernel(PhysArgs P);
 __global__ void solverKernel(PhysArgs P);
 
 size_t findOverlapsSharedBytes(const PhysArgs &P);
 size_t solverSharedBytes(const PhysArgs &P);
 size_t narrowphaseSharedBytes(const PhysArgs &P);
+size_t contactSharedBytes(const PhysArgs &P);
 
 constexpr int32_t kOverlapBlock = 192;
 constexpr int32_t kNarrowBlock = 256;
+constexpr int32_t kContactBlock = 128;
 constexpr int32_t kSolverBlock = 64;
 
 }

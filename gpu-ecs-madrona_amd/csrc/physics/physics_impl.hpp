@@ -82,6 +82,21 @@ struct SatWork {
 };
 static_assert(sizeof(SatWork) == 48);
 
+// A narrowphase pair that needs a contact manifold, with the feature the SAT
+// chose: hull-plane (from the filter), reference/incident face or edge pair
+// (from the SAT kernel).
+enum : int32_t { kJobNone = -1, kJobPlane = 0, kJobFace = 1, kJobEdge = 2 };
+
+struct alignas(16) ContactJob {
+    SatWork pair;
+    int32_t kind;
+    int32_t refIsA;               // face: the reference face belongs to hull a
+    int32_t feature0;             // face: reference face; edge: edge of hull a
+    int32_t feature1;             // face: incident face; edge: edge of hull b
+    geometry::Plane plane;        // face: world reference plane; edge: {normal, separation}
+};
+static_assert(sizeof(ContactJob) == 80);
+
 // Everything a physics kernel needs, passed by value (< 1 KB).
 struct PhysArgs {
     int32_t numWorlds;
@@ -116,6 +131,14 @@ struct PhysArgs {
     int32_t *survCount;           // [W] survivors per world
     struct SatWork *satWork;      // [W * candCapacity] SAT work list (one per survivor)
     int32_t *satWorkCount;        // [1] entries in satWork this substep
+    SatWork *satStage;            // [W][candCapacity] survivors per world (filter output)
+    int32_t *hhCount, *planeCount;    // [W] hull-hull / hull-plane survivors
+    int32_t *hhOffset, *planeOffset;  // [W] world offsets in the flat lists
+    ContactJob *planeJobs;        // [W * candCapacity] flat hull-plane contact jobs
+    ContactJob *hhJobs;           // [W * candCapacity] SAT verdict per satWork entry
+    int32_t *jobCount;            // [1] hull-plane jobs this substep
+    int32_t contactGrid;          // persistent contact-kernel grid (blocks)
+    int32_t clipCap;              // clip polygon capacity (2 x largest face)
     int32_t satGrid;              // persistent SAT grid (blocks)
     Contact *candContacts;        // [W][candCapacity] manifold per survivor slot
     int32_t maxContacts;          // SolverData::maxContacts (reference assert)
