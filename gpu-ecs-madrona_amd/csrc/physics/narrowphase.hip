@@ -643,7 +643,10 @@ __device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS
 // and leaves its verdict in the job at the same index (kind kJobNone when
 // separated).  The grid is what is resident at once; every group reaches
 // the end of the list and exits.
-__global__ void __launch_bounds__(kNarrowBlock) narrowSATKernel(PhysArgs P)
+#ifndef MW_SAT_MIN_BLOCKS
+#define MW_SAT_MIN_BLOCKS 1
+#endif
+__global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKernel(PhysArgs P)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int32_t group = threadIdx.x / kGroup;

@@ -329,6 +329,7 @@ void PhysicsModule::upload(void *stream_ptr)
     P.maxContacts = maxContacts;
     P.contactOrder = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
     P.solverRecs = devAlloc<uint64_t>((size_t)W * P.candCapacity, stream);
+    P.solverPrevs = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
     P.lastNumContacts = devAlloc<int32_t>(W, stream);
     P.lastNumCands = devAlloc<int32_t>(W, stream);
 

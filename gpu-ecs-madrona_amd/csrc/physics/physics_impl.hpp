@@ -145,6 +145,7 @@ struct PhysArgs {
     int32_t *contactOrder;        // [W][candCapacity] scratch: ordered contact list
     uint64_t *solverRecs;         // [W][candCapacity] solver contact records when K
                                   // exceeds the LDS-resident budget
+    int32_t *solverPrevs;         // [W][candCapacity] predecessor pairs, same condition
     int32_t *lastNumContacts;     // [W] debug: contacts of the last substep
     int32_t *lastNumCands;        // [W] debug: candidates of the last step
 

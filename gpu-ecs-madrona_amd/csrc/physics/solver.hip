@@ -240,18 +240,20 @@ static_assert(sizeof(CRec) == 8);
 // Contacts whose records stay in LDS; worlds with more contacts keep them
 // in a global slab instead, so the LDS footprint (and with it the number of
 // worlds resident per CU) does not scale with SolverData::maxContacts.
-constexpr int32_t kSolverLDSContacts = 512;
+constexpr int32_t kSolverLDSContacts = 256;
 
 struct SolverLDS {
     SBody *bodies;        // [nb]
-    int16_t *lastLevel;   // [nb]
+    int16_t *lastLevel;   // [nb] -1: invariant static body (no ordering edges)
     CRec *recs;           // [kSolverLDSContacts]
+    int32_t *prevs;       // [kSolverLDSContacts] (prev contact on s1, on s2) as 2 x int16
 };
 
 __host__ __device__ inline size_t solverLDSBytes(int32_t nb)
 {
     auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-    return a16(sizeof(SBody) * nb) + a16(sizeof(int16_t) * nb) + sizeof(CRec) * kSolverLDSContacts;
+    return a16(sizeof(SBody) * nb) + a16(sizeof(int16_t) * nb) +
+           (sizeof(CRec) + sizeof(int32_t)) * kSolverLDSContacts;
 }
 
 __device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb)
@@ -263,6 +265,8 @@ __device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb)
     L.lastLevel = (int16_t *)p;
     p += a16(sizeof(int16_t) * nb);
     L.recs = (CRec *)p;
+    p += sizeof(CRec) * kSolverLDSContacts;
+    L.prevs = (int32_t *)p;
     return L;
 }
 
@@ -273,7 +277,6 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
     const int32_t nb = P.maxBodiesPerWorld;
     SolverLDS L = solverLDS(smem, nb);
     SBody *bodies = L.bodies;
-    __shared__ int32_t s_max_level;
 
     // 1. load bodies into LDS
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
@@ -324,7 +327,9 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
         if (lane == 0) atomicOr(P.errorFlags + w, kErrContactOverflow);
         K = P.maxContacts;
     }
-    CRec *recs = K <= kSolverLDSContacts ? L.recs : (CRec *)(P.solverRecs + (size_t)w * P.candCapacity);
+    const bool in_lds = K <= kSolverLDSContacts;
+    CRec *recs = in_lds ? L.recs : (CRec *)(P.solverRecs + (size_t)w * P.candCapacity);
+    int32_t *prevs = in_lds ? L.prevs : P.solverPrevs + (size_t)w * P.candCapacity;
     int32_t k0 = 0;
     for (int32_t chunk = 0; chunk < S && k0 < K; chunk += kSolverBlock) {
         const int32_t s = chunk + lane;
@@ -343,24 +348,46 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
     }
     __syncthreads();
 
-    // 3. levels (serial, one lane)
-    if (threadIdx.x == 0) {
-        int32_t max_level = 0;
-        for (int32_t k = 0; k < K; k++) {
-            CRec r = recs[k];
-            const int32_t l1 = L.lastLevel[r.s1], l2 = L.lastLevel[r.s2];
-            const int32_t l = max(max(l1, l2), 0) + 1;
-            r.lvl = (int16_t)l;
-            recs[k] = r;
-            if (l1 >= 0) L.lastLevel[r.s1] = (int16_t)l;
-            if (l2 >= 0) L.lastLevel[r.s2] = (int16_t)l;
-            max_level = max(max_level, l);
+    // 3. levels.  The reference solves contacts serially (Gauss-Seidel); a
+    //    contact only has to wait for the latest earlier contact on each of
+    //    its bodies (invariant static bodies excepted).  Find those two
+    //    predecessors per contact in parallel, then level = 1 + max(levels
+    //    of the predecessors), relaxed to its fixpoint (one round per level).
+    for (int32_t k = lane; k < K; k += kSolverBlock) {
+        CRec r = recs[k];
+        const bool on1 = L.lastLevel[r.s1] >= 0, on2 = L.lastLevel[r.s2] >= 0;
+        int32_t p1 = -1, p2 = -1;
+        for (int32_t j = k - 1; j >= 0 && ((on1 && p1 < 0) || (on2 && p2 < 0)); j--) {
+            const CRec q = recs[j];
+            if (on1 && p1 < 0 && (q.s1 == r.s1 || q.s2 == r.s1)) p1 = j;
+            if (on2 && p2 < 0 && (q.s1 == r.s2 || q.s2 == r.s2)) p2 = j;
         }
-        s_max_level = max_level;
-        P.lastNumContacts[w] = K;
+        prevs[k] = (p1 & 0xffff) | (p2 << 16);
+        r.lvl = 1;
+        recs[k] = r;
     }
     __syncthreads();
-    const int32_t max_level = s_max_level;
+    for (;;) {
+        bool changed = false;
+        for (int32_t k = lane; k < K; k += kSolverBlock) {
+            const int32_t pv = prevs[k];
+            const int32_t p1 = (int16_t)(pv & 0xffff), p2 = pv >> 16;
+            const int32_t l1 = p1 >= 0 ? recs[p1].lvl : 0;
+            const int32_t l2 = p2 >= 0 ? recs[p2].lvl : 0;
+            const int32_t l = max(l1, l2) + 1;
+            if (l != recs[k].lvl) {
+                recs[k].lvl = (int16_t)l;
+                changed = true;
+            }
+        }
+        __syncthreads();
+        if (!__any(changed)) break;
+    }
+    int32_t max_level = 0;
+    for (int32_t k = lane; k < K; k += kSolverBlock) max_level = max(max_level, (int32_t)recs[k].lvl);
+#pragma unroll
+    for (int32_t off = 32; off > 0; off >>= 1) max_level = max(max_level, __shfl_xor(max_level, off));
+    if (lane == 0) P.lastNumContacts[w] = K;
     const SolverData &sd = P.solver[w];
 
     // 4. solvePositions, level by level
