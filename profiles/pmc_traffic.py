@@ -27,7 +27,10 @@ NODE_OF = {
     "findOverlapsKernel": "FindOverlappingNode",
     "integrateKernel": "SubstepRigidBodiesNode",
     "narrowFilterKernel": "NarrowphaseNode",
+    "narrowScanKernel": "NarrowphaseNode",
+    "narrowCompactKernel": "NarrowphaseNode",
     "narrowSATKernel": "NarrowphaseNode",
+    "narrowContactKernel": "NarrowphaseNode",
     "solverKernel": "SolverNode",
 }
 PER_STEP = {"UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
