@@ -85,6 +85,16 @@ void TaskGraph::launch(LaunchCtx &lc) const
 // ---------------------------------------------------------------------------
 namespace detail {
 
+void launchWorldKernel(const void *kernel, LaunchCtx &lc)
+{
+    StateView *st = lc.devState;
+    void *args[] = { &st };
+    const uint32_t blocks = (uint32_t)((lc.numWorlds + 63) / 64);
+    if (blocks == 0) return;
+    MW_HIP_CHECK(hipLaunchKernel(kernel, dim3(blocks), dim3(64), args, 0,
+                                 (hipStream_t)lc.stream));
+}
+
 void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype,
                      const void *args, size_t)
 {

@@ -204,6 +204,51 @@ ParallelForNode<ContextT, Fn, ComponentTs...>::ParallelForNode(Context &ctx)
     : query_(ctx.query<ComponentTs...>())
 {}
 
+// ---------------------------------------------------------------------------
+// Per-world node: Fn(ContextT &) once per world, worlds in parallel (one lane
+// each).  The reference runs every node once per world (taskgraph.cpp:
+// 111-122); this is its general custom-node form, and the place for
+// structural mutation (makeEntityNow / destroyEntityNow / clearArchetype),
+// which must not race with other lanes of the same world.
+// ---------------------------------------------------------------------------
+namespace detail {
+void launchWorldKernel(const void *kernel, LaunchCtx &lc);
+
+#if defined(__HIPCC__)
+template <typename ContextT, auto Fn>
+__global__ void __launch_bounds__(64) perWorldKernel(StateView *st)
+{
+    const int32_t w = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (w >= st->numWorlds) return;
+    using WorldT = typename WorldOf<ContextT>::type;
+    ContextT ctx((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
+                 WorkerInit { st, w, nullptr });
+    Fn(ctx);
+}
+#endif
+}
+
+template <typename ContextT, auto Fn>
+class PerWorldNode : public NodeBase {
+public:
+    static TaskGraph::NodeID addToGraph(Context &, TaskGraph::Builder &builder,
+                                        Span<const TaskGraph::NodeID> deps)
+    {
+        return builder.addDefaultNode<PerWorldNode>(deps);
+    }
+
+    static void launch(PerWorldNode *, LaunchCtx &lc)
+    {
+#if defined(__HIPCC__)
+        detail::launchWorldKernel((const void *)&detail::perWorldKernel<ContextT, Fn>, lc);
+#else
+        (void)lc;
+#endif
+    }
+
+    static const char *nodeName() { return "PerWorldNode"; }
+};
+
 // Clear a temporary archetype in every world (taskgraph.inl:94-104).
 void launchClearRows(LaunchCtx &lc, int32_t archetype);
 

@@ -59,6 +59,16 @@ class CollisionsConfig(ctypes.Structure):
                 ("mu_s", ctypes.c_float), ("mu_d", ctypes.c_float)]
 
 
+class FvsConfig(ctypes.Structure):
+    _fields_ = [("num_dragons", ctypes.c_int32), ("num_knights", ctypes.c_int32)]
+
+
+class FvsInit(ctypes.Structure):
+    _fields_ = [("dragon_pos", ctypes.c_void_p), ("dragon_mana", ctypes.c_void_p),
+                ("knight_pos", ctypes.c_void_p), ("knight_arrows", ctypes.c_void_p),
+                ("world_index", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
 class CollisionsInit(ctypes.Structure):
     _fields_ = [("pos", ctypes.c_void_p), ("rot", ctypes.c_void_p)]
 
@@ -91,6 +101,7 @@ _lib.mw_copy_exported.restype = ctypes.c_int64
 _lib.mw_copy_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
 _lib.mw_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+_lib.mw_gen_fvs_inits.argtypes = [ctypes.c_int32] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
 _lib.mw_phys_time_node.restype = ctypes.c_double
 _lib.mw_phys_time_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
 _lib.mw_rccl_get_unique_id.argtypes = [ctypes.c_void_p]
@@ -114,7 +125,7 @@ C_ABI_SYMBOLS = (
     "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_copy_exported",
     "mw_gen_collisions_inits", "mw_set_timed_node", "mw_timed_node_ms",
     "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
-    "mw_device_free",
+    "mw_device_free", "mw_gen_fvs_inits",
 )
 
 
@@ -372,3 +383,63 @@ class CollisionsSim(Executor):
         if n < 0:
             raise _err()
         return nodes[:n], aabbs
+
+
+# ---------------------------------------------------------------------------
+# fantasy_vs (BASELINE.json configs[4])
+# ---------------------------------------------------------------------------
+FVS_ROW_DTYPE = np.dtype([("gen", np.uint32), ("id", np.int32), ("pos", np.float32, 3),
+                          ("hp", np.int32), ("remaining", np.float32), ("extra", np.uint32)])
+
+
+def gen_fvs_inits(num_worlds, num_dragons=50, num_knights=200, seed=0, first_world=0):
+    """Reference example init (fvs.cpp:88-108), serial mt19937 over worlds;
+    first_world selects a shard."""
+    d = {"dragon_pos": np.zeros((num_worlds, num_dragons, 3), np.float32),
+         "dragon_mana": np.zeros((num_worlds, num_dragons), np.float32),
+         "knight_pos": np.zeros((num_worlds, num_knights, 3), np.float32),
+         "knight_arrows": np.zeros((num_worlds, num_knights), np.int32)}
+    _lib.mw_gen_fvs_inits(first_world, num_worlds, num_dragons, num_knights, seed,
+                          *[d[k].ctypes.data_as(ctypes.c_void_p) for k in
+                            ("dragon_pos", "dragon_mana", "knight_pos", "knight_arrows")])
+    return d
+
+
+class FvsSim(Executor):
+    """The `fantasy_vs` environment: casters / archers, deaths destroy entities."""
+    DRAGON, KNIGHT, TRACKER = 0, 1, 2
+
+    def __init__(self, num_worlds, inits, first_world=0, gpu_id=0, use_graph=True):
+        self._inits = {k: np.ascontiguousarray(v) for k, v in inits.items()}
+        nd = self._inits["dragon_mana"].shape[1]
+        nk = self._inits["knight_arrows"].shape[1]
+        assert self._inits["dragon_mana"].shape[0] == num_worlds
+        self.cfg = FvsConfig(nd, nk)
+        arr = (FvsInit * num_worlds)()
+        base = {k: v.ctypes.data for k, v in self._inits.items()}
+        for w in range(num_worlds):
+            arr[w].dragon_pos = base["dragon_pos"] + w * nd * 12
+            arr[w].dragon_mana = base["dragon_mana"] + w * nd * 4
+            arr[w].knight_pos = base["knight_pos"] + w * nk * 12
+            arr[w].knight_arrows = base["knight_arrows"] + w * nk * 4
+            arr[w].world_index = first_world + w
+        super().__init__("fantasy_vs", num_worlds, self.cfg, arr, ctypes.sizeof(FvsInit),
+                         gpu_id=gpu_id, default_capacity=64, use_graph=use_graph)
+
+    def table(self, w, arch):
+        """Rows of Dragon / Knight of world w in the oracle's record layout."""
+        ent = self.read_column(arch, 0, w, np.uint32).reshape(-1, 2)
+        n = len(ent)
+        out = np.zeros(n, FVS_ROW_DTYPE)
+        if n == 0:
+            return out
+        out["gen"] = ent[:, 0]
+        out["id"] = ent[:, 1].view(np.int32)
+        out["pos"] = self.read_column(arch, 1, w, np.float32).reshape(n, 3)
+        out["hp"] = self.read_column(arch, 2, w, np.int32).reshape(n, 16)[:, 0]
+        out["remaining"] = self.read_column(arch, 3, w, np.float32)
+        out["extra"] = self.read_column(arch, 4, w, np.uint32)
+        return out
+
+    def num_rows(self, w, arch):
+        return len(self.read_column(arch, 0, w, np.uint64))

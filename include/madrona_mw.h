@@ -139,6 +139,30 @@ double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps
 int32_t mw_set_timed_node(mw_exec *exec, const char *node_name);
 double mw_timed_node_ms(mw_exec *exec, int64_t *launches);
 
+/* ---- "fantasy_vs" environment (BASELINE.json configs[4]) -----------------
+ * per world num_dragons casters + num_knights archers; dead entities are
+ * destroyed every tick (examples/fantasy_vs/fvs.cpp, restated onto the
+ * TaskGraph API).                                            */
+typedef struct mw_fvs_config {
+    int32_t num_dragons;       /* 50 in the reference benchmark (main.cpp:86) */
+    int32_t num_knights;       /* 200 (main.cpp:87) */
+} mw_fvs_config;
+
+typedef struct mw_fvs_init {
+    const float *dragon_pos;   /* num_dragons * 3 */
+    const float *dragon_mana;  /* num_dragons */
+    const float *knight_pos;   /* num_knights * 3 */
+    const int32_t *knight_arrows; /* num_knights */
+    int32_t world_index;       /* global world index (keys the per-world draws) */
+    int32_t pad;
+} mw_fvs_init;
+
+/* Initial state of the reference example (fvs.cpp:88-108): one mt19937 drawn
+ * serially over worlds; first_world selects a shard of that sequence.      */
+void mw_gen_fvs_inits(int32_t first_world, int32_t num_worlds, int32_t num_dragons,
+                      int32_t num_knights, uint32_t seed, float *dragon_pos,
+                      float *dragon_mana, float *knight_pos, int32_t *knight_arrows);
+
 /* ---- training hand-off across world shards (RCCL over xGMI) -------------
  * One process per GPU; rank 0 creates the id, the launcher distributes the
  * 128 bytes (e.g. over the torch.distributed TCP store), every rank calls

@@ -1,0 +1,263 @@
+// Reference harness, fantasy_vs (TEST INFRASTRUCTURE ONLY).
+//
+// The restated fantasy_vs tick written against the
+// reference's own ECS and TaskGraph (compiled from /root/reference by
+// oracle/Makefile.ref), single-world mode: each world owns a StateManager,
+// StateCache and TaskGraph.  Entity IDs, generations, row order after
+// swap-remove and ID reuse therefore come from the reference's IDMap /
+// Table code itself; tests/test_fvs_oracle.py pins oracle/fvs_oracle.cpp to
+// this.  Systems follow examples/fantasy_vs/fvs.cpp:111-240 (Game::tick)
+// with the draws of fvs_rules.hpp.
+
+#include <madrona/taskgraph.hpp>
+#include <madrona/custom_context.hpp>
+#include <madrona/state.hpp>
+#include <madrona/math.hpp>
+
+#include "core/worker_init.hpp"
+#include "../gpu-ecs-madrona_amd/csrc/envs/fvs_rules.hpp"
+
+#include <cstring>
+#include <new>
+#include <vector>
+
+using namespace madrona;
+using namespace madrona::math;
+using namespace fvs_rules;
+
+namespace reffvs {
+
+struct Position : Vector3 {};
+struct alignas(64) Health { int32_t hp; };
+struct Mana { float mp; };
+struct Quiver { int32_t numArrows; };
+struct Action { float remainingTime; };
+struct CleanupEntity : Entity {};
+
+struct Dragon : Archetype<Position, Health, Action, Mana> {};
+struct Knight : Archetype<Position, Health, Action, Quiver> {};
+struct CleanupTracker : Archetype<CleanupEntity> {};
+
+class Engine;
+
+struct Game : public WorldBase {
+    Game(Engine &ctx, uint32_t seed, int32_t nd, int32_t nk, const float *dpos,
+         const float *dmana, const float *kpos, const int32_t *karrows);
+
+    uint32_t seed;
+    uint32_t tickCount;
+    Query<Position, Health> healthQuery;
+    Query<Health, Mana> dragonHealthQuery;
+    Query<Entity, Health> cleanupQuery;
+    Query<CleanupEntity> trackerQuery;
+};
+
+class Engine : public CustomContext<Engine, Game> {
+public:
+    using CustomContext::CustomContext;
+};
+
+static const Vector3 kMin { -10, -10, 0 }, kMax { 10, 10, 10 };
+
+static void actionSelectSystem(Engine &ctx, Entity e, Position &pos, Action &action)
+{
+    Game &g = ctx.data();
+    if (action.remainingTime > 0) {
+        action.remainingTime -= kDeltaT;
+        return;
+    }
+    const Draw d { g.seed, (uint32_t)e.id, g.tickCount };
+    if (d.uniform(kDrawMoveProb) <= kMoveCutoff) {
+        Vector3 new_pos = pos + Vector3 { d.uniform(kDrawMoveX, -1.f, 1.f),
+                                          d.uniform(kDrawMoveY, -1.f, 1.f),
+                                          d.uniform(kDrawMoveZ, -1.f, 1.f) };
+        new_pos.x = clampRef(new_pos.x, kMin.x, kMax.x);
+        new_pos.y = clampRef(new_pos.y, kMin.y, kMax.y);
+        new_pos.z = clampRef(new_pos.x, kMin.z, kMax.z);
+        Vector3 pos_delta = new_pos - pos;
+        pos = Position { new_pos };
+        action.remainingTime = pos_delta.length() / kMoveSpeed;
+    }
+}
+
+static void casterSystem(Engine &ctx, Entity e, Action &action, Mana &mana)
+{
+    Game &g = ctx.data();
+    mana.mp += kManaRegenRate * kDeltaT;
+    if (action.remainingTime > 0) return;
+    if (mana.mp < kCastCost) return;
+    mana.mp -= kCastCost;
+    const Draw d { g.seed, (uint32_t)e.id, g.tickCount };
+    const Vector3 target { d.uniform(kDrawTargetX, kMin.x, kMax.x),
+                           d.uniform(kDrawTargetY, kMin.y, kMax.y),
+                           d.uniform(kDrawTargetZ, kMin.z, kMax.z) };
+    ctx.forEach(g.healthQuery, [&](Position &p, Health &h) {
+        if (target.distance(p) <= kBlastRadius) h.hp -= kBlastDamage;
+    });
+    action.remainingTime = kCastTime;
+}
+
+static void archerSystem(Engine &ctx, Entity e, Action &action, Quiver &quiver)
+{
+    Game &g = ctx.data();
+    if (action.remainingTime > 0 || quiver.numArrows == 0) return;
+    const uint32_t num_dragons = ctx.numMatches(g.dragonHealthQuery);
+    if (num_dragons > 0) {
+        const Draw d { g.seed, (uint32_t)e.id, g.tickCount };
+        const uint32_t idx = d.index(kDrawDragon, num_dragons);
+        uint32_t i = 0;
+        ctx.forEach(g.dragonHealthQuery, [&](Health &h, Mana &) {
+            if (i++ == idx) h.hp -= kArrowDamage;
+        });
+    }
+    quiver.numArrows -= 1;
+    action.remainingTime = kShootTime;
+}
+
+struct CleanupNode : NodeBase {
+    static TaskGraph::NodeID addToGraph(Context &, TaskGraph::Builder &builder,
+                                        Span<const TaskGraph::NodeID> deps)
+    {
+        return builder.addDefaultNode<CleanupNode>(deps);
+    }
+
+    void run(Context *ctx_base)
+    {
+        Engine &ctx = *static_cast<Engine *>(ctx_base);
+        Game &g = ctx.data();
+        ctx.forEach(g.cleanupQuery, [&](Entity e, Health &h) {
+            if (h.hp <= 0) ctx.makeEntityNow<CleanupTracker>(CleanupEntity { e });
+        });
+        std::vector<Entity> dead;
+        ctx.forEach(g.trackerQuery, [&](CleanupEntity &c) { dead.push_back(c); });
+        for (Entity e : dead) ctx.destroyEntityNow(e);
+        ctx.clearArchetype<CleanupTracker>();
+        g.tickCount += 1;
+    }
+};
+
+static void registerTypes(ECSRegistry &reg)
+{
+    reg.registerComponent<Position>();
+    reg.registerComponent<Health>();
+    reg.registerComponent<Action>();
+    reg.registerComponent<Mana>();
+    reg.registerComponent<Quiver>();
+    reg.registerComponent<CleanupEntity>();
+    reg.registerArchetype<Dragon>();
+    reg.registerArchetype<Knight>();
+    reg.registerArchetype<CleanupTracker>();
+}
+
+static void setupTasks(TaskGraph::Builder &b)
+{
+    auto act = b.addToGraph<ParallelForNode<Engine, actionSelectSystem, Entity, Position, Action>>({});
+    auto cast = b.addToGraph<ParallelForNode<Engine, casterSystem, Entity, Action, Mana>>({ act });
+    auto shoot = b.addToGraph<ParallelForNode<Engine, archerSystem, Entity, Action, Quiver>>({ act });
+    b.addToGraph<CleanupNode>({ cast, shoot });
+}
+
+Game::Game(Engine &ctx, uint32_t s, int32_t nd, int32_t nk, const float *dpos,
+           const float *dmana, const float *kpos, const int32_t *karrows)
+    : WorldBase(ctx), seed(s), tickCount(0)
+{
+    for (int32_t i = 0; i < nd; i++) {
+        ctx.makeEntityNow<Dragon>(
+            Position { Vector3 { dpos[3 * i], dpos[3 * i + 1], dpos[3 * i + 2] } },
+            Health { kDragonHP }, Action { 0.f }, Mana { dmana[i] });
+    }
+    for (int32_t i = 0; i < nk; i++) {
+        ctx.makeEntityNow<Knight>(
+            Position { Vector3 { kpos[3 * i], kpos[3 * i + 1], kpos[3 * i + 2] } },
+            Health { kKnightHP }, Action { 0.f }, Quiver { karrows[i] });
+    }
+    healthQuery = ctx.query<Position, Health>();
+    dragonHealthQuery = ctx.query<Health, Mana>();
+    cleanupQuery = ctx.query<Entity, Health>();
+    trackerQuery = ctx.query<CleanupEntity>();
+}
+
+struct RefWorld {
+    StateManager sm;
+    StateCache sc;
+    Game *game;
+    Engine *ctx;
+    TaskGraph *graph;
+};
+
+}
+
+using namespace reffvs;
+
+extern "C" {
+
+struct RefFvsRow {
+    uint32_t gen;
+    int32_t id;
+    float pos[3];
+    int32_t hp;
+    float remaining;
+    uint32_t extra;
+};
+
+MADRONA_EXPORT void *ref_fvs_create(int32_t num_worlds, int32_t nd, int32_t nk,
+                                    const float *dpos, const float *dmana,
+                                    const float *kpos, const int32_t *karrows,
+                                    int32_t first_world_index)
+{
+    auto *v = new std::vector<RefWorld *>();
+    for (int32_t w = 0; w < num_worlds; w++) {
+        auto *rw = new RefWorld {};
+        ECSRegistry reg(&rw->sm, nullptr);
+        registerTypes(reg);
+        rw->game = (Game *)::operator new(sizeof(Game));
+        rw->ctx = new Engine(rw->game, WorkerInit { &rw->sm, &rw->sc });
+        new (rw->game) Game(*rw->ctx, (uint32_t)(first_world_index + w), nd, nk,
+                            dpos + (size_t)w * nd * 3, dmana + (size_t)w * nd,
+                            kpos + (size_t)w * nk * 3, karrows + (size_t)w * nk);
+        TaskGraph::Builder builder(*rw->ctx);
+        setupTasks(builder);
+        rw->graph = new TaskGraph(builder.build());
+        v->push_back(rw);
+    }
+    return v;
+}
+
+MADRONA_EXPORT void ref_fvs_step(void *handle, int32_t num_ticks)
+{
+    auto *v = (std::vector<RefWorld *> *)handle;
+    for (int32_t t = 0; t < num_ticks; t++) {
+        for (RefWorld *rw : *v) rw->graph->run(rw->ctx);
+    }
+}
+
+// Rows of Dragon (arch 0) or Knight (arch 1) of one world, in table order.
+MADRONA_EXPORT int32_t ref_fvs_read(void *handle, int32_t world, int32_t arch,
+                                    RefFvsRow *out, int32_t cap)
+{
+    auto *v = (std::vector<RefWorld *> *)handle;
+    RefWorld *rw = (*v)[world];
+    int32_t n = 0;
+    auto put = [&](Entity e, Position &p, Health &h, Action &a, uint32_t extra) {
+        if (n < cap) {
+            out[n] = RefFvsRow { e.gen, e.id, { p.x, p.y, p.z }, h.hp, a.remainingTime, extra };
+        }
+        n++;
+    };
+    if (arch == 0) {
+        auto q = rw->ctx->query<Entity, Position, Health, Action, Mana>();
+        rw->ctx->forEach(q, [&](Entity e, Position &p, Health &h, Action &a, Mana &m) {
+            uint32_t bits;
+            memcpy(&bits, &m.mp, 4);
+            put(e, p, h, a, bits);
+        });
+    } else {
+        auto q = rw->ctx->query<Entity, Position, Health, Action, Quiver>();
+        rw->ctx->forEach(q, [&](Entity e, Position &p, Health &h, Action &a, Quiver &qv) {
+            put(e, p, h, a, (uint32_t)qv.numArrows);
+        });
+    }
+    return n;
+}
+
+}

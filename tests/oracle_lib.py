@@ -194,3 +194,65 @@ class ReferencePhys:
         out = np.zeros(self.cfg.maxContacts, CONTACT_DTYPE)
         self.lib.ref_phys_read_contacts(self.h, w, _vp(out))
         return out
+
+
+# ---------------------------------------------------------------------------
+# fantasy_vs (C5): oracle/fvs_oracle.cpp and the reference ECS (oracle/ref_fvs.cpp)
+# ---------------------------------------------------------------------------
+FVS_ROW_DTYPE = np.dtype([("gen", np.uint32), ("id", np.int32), ("pos", np.float32, 3),
+                          ("hp", np.int32), ("remaining", np.float32), ("extra", np.uint32)])
+
+
+def gen_fvs_inits(num_worlds, num_dragons=50, num_knights=200, seed=0):
+    lib = load_orc()
+    dpos = np.zeros((num_worlds, num_dragons, 3), np.float32)
+    dmana = np.zeros((num_worlds, num_dragons), np.float32)
+    kpos = np.zeros((num_worlds, num_knights, 3), np.float32)
+    karrows = np.zeros((num_worlds, num_knights), np.int32)
+    lib.orc_gen_fvs_inits(num_worlds, num_dragons, num_knights, ctypes.c_uint32(seed),
+                          _vp(dpos), _vp(dmana), _vp(kpos), _vp(karrows))
+    return {"dragon_pos": dpos, "dragon_mana": dmana, "knight_pos": kpos,
+            "knight_arrows": karrows}
+
+
+class _FvsBase:
+    prefix = None
+
+    def __init__(self, lib, inits, first_world_index=0):
+        self.lib = lib
+        self.inits = {k: np.ascontiguousarray(v) for k, v in inits.items()}
+        self.num_worlds, self.nd = self.inits["dragon_mana"].shape
+        self.nk = self.inits["knight_arrows"].shape[1]
+        create = getattr(lib, self.prefix + "_create")
+        create.restype = ctypes.c_void_p
+        self.h = create(self.num_worlds, self.nd, self.nk, _vp(self.inits["dragon_pos"]),
+                        _vp(self.inits["dragon_mana"]), _vp(self.inits["knight_pos"]),
+                        _vp(self.inits["knight_arrows"]), first_world_index)
+        getattr(lib, self.prefix + "_step").argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        getattr(lib, self.prefix + "_read").argtypes = [ctypes.c_void_p, ctypes.c_int32,
+                                                        ctypes.c_int32, ctypes.c_void_p,
+                                                        ctypes.c_int32]
+
+    def step(self, n=1):
+        getattr(self.lib, self.prefix + "_step")(self.h, n)
+
+    def table(self, w, arch):
+        """Rows of Dragon (arch 0) / Knight (arch 1) in table order."""
+        cap = self.nd + self.nk
+        out = np.zeros(cap, FVS_ROW_DTYPE)
+        n = getattr(self.lib, self.prefix + "_read")(self.h, w, arch, _vp(out), cap)
+        return out[:n]
+
+
+class OracleFvs(_FvsBase):
+    prefix = "orc_fvs"
+
+    def __init__(self, inits, first_world_index=0):
+        super().__init__(load_orc(), inits, first_world_index)
+
+
+class ReferenceFvs(_FvsBase):
+    prefix = "ref_fvs"
+
+    def __init__(self, inits, first_world_index=0):
+        super().__init__(load_ref(), inits, first_world_index)
