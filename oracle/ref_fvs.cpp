@@ -19,6 +19,7 @@
 
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 using namespace madrona;
@@ -229,6 +230,24 @@ MADRONA_EXPORT void ref_fvs_step(void *handle, int32_t num_ticks)
     for (int32_t t = 0; t < num_ticks; t++) {
         for (RefWorld *rw : *v) rw->graph->run(rw->ctx);
     }
+}
+
+// World-parallel over host threads (the reference ThreadPoolExecutor's job
+// model, src/mw/cpu_exec.cpp:244-284): worlds are independent.
+MADRONA_EXPORT void ref_fvs_step_mt(void *handle, int32_t num_ticks, int32_t num_threads)
+{
+    auto *v = (std::vector<RefWorld *> *)handle;
+    const int32_t W = (int32_t)v->size();
+    std::vector<std::thread> pool;
+    for (int32_t t = 0; t < num_threads; t++) {
+        pool.emplace_back([=]() {
+            for (int32_t w = t; w < W; w += num_threads) {
+                RefWorld *rw = (*v)[w];
+                for (int32_t s = 0; s < num_ticks; s++) rw->graph->run(rw->ctx);
+            }
+        });
+    }
+    for (auto &th : pool) th.join();
 }
 
 // Rows of Dragon (arch 0) or Knight (arch 1) of one world, in table order.

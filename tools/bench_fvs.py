@@ -1,0 +1,143 @@
+#!/usr/bin/env python3
+"""Benchmark of the fantasy_vs workload (BASELINE.json configs[4]: 16 384
+worlds x 50 dragons + 200 knights, deaths destroy entities) on one MI355X.
+Same JSON contract as bench.py; a step = one tick of every world (action
+select, casters, archers, cleanup with device-side destroy / ID release).
+Timed window: ticks warmup+1 .. warmup+K from the reference init, which
+covers the dragons' deaths when K + warmup >= ~1500.
+
+    python tools/bench_fvs.py [--worlds 16384 --steps 1500 --warmup 5]
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
+
+HBM_PEAK_GBS = 8000.0
+# Algorithmic bytes per launch and world (Entity 8,
+# Position 12, Health 64 (cache-line aligned), Action 4, Mana / Quiver 4).
+# The three ParallelForNodes are timed together, so their bytes are averaged:
+# actionSelect reads Entity + Position + Action and writes Position + Action
+# on every row, the caster reads Entity + Action + Mana and writes Mana on
+# dragon rows, the archer reads Entity + Action + Quiver on knight rows.
+def world_bytes(node, nd, nk):
+    if node == "ParallelForNode":
+        return ((nd + nk) * (8 + 2 * 12 + 2 * 4) + nd * (8 + 4 + 2 * 4) + nk * (8 + 4 + 4)) / 3
+    return (nd + nk) * (8 + 64)                     # cleanup scan: Entity + Health
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--worlds", type=int, default=16384)
+    p.add_argument("--steps", type=int, default=1500)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--dragons", type=int, default=50)
+    p.add_argument("--knights", type=int, default=200)
+    p.add_argument("--cpu-worlds", type=int, default=512)
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
+    return p.parse_args()
+
+
+def cpu_child(args):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as ol
+    inits = ol.gen_fvs_inits(args.cpu_worlds, args.dragons, args.knights, seed=0)
+    threads = max(1, args.cpu_threads)
+    if ol.ref_available():
+        ref = ol.ReferenceFvs(inits)
+        ref.lib.ref_fvs_step_mt.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+        ref.lib.ref_fvs_step_mt(ref.h, args.warmup, threads)
+        t0 = time.perf_counter()
+        ref.lib.ref_fvs_step_mt(ref.h, args.steps, threads)
+        dt = time.perf_counter() - t0
+        kind = "reference"
+    else:
+        orc = ol.OracleFvs(inits)
+        orc.step(args.warmup)
+        t0 = time.perf_counter()
+        orc.step(args.steps)
+        dt = time.perf_counter() - t0
+        kind = "port"
+        threads = 1
+    print(json.dumps({"kind": kind, "seconds": dt, "threads": threads}))
+
+
+def main():
+    args = parse()
+    if args.cpu_child:
+        return cpu_child(args)
+    import madrona_mi355x as mw
+    W = args.worlds
+    inits = mw.gen_fvs_inits(W, args.dragons, args.knights, seed=0)
+    sim = mw.FvsSim(W, inits)
+
+    node_ms = {}
+    for name in ("ParallelForNode", "PerWorldNode"):
+        node_ms[name] = sim.time_node(name, 1)     # untimed pre-roll (2 ticks)
+    # restart from the init so the timed window is ticks warmup+1..warmup+K
+    sim.close()
+    sim = mw.FvsSim(W, inits)
+    dom = max(node_ms, key=lambda n: node_ms[n] * (3 if n == "ParallelForNode" else 1))
+    sim.set_timed_node(dom)
+    for _ in range(args.warmup):
+        sim.step(1)
+    ms0, n0 = sim.timed_node()
+    sim.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sim.step(1)
+    sim.sync()
+    elapsed = time.perf_counter() - t0
+    ms1, n1 = sim.timed_node()
+    flags = sim.error_flags()
+    alive = sum(sim.num_rows(w, 0) for w in range(0, W, max(1, W // 64)))
+
+    launch_ms = (ms1 - ms0) / max(1, n1 - n0)
+    nbytes = W * world_bytes(dom, args.dragons, args.knights)
+    achieved = nbytes / (launch_ms * 1e-3) / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child",
+                            "--cpu-worlds", str(args.cpu_worlds), "--cpu-threads",
+                            str(args.cpu_threads), "--steps", str(args.steps), "--warmup",
+                            str(args.warmup), "--dragons", str(args.dragons), "--knights",
+                            str(args.knights)], capture_output=True, text=True, timeout=1200)
+        if r.returncode == 0:
+            res = json.loads(r.stdout.strip().splitlines()[-1])
+            cpu = {"value": round(args.cpu_worlds * args.steps / res["seconds"], 1),
+                   "unit": "env-steps/s", "cores": res["threads"], "kind": res["kind"],
+                   "sample": f"fantasy_vs {args.cpu_worlds} worlds x ({args.dragons} dragons + "
+                             f"{args.knights} knights), ticks {args.warmup + 1}-"
+                             f"{args.warmup + args.steps}, {res['threads']} host threads, "
+                             f"{res['seconds']:.2f} s"}
+    out = {
+        "metric": "env-steps/sec (summed worlds)", "value": round(W * args.steps / elapsed, 1),
+        "unit": "env-steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32+i32",
+        "data": "synthetic (reference example init, mt19937 seed 0; counter-based in-tick draws)",
+        "config": {"workload": f"examples/fantasy_vs restated: {W} worlds x ({args.dragons} "
+                               f"dragons + {args.knights} knights), Game::tick with cleanup",
+                   "timed_ticks": f"{args.warmup + 1}-{args.warmup + args.steps}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": None, "ms_per_launch": round(launch_ms, 4),
+                     "bytes_per_launch": int(nbytes)},
+        "cpu_baseline": cpu, "error_flags": flags,
+        "nodes_ms_per_launch_preroll": {k: round(v, 4) for k, v in node_ms.items()},
+        "dragons_alive_sampled_worlds": int(alive),
+    }
+    print(json.dumps(out))
+    sim.close()
+
+
+if __name__ == "__main__":
+    main()
