@@ -6,7 +6,8 @@
 //   actionSelect  ParallelForNode<Entity, Position, Action>   (fvs.cpp:111-151)
 //   caster        ParallelForNode<Entity, Action, Mana>       (fvs.cpp:153-190)
 //   archer        ParallelForNode<Entity, Action, Quiver>     (fvs.cpp:192-214)
-//   cleanup       PerWorldNode                                (fvs.cpp:224-239)
+//   cleanup       ParallelForNode<Entity, Health> marks the dead, then a
+//                 PerWorldNode replays fvs.cpp:224-239 on them  (see below)
 // The reference draws from a racy thread_local mt19937 inside systems; here
 // every draw is a counter-based hash of (world, entity id, tick, draw index)
 // (SURVEY.md §8d), so any executor (this one, oracle/fvs_oracle.cpp,
@@ -72,8 +73,7 @@ struct Game : public WorldBase {
         reg.registerFixedSizeArchetype<Dragon>(cfg.c.num_dragons);
         reg.registerFixedSizeArchetype<Knight>(cfg.c.num_knights);
         reg.registerFixedSizeArchetype<CleanupTracker>(cfg.c.num_dragons + cfg.c.num_knights);
-        reg.exportColumn<Dragon, Health>(0);
-        reg.exportColumn<Knight, Health>(1);
+        // the reference example exports nothing (no learner hand-off)
     }
 
     static void setupTasks(TaskGraph::Builder &builder, const Config &)
@@ -84,7 +84,9 @@ struct Game : public WorldBase {
             ParallelForNode<Engine, casterSystem, Entity, Action, Mana>>({ act });
         auto shoot = builder.addToGraph<
             ParallelForNode<Engine, archerSystem, Entity, Action, Quiver>>({ act });
-        builder.addToGraph<PerWorldNode<Engine, cleanupSystem>>({ cast, shoot });
+        auto mark = builder.addToGraph<
+            ParallelForNode<Engine, markDeadSystem, Entity, Health>>({ cast, shoot });
+        builder.addToGraph<PerWorldNode<Engine, cleanupSystem>>({ mark });
     }
 
     Game(Engine &ctx, const Config &cfg, const mw_fvs_init &init);
@@ -92,7 +94,18 @@ struct Game : public WorldBase {
     static MW_HD void actionSelectSystem(Engine &ctx, Entity &e, Position &pos, Action &action);
     static MW_HD void casterSystem(Engine &ctx, Entity &e, Action &action, Mana &mana);
     static MW_HD void archerSystem(Engine &ctx, Entity &e, Action &action, Quiver &quiver);
+    static MW_HD void markDeadSystem(Engine &ctx, Entity &e, Health &h);
     static MW_HD void cleanupSystem(Engine &ctx);
+
+    // Entities found dead by markDeadSystem this tick, in arbitrary order;
+    // cleanupSystem restores the reference's query order (archetype, row).
+    static constexpr int32_t kMaxDead = 512;
+    struct Dead {
+        Entity e;
+        Loc loc;
+    };
+    int32_t numDead;
+    Dead dead[kMaxDead];
 
     uint32_t worldSeed;                  // global world index (shard-independent draws)
     uint32_t tickCount;
@@ -175,19 +188,48 @@ MW_HD void Game::archerSystem(Engine &ctx, Entity &e, Action &action, Quiver &qu
     action.remainingTime = kShootTime;
 }
 
+// The reference's cleanup (fvs.cpp:224-239) walks cleanupQuery serially and
+// makes a CleanupTracker for every entity with hp <= 0, then destroys them
+// all.  The walk is split: every row checks itself in parallel (this node),
+// and the per-world node below sorts the (few) hits back into the walk's
+// order -- query archetype order, then row -- before the serial part.
+MW_HD void Game::markDeadSystem(Engine &ctx, Entity &e, Health &h)
+{
+    if (h.hp > 0) return;
+    Game &g = ctx.data();
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int32_t slot = atomicAdd(&g.numDead, 1);
+#else
+    const int32_t slot = g.numDead++;
+#endif
+    if (slot < kMaxDead) g.dead[slot] = Dead { e, ctx.getLoc(e) };
+}
+
 MW_HD void Game::cleanupSystem(Engine &ctx)
 {                                                          // fvs.cpp:224-239
     Game &g = ctx.data();
-    ctx.forEach(g.cleanupQuery, [&](Entity &e, Health &h) {
-        if (h.hp <= 0) ctx.makeEntityNow<CleanupTracker>(CleanupEntity { e });
-    });
+    const int32_t n = g.numDead < kMaxDead ? g.numDead : kMaxDead;
+    if (g.numDead > kMaxDead) ctx.state().errorFlags[ctx.worldID().idx] |= 2;
+    for (int32_t i = 1; i < n; i++) {                     // insertion sort by (archetype, row)
+        const Dead d = g.dead[i];
+        int32_t j = i - 1;
+        while (j >= 0 && (g.dead[j].loc.archetype > d.loc.archetype ||
+                          (g.dead[j].loc.archetype == d.loc.archetype &&
+                           g.dead[j].loc.row > d.loc.row))) {
+            g.dead[j + 1] = g.dead[j];
+            j--;
+        }
+        g.dead[j + 1] = d;
+    }
+    for (int32_t i = 0; i < n; i++) ctx.makeEntityNow<CleanupTracker>(CleanupEntity { g.dead[i].e });
     StateView &st = ctx.state();
     const int32_t w = ctx.worldID().idx;
     const int32_t tracker = st.findArchetype(typeKey<CleanupTracker>());
-    const int32_t n = st.arch[tracker].numRows[w];
+    const int32_t m = st.arch[tracker].numRows[w];
     const CleanupEntity *dead = st.column<CleanupEntity>(tracker, 1, w);
-    for (int32_t i = 0; i < n; i++) ctx.destroyEntityNow(dead[i]);
+    for (int32_t i = 0; i < m; i++) ctx.destroyEntityNow(dead[i]);
     ctx.clearArchetype<CleanupTracker>();
+    g.numDead = 0;
     g.tickCount += 1;
 }
 
@@ -196,6 +238,7 @@ Game::Game(Engine &ctx, const Config &cfg, const mw_fvs_init &init)
 {                                                          // fvs.cpp:42-109
     worldSeed = (uint32_t)init.world_index;
     tickCount = 0;
+    numDead = 0;
     worldBounds = AABB { { -10, -10, 0 }, { 10, 10, 10 } };
     for (int32_t i = 0; i < cfg.c.num_dragons; i++) {
         ctx.makeEntityNow<Dragon>(
