@@ -8,6 +8,7 @@
 #include <madrona/physics.hpp>
 
 #include "../runtime/env_registry.hpp"
+#include "cube_assets.hpp"
 #include "../../../include/madrona_mw.h"
 
 #include <cfloat>
@@ -128,40 +129,6 @@ PhysWorld::PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &i
     bodyQuery = ctx.query<Position, ResponseType>();
 }
 
-// Object table: 0 = cube hull (half extent 1), 1 = ground plane.
-static ObjectManager *makeObjectManager(const mw_collisions_config &c)
-{
-    auto *mgr = new ObjectManager {};
-    mgr->numObjects = 2;
-    mgr->metadata = new RigidBodyMetadata[2];
-    mgr->aabbs = new AABB[2];
-    mgr->primitives = new CollisionPrimitive[2];
-
-    const Vector3 verts[8] = {
-        { -1, -1, -1 }, { 1, -1, -1 }, { 1, 1, -1 }, { -1, 1, -1 },
-        { -1, -1, 1 }, { 1, -1, 1 }, { 1, 1, 1 }, { -1, 1, 1 },
-    };
-    const uint32_t faces[6][4] = {
-        { 0, 3, 2, 1 }, { 4, 5, 6, 7 }, { 0, 1, 5, 4 },
-        { 3, 7, 6, 2 }, { 0, 4, 7, 3 }, { 1, 2, 6, 5 },
-    };
-    geometry::FastPolygonList pl {};
-    pl.allocate(6 * 5);
-    for (int f = 0; f < 6; f++) pl.addPolygon(Span<const uint32_t>(faces[f], 4));
-    mgr->primitives[0].type = CollisionPrimitive::Type::Hull;
-    mgr->primitives[0].hull.halfEdgeMesh.construct(pl, 8, verts);
-    pl.free();
-    mgr->metadata[0] = RigidBodyMetadata {
-        { c.cube_inv_inertia, c.cube_inv_inertia, c.cube_inv_inertia }, c.cube_inv_mass,
-        c.mu_s, c.mu_d };
-    mgr->aabbs[0] = AABB { { -1, -1, -1 }, { 1, 1, 1 } };
-
-    mgr->primitives[1].type = CollisionPrimitive::Type::Plane;
-    mgr->metadata[1] = RigidBodyMetadata { { 0.f, 0.f, 0.f }, 0.f, c.mu_s, c.mu_d };
-    mgr->aabbs[1] = AABB { { -FLT_MAX, -FLT_MAX, -FLT_MAX }, { FLT_MAX, FLT_MAX, 0.f } };
-    return mgr;
-}
-
 using Exec = TaskGraphExecutor<Engine, PhysWorld, Config, mw_collisions_init>;
 
 static Executor *create(const ExecConfig &ecfg, const void *user_cfg, size_t cfg_bytes,
@@ -172,7 +139,7 @@ static Executor *create(const ExecConfig &ecfg, const void *user_cfg, size_t cfg
     }
     Config cfg;
     memcpy(&cfg.c, user_cfg, sizeof(cfg.c));
-    cfg.objMgr = makeObjectManager(cfg.c);
+    cfg.objMgr = envs::makeCubeObjectManager(cfg.c);
     std::vector<mw_collisions_init> init_vec(ecfg.numWorlds);
     for (int32_t w = 0; w < ecfg.numWorlds; w++) {
         memcpy(&init_vec[w], (const char *)inits + (size_t)w * init_stride, sizeof(mw_collisions_init));

@@ -333,7 +333,9 @@ class CollisionsSim(Executor):
 
     def bodies(self, w):
         """Per-body state of world w in the oracle's record layout."""
-        A = BODY_ARCHETYPE
+        return self._bodies_of(BODY_ARCHETYPE, w)
+
+    def _bodies_of(self, A, w):
         out = np.zeros(self.num_bodies, BODY_DTYPE)
         ent = self.read_column(A, 0, w, np.uint32).reshape(-1, 2)
         n = len(ent)
@@ -443,3 +445,27 @@ class FvsSim(Executor):
 
     def num_rows(self, w, arch):
         return len(self.read_column(arch, 0, w, np.uint64))
+
+
+class SimpleSim(CollisionsSim):
+    """The `simple_taskgraph` environment: clamp + physics over two body
+    archetypes (Sphere: objects + test object, Agent)."""
+    SPHERE, AGENT = BODY_ARCHETYPE, BODY_ARCHETYPE + 1
+
+    def __init__(self, num_worlds, pos, rot, cfg=None, gpu_id=0, use_graph=True):
+        cfg = cfg or default_collisions_config(num_cubes=pos.shape[1])
+        self._pos = np.ascontiguousarray(pos, np.float32)
+        self._rot = np.ascontiguousarray(rot, np.float32)
+        inits = (CollisionsInit * num_worlds)()
+        for w in range(num_worlds):
+            inits[w].pos = self._pos.ctypes.data + w * cfg.num_cubes * 12
+            inits[w].rot = self._rot.ctypes.data + w * cfg.num_cubes * 16
+        self.cfg = cfg
+        self.num_bodies = cfg.num_cubes + 2
+        Executor.__init__(self, "simple_taskgraph", num_worlds, cfg, inits,
+                          ctypes.sizeof(CollisionsInit), gpu_id=gpu_id, default_capacity=64,
+                          use_graph=use_graph)
+
+    def bodies(self, w):
+        """Sphere rows then Agent rows (the reference query order)."""
+        return np.concatenate([self._bodies_of(self.SPHERE, w), self._bodies_of(self.AGENT, w)])

@@ -43,6 +43,19 @@ struct PhysicsBody : Archetype<
     solver::PreSolveVelocity, ExternalForce, ExternalTorque,
     broadphase::LeafID> {};
 
+// simple_taskgraph bodies (examples/simple_taskgraph/simple.hpp), same
+// physics column layout, two archetypes.
+struct SphereBody : Archetype<
+    Position, Rotation, Scale, Velocity, ObjectID, ResponseType,
+    solver::SubstepPrevState, solver::PreSolvePositional,
+    solver::PreSolveVelocity, ExternalForce, ExternalTorque,
+    broadphase::LeafID> {};
+struct AgentBody : Archetype<
+    Position, Rotation, Scale, Velocity, ObjectID, ResponseType,
+    solver::SubstepPrevState, solver::PreSolvePositional,
+    solver::PreSolveVelocity, ExternalForce, ExternalTorque,
+    broadphase::LeafID> {};
+
 struct RefPhysConfig {
     int32_t numCubes;
     int32_t numSubsteps;
@@ -64,7 +77,9 @@ class Engine;
 
 struct PhysWorld : public WorldBase {
     PhysWorld(Engine &ctx, ObjectManager *mgr, const RefPhysConfig &cfg,
-              const WorldInit &init);
+              const WorldInit &init, bool simple = false);
+
+    AABB worldBounds;
 };
 
 class Engine : public CustomContext<Engine, PhysWorld> {
@@ -79,6 +94,32 @@ static void registerWorldTypes(ECSRegistry &reg)
     reg.registerArchetype<PhysicsBody>();
 }
 
+// simple_taskgraph (examples/simple_taskgraph/simple.cpp:22-66), restated
+// with cube hulls: clamp Position to the world bounds, then physics.
+static void registerSimpleTypes(ECSRegistry &reg)
+{
+    base::registerTypes(reg);
+    RigidBodyPhysicsSystem::registerTypes(reg);
+    reg.registerArchetype<SphereBody>();
+    reg.registerArchetype<AgentBody>();
+}
+
+static inline float clampRef(float v, float lo, float hi)
+{
+    return v < lo ? lo : (hi < v ? hi : v);
+}
+
+static void clampSystem(Engine &ctx, Position &position);
+
+static void setupSimpleTasks(TaskGraph::Builder &builder, int32_t num_substeps)
+{
+    auto clamp = builder.addToGraph<ParallelForNode<Engine, clampSystem, Position>>({});
+    auto bp = RigidBodyPhysicsSystem::setupBroadphaseTasks(builder, { clamp });
+    auto sub = RigidBodyPhysicsSystem::setupSubstepTasks(builder, {bp},
+                                                         num_substeps);
+    RigidBodyPhysicsSystem::setupCleanupTasks(builder, {sub});
+}
+
 static void setupTasks(TaskGraph::Builder &builder, int32_t num_substeps)
 {
     auto bp = RigidBodyPhysicsSystem::setupBroadphaseTasks(builder, {});
@@ -87,12 +128,21 @@ static void setupTasks(TaskGraph::Builder &builder, int32_t num_substeps)
     RigidBodyPhysicsSystem::setupCleanupTasks(builder, {sub});
 }
 
+static void clampSystem(Engine &ctx, Position &position)
+{
+    const AABB &b = ctx.data().worldBounds;
+    position.x = clampRef(position.x, b.pMin.x, b.pMax.x);
+    position.y = clampRef(position.y, b.pMin.y, b.pMax.y);
+    position.z = clampRef(position.z, b.pMin.z, b.pMax.z);
+}
+
 PhysWorld::PhysWorld(Engine &ctx, ObjectManager *mgr,
-                     const RefPhysConfig &cfg, const WorldInit &init)
-    : WorldBase(ctx)
+                     const RefPhysConfig &cfg, const WorldInit &init, bool simple)
+    : WorldBase(ctx),
+      worldBounds { { -10, -10, 0 }, { 10, 10, 10 } }
 {
     RigidBodyPhysicsSystem::init(ctx, mgr, cfg.deltaT, cfg.numSubsteps,
-        Vector3 { 0.f, 0.f, cfg.gravityZ }, cfg.numCubes + 1,
+        Vector3 { 0.f, 0.f, cfg.gravityZ }, cfg.numCubes + (simple ? 2 : 1),
         cfg.maxContacts, 16);
 
     auto setup = [&](Entity e, Vector3 p, Quat q, int32_t obj,
@@ -113,6 +163,24 @@ PhysWorld::PhysWorld(Engine &ctx, ObjectManager *mgr,
         ctx.getUnsafe<broadphase::LeafID>(e) =
             RigidBodyPhysicsSystem::registerEntity(ctx, e, ObjectID { obj });
     };
+
+    if (simple) {                          // simple.cpp:94-117
+        for (int32_t i = 0; i < cfg.numCubes; i++) {
+            Entity e = ctx.makeEntityNow<SphereBody>();
+            Vector3 p { init.pos[3 * i], init.pos[3 * i + 1], init.pos[3 * i + 2] };
+            Quat q { init.rot[4 * i], init.rot[4 * i + 1], init.rot[4 * i + 2],
+                     init.rot[4 * i + 3] };
+            setup(e, p, q, 0, ResponseType::Dynamic);
+        }
+        Entity agent = ctx.makeEntityNow<AgentBody>();
+        setup(agent, Vector3 { 0, 0, 0 }, Quat::angleAxis(0.f, { 0, 1, 0 }), 0,
+              ResponseType::Dynamic);
+        Entity test = ctx.makeEntityNow<SphereBody>();
+        setup(test, Vector3 { -10, 0, 0 }, Quat::angleAxis(0.f, { 0, 1, 0 }), 0,
+              ResponseType::Dynamic);
+        ctx.getSingleton<broadphase::BVH>().rebuildOnUpdate();
+        return;
+    }
 
     for (int32_t i = 0; i < cfg.numCubes; i++) {
         Entity e = ctx.makeEntityNow<PhysicsBody>();
@@ -232,7 +300,7 @@ struct RefBodyState {
     uint32_t responseType;
 };
 
-MADRONA_EXPORT void * ref_phys_create(int32_t num_worlds,
+static void * createWorlds(bool simple, int32_t num_worlds,
                                       const RefPhysConfig *cfg,
                                       const float *init_pos,
                                       const float *init_rot)
@@ -244,7 +312,7 @@ MADRONA_EXPORT void * ref_phys_create(int32_t num_worlds,
     for (int32_t w = 0; w < num_worlds; w++) {
         auto *rw = new RefWorld {};
         ECSRegistry reg(&rw->sm, nullptr);
-        registerWorldTypes(reg);
+        if (simple) registerSimpleTypes(reg); else registerWorldTypes(reg);
 
         rw->world = (PhysWorld *)::operator new(sizeof(PhysWorld));
         rw->ctx = new Engine(rw->world, WorkerInit { &rw->sm, &rw->sc });
@@ -253,15 +321,33 @@ MADRONA_EXPORT void * ref_phys_create(int32_t num_worlds,
             init_pos + (size_t)w * cfg->numCubes * 3,
             init_rot + (size_t)w * cfg->numCubes * 4,
         };
-        new (rw->world) PhysWorld(*rw->ctx, h->mgr, *cfg, init);
+        new (rw->world) PhysWorld(*rw->ctx, h->mgr, *cfg, init, simple);
 
         TaskGraph::Builder builder(*rw->ctx);
-        setupTasks(builder, cfg->numSubsteps);
+        if (simple) setupSimpleTasks(builder, cfg->numSubsteps);
+        else setupTasks(builder, cfg->numSubsteps);
         rw->graph = new TaskGraph(builder.build());
         h->worlds.push_back(rw);
     }
 
     return h;
+}
+
+MADRONA_EXPORT void * ref_phys_create(int32_t num_worlds,
+                                      const RefPhysConfig *cfg,
+                                      const float *init_pos,
+                                      const float *init_rot)
+{
+    return createWorlds(false, num_worlds, cfg, init_pos, init_rot);
+}
+
+// simple_taskgraph worlds: cfg->numCubes objects + agent + test object.
+MADRONA_EXPORT void * ref_simple_create(int32_t num_worlds,
+                                        const RefPhysConfig *cfg,
+                                        const float *init_pos,
+                                        const float *init_rot)
+{
+    return createWorlds(true, num_worlds, cfg, init_pos, init_rot);
 }
 
 MADRONA_EXPORT void ref_phys_step(void *handle, int32_t num_steps)

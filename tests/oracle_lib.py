@@ -256,3 +256,21 @@ class ReferenceFvs(_FvsBase):
 
     def __init__(self, inits, first_world_index=0):
         super().__init__(load_ref(), inits, first_world_index)
+
+
+class ReferenceSimple(ReferencePhys):
+    """simple_taskgraph worlds on the reference (oracle/ref_harness.cpp):
+    numCubes objects + agent + test object, clamp node before physics."""
+
+    def __init__(self, cfg, pos, rot):
+        self.lib = load_ref()
+        self.lib.ref_simple_create.restype = ctypes.c_void_p
+        self.lib.ref_simple_create.argtypes = [ctypes.c_int32, ctypes.POINTER(PhysConfig),
+                                               ctypes.c_void_p, ctypes.c_void_p]
+        self.cfg = cfg
+        self.num_worlds = pos.shape[0]
+        self.nb = cfg.numCubes + 2
+        self._pos = np.ascontiguousarray(pos, np.float32)
+        self._rot = np.ascontiguousarray(rot, np.float32)
+        self.h = self.lib.ref_simple_create(self.num_worlds, ctypes.byref(cfg),
+                                            _vp(self._pos), _vp(self._rot))
