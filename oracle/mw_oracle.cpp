@@ -157,6 +157,10 @@ struct Config {
 };
 
 static constexpr uint32_t kBodyArchetype = 6;   // registration order, see DESIGN.md
+// simple_taskgraph (examples/simple_taskgraph/simple.cpp:37-49): Sphere is
+// registered where the collisions body archetype is, Agent right after it.
+static constexpr uint32_t kSphereArchetype = kBodyArchetype;
+static constexpr uint32_t kAgentArchetype = kBodyArchetype + 1;
 
 struct World {
     IDMap ids;
@@ -186,13 +190,26 @@ struct World {
     // trace (debug visibility for the GPU parity tests)
     std::vector<std::pair<Loc, Loc>> lastCandidates;
     std::vector<Contact> lastContacts;
+
+    // Body vector = query order: archetype by archetype, rows in table
+    // order.  agentBase = index of Agent row 0 (simple mode only).
+    int32_t agentBase = 0;
+    // Face manifolds that left contactPoints[2] or [3] unwritten in the
+    // reference (narrowphase.cpp:828-853): undefined there, zero here.
+    int32_t ubManifolds = 0;
 };
 
 struct Sim {
     Config cfg;
     Objects objs;
     std::vector<World> worlds;
+    bool simple = false;      // simple_taskgraph worlds: clamp node, two archetypes, no plane
 };
+
+static inline int32_t bodyIndex(const World &w, Loc l)
+{
+    return l.archetype == kAgentArchetype ? w.agentBase + l.row : l.row;
+}
 
 static int32_t numInternalNodes(int32_t num_leaves)     // broadphase.cpp:33-40
 {
@@ -207,7 +224,7 @@ static void initWorld(const Sim &sim, World &w, const float *pos, const float *r
     for (int i = 0; i < 3; i++) (void)w.ids.acquireID(w.initCache);
 
     // RigidBodyPhysicsSystem::init (physics.cpp:1012-1036)
-    int32_t max_leaves = cfg.numCubes + 1;
+    int32_t max_leaves = cfg.numCubes + (sim.simple ? 2 : 1);
     w.nodes.resize(numInternalNodes(max_leaves));
     w.leafEntities.resize(max_leaves);
     w.leafAABBs.resize(max_leaves);
@@ -221,9 +238,15 @@ static void initWorld(const Sim &sim, World &w, const float *pos, const float *r
     w.gMag = w.g.length();
     w.restThresh = 2.f * w.gMag * w.h;
 
-    auto make = [&](V3 p, Q q, int32_t obj, Response rt) {
+    if (sim.simple) {
+        w.bodies.resize(cfg.numCubes + 2);
+        w.agentBase = cfg.numCubes + 1;
+    }
+    int32_t sphere_rows = 0;
+    auto make = [&](V3 p, Q q, int32_t obj, Response rt, uint32_t arch = kBodyArchetype) {
         Entity e = w.ids.acquireID(w.worldCache);
-        int32_t row = (int32_t)w.bodies.size();
+        int32_t row = sim.simple ? (arch == kAgentArchetype ? 0 : sphere_rows++)
+                                 : (int32_t)w.bodies.size();
         Body b {};
         b.e = e;
         b.pos = p; b.rot = q; b.scale = { 1.f, 1.f, 1.f };
@@ -236,9 +259,25 @@ static void initWorld(const Sim &sim, World &w, const float *pos, const float *r
         int32_t leaf = w.numLeaves++;                    // BVH::reserveLeaf
         w.leafEntities[leaf] = e;
         b.leafID = leaf;
-        w.bodies.push_back(b);
-        w.ids.ref(e.id) = Loc { kBodyArchetype, row };
+        const Loc loc { arch, row };
+        if (sim.simple) w.bodies[bodyIndex(w, loc)] = b;
+        else w.bodies.push_back(b);
+        w.ids.ref(e.id) = loc;
     };
+
+    if (sim.simple) {                                    // simple.cpp:94-117
+        for (int32_t i = 0; i < cfg.numCubes; i++) {
+            make(V3 { pos[3 * i], pos[3 * i + 1], pos[3 * i + 2] },
+                 Q { rot[4 * i], rot[4 * i + 1], rot[4 * i + 2], rot[4 * i + 3] },
+                 0, Response::Dynamic, kSphereArchetype);
+        }
+        make(V3::zero(), Q { 1.f, 0.f, 0.f, 0.f }, 0, Response::Dynamic,
+             kAgentArchetype);
+        make(V3 { -10.f, 0.f, 0.f }, Q { 1.f, 0.f, 0.f, 0.f }, 0, Response::Dynamic,
+             kSphereArchetype);
+        w.forceRebuild = true;
+        return;
+    }
 
     for (int32_t i = 0; i < cfg.numCubes; i++) {
         make(V3 { pos[3 * i], pos[3 * i + 1], pos[3 * i + 2] },
@@ -450,7 +489,7 @@ static void findOverlapping(World &w)                     // broadphase.cpp:897-
                     Entity o = w.leafEntities[n.leafIDX(i)];
                     if (ba.e.id < o.id) {
                         Loc b_loc = w.ids.lookup(o);
-                        if (a_static && isStatic(w.bodies[b_loc.row])) continue;
+                        if (a_static && isStatic(w.bodies[bodyIndex(w, b_loc)])) continue;
                         w.candidates.push_back({ a_loc, b_loc });
                     }
                 } else {
@@ -626,7 +665,7 @@ static int clipPolygon(V3 *dst, Plane cp, const V3 *in, int n)   // :626-661
     return out;
 }
 
-struct Manifold { V3 cp[4]; float depth[4]; int32_t num; V3 normal; };
+struct Manifold { V3 cp[4]; float depth[4]; int32_t num; V3 normal; bool ub; };
 
 static Manifold buildFaceContactManifold(V3 n, V3 *contacts, float *depths, int num)
 {                                                          // narrowphase.cpp:790-864
@@ -654,6 +693,7 @@ static Manifold buildFaceContactManifold(V3 n, V3 *contacts, float *depths, int 
         V3 diff0 = m.cp[1] - p0;
         float largest_area = 0.0f;         // never updated in the reference
         int largest_area_idx = 0;
+        bool wrote2 = false, wrote3 = false;
         for (int i = 1; i < num; i++) {
             V3 c = contacts[i];
             V3 diff1 = c - p0;
@@ -661,6 +701,7 @@ static Manifold buildFaceContactManifold(V3 n, V3 *contacts, float *depths, int 
             if (area > largest_area) {
                 m.cp[2] = c; m.depth[2] = depths[i];
                 largest_area_idx = i;
+                wrote2 = true;
             }
         }
         contacts[largest_area_idx] = m.cp[0];
@@ -668,8 +709,12 @@ static Manifold buildFaceContactManifold(V3 n, V3 *contacts, float *depths, int 
             V3 c = contacts[i];
             V3 diff1 = c - p0;
             float area = n.dot(diff0.cross(diff1));
-            if (area < largest_area) { m.cp[3] = c; m.depth[3] = depths[i]; }
+            if (area < largest_area) { m.cp[3] = c; m.depth[3] = depths[i]; wrote3 = true; }
         }
+        // All points on one side of the p0-p1 line: the reference leaves a
+        // slot of its uninitialised Manifold unwritten (undefined value);
+        // the oracle and the HIP kernel define it as zero.
+        m.ub = !(wrote2 && wrote3);
     }
     const Q ident { 1, 0, 0, 0 };
     for (int i = 0; i < m.num; i++) m.cp[i] = ident.rotateVec(m.cp[i]) + V3::zero();
@@ -718,8 +763,8 @@ static void addManifold(World &w, const Manifold &m, Loc ref, Loc other)
 
 static void runNarrowphase(const Sim &sim, World &w, Loc a_loc, Loc b_loc)
 {                                                          // narrowphase.cpp:1515-1728
-    const Body *ba = &w.bodies[a_loc.row];
-    const Body *bb = &w.bodies[b_loc.row];
+    const Body *ba = &w.bodies[bodyIndex(w, a_loc)];
+    const Body *bb = &w.bodies[bodyIndex(w, b_loc)];
     uint32_t ta = (uint32_t)sim.objs.types[ba->objID];
     uint32_t tb = (uint32_t)sim.objs.types[bb->objID];
     if (ta > tb) {
@@ -804,6 +849,7 @@ static void runNarrowphase(const Sim &sim, World &w, Loc a_loc, Loc b_loc)
                 }
             }
             m = buildFaceContactManifold(ref_plane.normal, cin, depths, n_below);
+            w.ubManifolds += m.ub;
         } else {
             // createEdgeContact (narrowphase.cpp:1053-1121)
             ref_loc = a_loc;
@@ -847,6 +893,7 @@ static void runNarrowphase(const Sim &sim, World &w, Loc a_loc, Loc b_loc)
             }
         } while (hidx != start);
         Manifold m = buildFaceContactManifold(plane.normal, tmp1, depths, n);
+        w.ubManifolds += m.ub;
         if (m.num > 0) addManifold(w, m, b_loc, a_loc);
     } else {
         assert(false && "sphere / plane-plane narrowphase unsupported (reference asserts)");
@@ -938,8 +985,8 @@ static float applyPositionalUpdateFull(V3 &x1, V3 &x2, Q &q1, Q &q2, V3 r1, V3 r
 
 static void handleContact(const Sim &sim, World &w, Contact &c)  // physics.cpp:387-476
 {
-    Body &b1 = w.bodies[c.ref.row];
-    Body &b2 = w.bodies[c.alt.row];
+    Body &b1 = w.bodies[bodyIndex(w, c.ref)];
+    Body &b2 = w.bodies[bodyIndex(w, c.alt)];
     V3 prev1p = b1.prevPos, prev2p = b2.prevPos;
     Q prev1q = b1.prevRot, prev2q = b2.prevRot;
     V3 ps1x = b1.psX, ps2x = b2.psX;
@@ -1049,8 +1096,8 @@ static void applyVelocityUpdate(V3 &v1, V3 &v2, V3 &o1, V3 &o2, Q q1, Q q2,
 
 static void solveVelocitiesForContact(const Sim &sim, World &w, const Contact &c)
 {                                                          // physics.cpp:865-993
-    Body &b1 = w.bodies[c.ref.row];
-    Body &b2 = w.bodies[c.alt.row];
+    Body &b1 = w.bodies[bodyIndex(w, c.ref)];
+    Body &b2 = w.bodies[bodyIndex(w, c.alt)];
     Q q1 = b1.rot, q2 = b2.rot;
     V3 ps1x = b1.psX, ps2x = b2.psX;
     Q ps1q = b1.psQ, ps2q = b2.psQ;
@@ -1133,8 +1180,20 @@ static void solveVelocities(const Sim &sim, World &w)     // physics.cpp:995-100
 // One taskgraph step (node order of setupBroadphaseTasks / setupSubstepTasks /
 // setupCleanupTasks; see DESIGN.md §2 for the table)
 // ---------------------------------------------------------------------------
+static float clampRef(float v, float lo, float hi)        // std::clamp
+{
+    return v < lo ? lo : (hi < v ? hi : v);
+}
+
 static void stepWorld(const Sim &sim, World &w)
 {
+    if (sim.simple) {                                     // 0 clampSystem (simple.cpp:22-35)
+        for (Body &b : w.bodies) {
+            b.pos.x = clampRef(b.pos.x, -10.f, 10.f);
+            b.pos.y = clampRef(b.pos.y, -10.f, 10.f);
+            b.pos.z = clampRef(b.pos.z, 0.f, 10.f);
+        }
+    }
     updateLeafPositions(sim, w);                          // 1 updateLeafPositionsEntry
     if (w.forceRebuild) {                                 // 2 updateBVHEntry
         w.forceRebuild = false;
@@ -1332,6 +1391,33 @@ int32_t orc_phys_read_contacts(void *handle, int32_t world, void *out, int32_t c
     int32_t n = (int32_t)w.lastContacts.size();
     memcpy(out, w.lastContacts.data(), sizeof(Contact) * std::min(n, cap));
     return n;
+}
+
+// Cumulative count of face manifolds whose reference result is undefined
+// (see buildFaceContactManifold); parity against the live reference holds
+// only while this is zero.
+__attribute__((visibility("default")))
+int32_t orc_phys_ub_manifolds(void *handle, int32_t world)
+{
+    return ((Sim *)handle)->worlds[world].ubManifolds;
+}
+
+// simple_taskgraph worlds (examples/simple_taskgraph/simple.cpp): numCubes
+// objects + agent (Agent archetype) + test object; clamp before physics.
+__attribute__((visibility("default")))
+void *orc_simple_create(int32_t num_worlds, const Config *cfg,
+                        const float *pos, const float *rot)
+{
+    auto *sim = new Sim {};
+    sim->cfg = *cfg;
+    sim->simple = true;
+    sim->objs = makeObjects(*cfg);
+    sim->worlds.resize(num_worlds);
+    for (int32_t w = 0; w < num_worlds; w++) {
+        initWorld(*sim, sim->worlds[w], pos + (size_t)w * cfg->numCubes * 3,
+                  rot + (size_t)w * cfg->numCubes * 4);
+    }
+    return sim;
 }
 
 __attribute__((visibility("default")))

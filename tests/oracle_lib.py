@@ -91,6 +91,10 @@ def load_orc():
         lib.orc_phys_read_contacts.argtypes = [ctypes.c_void_p, ctypes.c_int32,
                                                ctypes.c_void_p, ctypes.c_int32]
         lib.orc_phys_destroy.argtypes = [ctypes.c_void_p]
+        lib.orc_simple_create.restype = ctypes.c_void_p
+        lib.orc_simple_create.argtypes = lib.orc_phys_create.argtypes
+        lib.orc_phys_ub_manifolds.restype = ctypes.c_int32
+        lib.orc_phys_ub_manifolds.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         lib.orc_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
                                                  ctypes.c_void_p, ctypes.c_void_p]
         _ORC = lib
@@ -154,11 +158,31 @@ class OraclePhys:
         n = self.lib.orc_phys_read_contacts(self.h, w, _vp(out), self.cfg.maxContacts)
         return out[:n]
 
+    def ub_manifolds(self, w):
+        """Face manifolds so far whose reference value is undefined (an
+        unwritten Manifold slot, narrowphase.cpp:828-853)."""
+        return int(self.lib.orc_phys_ub_manifolds(self.h, w))
+
     def __del__(self):
         try:
             self.lib.orc_phys_destroy(self.h)
         except Exception:
             pass
+
+
+class OracleSimple(OraclePhys):
+    """simple_taskgraph worlds on the restated oracle (orc_simple_create):
+    body order = Sphere rows (objects, then the test object), Agent row."""
+
+    def __init__(self, cfg, pos, rot):
+        self.lib = load_orc()
+        self.lib.orc_simple_create.restype = ctypes.c_void_p
+        self.cfg = cfg
+        self.num_worlds = pos.shape[0]
+        self.nb = cfg.numCubes + 2
+        pos = np.ascontiguousarray(pos, np.float32)
+        rot = np.ascontiguousarray(rot, np.float32)
+        self.h = self.lib.orc_simple_create(self.num_worlds, ctypes.byref(cfg), _vp(pos), _vp(rot))
 
 
 class ReferencePhys:

@@ -1,7 +1,15 @@
 """GPU parity for simple_taskgraph (BASELINE.json configs[0] / [1]): clamp
 ParallelForNode + rigid-body physics over two body archetypes (Sphere,
-Agent), against the reference itself (oracle/_ref simple worlds, live when
-present) and the golden fixtures generated from it.  Bit-exact bodies."""
+Agent).  Bit-exact bodies against
+
+  * the reference's own golden snapshots (steps 1, 10, 50: before any face
+    manifold whose reference value is undefined, see test_simple_oracle.py);
+  * the live reference (oracle/_ref) on every step before the oracle reports
+    the first such manifold in a world;
+  * the oracle (oracle/mw_oracle.cpp simple mode, pinned to the reference
+    above) on every step, through and past those manifolds, and its golden
+    snapshot at step 150.
+"""
 import os
 
 import numpy as np
@@ -20,36 +28,50 @@ def _mw():
     return mw
 
 
-def test_simple_taskgraph_matches_reference_golden():
+def test_simple_taskgraph_matches_golden():
     mw = _mw()
     g = np.load(GOLDEN)
     gcfg, _ = _cfg_pair(num_cubes=100)
     W = g["pos"].shape[0]
     sim = mw.SimpleSim(W, g["pos"], g["rot"], gcfg)
     done = 0
-    for s in (1, 10, 60):
+    for s in (1, 10, 50, 150):
         sim.step(s - done)
         done = s
         assert sim.error_flags() == 0, mw.ERR_BITS
         for w in range(W):
-            d = _diff(sim.bodies(w), g[f"s{s}/w{w}"])
-            assert d is None, f"step {s} world {w}: {d}"
+            key = f"s{s}/w{w}" if f"s{s}/w{w}" in g else f"orc_s{s}/w{w}"
+            d = _diff(sim.bodies(w), g[key])
+            assert d is None, f"{key}: {d}"
 
 
-@pytest.mark.skipif(not ol.ref_available(), reason="reference build absent")
-def test_simple_taskgraph_matches_live_reference_long():
+@pytest.mark.parametrize("nsub,seed", [(4, 9), (1, 0)])
+def test_simple_taskgraph_matches_oracle_and_reference(nsub, seed):
     mw = _mw()
-    gcfg, ocfg = _cfg_pair(num_cubes=100)
-    W = 6
-    pos, rot = ol.gen_collisions_inits(W, 100, seed=9)
+    gcfg, ocfg = _cfg_pair(num_cubes=100, num_substeps=nsub)
+    W, STEPS = 6, 200
+    pos, rot = ol.gen_collisions_inits(W, 100, seed=seed)
     sim = mw.SimpleSim(W, pos, rot, gcfg)
-    ref = ol.ReferenceSimple(ocfg, pos, rot)
-    for chunk in range(10):
-        sim.step(20)
-        ref.step(20)
+    orc = ol.OracleSimple(ocfg, pos, rot)
+    ref = ol.ReferenceSimple(ocfg, pos, rot) if ol.ref_available() else None
+    live = [True] * W
+    for s in range(1, STEPS + 1):
+        sim.step(1)
+        orc.step(1)
+        if ref is not None and any(live):
+            ref.step(1)
         for w in range(W):
-            d = _diff(sim.bodies(w), ref.bodies(w))
-            assert d is None, f"step {20 * (chunk + 1)} world {w}: {d}"
+            got = sim.bodies(w)
+            d = _diff(got, orc.bodies(w))
+            assert d is None, f"vs oracle, step {s} world {w}: {d}"
+            if live[w] and orc.ub_manifolds(w):
+                live[w] = False
+            if ref is not None and live[w]:
+                d = _diff(got, ref.bodies(w))
+                assert d is None, f"vs reference, step {s} world {w}: {d}"
+        if s % 50 == 0:
+            assert sim.error_flags() == 0, mw.ERR_BITS
+    assert not all(live), "no world reached an undefined manifold: UB path not covered"
 
 
 def test_simple_taskgraph_full_size_runs_clean():
