@@ -73,7 +73,7 @@ def gen_collisions_inits(num_worlds, num_cubes=128, seed=0):
 
 
 _ORC = None
-_REF = None
+_REF = {}
 
 
 def load_orc():
@@ -105,10 +105,16 @@ def ref_available():
     return os.path.exists(REF_PATH)
 
 
-def load_ref():
-    global _REF
-    if _REF is None:
-        lib = ctypes.CDLL(REF_PATH)
+def load_ref(image="main"):
+    """The reference harness.  The reference's type registry is process-global
+    (src/common/type_tracker.cpp:87-160: IDs in first-registration order), so
+    simple_taskgraph worlds get their own image of the library
+    (oracle/Makefile.ref), as each reference example is its own binary; in a
+    shared image their archetype IDs would depend on which env ran first."""
+    key = image
+    if key not in _REF:
+        path = REF_PATH if image == "main" else REF_PATH.replace(".so", f"_{image}.so")
+        lib = ctypes.CDLL(path)
         lib.ref_phys_create.restype = ctypes.c_void_p
         lib.ref_phys_create.argtypes = [ctypes.c_int32, ctypes.POINTER(PhysConfig),
                                         ctypes.c_void_p, ctypes.c_void_p]
@@ -116,8 +122,8 @@ def load_ref():
         lib.ref_phys_read_bodies.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
         lib.ref_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 4
         lib.ref_phys_read_contacts.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
-        _REF = lib
-    return _REF
+        _REF[key] = lib
+    return _REF[key]
 
 
 class OraclePhys:
@@ -287,7 +293,7 @@ class ReferenceSimple(ReferencePhys):
     numCubes objects + agent + test object, clamp node before physics."""
 
     def __init__(self, cfg, pos, rot):
-        self.lib = load_ref()
+        self.lib = load_ref("simple")
         self.lib.ref_simple_create.restype = ctypes.c_void_p
         self.lib.ref_simple_create.argtypes = [ctypes.c_int32, ctypes.POINTER(PhysConfig),
                                                ctypes.c_void_p, ctypes.c_void_p]
