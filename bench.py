@@ -168,17 +168,19 @@ def main():
     if world_size != args.gpus and world_size > 1:
         print(f"warning: WORLD_SIZE={world_size} != --gpus {args.gpus}", file=sys.stderr)
 
-    # The framework owns the GPU in this process: device memory, the step
-    # stream, and the hand-off collective (RCCL over xGMI from the C ABI).
-    # torch is used on the CPU only (gloo rendezvous, barrier, max-reduce):
-    # initialising torch's own HIP context next to the framework's mixes two
-    # HIP runtime builds in one process (madrona_mi355x/__init__.py).
+    # The framework owns the step stream and the hand-off collective (RCCL
+    # over xGMI from the C ABI, enqueued right behind the step); the hand-off
+    # lands in a learner-owned torch tensor on the same device.  torch and the
+    # framework share one HIP runtime (madrona_mi355x imports torch first);
+    # the timing barrier / max-reduce run over gloo on the CPU.
     import madrona_mi355x as mw
+    import torch
     from madrona_mi355x.sharding import bootstrap_rccl, world_shard
     dist = None
     if world_size > 1:
         import torch.distributed as dist
         dist.init_process_group(backend="gloo")
+    torch.cuda.set_device(local_rank)
 
     cfg = mw.default_collisions_config(args.cubes, args.substeps, max_contacts=4096,
                                        max_candidates=4096)
@@ -189,8 +191,9 @@ def main():
 
     if dist is not None:
         bootstrap_rccl(sim, rank, world_size)
-    # per-world returns of every rank, in world order (device memory)
-    handoff = sim.device_alloc(4 * W * world_size)
+    # per-world returns of every rank, in world order: a torch tensor
+    returns = torch.empty(W * world_size, dtype=torch.float32, device=f"cuda:{local_rank}")
+    handoff = returns.data_ptr()
 
     def step():
         if args.no_handoff:
@@ -243,7 +246,6 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -309,7 +311,8 @@ def main():
             "nodes": node_table,
         }
         print(json.dumps(out))
-    sim.device_free(handoff)
+    assert bool(torch.isfinite(returns).all()), "non-finite returns in the hand-off tensor"
+    del returns
     sim.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -9,12 +9,47 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstring>
 #include <exception>
 #include <map>
 #include <string>
 #include <vector>
+
+// RCCL is resolved at first use (dlopen of librccl.so.1) rather than linked:
+// a process that already holds an RCCL (PyTorch's bundled one) shares it and
+// its HIP runtime instead of mapping a second copy next to it.
+struct RcclApi {
+    ncclResult_t (*getUniqueId)(ncclUniqueId *);
+    ncclResult_t (*commInitRank)(ncclComm_t *, int, ncclUniqueId, int);
+    ncclResult_t (*allGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t,
+                              hipStream_t);
+    ncclResult_t (*commDestroy)(ncclComm_t);
+    const char *(*getErrorString)(ncclResult_t);
+};
+
+static const RcclApi &rccl()
+{
+    static RcclApi api = []() {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) throw std::runtime_error(std::string("RCCL unavailable: ") + dlerror());
+        auto sym = [h](const char *name) {
+            void *f = dlsym(h, name);
+            if (!f) throw std::runtime_error(std::string("RCCL symbol missing: ") + name);
+            return f;
+        };
+        RcclApi a;
+        a.getUniqueId = (decltype(a.getUniqueId))sym("ncclGetUniqueId");
+        a.commInitRank = (decltype(a.commInitRank))sym("ncclCommInitRank");
+        a.allGather = (decltype(a.allGather))sym("ncclAllGather");
+        a.commDestroy = (decltype(a.commDestroy))sym("ncclCommDestroy");
+        a.getErrorString = (decltype(a.getErrorString))sym("ncclGetErrorString");
+        return a;
+    }();
+    return api;
+}
 
 namespace madrona {
 namespace phys { PhysArgs *physicsArgs(StateManager &mgr); }
@@ -142,7 +177,7 @@ int mw_destroy(mw_exec *exec)
 {
     MW_TRY({
         if (exec) {
-            if (exec->comm) (void)ncclCommDestroy(exec->comm);
+            if (exec->comm) (void)rccl().commDestroy(exec->comm);
             delete exec->exec;
             delete exec;
         }
@@ -159,7 +194,7 @@ const char *mw_last_error(void) { return g_last_error.c_str(); }
 #define MW_NCCL_OK(expr)                                                     \
     do {                                                                     \
         ncclResult_t r__ = (expr);                                           \
-        if (r__ != ncclSuccess) throw std::runtime_error(ncclGetErrorString(r__)); \
+        if (r__ != ncclSuccess) throw std::runtime_error(rccl().getErrorString(r__)); \
     } while (0)
 
 static_assert(sizeof(ncclUniqueId) == MW_RCCL_ID_BYTES, "RCCL unique id size");
@@ -168,7 +203,7 @@ int mw_rccl_get_unique_id(void *id_out)
 {
     MW_TRY({
         ncclUniqueId id;
-        MW_NCCL_OK(ncclGetUniqueId(&id));
+        MW_NCCL_OK(rccl().getUniqueId(&id));
         memcpy(id_out, &id, sizeof(id));
         return 0;
     }, -1)
@@ -180,7 +215,7 @@ int mw_rccl_init(mw_exec *exec, const void *id, int32_t nranks, int32_t rank)
         if (exec->comm) throw std::runtime_error("mw_rccl_init: communicator already set");
         ncclUniqueId uid;
         memcpy(&uid, id, sizeof(uid));
-        MW_NCCL_OK(ncclCommInitRank(&exec->comm, nranks, uid, rank));
+        MW_NCCL_OK(rccl().commInitRank(&exec->comm, nranks, uid, rank));
         return 0;
     }, -1)
 }
@@ -191,7 +226,7 @@ int mw_allgather_exported(mw_exec *exec, int32_t slot, void *dst, int64_t bytes_
         if (!exec->comm) throw std::runtime_error("mw_allgather_exported: call mw_rccl_init first");
         void *src = exec->exec->getExported(slot, nullptr);
         if (!src) throw std::runtime_error("mw_allgather_exported: no such export slot");
-        MW_NCCL_OK(ncclAllGather(src, dst, (size_t)bytes_per_rank, ncclChar, exec->comm,
+        MW_NCCL_OK(rccl().allGather(src, dst, (size_t)bytes_per_rank, ncclChar, exec->comm,
                                  (hipStream_t)exec->exec->stream()));
         return 0;
     }, -1)

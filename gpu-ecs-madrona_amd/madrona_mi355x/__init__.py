@@ -24,26 +24,31 @@ if not os.path.exists(LIB_PATH):
 def _mapped_hip_runtimes():
     try:
         with open("/proc/self/maps") as f:
-            return sorted({l.split()[-1] for l in f if "libamdhip64" in l and "/" in l})
+            return sorted({os.path.realpath(l.split()[-1]) for l in f
+                           if "libamdhip64" in l and "/" in l})
     except OSError:
         return []
 
 
-# The library is built by the system ROCm compiler and must run on the
-# matching HIP runtime.  PyTorch wheels bundle an older libamdhip64 with the
-# same soname: if torch was imported first, the dynamic linker binds this
-# library to torch's runtime, whose loader mis-handles these code objects
-# (device memory faults).  Import madrona_mi355x before torch; torch then
-# binds to the system runtime, which is backward compatible.
-_preloaded = [p for p in _mapped_hip_runtimes()
-              if not os.path.realpath(p).startswith(os.path.realpath(
-                  os.environ.get("ROCM_PATH", "/opt/rocm")))]
-if _preloaded and not os.environ.get("MADRONA_MW_ALLOW_FOREIGN_HIP"):
-    raise ImportError(
-        "madrona_mi355x: a different HIP runtime is already loaded "
-        f"({_preloaded[0]}); import madrona_mi355x before torch")
+# One HIP runtime per process.  PyTorch-ROCm wheels bundle their own
+# libamdhip64 (soname libamdhip64.so.7, the same as the system ROCm's) and
+# load it by path, so a process that loaded the system runtime first ends up
+# with two runtimes and neither sees the device.  The library is built as
+# code object v5 so it runs on either runtime; when torch is installed it is
+# imported first and the library binds to torch's runtime (and, at first
+# use, to torch's RCCL), so executor buffers are valid torch device memory.
+# MADRONA_MW_NO_TORCH=1 skips this (C-ABI-only processes).
+if not os.environ.get("MADRONA_MW_NO_TORCH"):
+    try:
+        import torch as _torch  # noqa: F401
+    except ImportError:
+        _torch = None
 
 _lib = ctypes.CDLL(LIB_PATH)
+
+if len(_mapped_hip_runtimes()) > 1:
+    raise ImportError("madrona_mi355x: more than one HIP runtime mapped in this process "
+                      f"({_mapped_hip_runtimes()}); import torch before loading the library")
 
 
 class MwConfig(ctypes.Structure):

@@ -7,8 +7,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
 
-# Bind the framework to the system HIP runtime before any test module
-# imports torch (madrona_mi355x/__init__.py explains why).
+# Load the framework early (it imports torch first so both share torch's
+# HIP runtime; madrona_mi355x/__init__.py explains why).
 try:
     import madrona_mi355x  # noqa: F401,E402
 except ImportError:
