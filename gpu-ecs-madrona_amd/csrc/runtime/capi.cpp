@@ -78,6 +78,7 @@ using namespace madrona;
 struct mw_exec {
     Executor *exec;
     ncclComm_t comm = nullptr;    // RCCL communicator for the world-shard hand-off
+    hipEvent_t stepDone = nullptr; // mw_stream_wait: recorded behind the enqueued steps
 };
 
 static thread_local std::string g_last_error;
@@ -173,11 +174,24 @@ int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_byt
 
 void *mw_stream(mw_exec *exec) { return exec ? exec->exec->stream() : nullptr; }
 
+int mw_stream_wait(mw_exec *exec, void *stream)
+{
+    MW_TRY({
+        if (!exec->stepDone) {
+            MW_HIP_OK(hipEventCreateWithFlags(&exec->stepDone, hipEventDisableTiming));
+        }
+        MW_HIP_OK(hipEventRecord(exec->stepDone, (hipStream_t)exec->exec->stream()));
+        MW_HIP_OK(hipStreamWaitEvent((hipStream_t)stream, exec->stepDone, 0));
+        return 0;
+    }, -1)
+}
+
 int mw_destroy(mw_exec *exec)
 {
     MW_TRY({
         if (exec) {
             if (exec->comm) (void)rccl().commDestroy(exec->comm);
+            if (exec->stepDone) (void)hipEventDestroy(exec->stepDone);
             delete exec->exec;
             delete exec;
         }

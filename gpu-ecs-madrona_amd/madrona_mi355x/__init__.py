@@ -88,6 +88,7 @@ _lib.mw_get_exported.restype = ctypes.c_void_p
 _lib.mw_get_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
 _lib.mw_stream.restype = ctypes.c_void_p
 _lib.mw_stream.argtypes = [ctypes.c_void_p]
+_lib.mw_stream_wait.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 _lib.mw_destroy.argtypes = [ctypes.c_void_p]
 _lib.mw_last_error.restype = ctypes.c_char_p
 _lib.mw_num_worlds.argtypes = [ctypes.c_void_p]
@@ -130,7 +131,7 @@ C_ABI_SYMBOLS = (
     "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_copy_exported",
     "mw_gen_collisions_inits", "mw_set_timed_node", "mw_timed_node_ms",
     "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
-    "mw_device_free", "mw_gen_fvs_inits",
+    "mw_device_free", "mw_gen_fvs_inits", "mw_stream_wait",
 )
 
 
@@ -211,6 +212,24 @@ class Executor:
         if not self.h:
             raise _err()
         self.num_worlds = num_worlds
+        self.gpu_id = gpu_id
+
+    def wait_on(self, stream):
+        """Device-side ordering: `stream` (an int hipStream_t, e.g.
+        torch.cuda.current_stream().cuda_stream) waits for every step
+        enqueued so far; no host sync (reference CudaSync::wait)."""
+        if _lib.mw_stream_wait(self.h, ctypes.c_void_p(stream)) != 0:
+            raise _err()
+
+    def exported_tensor(self, slot, element_type, dims):
+        """Zero-copy view of export `slot` as a madrona_mi355x.python.Tensor
+        (reference: getExported + madrona_python.Tensor(ptr, type, dims));
+        dims must describe exactly the exported rows."""
+        from .python import Tensor
+        ptr, rows = self.exported(slot)
+        if not ptr:
+            raise MadronaError(f"no export slot {slot}")
+        return Tensor.from_device_ptr(ptr, element_type, dims, self.gpu_id, owner=self)
 
     def step(self, n=1):
         if _lib.mw_step(self.h, n) != 0:

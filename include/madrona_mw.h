@@ -97,6 +97,12 @@ int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_byt
 /* hipStream_t of the executor (device work ordering for callers). */
 void *mw_stream(mw_exec *exec);
 
+/* Make the caller's hipStream_t `stream` (e.g. torch's current stream) wait,
+ * on the device and without a host sync, for every step enqueued so far.
+ * Replaces CudaSync::wait (include/madrona/python.hpp:20-35,
+ * src/python/utils.cpp:15-48), which waits on an external semaphore. */
+int mw_stream_wait(mw_exec *exec, void *stream);
+
 int mw_destroy(mw_exec *exec);
 const char *mw_last_error(void);
 

@@ -50,3 +50,20 @@ def test_rccl_single_rank_allgather_into_torch():
     sim.allgather_exported(2, t.data_ptr(), 16)
     sim.sync()
     assert t.cpu().numpy().tobytes() == want.tobytes()
+
+
+def test_exported_tensor_zero_copy_dlpack():
+    """getExported -> Tensor -> to_torch aliases the executor's export buffer
+    (device kDLROCM): later steps show through without another copy."""
+    import torch
+    from madrona_mi355x.python import HipSync, Tensor
+    mw, sim = _sim()
+    t = sim.exported_tensor(2, Tensor.ElementType.Float32, (4,))
+    view = t.to_torch()
+    assert view.is_cuda and view.data_ptr() == sim.exported(2)[0]
+    assert view.cpu().numpy().tobytes() == np.array(sim.exported_array(2, np.float32)).tobytes()
+    sim.step_async(3)
+    HipSync(sim).wait(torch.cuda.current_stream().cuda_stream)
+    after = view.clone()            # ordered after the steps on torch's stream
+    torch.cuda.synchronize()
+    assert after.cpu().numpy().tobytes() == np.array(sim.exported_array(2, np.float32)).tobytes()
