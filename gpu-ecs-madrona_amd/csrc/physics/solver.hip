@@ -10,25 +10,36 @@ namespace madrona::phys {
 // (physics.cpp:166-1008), one wave per world, body state in LDS,
 // level-scheduled contacts.
 // ===========================================================================
-struct SBody {
+// Mutable body state kept in LDS (random access by contact); the read-only
+// substep state (prev / pre-solve pose and velocity, mass properties) is
+// read from its columns when a contact needs it, so a world's LDS image is
+// 56 B per body and ~2.5x more worlds stay resident per CU.
+struct SMut {
     Vector3 x;
     Quat q;
     Vector3 v;
     Vector3 omega;
-    Vector3 prevX;
-    Quat prevQ;
-    Vector3 psX;
-    Quat psQ;
-    Vector3 psV;
-    Vector3 psOmega;
-    Vector3 invI;
-    float invMass;
-    float muS;
-    float muD;
-    uint32_t resp;
+    uint32_t meta;        // ResponseType | body arch index << 8 | ObjectID << 16
+};
+static_assert(sizeof(SMut) == 56);
+
+__device__ __forceinline__ bool isStaticBody(uint32_t meta)
+{
+    return (meta & 0xffu) == (uint32_t)ResponseType::Static;
+}
+
+// Read-only state of the body in LDS slot `slot` (physics.cpp:281-476,
+// 865-993 read these through the contact's Locs).
+struct BodyRO {
+    int32_t arch, row;
+    uint32_t obj;
 };
 
-
+__device__ __forceinline__ BodyRO bodyRO(const PhysArgs &P, int32_t slot, uint32_t meta)
+{
+    const int32_t a = (int32_t)((meta >> 8) & 0xffu);
+    return BodyRO { a, slot - P.body[a].slotBase, meta >> 16 };
+}
 
 __device__ __forceinline__ int32_t bodySlot(const PhysArgs &P, Loc l)
 {
@@ -59,23 +70,31 @@ __device__ __forceinline__ void applyPositionalUpdate(Vector3 &x1, Vector3 &x2, 
     q2 = q2.normalize();
 }
 
-__device__ void solveContactPositions(SBody &b1, SBody &b2, Contact &c)
+__device__ void solveContactPositions(const PhysArgs &P, int32_t w, SMut &b1, int32_t s1,
+                                      SMut &b2, int32_t s2, Contact &c)
 {                                                          // physics.cpp:281-476
+    const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
+    const auto ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
+    const auto ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
+    const auto pv1 = bcol<solver::SubstepPrevState>(P.body[o1.arch], Cols::SubstepPrevState, w, o1.row);
+    const auto pv2 = bcol<solver::SubstepPrevState>(P.body[o2.arch], Cols::SubstepPrevState, w, o2.row);
+    const RigidBodyMetadata m1 = P.objs.metadata[o1.obj], m2 = P.objs.metadata[o2.obj];
     Vector3 x1 = b1.x, x2 = b2.x;
     Quat q1 = b1.q, q2 = b2.q;
-    float im1 = b1.invMass, im2 = b2.invMass;
-    Vector3 iI1 = b1.invI, iI2 = b2.invI;
-    if (b1.resp == (uint32_t)ResponseType::Static) { im1 = 0.f; iI1 = Vector3::zero(); }
-    if (b2.resp == (uint32_t)ResponseType::Static) { im2 = 0.f; iI2 = Vector3::zero(); }
-    const float avg_mu_s = 0.5f * (b1.muS + b2.muS);
+    float im1 = m1.invMass, im2 = m2.invMass;
+    Vector3 iI1 = m1.invInertiaTensor, iI2 = m2.invInertiaTensor;
+    if (isStaticBody(b1.meta)) { im1 = 0.f; iI1 = Vector3::zero(); }
+    if (isStaticBody(b2.meta)) { im2 = 0.f; iI2 = Vector3::zero(); }
+    const float avg_mu_s = 0.5f * (m1.muS + m2.muS);
     const Vector3 n = c.normal;
-    for (int i = 0; i < 4; i++) {
-        if (i >= c.numPoints) continue;
+    const int32_t np = c.numPoints;
+#pragma unroll 1
+    for (int i = 0; i < np; i++) {
         Vector3 c1 = c.points[i].xyz();
         float depth = c.points[i].w;
         Vector3 c2 = c1 - n * depth;
-        Vector3 r1 = b1.psQ.inv().rotateVec(c1 - b1.psX);
-        Vector3 r2 = b2.psQ.inv().rotateVec(c2 - b2.psX);
+        Vector3 r1 = ps1.q.inv().rotateVec(c1 - ps1.x);
+        Vector3 r2 = ps2.q.inv().rotateVec(c2 - ps2.x);
         float lambda_n = 0.f;
         Vector3 p1 = q1.rotateVec(r1) + x1;
         Vector3 p2 = q2.rotateVec(r2) + x2;
@@ -90,8 +109,8 @@ __device__ void solveContactPositions(SBody &b1, SBody &b2, Contact &c)
             lambda_n = computePositionalLambda(ta1, ta2, ra1, ra2, im1, im2, d, 0);
             applyPositionalUpdate(x1, x2, q1, q2, ra1, ra2, im1, im2, n, lambda_n);
 
-            Vector3 p1_hat = b1.prevQ.rotateVec(r1) + b1.prevX;
-            Vector3 p2_hat = b2.prevQ.rotateVec(r2) + b2.prevX;
+            Vector3 p1_hat = pv1.prevRotation.rotateVec(r1) + pv1.prevPosition;
+            Vector3 p2_hat = pv2.prevRotation.rotateVec(r2) + pv2.prevPosition;
             p1 = q1.rotateVec(r1) + x1;
             p2 = q2.rotateVec(r2) + x2;
             Vector3 dp = (p1 - p1_hat) - (p2 - p2_hat);
@@ -143,56 +162,66 @@ __device__ __forceinline__ void applyVelocityUpdate(Vector3 &v1, Vector3 &v2, Ve
     o2 -= q2.rotateVec(o2u);
 }
 
-__device__ void solveContactVelocities(SBody &b1, SBody &b2, const Contact &c, float h,
+__device__ void solveContactVelocities(const PhysArgs &P, int32_t w, SMut &b1, int32_t s1,
+                                       SMut &b2, int32_t s2, const Contact &c, float h,
                                        float rest_thresh)
 {                                                          // physics.cpp:865-993
+    const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
+    const auto ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
+    const auto ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
+    const auto pv1 = bcol<solver::PreSolveVelocity>(P.body[o1.arch], Cols::PreSolveVelocity, w, o1.row);
+    const auto pv2 = bcol<solver::PreSolveVelocity>(P.body[o2.arch], Cols::PreSolveVelocity, w, o2.row);
+    const RigidBodyMetadata m1 = P.objs.metadata[o1.obj], m2 = P.objs.metadata[o2.obj];
     const Quat q1 = b1.q, q2 = b2.q;
-    Vector3 v1 = b1.v, o1 = b1.omega, v2 = b2.v, o2 = b2.omega;
-    float im1 = b1.invMass, im2 = b2.invMass;
-    Vector3 iI1 = b1.invI, iI2 = b2.invI;
-    if (b1.resp == (uint32_t)ResponseType::Static) { im1 = 0.f; iI1 = Vector3::zero(); }
-    if (b2.resp == (uint32_t)ResponseType::Static) { im2 = 0.f; iI2 = Vector3::zero(); }
-    const float mu_d = 0.5f * (b1.muD + b2.muD);
+    Vector3 v1 = b1.v, o1v = b1.omega, v2 = b2.v, o2v = b2.omega;
+    float im1 = m1.invMass, im2 = m2.invMass;
+    Vector3 iI1 = m1.invInertiaTensor, iI2 = m2.invInertiaTensor;
+    if (isStaticBody(b1.meta)) { im1 = 0.f; iI1 = Vector3::zero(); }
+    if (isStaticBody(b2.meta)) { im2 = 0.f; iI2 = Vector3::zero(); }
+    const float mu_d = 0.5f * (m1.muD + m2.muD);
     const Vector3 n = c.normal;
 
-    Vector3 r1l[4], r2l[4], r1w[4], r2w[4], rt1[4], rt2[4];
+    // Per point only the body-local lever arms and the pre-solve normal
+    // velocity stay live; the world-space arms (q fixed during this phase)
+    // and the angular terms are recomputed where used -- the same operations
+    // on the same inputs, so bit-identical, at a third of the registers.
+    Vector3 r1l[4], r2l[4];
     float vn_bars[4];
+    const Vector3 nl1 = q1.inv().rotateVec(n);
+    const Vector3 nl2 = q2.inv().rotateVec(n);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         if (i >= c.numPoints) continue;
         Vector3 c1 = c.points[i].xyz();
         float depth = c.points[i].w;
         Vector3 c2 = c1 - n * depth;
-        Vector3 r1 = b1.psQ.inv().rotateVec(c1 - b1.psX);
-        Vector3 r2 = b2.psQ.inv().rotateVec(c2 - b2.psX);
-        Vector3 r1p = b1.psQ.rotateVec(r1);
-        Vector3 r2p = b2.psQ.rotateVec(r2);
-        Vector3 vbar = relVel(b1.psV, b2.psV, b1.psOmega, b2.psOmega, r1p, r2p);
+        Vector3 r1 = ps1.q.inv().rotateVec(c1 - ps1.x);
+        Vector3 r2 = ps2.q.inv().rotateVec(c2 - ps2.x);
+        Vector3 r1p = ps1.q.rotateVec(r1);
+        Vector3 r2p = ps2.q.rotateVec(r2);
+        Vector3 vbar = relVel(pv1.v, pv2.v, pv1.omega, pv2.omega, r1p, r2p);
         vn_bars[i] = dot(n, vbar);
         r1l[i] = r1;
         r2l[i] = r2;
-        r1w[i] = q1.rotateVec(r1);
-        r2w[i] = q2.rotateVec(r2);
-        rt1[i] = cross(r1, q1.inv().rotateVec(n));
-        rt2[i] = cross(r2, q2.inv().rotateVec(n));
     }
     for (int it = 0; it < 2; it++) {                       // :813-863
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             if (i >= c.numPoints) continue;
-            Vector3 v = relVel(v1, v2, o1, o2, r1w[i], r2w[i]);
+            Vector3 v = relVel(v1, v2, o1v, o2v, q1.rotateVec(r1l[i]), q2.rotateVec(r2l[i]));
             float vn = dot(n, v);
             float vn_bar = vn_bars[i];
             float e = 0.3f;
             if (fabsf(vn_bar) <= rest_thresh) e = 0.f;
             float mag = fminRef(-e * vn_bar, 0) - vn;
-            applyVelocityUpdate(v1, v2, o1, o2, q1, q2, rt1[i], rt2[i], im1, im2, iI1, iI2, n, mag);
+            applyVelocityUpdate(v1, v2, o1v, o2v, q1, q2, cross(r1l[i], nl1), cross(r2l[i], nl2),
+                                im1, im2, iI1, iI2, n, mag);
         }
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) {                          // :752-811
         if (i >= c.numPoints) continue;
-        Vector3 v = relVel(v1, v2, o1, o2, r1w[i], r2w[i]);
+        Vector3 v = relVel(v1, v2, o1v, o2v, q1.rotateVec(r1l[i]), q2.rotateVec(r2l[i]));
         float dfm = mu_d * fabsf(c.lambdaN[i]) / h;
         float vn = dot(n, v);
         Vector3 vt = v - n * vn;
@@ -204,12 +233,12 @@ __device__ void solveContactVelocities(SBody &b1, SBody &b2, const Contact &c, f
             Vector3 d2l = q2.inv().rotateVec(dw);
             Vector3 fta1 = cross(r1l[i], d1l);
             Vector3 fta2 = cross(r2l[i], d2l);
-            applyVelocityUpdate(v1, v2, o1, o2, q1, q2, fta1, fta2, im1, im2, iI1, iI2, dw,
+            applyVelocityUpdate(v1, v2, o1v, o2v, q1, q2, fta1, fta2, im1, im2, iI1, iI2, dw,
                                 corrected);
         }
     }
-    b1.v = v1; b1.omega = o1;
-    b2.v = v2; b2.omega = o2;
+    b1.v = v1; b1.omega = o1v;
+    b2.v = v2; b2.omega = o2v;
 }
 
 __device__ __forceinline__ bool isNegZero(float f) { return __float_as_uint(f) == 0x80000000u; }
@@ -218,9 +247,9 @@ __device__ __forceinline__ bool isNegZero(float f) { return __float_as_uint(f) =
 // exact no-op: x +- (+-0) and q +- (+-0) keep bits when no component is -0,
 // and normalize() must be idempotent on its rotation (static velocities are
 // always +0 after setVelocities).  Such bodies add no ordering edge.
-__device__ __forceinline__ bool staticInvariant(const SBody &b)
+__device__ __forceinline__ bool staticInvariant(const SMut &b)
 {
-    if (b.resp != (uint32_t)ResponseType::Static) return false;
+    if (!isStaticBody(b.meta)) return false;
     if (isNegZero(b.x.x) || isNegZero(b.x.y) || isNegZero(b.x.z)) return false;
     if (isNegZero(b.q.w) || isNegZero(b.q.x) || isNegZero(b.q.y) || isNegZero(b.q.z)) return false;
     Quat nq = b.q.normalize();
@@ -240,10 +269,10 @@ static_assert(sizeof(CRec) == 8);
 // Contacts whose records stay in LDS; worlds with more contacts keep them
 // in a global slab instead, so the LDS footprint (and with it the number of
 // worlds resident per CU) does not scale with SolverData::maxContacts.
-constexpr int32_t kSolverLDSContacts = 256;
+constexpr int32_t kSolverLDSContacts = 128;
 
 struct SolverLDS {
-    SBody *bodies;        // [nb]
+    SMut *bodies;         // [nb]
     int16_t *lastLevel;   // [nb] -1: invariant static body (no ordering edges)
     CRec *recs;           // [kSolverLDSContacts]
     int32_t *prevs;       // [kSolverLDSContacts] (prev contact on s1, on s2) as 2 x int16
@@ -252,7 +281,7 @@ struct SolverLDS {
 __host__ __device__ inline size_t solverLDSBytes(int32_t nb)
 {
     auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-    return a16(sizeof(SBody) * nb) + a16(sizeof(int16_t) * nb) +
+    return a16(sizeof(SMut) * nb) + a16(sizeof(int16_t) * nb) +
            (sizeof(CRec) + sizeof(int32_t)) * kSolverLDSContacts;
 }
 
@@ -260,8 +289,8 @@ __device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb)
 {
     auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
     SolverLDS L;
-    L.bodies = (SBody *)smem;
-    char *p = smem + a16(sizeof(SBody) * nb);
+    L.bodies = (SMut *)smem;
+    char *p = smem + a16(sizeof(SMut) * nb);
     L.lastLevel = (int16_t *)p;
     p += a16(sizeof(int16_t) * nb);
     L.recs = (CRec *)p;
@@ -270,41 +299,37 @@ __device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb)
     return L;
 }
 
-__global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
+// Occupancy: the kernel is latency bound (one wave per world, dependent
+// LDS / column reads per contact), so residency matters more than packed
+// math; built without SLP vectorisation (Makefile) it fits 3 waves per SIMD
+// without spills.
+#ifndef MW_SOLVER_WAVES_PER_EU
+#define MW_SOLVER_WAVES_PER_EU 3
+#endif
+__global__ void __launch_bounds__(kSolverBlock)
+__attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(PhysArgs P)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int32_t w = blockIdx.x;
     const int32_t nb = P.maxBodiesPerWorld;
     SolverLDS L = solverLDS(smem, nb);
-    SBody *bodies = L.bodies;
+    SMut *bodies = L.bodies;
 
     // 1. load bodies into LDS
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
         for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
-            SBody &s = bodies[B.slotBase + r];
+            SMut s;
             s.x = bcol<Vector3>(B, Cols::Position, w, r);
             s.q = bcol<Quat>(B, Cols::Rotation, w, r);
             const Velocity vel = bcol<Velocity>(B, Cols::Velocity, w, r);
             s.v = vel.linear;
             s.omega = vel.angular;
-            const auto prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
-            s.prevX = prev.prevPosition;
-            s.prevQ = prev.prevRotation;
-            const auto psp = bcol<solver::PreSolvePositional>(B, Cols::PreSolvePositional, w, r);
-            s.psX = psp.x;
-            s.psQ = psp.q;
-            const auto psv = bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
-            s.psV = psv.v;
-            s.psOmega = psv.omega;
-            const int32_t obj = bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
-            const RigidBodyMetadata md = P.objs.metadata[obj];
-            s.invI = md.invInertiaTensor;
-            s.invMass = md.invMass;
-            s.muS = md.muS;
-            s.muD = md.muD;
-            s.resp = (uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r);
+            const uint32_t obj = (uint32_t)bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
+            s.meta = ((uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r) & 0xffu) |
+                     ((uint32_t)ba << 8) | (obj << 16);
+            bodies[B.slotBase + r] = s;
             L.lastLevel[B.slotBase + r] = staticInvariant(s) ? (int16_t)-1 : (int16_t)0;
         }
     }
@@ -396,7 +421,7 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
             const CRec r = recs[k];
             if (r.lvl != l) continue;
             Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
-            solveContactPositions(bodies[r.s1], bodies[r.s2], c);
+            solveContactPositions(P, w, bodies[r.s1], r.s1, bodies[r.s2], r.s2, c);
         }
         __syncthreads();
     }
@@ -407,8 +432,9 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
         for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
-            SBody &s = bodies[B.slotBase + r];
-            const Quat q = s.q, qp = s.prevQ;
+            SMut &s = bodies[B.slotBase + r];
+            const auto prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
+            const Quat q = s.q, qp = prev.prevRotation;
             Quat dq;
             if (q.w != qp.w || q.x != qp.x || q.y != qp.y || q.z != qp.z) {
                 dq = q * qp.inv();
@@ -416,7 +442,7 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
                 dq = Quat { 1, 0, 0, 0 };
             }
             Vector3 new_omega = 2.f / h * Vector3 { dq.x, dq.y, dq.z };
-            s.v = (s.x - s.prevX) / h;
+            s.v = (s.x - prev.prevPosition) / h;
             s.omega = dq.w > 0.f ? new_omega : -new_omega;
         }
     }
@@ -428,7 +454,8 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
             const CRec r = recs[k];
             if (r.lvl != l) continue;
             const Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
-            solveContactVelocities(bodies[r.s1], bodies[r.s2], c, h, sd.restitutionThreshold);
+            solveContactVelocities(P, w, bodies[r.s1], r.s1, bodies[r.s2], r.s2, c, h,
+                                   sd.restitutionThreshold);
         }
         __syncthreads();
     }
@@ -438,7 +465,7 @@ __global__ void __launch_bounds__(kSolverBlock) solverKernel(PhysArgs P)
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
         for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
-            const SBody &s = bodies[B.slotBase + r];
+            const SMut &s = bodies[B.slotBase + r];
             bcol<Vector3>(B, Cols::Position, w, r) = s.x;
             bcol<Quat>(B, Cols::Rotation, w, r) = s.q;
             bcol<Velocity>(B, Cols::Velocity, w, r) = Velocity { s.v, s.omega };
