@@ -188,60 +188,127 @@ __global__ void __launch_bounds__(64) bvhRebuildKernel(PhysArgs P)
     }
 }
 
-// refitEntry -> BVH::refitLeaf (broadphase.cpp:545-642, 891-895)
-__global__ void __launch_bounds__(256) refitKernel(PhysArgs P)
+// refitEntry -> BVH::refitLeaf (broadphase.cpp:545-642, 891-895), one block
+// per world with the world's used BVH nodes staged in LDS: every leaf's slot
+// read-modify-write and its expansion walk to the root run on LDS (atomic
+// float min / max where walks meet), then the used node prefix goes back to
+// HBM in one coalesced pass.  The result is order-independent: a slot ends
+// as the union of its previous bounds and every descendant leaf that
+// expanded it (ancestors contain their children's slots -- rebuild merges,
+// refit only grows and propagates growth), which is what the reference's
+// serial row-order walk produces.
+__device__ __forceinline__ float ldsAtomicMinRef(float *addr, float v)
 {
-    const BodyArch &B = P.body[blockIdx.y];
-    RowIdx ri = rowIndex(P, B);
-    if (!ri.valid) return;
-    const int32_t w = ri.w;
-    const int32_t leaf = guardIndex(bcol<broadphase::LeafID>(B, Cols::LeafID, w, ri.r).id,
-                                    P.maxLeaves, P.errorFlags + w, kGuardLeaf);
-    const size_t li = (size_t)w * P.maxLeaves + leaf;
-    const AABB a = P.leafAABBs[li];
-    const uint32_t lp = P.leafParents[li];
-    BVHNode *nodes = P.nodes + (size_t)w * P.maxNodes;
-    int32_t node_idx = guardIndex((int32_t)(lp >> 2), P.maxNodes, P.errorFlags + w, kGuardNode);
-    const int sub = (int)(lp & 3);
-
-    {   // leaf slot: owned by this leaf alone -> plain read-modify-write
-        BVHNode &n = nodes[node_idx];
-        float xm = n.minX[sub], ym = n.minY[sub], zm = n.minZ[sub];
-        float xM = n.maxX[sub], yM = n.maxY[sub], zM = n.maxZ[sub];
-        if (a.pMin.x < xm) n.minX[sub] = a.pMin.x;
-        if (a.pMin.y < ym) n.minY[sub] = a.pMin.y;
-        if (a.pMin.z < zm) n.minZ[sub] = a.pMin.z;
-        if (a.pMax.x > xM) n.maxX[sub] = a.pMax.x;
-        if (a.pMax.y > yM) n.maxY[sub] = a.pMax.y;
-        if (a.pMax.z > zM) n.maxZ[sub] = a.pMax.z;
-        bool expanded = a.pMin.x < xm || a.pMin.y < ym || a.pMin.z < zm ||
-                        a.pMax.x > xM || a.pMax.y > yM || a.pMax.z > zM;
-        if (!expanded) return;
+    uint32_t *p = (uint32_t *)addr;
+    uint32_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (true) {
+        float of = __uint_as_float(old);
+        if (!(v < of)) return of;
+        uint32_t prev = old;
+        if (__hip_atomic_compare_exchange_strong(p, &prev, __float_as_uint(v), __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+            return of;
+        old = prev;
     }
-    int32_t child_idx = node_idx;
-    node_idx = nodes[node_idx].parentID;
-    while (node_idx != -1) {
-        if ((uint32_t)node_idx >= (uint32_t)P.maxNodes) {
-            atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardNode << 8));
-            return;
+}
+
+__device__ __forceinline__ float ldsAtomicMaxRef(float *addr, float v)
+{
+    uint32_t *p = (uint32_t *)addr;
+    uint32_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (true) {
+        float of = __uint_as_float(old);
+        if (!(v > of)) return of;
+        uint32_t prev = old;
+        if (__hip_atomic_compare_exchange_strong(p, &prev, __float_as_uint(v), __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+            return of;
+        old = prev;
+    }
+}
+
+size_t refitSharedBytes(const PhysArgs &P)
+{
+    return sizeof(BVHNode) * (size_t)P.maxNodes;
+}
+
+__global__ void __launch_bounds__(kRefitBlock) refitKernel(PhysArgs P)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    BVHNode *lnodes = (BVHNode *)smem;
+    const int32_t w = blockIdx.x;
+    const int32_t used = min(P.bvh[w].usedNodes, P.maxNodes);
+    if (used <= 0) return;
+    BVHNode *gnodes = P.nodes + (size_t)w * P.maxNodes;
+    {
+        const uint32_t *src = (const uint32_t *)gnodes;
+        uint32_t *dst = (uint32_t *)lnodes;
+        const int32_t words = used * (int32_t)(sizeof(BVHNode) / 4);
+        for (int32_t i = threadIdx.x; i < words; i += kRefitBlock) dst[i] = src[i];
+    }
+    __syncthreads();
+
+    int32_t *flags = P.errorFlags + w;
+    for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
+        const BodyArch &B = P.body[ba];
+        const int32_t rows = B.numRows[w];
+        for (int32_t r = threadIdx.x; r < rows; r += kRefitBlock) {
+            const int32_t leaf = guardIndex(bcol<broadphase::LeafID>(B, Cols::LeafID, w, r).id,
+                                            P.maxLeaves, flags, kGuardLeaf);
+            const size_t li = (size_t)w * P.maxLeaves + leaf;
+            const AABB a = P.leafAABBs[li];
+            const uint32_t lp = P.leafParents[li];
+            int32_t node_idx = guardIndex((int32_t)(lp >> 2), used, flags, kGuardNode);
+            const int sub = (int)(lp & 3);
+            {   // leaf slot: owned by this leaf alone -> plain read-modify-write
+                BVHNode &n = lnodes[node_idx];
+                float xm = n.minX[sub], ym = n.minY[sub], zm = n.minZ[sub];
+                float xM = n.maxX[sub], yM = n.maxY[sub], zM = n.maxZ[sub];
+                if (a.pMin.x < xm) n.minX[sub] = a.pMin.x;
+                if (a.pMin.y < ym) n.minY[sub] = a.pMin.y;
+                if (a.pMin.z < zm) n.minZ[sub] = a.pMin.z;
+                if (a.pMax.x > xM) n.maxX[sub] = a.pMax.x;
+                if (a.pMax.y > yM) n.maxY[sub] = a.pMax.y;
+                if (a.pMax.z > zM) n.maxZ[sub] = a.pMax.z;
+                bool expanded = a.pMin.x < xm || a.pMin.y < ym || a.pMin.z < zm ||
+                                a.pMax.x > xM || a.pMax.y > yM || a.pMax.z > zM;
+                if (!expanded) continue;
+            }
+            int32_t child_idx = node_idx;
+            node_idx = lnodes[node_idx].parentID;
+            int32_t hops = 0;
+            while (node_idx != -1) {
+                if ((uint32_t)node_idx >= (uint32_t)used || ++hops > used) {
+                    atomicOr(flags, kErrIndexGuard | (kGuardNode << 8));
+                    break;
+                }
+                BVHNode &n = lnodes[node_idx];
+                int c = -1;
+                for (int j = 0; j < 4; j++) {
+                    if (n.children[j] == child_idx) { c = j; break; }
+                }
+                if (c < 0) break;
+                float xm = ldsAtomicMinRef(&n.minX[c], a.pMin.x);
+                float ym = ldsAtomicMinRef(&n.minY[c], a.pMin.y);
+                float zm = ldsAtomicMinRef(&n.minZ[c], a.pMin.z);
+                float xM = ldsAtomicMaxRef(&n.maxX[c], a.pMax.x);
+                float yM = ldsAtomicMaxRef(&n.maxY[c], a.pMax.y);
+                float zM = ldsAtomicMaxRef(&n.maxZ[c], a.pMax.z);
+                bool expanded = a.pMin.x < xm || a.pMin.y < ym || a.pMin.z < zm ||
+                                a.pMax.x > xM || a.pMax.y > yM || a.pMax.z > zM;
+                if (!expanded) break;
+                child_idx = node_idx;
+                node_idx = n.parentID;
+            }
         }
-        BVHNode &n = nodes[node_idx];
-        int c = -1;
-        for (int j = 0; j < 4; j++) {
-            if (n.children[j] == child_idx) { c = j; break; }
+    }
+    __syncthreads();
+    {   // bounds only: children / parents are unchanged by a refit
+        const int32_t per = 24;                          // minX..maxZ dwords per node
+        for (int32_t i = threadIdx.x; i < used * per; i += kRefitBlock) {
+            const int32_t n = i / per, k = i - n * per;
+            ((uint32_t *)&gnodes[n])[k] = ((const uint32_t *)&lnodes[n])[k];
         }
-        if (c < 0) return;
-        float xm = atomicMinRef(&n.minX[c], a.pMin.x);
-        float ym = atomicMinRef(&n.minY[c], a.pMin.y);
-        float zm = atomicMinRef(&n.minZ[c], a.pMin.z);
-        float xM = atomicMaxRef(&n.maxX[c], a.pMax.x);
-        float yM = atomicMaxRef(&n.maxY[c], a.pMax.y);
-        float zM = atomicMaxRef(&n.maxZ[c], a.pMax.z);
-        bool expanded = a.pMin.x < xm || a.pMin.y < ym || a.pMin.z < zm ||
-                        a.pMax.x > xM || a.pMax.y > yM || a.pMax.z > zM;
-        if (!expanded) break;
-        child_idx = node_idx;
-        node_idx = n.parentID;
     }
 }
 

@@ -404,7 +404,8 @@ MW_PHYS_NODE(UpdateBVHNode,
 
 MW_PHYS_NODE(RefitNode,
     if (P.numBodyArchs > 0)
-        hipLaunchKernelGGL(refitKernel, rowGrid(P), dim3(256), 0, stream, P);)
+        hipLaunchKernelGGL(refitKernel, dim3(P.numWorlds), dim3(kRefitBlock),
+                           refitSharedBytes(P), stream, P);)
 
 MW_PHYS_NODE(FindOverlappingNode,
     hipLaunchKernelGGL(findOverlapsKernel, dim3(P.numWorlds), dim3(kOverlapBlock),

@@ -148,6 +148,7 @@ __global__ void narrowContactKernel(PhysArgs P);
 __global__ void solverKernel(PhysArgs P);
 
 size_t findOverlapsSharedBytes(const PhysArgs &P);
+size_t refitSharedBytes(const PhysArgs &P);
 size_t solverSharedBytes(const PhysArgs &P);
 size_t narrowphaseSharedBytes(const PhysArgs &P);
 size_t contactSharedBytes(const PhysArgs &P);
@@ -156,5 +157,6 @@ constexpr int32_t kOverlapBlock = 192;
 constexpr int32_t kNarrowBlock = 256;
 constexpr int32_t kContactBlock = 128;
 constexpr int32_t kSolverBlock = 64;
+constexpr int32_t kRefitBlock = 128;
 
 }
