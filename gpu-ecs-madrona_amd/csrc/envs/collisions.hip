@@ -83,10 +83,12 @@ MW_HD void PhysWorld::accumulateReturn(Engine &ctx, EpisodeReturn &ret)
     float sum = 0.f;
     int32_t n = 0;
     ctx.forEach(ctx.data().bodyQuery, [&](const Position &p, const ResponseType &rt) {
-        if (rt == ResponseType::Dynamic) {
-            sum += p.z;
-            n++;
-        }
+        // branch-free select (same sums): every row's loads issue without
+        // waiting on the previous row's ResponseType
+        const bool dyn = rt == ResponseType::Dynamic;
+        const float z = p.z;
+        sum = dyn ? sum + z : sum;
+        n += dyn ? 1 : 0;
     });
     ret.value += n > 0 ? sum / (float)n : 0.f;
 }

@@ -182,7 +182,7 @@ MW_HD void Game::archerSystem(Engine &ctx, Entity &e, Action &action, Quiver &qu
     if (num_dragons > 0) {            // the reference's uniform_int_distribution(0, -1) is UB
         const Draw d { g.worldSeed, (uint32_t)e.id, g.tickCount };
         const uint32_t idx = d.index(kDrawDragon, (uint32_t)num_dragons);
-        damage(st.column<Health>(g.dragonArch, g.dragonHealthCol, w)[idx], kArrowDamage);
+        damage(rowRef(st.column<Health>(g.dragonArch, g.dragonHealthCol, w), idx), kArrowDamage);
     }
     quiver.numArrows -= 1;
     action.remainingTime = kShootTime;

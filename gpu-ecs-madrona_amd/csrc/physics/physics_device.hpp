@@ -157,6 +157,9 @@ constexpr int32_t kOverlapBlock = 192;
 constexpr int32_t kNarrowBlock = 256;
 constexpr int32_t kContactBlock = 128;
 constexpr int32_t kSolverBlock = 64;
-constexpr int32_t kRefitBlock = 128;
+#ifndef MW_REFIT_BLOCK
+#define MW_REFIT_BLOCK 128
+#endif
+constexpr int32_t kRefitBlock = MW_REFIT_BLOCK;
 
 }

@@ -71,7 +71,7 @@ public:
     template <typename ComponentT>
     MW_INLINE ComponentT &getDirect(int32_t column_idx, Loc loc)
     {
-        return state_->column<ComponentT>(loc.archetype, column_idx, world_)[loc.row];
+        return rowRef(state_->column<ComponentT>(loc.archetype, column_idx, world_), loc.row);
     }
     template <typename SingletonT> MW_INLINE SingletonT &getSingleton();
 
@@ -96,7 +96,7 @@ public:
     MW_INLINE void resetTmpAlloc() {}
 
     MW_INLINE WorldID worldID() const { return WorldID { world_ }; }
-    MW_INLINE WorldBase &data() { return *data_; }
+    MW_INLINE WorldBase &data() { return rowRef(data_, 0); }
     MW_INLINE StateView &state() { return *state_; }
 
     // registration forwarding used by some reference examples' ctors
@@ -118,7 +118,7 @@ public:
     MW_INLINE CustomContext(DataT *world_data, const WorkerInit &init)
         : Context(world_data, init)
     {}
-    MW_INLINE DataT &data() const { return *static_cast<DataT *>(data_); }
+    MW_INLINE DataT &data() const { return rowRef(static_cast<DataT *>(data_), 0); }
 
     using WorldDataT = DataT;
 };
@@ -132,11 +132,11 @@ MW_INLINE Entity Context::makeEntityNow(Args &&...args)
     Entity e = ids.acquire(ids.st->worldCache);
     int32_t row = state_->addRow(arch, world_);
     if (row < 0 || e.id < 0) return Entity::none();
-    state_->column<Entity>(arch, 0, world_)[row] = e;
+    rowRef(state_->column<Entity>(arch, 0, world_), row) = e;
     int32_t col = 1;
     auto construct = [&](auto &&arg) {
         using T = std::remove_cv_t<std::remove_reference_t<decltype(arg)>>;
-        new (&state_->column<T>(arch, col, world_)[row]) T(std::forward<decltype(arg)>(arg));
+        new (&rowRef(state_->column<T>(arch, col, world_), row)) T(std::forward<decltype(arg)>(arg));
         col++;
     };
     (construct(std::forward<Args>(args)), ...);
@@ -151,7 +151,7 @@ MW_INLINE void Context::destroyEntityNow(Entity e)
     if (!loc.valid()) return;
     bool moved = state_->removeRow(loc.archetype, world_, loc.row);
     if (moved) {
-        Entity m = state_->column<Entity>(loc.archetype, 0, world_)[loc.row];
+        Entity m = rowRef(state_->column<Entity>(loc.archetype, 0, world_), loc.row);
         ids.nodes[m.id].val.row = loc.row;
     }
     ids.release(ids.st->worldCache, e.id);
@@ -180,7 +180,7 @@ MW_INLINE ResultRef<ComponentT> Context::get(Loc loc)
 {
     int32_t col = state_->findColumn(loc.archetype, typeKey<ComponentT>());
     if (col < 0) return ResultRef<ComponentT>(nullptr);
-    return ResultRef<ComponentT>(&state_->column<ComponentT>(loc.archetype, col, world_)[loc.row]);
+    return ResultRef<ComponentT>(&rowRef(state_->column<ComponentT>(loc.archetype, col, world_), loc.row));
 }
 
 template <typename ComponentT>
@@ -202,14 +202,14 @@ template <typename ComponentT>
 MW_INLINE ComponentT &Context::getUnsafe(Loc loc)
 {
     int32_t col = state_->findColumn(loc.archetype, typeKey<ComponentT>());
-    return state_->column<ComponentT>(loc.archetype, col, world_)[loc.row];
+    return rowRef(state_->column<ComponentT>(loc.archetype, col, world_), loc.row);
 }
 
 template <typename SingletonT>
 MW_INLINE SingletonT &Context::getSingleton()
 {
     int32_t arch = state_->findArchetype(typeKey<SingletonArchetype<SingletonT>>());
-    return state_->column<SingletonT>(arch, 1, world_)[0];
+    return rowRef(state_->column<SingletonT>(arch, 1, world_), 0);
 }
 
 template <typename... ComponentTs, typename Fn>
@@ -233,7 +233,7 @@ MW_INLINE void Context::forEachRows(int32_t arch, const int32_t *cols, int32_t n
     // unrolled so a device lane keeps several rows' loads in flight
 #pragma unroll 4
     for (int32_t r = 0; r < n; r++) {
-        fn(std::get<Is>(ptrs)[r]...);
+        fn(rowRef(std::get<Is>(ptrs), r)...);
     }
 }
 

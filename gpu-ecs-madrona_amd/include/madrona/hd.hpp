@@ -23,4 +23,21 @@
 
 namespace madrona {
 using CountT = int64_t;
+
+// State slabs are HBM allocations, but pointers read out of a StateView are
+// generic to the compiler, which then emits flat loads that wait on both
+// memory counters (every access serialised).  rowRef indexes a slab in the
+// global address space and hands back an ordinary reference, so the backend
+// emits global loads / stores with partial waits.
+template <typename T>
+MW_INLINE T &rowRef(T *base, int64_t r)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    using GT = __attribute__((address_space(1))) T;
+    GT *g = (GT *)base;
+    return *(T *)&g[r];
+#else
+    return base[r];
+#endif
+}
 }

@@ -144,13 +144,18 @@ __device__ inline void invokeRow(ContextT &ctx, StateView *st, int32_t arch,
                                  const ColArgs<sizeof...(ComponentTs)> &cols,
                                  int32_t w, int32_t r, std::index_sequence<Is...>)
 {
-    Fn(ctx, st->column<std::remove_const_t<ComponentTs>>(arch, cols.c[Is], w)[r]...);
+    Fn(ctx, rowRef(st->column<std::remove_const_t<ComponentTs>>(arch, cols.c[Is], w), r)...);
 }
 
 template <typename ContextT, auto Fn, typename... ComponentTs>
 __global__ void __launch_bounds__(256)
-parallelForKernel(StateView *st, int32_t arch, ColArgs<sizeof...(ComponentTs)> cols)
+parallelForKernel(const StateView *__restrict__ st_in, int32_t arch,
+                  ColArgs<sizeof...(ComponentTs)> cols)
 {
+    // The StateView itself is read-only inside a node (only the slabs it
+    // points to are written); const + restrict lets the backend treat the
+    // column pointers loaded from it as global (no flat accesses).
+    StateView *st = const_cast<StateView *>(st_in);
     const int32_t cap = st->arch[arch].capacity;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int32_t w = (int32_t)(t / cap);
@@ -216,8 +221,9 @@ void launchWorldKernel(const void *kernel, LaunchCtx &lc);
 
 #if defined(__HIPCC__)
 template <typename ContextT, auto Fn>
-__global__ void __launch_bounds__(64) perWorldKernel(StateView *st)
+__global__ void __launch_bounds__(64) perWorldKernel(const StateView *__restrict__ st_in)
 {
+    StateView *st = const_cast<StateView *>(st_in);
     const int32_t w = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (w >= st->numWorlds) return;
     using WorldT = typename WorldOf<ContextT>::type;
