@@ -306,55 +306,17 @@ __device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb)
 #ifndef MW_SOLVER_WAVES_PER_EU
 #define MW_SOLVER_WAVES_PER_EU 3
 #endif
-__global__ void __launch_bounds__(kSolverBlock)
-__attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(PhysArgs P)
+// Phases 2-7 of the solver for one world.  Instantiated twice (records in
+// LDS / in the global fallback slab) so every access has a known address
+// space: no flat loads with full waits in the level search.
+__device__ __forceinline__ void solveWorld(const PhysArgs &P, const int32_t w, SolverLDS &L,
+                                           SMut *bodies, const int32_t nb,
+                                           const Contact *cslots, int32_t *order,
+                                           const int32_t S, const int32_t K, CRec *recs,
+                                           int32_t *prevs)
 {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int32_t w = blockIdx.x;
-    const int32_t nb = P.maxBodiesPerWorld;
-    SolverLDS L = solverLDS(smem, nb);
-    SMut *bodies = L.bodies;
-
-    // 1. load bodies into LDS
-    for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
-        const BodyArch &B = P.body[ba];
-        const int32_t rows = B.numRows[w];
-        for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
-            SMut s;
-            s.x = bcol<Vector3>(B, Cols::Position, w, r);
-            s.q = bcol<Quat>(B, Cols::Rotation, w, r);
-            const Velocity vel = bcol<Velocity>(B, Cols::Velocity, w, r);
-            s.v = vel.linear;
-            s.omega = vel.angular;
-            const uint32_t obj = (uint32_t)bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
-            s.meta = ((uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r) & 0xffu) |
-                     ((uint32_t)ba << 8) | (obj << 16);
-            bodies[B.slotBase + r] = s;
-            L.lastLevel[B.slotBase + r] = staticInvariant(s) ? (int16_t)-1 : (int16_t)0;
-        }
-    }
-
-    // 2. ordered contact list: survivors with a manifold, in survivor order
-    //    (== the reference's addManifoldToSolver append order,
-    //    narrowphase.cpp:1123-1162).  Pass 1 counts, pass 2 writes.
-    const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
-    int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
-    const int32_t S = P.survCount[w];
     const int32_t lane = threadIdx.x;
     const uint64_t lt_mask = (1ull << lane) - 1;
-    int32_t K = 0;
-    for (int32_t chunk = 0; chunk < S; chunk += kSolverBlock) {
-        const int32_t s = chunk + lane;
-        K += __popcll(__ballot(s < S && cslots[s].numPoints > 0));
-    }
-    if (K > P.maxContacts) {
-        // The reference asserts here (narrowphase.cpp:1130); flag, truncate.
-        if (lane == 0) atomicOr(P.errorFlags + w, kErrContactOverflow);
-        K = P.maxContacts;
-    }
-    const bool in_lds = K <= kSolverLDSContacts;
-    CRec *recs = in_lds ? L.recs : (CRec *)(P.solverRecs + (size_t)w * P.candCapacity);
-    int32_t *prevs = in_lds ? L.prevs : P.solverPrevs + (size_t)w * P.candCapacity;
     int32_t k0 = 0;
     for (int32_t chunk = 0; chunk < S && k0 < K; chunk += kSolverBlock) {
         const int32_t s = chunk + lane;
@@ -472,6 +434,61 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
         }
     }
     if (threadIdx.x == 0) P.solver[w].numContacts = 0;     // physics.cpp:1007
+}
+
+__global__ void __launch_bounds__(kSolverBlock)
+__attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(PhysArgs P)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int32_t w = blockIdx.x;
+    const int32_t nb = P.maxBodiesPerWorld;
+    SolverLDS L = solverLDS(smem, nb);
+    SMut *bodies = L.bodies;
+
+    // 1. load bodies into LDS
+    for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
+        const BodyArch &B = P.body[ba];
+        const int32_t rows = B.numRows[w];
+        for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
+            SMut s;
+            s.x = bcol<Vector3>(B, Cols::Position, w, r);
+            s.q = bcol<Quat>(B, Cols::Rotation, w, r);
+            const Velocity vel = bcol<Velocity>(B, Cols::Velocity, w, r);
+            s.v = vel.linear;
+            s.omega = vel.angular;
+            const uint32_t obj = (uint32_t)bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
+            s.meta = ((uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r) & 0xffu) |
+                     ((uint32_t)ba << 8) | (obj << 16);
+            bodies[B.slotBase + r] = s;
+            L.lastLevel[B.slotBase + r] = staticInvariant(s) ? (int16_t)-1 : (int16_t)0;
+        }
+    }
+
+    // 2. ordered contact list: survivors with a manifold, in survivor order
+    //    (== the reference's addManifoldToSolver append order,
+    //    narrowphase.cpp:1123-1162).  Pass 1 counts, pass 2 writes.
+    const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
+    int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
+    const int32_t S = P.survCount[w];
+    const int32_t lane = threadIdx.x;
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    int32_t K = 0;
+    for (int32_t chunk = 0; chunk < S; chunk += kSolverBlock) {
+        const int32_t s = chunk + lane;
+        K += __popcll(__ballot(s < S && cslots[s].numPoints > 0));
+    }
+    if (K > P.maxContacts) {
+        // The reference asserts here (narrowphase.cpp:1130); flag, truncate.
+        if (lane == 0) atomicOr(P.errorFlags + w, kErrContactOverflow);
+        K = P.maxContacts;
+    }
+    if (K <= kSolverLDSContacts) {
+        solveWorld(P, w, L, bodies, nb, cslots, order, S, K, L.recs, L.prevs);
+    } else {
+        solveWorld(P, w, L, bodies, nb, cslots, order, S, K,
+                   (CRec *)(P.solverRecs + (size_t)w * P.candCapacity),
+                   P.solverPrevs + (size_t)w * P.candCapacity);
+    }
 }
 
 size_t solverSharedBytes(const PhysArgs &P)
