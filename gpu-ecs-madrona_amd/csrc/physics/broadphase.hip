@@ -337,6 +337,22 @@ struct alignas(16) OrderedLeaf {
 static_assert(sizeof(OrderedLeaf) == 48);
 
 // AABB::overlaps (math.hpp) of the query against a leaf slot.
+// e.id < other.id, not both static, and the slot overlaps the query
+// (AABB::overlaps, strict): all terms evaluated, combined with bitwise ands.
+__device__ __forceinline__ bool leafHit(const OrderedLeaf *leaves, int32_t k, const AABB &q,
+                                        int32_t e_id, bool a_static)
+{
+    const float4 *l4 = (const float4 *)leaves + 3 * k;
+    const float4 lo = l4[0];                  // minX minY minZ maxX
+    const float4 hi = l4[1];                  // maxY maxZ id isStatic
+    const int32_t id = __float_as_int(hi.z);
+    const bool st = __float_as_int(hi.w) != 0;
+    return (e_id < id) & !(a_static & st) &
+           (q.pMin.x < lo.w) & (lo.x < q.pMax.x) &
+           (q.pMin.y < hi.x) & (lo.y < q.pMax.y) &
+           (q.pMin.z < hi.y) & (lo.z < q.pMax.z);
+}
+
 __device__ __forceinline__ bool slotOverlaps(const AABB &q, const OrderedLeaf &o)
 {
     return q.pMin.x < o.maxX && o.minX < q.pMax.x &&
@@ -413,11 +429,13 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
             const int32_t e_id = me.id;
             const bool a_static = me.isStatic != 0;
             const bool active = row < rows;
-            // sweep 1: count hits, keep the first kOverlapBuf ranks
+            // sweep 1: count hits, keep the first kOverlapBuf ranks.  The
+            // hit test is evaluated branch-free on one 32-byte broadcast read
+            // per leaf (short-circuit && became nested exec-mask branches with
+            // a dependent LDS read per field).
+#pragma unroll 4
             for (int32_t k = 0; k < nleaves; k++) {
-                const OrderedLeaf &o = leaves[k];            // LDS broadcast
-                const bool hit = active && e_id < o.id && !(a_static && o.isStatic) &&
-                                 slotOverlaps(q, o);
+                const bool hit = active & leafHit(leaves, k, q, e_id, a_static);
                 if (hit) {
                     if (cnt < kOverlapBuf) buf[cnt] = (uint16_t)k;
                     cnt++;
@@ -436,12 +454,10 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
                 } else {
                     int32_t i = 0;
                     for (int32_t k = 0; k < nleaves; k++) {
-                        const OrderedLeaf &o = leaves[k];
-                        const bool hit = e_id < o.id && !(a_static && o.isStatic) &&
-                                         slotOverlaps(q, o);
-                        if (hit) {
+                        if (leafHit(leaves, k, q, e_id, a_static)) {
                             const int32_t slot = base + off + i++;
-                            if (slot < P.candCapacity) out[slot] = CandidateCollision { a_loc, o.loc };
+                            if (slot < P.candCapacity)
+                                out[slot] = CandidateCollision { a_loc, leaves[k].loc };
                         }
                     }
                 }
