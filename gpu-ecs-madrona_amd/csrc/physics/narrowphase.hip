@@ -220,17 +220,38 @@ __device__ __forceinline__ void groupArgMax(float &v, int32_t &k)
 }
 
 // Transform one body's hull into the group's LDS and copy its edge topology.
+// Not inlined: the two transforms, interleaved into the SAT body by the
+// scheduler, set the kernel's register peak (156 -> ~110 VGPRs apart), and
+// the call only takes plain values and pointers.
+__device__ __noinline__ void stageHullRaw(const Vector3 *obj_verts,
+                                          const geometry::Plane *obj_planes,
+                                          const EdgeQuad *obj_quads, const HullDev hd,
+                                          const Vector3 x, const Quat rot,
+                                          const Diag3x3 scale, Vector3 *v,
+                                          geometry::Plane *pl, EdgeQuad *q, int32_t lane)
+{
+    const Mat3x3 unscaled_rot = Mat3x3::fromQuat(rot);
+    const HullXform xf { unscaled_rot * scale, unscaled_rot * scale.inv(), x };
+    for (int32_t i = lane; i < hd.numVerts; i += kGroup)
+        v[i] = xf.vtx * obj_verts[hd.vertOffset + i] + xf.x;
+    for (int32_t i = lane; i < hd.numFaces; i += kGroup) {
+        const geometry::Plane op = obj_planes[hd.faceOffset + i];
+        const Vector3 origin = xf.vtx * (op.normal * op.d) + xf.x;
+        const Vector3 n = (xf.nrm * op.normal).normalize();
+        pl[i] = geometry::Plane { n, dot(n, origin) };
+    }
+    for (int32_t i = lane; i < hd.numEdges; i += kGroup) q[i] = obj_quads[hd.edgeOffset + i];
+}
+
 __device__ __forceinline__ Vector3 stageHull(const PhysArgs &P, int32_t w, const BodyArch &B,
                                              int32_t row, const HullDev &hd, Vector3 *v,
                                              geometry::Plane *pl, EdgeQuad *q, int32_t lane)
 {
     const ObjDev &O = P.objs;
-    const HullXform xf = hullXform(P, w, B, row);
-    for (int32_t i = lane; i < hd.numVerts; i += kGroup) v[i] = worldVertex(O, hd, xf, i);
-    for (int32_t i = lane; i < hd.numFaces; i += kGroup) pl[i] = worldPlane(O, hd, xf, i);
-    const EdgeQuad *gq = O.edgeQuads + hd.edgeOffset;
-    for (int32_t i = lane; i < hd.numEdges; i += kGroup) q[i] = gq[i];
-    return xf.x;
+    const Vector3 x = bcol<Vector3>(B, Cols::Position, w, row);
+    stageHullRaw(O.vertices, O.planes, O.edgeQuads, hd, x, bcol<Quat>(B, Cols::Rotation, w, row),
+                 bcol<Diag3x3>(B, Cols::Scale, w, row), v, pl, q, lane);
+    return x;
 }
 
 __device__ __forceinline__ float hullDistFromPlane(const geometry::Plane &p, const HullRef &h)
@@ -644,7 +665,7 @@ __device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS
 // separated).  The grid is what is resident at once; every group reaches
 // the end of the list and exits.
 #ifndef MW_SAT_MIN_BLOCKS
-#define MW_SAT_MIN_BLOCKS 1
+#define MW_SAT_MIN_BLOCKS 4
 #endif
 __global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKernel(PhysArgs P)
 {
