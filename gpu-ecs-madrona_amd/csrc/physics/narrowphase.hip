@@ -491,22 +491,27 @@ __device__ __forceinline__ geometry::Segment shortestSegmentBetween(const geomet
 __device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
                                             const CandidateCollision &cand, SatWork &out)
 {
+    // Every load is issued unconditionally (rows clamped into range) so the
+    // AABB, ObjectID and type reads overlap instead of forming a chain of
+    // branches; the verdict is combined at the end.
     const int32_t ia = bodyArchIndex(P, cand.a.archetype);
     const int32_t ib = bodyArchIndex(P, cand.b.archetype);
     const BodyArch &BA = P.body[ia];
     const BodyArch &BB = P.body[ib];
-    if ((uint32_t)cand.a.row >= (uint32_t)BA.capacity ||
-        (uint32_t)cand.b.row >= (uint32_t)BB.capacity) {
+    const bool rows_ok = (uint32_t)cand.a.row < (uint32_t)BA.capacity &&
+                         (uint32_t)cand.b.row < (uint32_t)BB.capacity;
+    const int32_t ra = rows_ok ? cand.a.row : 0, rb = rows_ok ? cand.b.row : 0;
+    const AABB *aabbs = P.bodyAABBs + (size_t)w * P.maxBodiesPerWorld;
+    const AABB a = aabbs[BA.slotBase + ra];
+    const AABB b = aabbs[BB.slotBase + rb];
+    const int32_t oa = bcol<ObjectID>(BA, Cols::ObjectID, w, ra).idx;
+    const int32_t ob = bcol<ObjectID>(BB, Cols::ObjectID, w, rb).idx;
+    const uint32_t ta = P.objs.types[oa], tb = P.objs.types[ob];
+    if (!rows_ok) {
         atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardWork << 8));
         return false;
     }
-    const AABB *aabbs = P.bodyAABBs + (size_t)w * P.maxBodiesPerWorld;
-    const AABB a = aabbs[BA.slotBase + cand.a.row];
-    const AABB b = aabbs[BB.slotBase + cand.b.row];
     if (!a.overlaps(b)) return false;
-    const int32_t oa = bcol<ObjectID>(BA, Cols::ObjectID, w, cand.a.row).idx;
-    const int32_t ob = bcol<ObjectID>(BB, Cols::ObjectID, w, cand.b.row).idx;
-    const uint32_t ta = P.objs.types[oa], tb = P.objs.types[ob];
     out.world = w;
     out.test = ta | tb;
     out.pad = 0;
@@ -572,25 +577,50 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
 // hull-plane counts -> each world's offset in the flat lists, and totals.
 __global__ void __launch_bounds__(1024) narrowScanKernel(PhysArgs P)
 {
+    // Each thread owns a contiguous run of worlds (counts held in registers):
+    // one block scan of the run sums instead of one per 1024 worlds.
     __shared__ int32_t s_scan[1024 / 64];
-    int32_t base_hh = 0, base_pl = 0;
-    for (int32_t chunk = 0; chunk < P.numWorlds; chunk += 1024) {
-        const int32_t w = chunk + threadIdx.x;
-        const int32_t hh = w < P.numWorlds ? P.hhCount[w] : 0;
-        const int32_t pl = w < P.numWorlds ? P.planeCount[w] : 0;
-        int32_t total_hh, total_pl;
-        const int32_t off_hh = blockExclusiveScan(hh, s_scan, &total_hh);
-        const int32_t off_pl = blockExclusiveScan(pl, s_scan, &total_pl);
-        if (w < P.numWorlds) {
-            P.hhOffset[w] = base_hh + off_hh;
-            P.planeOffset[w] = base_pl + off_pl;
+    const int32_t W = P.numWorlds;
+    const int32_t per = (W + 1023) / 1024;
+    const int32_t w0 = threadIdx.x * per;
+    const int32_t w1 = min(w0 + per, W);
+    constexpr int32_t kRun = 16;
+    int32_t hc[kRun], pc[kRun];
+    int32_t hh = 0, pl = 0;
+#pragma unroll
+    for (int32_t i = 0; i < kRun; i++) {
+        const int32_t w = w0 + i;
+        hc[i] = (i < per && w < w1) ? P.hhCount[w] : 0;
+        pc[i] = (i < per && w < w1) ? P.planeCount[w] : 0;
+    }
+#pragma unroll
+    for (int32_t i = 0; i < kRun; i++) { hh += hc[i]; pl += pc[i]; }
+    for (int32_t w = w0 + kRun; w < w1; w++) {      // more than 16 K worlds
+        hh += P.hhCount[w];
+        pl += P.planeCount[w];
+    }
+    int32_t total_hh, total_pl;
+    int32_t off_hh = blockExclusiveScan(hh, s_scan, &total_hh);
+    int32_t off_pl = blockExclusiveScan(pl, s_scan, &total_pl);
+#pragma unroll
+    for (int32_t i = 0; i < kRun; i++) {
+        const int32_t w = w0 + i;
+        if (i < per && w < w1) {
+            P.hhOffset[w] = off_hh;
+            P.planeOffset[w] = off_pl;
+            off_hh += hc[i];
+            off_pl += pc[i];
         }
-        base_hh += total_hh;
-        base_pl += total_pl;
+    }
+    for (int32_t w = w0 + kRun; w < w1; w++) {
+        P.hhOffset[w] = off_hh;
+        P.planeOffset[w] = off_pl;
+        off_hh += P.hhCount[w];
+        off_pl += P.planeCount[w];
     }
     if (threadIdx.x == 0) {
-        *P.satWorkCount = base_hh;
-        *P.jobCount = base_pl;
+        *P.satWorkCount = total_hh;
+        *P.jobCount = total_pl;
     }
 }
 

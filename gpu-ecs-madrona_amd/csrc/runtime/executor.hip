@@ -126,41 +126,47 @@ void launchClearRows(LaunchCtx &lc, int32_t archetype)
 
 // Packed export: world w's rows land at offset prefix(numRows)[w]
 // (reference madronaMWGPUExportCopyOut, src/mw/device/consts.cpp:190-273,
-// here a single block-wide scan per launch instead of O(blocks^2)).
+// here one block-wide scan per exported archetype per step instead of
+// O(blocks^2)).  Each thread owns a contiguous run of worlds; the run sums
+// are scanned with wave shuffles and one LDS pass.
 __global__ void __launch_bounds__(1024)
 exportScanKernel(const int32_t *num_rows, int32_t num_worlds, int64_t *offsets)
 {
-    __shared__ int64_t partial[1024];
-    const int32_t tid = threadIdx.x;
+    __shared__ int64_t wave_sums[1024 / 64];
+    const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int32_t per = (num_worlds + 1023) / 1024;
-    const int32_t beg = tid * per;
+    const int32_t beg = min(tid * per, num_worlds);
     const int32_t end = min(beg + per, num_worlds);
     int64_t s = 0;
     for (int32_t w = beg; w < end; w++) s += num_rows[w];
-    partial[tid] = s;
-    __syncthreads();
-    for (int32_t off = 1; off < 1024; off <<= 1) {
-        int64_t v = tid >= off ? partial[tid - off] : 0;
-        __syncthreads();
-        partial[tid] += v;
-        __syncthreads();
+    int64_t x = s;
+#pragma unroll
+    for (int32_t off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
     }
-    int64_t run = partial[tid] - s;
+    if (lane == 63) wave_sums[wave] = x;
+    __syncthreads();
+    int64_t base = 0;
+    for (int32_t i = 0; i < wave; i++) base += wave_sums[i];
+    int64_t run = base + x - s;
     for (int32_t w = beg; w < end; w++) {
         offsets[w] = run;
         run += num_rows[w];
     }
-    if (tid == 1023) offsets[num_worlds] = partial[1023];
+    if (tid == 1023) offsets[num_worlds] = base + x;
 }
 
-__global__ void exportCopyKernel(const char *col, int32_t capacity, uint32_t bytes,
-                                 const int32_t *num_rows, const int64_t *offsets,
-                                 char *out)
+// Rows are whole 4-byte words for every exported component, so the gather
+// moves dwords (one world per blockIdx.y).
+__global__ void __launch_bounds__(256)
+exportCopyKernel(const uint32_t *col, int32_t capacity, uint32_t words_per_row,
+                 const int32_t *num_rows, const int64_t *offsets, uint32_t *out)
 {
     const int32_t w = blockIdx.y;
-    const int32_t n = num_rows[w] * (int32_t)bytes;
-    const char *src = col + (size_t)w * capacity * bytes;
-    char *dst = out + (size_t)offsets[w] * bytes;
+    const int32_t n = num_rows[w] * (int32_t)words_per_row;
+    const uint32_t *src = col + (size_t)w * capacity * words_per_row;
+    uint32_t *dst = out + (size_t)offsets[w] * words_per_row;
     for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         dst[i] = src[i];
     }
@@ -173,7 +179,8 @@ struct ExportBuf {
     int32_t slot, archetype, column;
     uint32_t bytes;
     char *buf;
-    int64_t *offsets;
+    int64_t *offsets;           // shared by the exports of one archetype
+    bool scanOwner;             // this export launches the archetype's scan
 };
 
 struct Executor::Impl {
@@ -223,7 +230,7 @@ Executor::~Executor()
     }
     for (auto &e : impl_->exports) {
         (void)hipFree(e.buf);
-        (void)hipFree(e.offsets);
+        if (e.scanOwner) (void)hipFree(e.offsets);
     }
     impl_->mgr.reset();
     if (impl_->stream) (void)hipStreamDestroy(impl_->stream);
@@ -265,8 +272,18 @@ void Executor::uploadState()
         b.column = ex[i].column;
         b.bytes = ex[i].bytes;
         size_t bytes = (size_t)dv.numWorlds * dv.arch[b.archetype].capacity * b.bytes;
+        if (b.bytes % 4 != 0) {
+            throw std::runtime_error("exportColumn: component size must be a multiple of 4 bytes");
+        }
         MW_HIP_CHECK(hipMalloc(&b.buf, std::max<size_t>(bytes, 256)));
-        MW_HIP_CHECK(hipMalloc(&b.offsets, sizeof(int64_t) * (dv.numWorlds + 1)));
+        // offsets are per archetype: exports of one archetype share them
+        for (const ExportBuf &o : impl_->exports) {
+            if (o.archetype == b.archetype) { b.offsets = o.offsets; b.scanOwner = false; }
+        }
+        if (!b.offsets) {
+            MW_HIP_CHECK(hipMalloc(&b.offsets, sizeof(int64_t) * (dv.numWorlds + 1)));
+            b.scanOwner = true;
+        }
         impl_->exports.push_back(b);
     }
 }
@@ -275,11 +292,15 @@ static void launchExports(Executor::Impl &I, const StateView &dv)
 {
     for (ExportBuf &b : I.exports) {
         const ArchetypeView &av = dv.arch[b.archetype];
-        hipLaunchKernelGGL(exportScanKernel, dim3(1), dim3(1024), 0, I.stream,
-                           av.numRows, dv.numWorlds, b.offsets);
-        hipLaunchKernelGGL(exportCopyKernel, dim3(4, dv.numWorlds), dim3(256), 0, I.stream,
-                           av.cols[b.column], av.capacity, b.bytes, av.numRows, b.offsets,
-                           b.buf);
+        if (b.scanOwner) {
+            hipLaunchKernelGGL(exportScanKernel, dim3(1), dim3(1024), 0, I.stream,
+                               av.numRows, dv.numWorlds, b.offsets);
+        }
+        const uint32_t words = b.bytes / 4;
+        const unsigned bx = (unsigned)std::max<int64_t>(1, ((int64_t)av.capacity * words + 255) / 256);
+        hipLaunchKernelGGL(exportCopyKernel, dim3(bx, dv.numWorlds), dim3(256), 0, I.stream,
+                           (const uint32_t *)av.cols[b.column], av.capacity, words, av.numRows,
+                           b.offsets, (uint32_t *)b.buf);
     }
 }
 
