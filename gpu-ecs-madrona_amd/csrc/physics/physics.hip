@@ -430,8 +430,8 @@ MW_PHYS_NODE(NarrowphaseNode,
                        contactSharedBytes(P), stream, P);)
 
 MW_PHYS_NODE(SolverNode,
-    hipLaunchKernelGGL(solverKernel, dim3(P.numWorlds), dim3(kSolverBlock),
-                       solverSharedBytes(P), stream, P);)
+    hipLaunchKernelGGL(solverKernel, dim3((P.numWorlds + kSolverWorlds - 1) / kSolverWorlds),
+                       dim3(kSolverThreads), solverSharedBytes(P), stream, P);)
 
 // Joint constraints are collected per substep in the reference
 // (collectConstraintsSystem, physics.cpp:34-40).  Joint solving is not on

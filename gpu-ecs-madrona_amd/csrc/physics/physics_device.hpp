@@ -156,7 +156,12 @@ size_t contactSharedBytes(const PhysArgs &P);
 constexpr int32_t kOverlapBlock = 192;
 constexpr int32_t kNarrowBlock = 256;
 constexpr int32_t kContactBlock = 128;
-constexpr int32_t kSolverBlock = 64;
+constexpr int32_t kSolverBlock = 64;      // lanes per world (one wave)
+#ifndef MW_SOLVER_WORLDS
+#define MW_SOLVER_WORLDS 2
+#endif
+constexpr int32_t kSolverWorlds = MW_SOLVER_WORLDS;       // worlds per solver block
+constexpr int32_t kSolverThreads = kSolverBlock * kSolverWorlds;
 #ifndef MW_REFIT_BLOCK
 #define MW_REFIT_BLOCK 128
 #endif

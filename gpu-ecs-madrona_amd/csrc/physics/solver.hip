@@ -269,8 +269,12 @@ static_assert(sizeof(CRec) == 8);
 // Contacts whose records stay in LDS; worlds with more contacts keep them
 // in a global slab instead, so the LDS footprint (and with it the number of
 // worlds resident per CU) does not scale with SolverData::maxContacts.
-constexpr int32_t kSolverLDSContacts = 128;
+#ifndef MW_SOLVER_LDS_CONTACTS
+#define MW_SOLVER_LDS_CONTACTS 128
+#endif
+constexpr int32_t kSolverLDSContacts = MW_SOLVER_LDS_CONTACTS;
 
+// Per-world LDS image: bodies, ordering flags, contact records.
 struct SolverLDS {
     SMut *bodies;         // [nb]
     int16_t *lastLevel;   // [nb] -1: invariant static body (no ordering edges)
@@ -278,44 +282,126 @@ struct SolverLDS {
     int32_t *prevs;       // [kSolverLDSContacts] (prev contact on s1, on s2) as 2 x int16
 };
 
-__host__ __device__ inline size_t solverLDSBytes(int32_t nb)
+__host__ __device__ inline size_t solverA16(size_t b) { return (b + 15) & ~size_t(15); }
+
+__host__ __device__ inline size_t solverWorldLDSBytes(int32_t nb)
 {
-    auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
-    return a16(sizeof(SMut) * nb) + a16(sizeof(int16_t) * nb) +
+    return solverA16(sizeof(SMut) * nb) + solverA16(sizeof(int16_t) * nb) +
            (sizeof(CRec) + sizeof(int32_t)) * kSolverLDSContacts;
 }
 
-__device__ __forceinline__ SolverLDS solverLDS(char *smem, int32_t nb)
+// Block-shared level schedule: every (world, contact) of the block sorted
+// by level, so one pass over a level keeps all of the block's lanes on that
+// level's contacts from all of its worlds.
+constexpr int32_t kSolverItems = kSolverWorlds * kSolverLDSContacts;
+
+__host__ __device__ inline size_t solverBlockLDSBytes(int32_t nb)
 {
-    auto a16 = [](size_t b) { return (b + 15) & ~size_t(15); };
+    return kSolverWorlds * solverWorldLDSBytes(nb) +
+           sizeof(uint32_t) * kSolverItems +               // items (world << 16 | k)
+           sizeof(int32_t) * 2 * (kSolverItems + 2) +      // level offsets / cursors
+           sizeof(int32_t) * 4;                            // block scalars
+}
+
+struct SolverBlockLDS {
+    uint32_t *items;
+    int32_t *levelOff;    // [Lmax + 2]
+    int32_t *levelCur;    // [Lmax + 2]
+    int32_t *scalars;     // [0] sum K, [1] max K, [2] max level
+};
+
+__device__ __forceinline__ SolverLDS solverWorldLDS(char *smem, int32_t nb, int32_t wi)
+{
     SolverLDS L;
-    L.bodies = (SMut *)smem;
-    char *p = smem + a16(sizeof(SMut) * nb);
+    char *p = smem + (size_t)wi * solverWorldLDSBytes(nb);
+    L.bodies = (SMut *)p;
+    p += solverA16(sizeof(SMut) * nb);
     L.lastLevel = (int16_t *)p;
-    p += a16(sizeof(int16_t) * nb);
+    p += solverA16(sizeof(int16_t) * nb);
     L.recs = (CRec *)p;
     p += sizeof(CRec) * kSolverLDSContacts;
     L.prevs = (int32_t *)p;
     return L;
 }
 
-// Occupancy: the kernel is latency bound (one wave per world, dependent
-// LDS / column reads per contact), so residency matters more than packed
-// math; built without SLP vectorisation (Makefile) it fits 3 waves per SIMD
-// without spills.
-#ifndef MW_SOLVER_WAVES_PER_EU
-#define MW_SOLVER_WAVES_PER_EU 3
-#endif
-// Phases 2-7 of the solver for one world.  Instantiated twice (records in
-// LDS / in the global fallback slab) so every access has a known address
-// space: no flat loads with full waits in the level search.
-__device__ __forceinline__ void solveWorld(const PhysArgs &P, const int32_t w, SolverLDS &L,
-                                           SMut *bodies, const int32_t nb,
-                                           const Contact *cslots, int32_t *order,
-                                           const int32_t S, const int32_t K, CRec *recs,
-                                           int32_t *prevs)
+__device__ __forceinline__ SolverBlockLDS solverBlockLDS(char *smem, int32_t nb)
 {
-    const int32_t lane = threadIdx.x;
+    SolverBlockLDS B;
+    char *p = smem + kSolverWorlds * solverWorldLDSBytes(nb);
+    B.items = (uint32_t *)p;
+    p += sizeof(uint32_t) * kSolverItems;
+    B.levelOff = (int32_t *)p;
+    p += sizeof(int32_t) * (kSolverItems + 2);
+    B.levelCur = (int32_t *)p;
+    p += sizeof(int32_t) * (kSolverItems + 2);
+    B.scalars = (int32_t *)p;
+    return B;
+}
+
+// One world's LDS is owned by one wave; within a wave LDS writes become
+// visible after the wave's LDS queue drains.
+__device__ __forceinline__ void waveSync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Load one world's bodies into its LDS image (wave `lane` 0..63).
+__device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, SolverLDS &L,
+                                                int32_t lane)
+{
+    for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
+        const BodyArch &B = P.body[ba];
+        const int32_t rows = B.numRows[w];
+        for (int32_t r = lane; r < rows; r += kSolverBlock) {
+            SMut s;
+            s.x = bcol<Vector3>(B, Cols::Position, w, r);
+            s.q = bcol<Quat>(B, Cols::Rotation, w, r);
+            const Velocity vel = bcol<Velocity>(B, Cols::Velocity, w, r);
+            s.v = vel.linear;
+            s.omega = vel.angular;
+            const uint32_t obj = (uint32_t)bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
+            s.meta = ((uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r) & 0xffu) |
+                     ((uint32_t)ba << 8) | (obj << 16);
+            L.bodies[B.slotBase + r] = s;
+            L.lastLevel[B.slotBase + r] = staticInvariant(s) ? (int16_t)-1 : (int16_t)0;
+        }
+    }
+}
+
+// Number of survivors with a manifold (the world's contact count), capped at
+// maxContacts like the reference's assert (narrowphase.cpp:1130).
+__device__ __forceinline__ int32_t worldContactCount(const PhysArgs &P, int32_t w, int32_t lane)
+{
+    const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
+    const int32_t S = P.survCount[w];
+    int32_t K = 0;
+    for (int32_t chunk = 0; chunk < S; chunk += kSolverBlock) {
+        const int32_t s = chunk + lane;
+        K += __popcll(__ballot(s < S && cslots[s].numPoints > 0));
+    }
+    if (K > P.maxContacts) {
+        if (lane == 0) atomicOr(P.errorFlags + w, kErrContactOverflow);
+        K = P.maxContacts;
+    }
+    return K;
+}
+
+// Contact records in survivor order (== the reference's addManifoldToSolver
+// append order, narrowphase.cpp:1123-1162) and their dependency levels: a
+// contact waits only for the latest earlier contact on each of its bodies
+// (invariant static bodies excepted); level = 1 + max(levels of those
+// predecessors), relaxed to its fixpoint.  One wave per world.
+template <typename RecPtr, typename PrevPtr>
+__device__ __forceinline__ int32_t orderAndLevel(const PhysArgs &P, int32_t w, SolverLDS &L,
+                                                 int32_t K, RecPtr recs, PrevPtr prevs,
+                                                 int32_t lane)
+{
+    const int32_t nb = P.maxBodiesPerWorld;
+    const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
+    int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
+    const int32_t S = P.survCount[w];
     const uint64_t lt_mask = (1ull << lane) - 1;
     int32_t k0 = 0;
     for (int32_t chunk = 0; chunk < S && k0 < K; chunk += kSolverBlock) {
@@ -333,13 +419,7 @@ __device__ __forceinline__ void solveWorld(const PhysArgs &P, const int32_t w, S
         }
         k0 += __popcll(mask);
     }
-    __syncthreads();
-
-    // 3. levels.  The reference solves contacts serially (Gauss-Seidel); a
-    //    contact only has to wait for the latest earlier contact on each of
-    //    its bodies (invariant static bodies excepted).  Find those two
-    //    predecessors per contact in parallel, then level = 1 + max(levels
-    //    of the predecessors), relaxed to its fixpoint (one round per level).
+    waveSync();
     for (int32_t k = lane; k < K; k += kSolverBlock) {
         CRec r = recs[k];
         const bool on1 = L.lastLevel[r.s1] >= 0, on2 = L.lastLevel[r.s2] >= 0;
@@ -353,7 +433,7 @@ __device__ __forceinline__ void solveWorld(const PhysArgs &P, const int32_t w, S
         r.lvl = 1;
         recs[k] = r;
     }
-    __syncthreads();
+    waveSync();
     for (;;) {
         bool changed = false;
         for (int32_t k = lane; k < K; k += kSolverBlock) {
@@ -367,7 +447,7 @@ __device__ __forceinline__ void solveWorld(const PhysArgs &P, const int32_t w, S
                 changed = true;
             }
         }
-        __syncthreads();
+        waveSync();
         if (!__any(changed)) break;
     }
     int32_t max_level = 0;
@@ -375,26 +455,18 @@ __device__ __forceinline__ void solveWorld(const PhysArgs &P, const int32_t w, S
 #pragma unroll
     for (int32_t off = 32; off > 0; off >>= 1) max_level = max(max_level, __shfl_xor(max_level, off));
     if (lane == 0) P.lastNumContacts[w] = K;
-    const SolverData &sd = P.solver[w];
+    return max_level;
+}
 
-    // 4. solvePositions, level by level
-    for (int32_t l = 1; l <= max_level; l++) {
-        for (int32_t k = threadIdx.x; k < K; k += kSolverBlock) {
-            const CRec r = recs[k];
-            if (r.lvl != l) continue;
-            Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
-            solveContactPositions(P, w, bodies[r.s1], r.s1, bodies[r.s2], r.s2, c);
-        }
-        __syncthreads();
-    }
-
-    // 5. setVelocities (physics.cpp:673-714)
-    const float h = sd.h;
+// setVelocities (physics.cpp:673-714) for one world, one wave.
+__device__ __forceinline__ void setWorldVelocities(const PhysArgs &P, int32_t w, SolverLDS &L,
+                                                   float h, int32_t lane)
+{
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
-        for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
-            SMut &s = bodies[B.slotBase + r];
+        for (int32_t r = lane; r < rows; r += kSolverBlock) {
+            SMut &s = L.bodies[B.slotBase + r];
             const auto prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
             const Quat q = s.q, qp = prev.prevRotation;
             Quat dq;
@@ -408,92 +480,176 @@ __device__ __forceinline__ void solveWorld(const PhysArgs &P, const int32_t w, S
             s.omega = dq.w > 0.f ? new_omega : -new_omega;
         }
     }
-    __syncthreads();
+}
 
-    // 6. solveVelocities, same levels
-    for (int32_t l = 1; l <= max_level; l++) {
-        for (int32_t k = threadIdx.x; k < K; k += kSolverBlock) {
-            const CRec r = recs[k];
-            if (r.lvl != l) continue;
-            const Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
-            solveContactVelocities(P, w, bodies[r.s1], r.s1, bodies[r.s2], r.s2, c, h,
-                                   sd.restitutionThreshold);
-        }
-        __syncthreads();
-    }
-
-    // 7. write back
+__device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, SolverLDS &L,
+                                                 int32_t lane)
+{
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
-        for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
-            const SMut &s = bodies[B.slotBase + r];
+        for (int32_t r = lane; r < rows; r += kSolverBlock) {
+            const SMut &s = L.bodies[B.slotBase + r];
             bcol<Vector3>(B, Cols::Position, w, r) = s.x;
             bcol<Quat>(B, Cols::Rotation, w, r) = s.q;
             bcol<Velocity>(B, Cols::Velocity, w, r) = Velocity { s.v, s.omega };
         }
     }
-    if (threadIdx.x == 0) P.solver[w].numContacts = 0;     // physics.cpp:1007
+    if (lane == 0) P.solver[w].numContacts = 0;           // physics.cpp:1007
 }
 
-__global__ void __launch_bounds__(kSolverBlock)
+// Fallback for a world whose contacts do not fit the LDS records: the whole
+// solve on its own wave, records in the global slab, level by level.
+__device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, SolverLDS L,
+                                              int32_t K, int32_t lane)
+{
+    CRec *recs = (CRec *)(P.solverRecs + (size_t)w * P.candCapacity);
+    int32_t *prevs = P.solverPrevs + (size_t)w * P.candCapacity;
+    const int32_t max_level = orderAndLevel(P, w, L, K, recs, prevs, lane);
+    const SolverData &sd = P.solver[w];
+    for (int32_t l = 1; l <= max_level; l++) {
+        for (int32_t k = lane; k < K; k += kSolverBlock) {
+            const CRec r = recs[k];
+            if (r.lvl != l) continue;
+            Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
+            solveContactPositions(P, w, L.bodies[r.s1], r.s1, L.bodies[r.s2], r.s2, c);
+        }
+        waveSync();
+    }
+    setWorldVelocities(P, w, L, sd.h, lane);
+    waveSync();
+    for (int32_t l = 1; l <= max_level; l++) {
+        for (int32_t k = lane; k < K; k += kSolverBlock) {
+            const CRec r = recs[k];
+            if (r.lvl != l) continue;
+            const Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
+            solveContactVelocities(P, w, L.bodies[r.s1], r.s1, L.bodies[r.s2], r.s2, c, sd.h,
+                                   sd.restitutionThreshold);
+        }
+        waveSync();
+    }
+}
+
+// Occupancy: latency bound (dependent LDS / column reads per contact), so
+// residency matters more than packed math; built without SLP vectorisation
+// (Makefile) it fits 3 waves per SIMD without spills.
+#ifndef MW_SOLVER_WAVES_PER_EU
+#define MW_SOLVER_WAVES_PER_EU 3
+#endif
+
+// XPBD solver, kSolverWorlds worlds per block (one wave each for the
+// per-world phases).  The Gauss-Seidel contact passes run level by level
+// over the block's level-sorted (world, contact) list, so a level's
+// contacts from all of the block's worlds share the lanes: sparse deep
+// levels no longer cost a full wave pass per world.
+__global__ void __launch_bounds__(kSolverThreads)
 __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(PhysArgs P)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int32_t w = blockIdx.x;
     const int32_t nb = P.maxBodiesPerWorld;
-    SolverLDS L = solverLDS(smem, nb);
-    SMut *bodies = L.bodies;
+    const int32_t wi = threadIdx.x / kSolverBlock;
+    const int32_t lane = threadIdx.x % kSolverBlock;
+    const int32_t w = blockIdx.x * kSolverWorlds + wi;
+    const bool live = w < P.numWorlds;
+    SolverLDS L = solverWorldLDS(smem, nb, wi);
+    SolverBlockLDS BL = solverBlockLDS(smem, nb);
 
-    // 1. load bodies into LDS
-    for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
-        const BodyArch &B = P.body[ba];
-        const int32_t rows = B.numRows[w];
-        for (int32_t r = threadIdx.x; r < rows; r += kSolverBlock) {
-            SMut s;
-            s.x = bcol<Vector3>(B, Cols::Position, w, r);
-            s.q = bcol<Quat>(B, Cols::Rotation, w, r);
-            const Velocity vel = bcol<Velocity>(B, Cols::Velocity, w, r);
-            s.v = vel.linear;
-            s.omega = vel.angular;
-            const uint32_t obj = (uint32_t)bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
-            s.meta = ((uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r) & 0xffu) |
-                     ((uint32_t)ba << 8) | (obj << 16);
-            bodies[B.slotBase + r] = s;
-            L.lastLevel[B.slotBase + r] = staticInvariant(s) ? (int16_t)-1 : (int16_t)0;
+    if (threadIdx.x == 0) { BL.scalars[0] = 0; BL.scalars[1] = 0; BL.scalars[2] = 0; }
+    int32_t K = 0;
+    if (live) {
+        loadWorldBodies(P, w, L, lane);
+        K = worldContactCount(P, w, lane);
+    }
+    __syncthreads();
+    if (live && lane == 0) atomicMax(&BL.scalars[1], K);
+    __syncthreads();
+    const bool fits = BL.scalars[1] <= kSolverLDSContacts;
+
+    if (!fits) {
+        // some world of the block overflows the LDS records: every world
+        // of the block solves on its own wave with global records
+        if (live) {
+            solveWorldGlobal(P, w, L, K, lane);
+            writeWorldBodies(P, w, L, lane);
+        }
+        return;
+    }
+
+    int32_t my_levels = 0;
+    if (live) my_levels = orderAndLevel(P, w, L, K, L.recs, L.prevs, lane);
+    if (live && lane == 0) atomicMax(&BL.scalars[2], my_levels);
+    __syncthreads();
+    const int32_t max_level = BL.scalars[2];
+
+    // counting sort of the block's contacts by level
+    for (int32_t i = threadIdx.x; i <= max_level + 1; i += kSolverThreads) {
+        BL.levelOff[i] = 0;
+        BL.levelCur[i] = 0;
+    }
+    __syncthreads();
+    if (live) {
+        for (int32_t k = lane; k < K; k += kSolverBlock) atomicAdd(&BL.levelOff[L.recs[k].lvl], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t run = 0;
+        for (int32_t l = 0; l <= max_level + 1; l++) {
+            const int32_t c = BL.levelOff[l];
+            BL.levelOff[l] = run;
+            run += c;
         }
     }
+    __syncthreads();
+    if (live) {
+        for (int32_t k = lane; k < K; k += kSolverBlock) {
+            const int32_t l = L.recs[k].lvl;
+            const int32_t pos = BL.levelOff[l] + atomicAdd(&BL.levelCur[l], 1);
+            BL.items[pos] = ((uint32_t)wi << 16) | (uint32_t)k;
+        }
+    }
+    __syncthreads();
 
-    // 2. ordered contact list: survivors with a manifold, in survivor order
-    //    (== the reference's addManifoldToSolver append order,
-    //    narrowphase.cpp:1123-1162).  Pass 1 counts, pass 2 writes.
-    const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
-    int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
-    const int32_t S = P.survCount[w];
-    const int32_t lane = threadIdx.x;
-    const uint64_t lt_mask = (1ull << lane) - 1;
-    int32_t K = 0;
-    for (int32_t chunk = 0; chunk < S; chunk += kSolverBlock) {
-        const int32_t s = chunk + lane;
-        K += __popcll(__ballot(s < S && cslots[s].numPoints > 0));
+    // solvePositions, level by level over the whole block
+    for (int32_t l = 1; l <= max_level; l++) {
+        const int32_t beg = BL.levelOff[l], end = BL.levelOff[l + 1];
+        for (int32_t t = beg + threadIdx.x; t < end; t += kSolverThreads) {
+            const uint32_t it = BL.items[t];
+            const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xffffu);
+            const int32_t ww = blockIdx.x * kSolverWorlds + iw;
+            SolverLDS LW = solverWorldLDS(smem, nb, iw);
+            const CRec r = LW.recs[k];
+            Contact &c = P.candContacts[(size_t)ww * P.candCapacity + r.slot];
+            solveContactPositions(P, ww, LW.bodies[r.s1], r.s1, LW.bodies[r.s2], r.s2, c);
+        }
+        __syncthreads();
     }
-    if (K > P.maxContacts) {
-        // The reference asserts here (narrowphase.cpp:1130); flag, truncate.
-        if (lane == 0) atomicOr(P.errorFlags + w, kErrContactOverflow);
-        K = P.maxContacts;
+
+    if (live) setWorldVelocities(P, w, L, P.solver[w].h, lane);
+    __syncthreads();
+
+    // solveVelocities, same schedule
+    for (int32_t l = 1; l <= max_level; l++) {
+        const int32_t beg = BL.levelOff[l], end = BL.levelOff[l + 1];
+        for (int32_t t = beg + threadIdx.x; t < end; t += kSolverThreads) {
+            const uint32_t it = BL.items[t];
+            const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xffffu);
+            const int32_t ww = blockIdx.x * kSolverWorlds + iw;
+            SolverLDS LW = solverWorldLDS(smem, nb, iw);
+            const CRec r = LW.recs[k];
+            const Contact &c = P.candContacts[(size_t)ww * P.candCapacity + r.slot];
+            const SolverData &sd = P.solver[ww];
+            solveContactVelocities(P, ww, LW.bodies[r.s1], r.s1, LW.bodies[r.s2], r.s2, c,
+                                   sd.h, sd.restitutionThreshold);
+        }
+        __syncthreads();
     }
-    if (K <= kSolverLDSContacts) {
-        solveWorld(P, w, L, bodies, nb, cslots, order, S, K, L.recs, L.prevs);
-    } else {
-        solveWorld(P, w, L, bodies, nb, cslots, order, S, K,
-                   (CRec *)(P.solverRecs + (size_t)w * P.candCapacity),
-                   P.solverPrevs + (size_t)w * P.candCapacity);
-    }
+
+    if (live) writeWorldBodies(P, w, L, lane);
 }
 
 size_t solverSharedBytes(const PhysArgs &P)
 {
-    return solverLDSBytes(P.maxBodiesPerWorld);
+    return solverBlockLDSBytes(P.maxBodiesPerWorld);
 }
 
 }
