@@ -99,7 +99,7 @@ PhysWorld::PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &i
     const mw_collisions_config &c = cfg.c;
     RigidBodyPhysicsSystem::init(ctx, cfg.objMgr, c.delta_t, c.num_substeps,
                                  Vector3 { 0.f, 0.f, c.gravity_z }, c.num_cubes + 1,
-                                 c.max_contacts, 16);
+                                 c.max_contacts, c.num_joints > 16 ? c.num_joints : 16);
 
     auto setup = [&](Entity e, Vector3 p, Quat q, int32_t obj, ResponseType rt) {
         ctx.getUnsafe<Position>(e) = Position { p };
@@ -117,14 +117,34 @@ PhysWorld::PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &i
             RigidBodyPhysicsSystem::registerEntity(ctx, e, ObjectID { obj });
     };
 
+    std::vector<Entity> cubes;
     for (int32_t i = 0; i < c.num_cubes; i++) {
         Entity e = ctx.makeEntityNow<PhysicsBody>();
         Vector3 p { init.pos[3 * i], init.pos[3 * i + 1], init.pos[3 * i + 2] };
         Quat q { init.rot[4 * i], init.rot[4 * i + 1], init.rot[4 * i + 2], init.rot[4 * i + 3] };
         setup(e, p, q, 0, ResponseType::Dynamic);
+        cubes.push_back(e);
     }
     Entity plane = ctx.makeEntityNow<PhysicsBody>();
     setup(plane, Vector3::zero(), Quat { 1.f, 0.f, 0.f, 0.f }, 1, ResponseType::Static);
+
+    // Joint workload (mw_collisions_config::num_joints): joint j ties cube
+    // 2j to cube 2j + 1, fixed, or hinge for the last num_hinge_joints --
+    // the same ConstraintData rows oracle/ref_harness.cpp builds on the
+    // reference.
+    for (int32_t j = 0; j < c.num_joints; j++) {
+        Entity e1 = cubes[2 * j], e2 = cubes[2 * j + 1];
+        Entity je = ctx.makeEntityNow<ConstraintData>();
+        if (j < c.num_joints - c.num_hinge_joints) {
+            ctx.getUnsafe<JointConstraint>(je) = JointConstraint::setupFixed(
+                e1, e2, Quat { 1.f, 0.f, 0.f, 0.f }, Quat { 0.70710678f, 0.f, 0.f, 0.70710678f },
+                Vector3 { 0.f, 1.5f, 0.f }, Vector3 { 0.f, -1.5f, 0.f }, 0.5f);
+        } else {
+            ctx.getUnsafe<JointConstraint>(je) = JointConstraint::setupHinge(
+                e1, e2, Vector3 { 1, 0, 0 }, Vector3 { 1, 0, 0 }, Vector3 { 0, 1, 0 },
+                Vector3 { 0, 1, 0 }, Vector3 { 0.f, 0.f, 1.5f }, Vector3 { 0.f, 0.f, -1.5f });
+        }
+    }
 
     ctx.getSingleton<broadphase::BVH>().rebuildOnUpdate();
     ctx.getSingleton<EpisodeReturn>().value = 0.f;
@@ -141,6 +161,11 @@ static Executor *create(const ExecConfig &ecfg, const void *user_cfg, size_t cfg
     }
     Config cfg;
     memcpy(&cfg.c, user_cfg, sizeof(cfg.c));
+    if (cfg.c.num_joints < 0 || 2 * cfg.c.num_joints > cfg.c.num_cubes ||
+        cfg.c.num_hinge_joints < 0 || cfg.c.num_hinge_joints > cfg.c.num_joints) {
+        throw std::runtime_error("collisions: need 0 <= 2 * num_joints <= num_cubes and "
+                                 "0 <= num_hinge_joints <= num_joints");
+    }
     cfg.objMgr = envs::makeCubeObjectManager(cfg.c);
     std::vector<mw_collisions_init> init_vec(ecfg.numWorlds);
     for (int32_t w = 0; w < ecfg.numWorlds; w++) {

@@ -152,6 +152,7 @@ struct PhysicsModule : StateExtension {
     int32_t maxLeaves = 0;
     int32_t maxNodes = 0;
     int32_t maxContacts = 0;
+    int32_t maxJoints = 0;
     int32_t candCapacity = 0;
 
     std::vector<Entity> leafEntitiesHost;        // [W][maxLeaves]
@@ -328,8 +329,17 @@ void PhysicsModule::upload(void *stream_ptr)
     P.candContacts = devAlloc<Contact>((size_t)W * P.candCapacity, stream);
     P.maxContacts = maxContacts;
     P.contactOrder = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
-    P.solverRecs = devAlloc<uint64_t>((size_t)W * P.candCapacity, stream);
-    P.solverPrevs = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
+    const int32_t joint_arch = mgr->archetypeIndex(typeKey<ConstraintData>());
+    P.jointCapacity = dv.arch[joint_arch].capacity;
+    P.numJointRows = dv.arch[joint_arch].numRows;
+    P.joints = (JointConstraint *)dv.arch[joint_arch].cols[1];
+    P.maxJoints = maxJoints;
+    P.recStride = P.candCapacity + std::min(maxJoints, P.jointCapacity);
+    if (P.recStride > 32767) {
+        throw std::runtime_error("physics: max candidates + joints per world must be <= 32767");
+    }
+    P.solverRecs = devAlloc<uint64_t>((size_t)W * P.recStride, stream);
+    P.solverPrevs = devAlloc<int32_t>((size_t)W * P.recStride, stream);
     P.lastNumContacts = devAlloc<int32_t>(W, stream);
     P.lastNumCands = devAlloc<int32_t>(W, stream);
 
@@ -434,8 +444,10 @@ MW_PHYS_NODE(SolverNode,
                        dim3(kSolverThreads), solverSharedBytes(P), stream, P);)
 
 // Joint constraints are collected per substep in the reference
-// (collectConstraintsSystem, physics.cpp:34-40).  Joint solving is not on
-// the scoped path; the node keeps the graph shape.
+// (collectConstraintsSystem, physics.cpp:34-40: ConstraintData rows copied
+// in row order into SolverData).  Nothing mutates those rows during a step,
+// so the solver kernel reads them in place, in the same order; the node only
+// keeps the graph shape.
 MW_PHYS_NODE(CollectConstraintsNode, (void)P;)
 
 // ===========================================================================
@@ -492,6 +504,7 @@ void RigidBodyPhysicsSystem::init(Context &ctx, ObjectManager *obj_mgr, float de
         m.maxLeaves = (int32_t)max_dynamic_objects;
         m.maxNodes = numInternalNodes((int32_t)max_dynamic_objects);
         m.maxContacts = (int32_t)max_contacts_per_world;
+        m.maxJoints = (int32_t)max_joint_constraints_per_world;
         m.leafEntitiesHost.assign((size_t)W * m.maxLeaves, Entity::none());
 
         // Flatten the host object table.
@@ -532,7 +545,8 @@ void RigidBodyPhysicsSystem::init(Context &ctx, ObjectManager *obj_mgr, float de
             m.hulls.push_back(hd);
         }
     } else if (m.maxLeaves != (int32_t)max_dynamic_objects ||
-               m.maxContacts != (int32_t)max_contacts_per_world) {
+               m.maxContacts != (int32_t)max_contacts_per_world ||
+               m.maxJoints != (int32_t)max_joint_constraints_per_world) {
         throw std::runtime_error("RigidBodyPhysicsSystem::init: per-world sizes must match");
     }
 

@@ -147,6 +147,15 @@ struct PhysArgs {
                                   // exceeds the LDS-resident budget
     int32_t *solverPrevs;         // [W][candCapacity] predecessor pairs, same condition
     int32_t *lastNumContacts;     // [W] debug: contacts of the last substep
+    int32_t recStride;            // solverRecs / solverPrevs entries per world
+                                  // (candCapacity + maxJoints)
+
+    // ConstraintData rows (JointConstraint column), solved after the
+    // contacts of each substep (physics.cpp:650-671)
+    int32_t jointCapacity;
+    int32_t maxJoints;            // SolverData::maxJointConstraints
+    int32_t *numJointRows;        // [W]
+    JointConstraint *joints;      // [W][jointCapacity]
     int32_t *lastNumCands;        // [W] debug: candidates of the last step
 
     ObjDev objs;
@@ -162,5 +171,8 @@ inline constexpr int32_t kErrSolverBodies = 32;
 // A data-derived index left its range (only reachable through corrupted
 // state); bits 8..15 carry the site (physics_device.hpp guardIndex).
 inline constexpr int32_t kErrIndexGuard = 64;
+// More ConstraintData rows than SolverData::maxJointConstraints (the
+// reference writes past its buffer, physics.cpp:34-40); the excess is dropped.
+inline constexpr int32_t kErrJointOverflow = 128;
 
 }

@@ -137,6 +137,89 @@ __device__ void solveContactPositions(const PhysArgs &P, int32_t w, SMut &b1, in
     b1.q = q1; b2.q = q2;
 }
 
+// Joint constraints (physics.cpp:247-279, 478-648), run after the contacts
+// of solvePositions in ConstraintData row order.
+__device__ __forceinline__ void angularCorrection(Quat &q1, Quat &q2, Vector3 dq, Vector3 iI1,
+                                                  Vector3 iI2)
+{                                                          // physics.cpp:490-504, 522-534
+    const float mag = dq.length();
+    if (mag > 0) {
+        dq /= mag;
+        const Vector3 n1 = q1.inv().rotateVec(dq);
+        const Vector3 n2 = q2.inv().rotateVec(dq);
+        // computeAngularUpdate (:247-271) + applyAngularUpdate (:273-279)
+        const Vector3 lra1 = multDiag(iI1, n1);
+        const Vector3 lra2 = multDiag(iI2, n2);
+        const float w1 = dot(n1, lra1);
+        const float w2 = dot(n2, lra2);
+        const float dl = -mag / (w1 + w2 + 0.f);
+        const float half = 0.5f * dl;
+        const Quat u1 = Quat::fromAngularVec(q1.rotateVec(half * lra1));
+        const Quat u2 = Quat::fromAngularVec(q2.rotateVec(half * lra2));
+        q1 = (q1 + u1 * q1).normalize();
+        q2 = (q2 - u2 * q2).normalize();
+    }
+}
+
+__device__ void solveJoint(const PhysArgs &P, SMut &b1, SMut &b2, const JointConstraint &j)
+{                                                          // handleJointConstraint, :537-648
+    const RigidBodyMetadata m1 = P.objs.metadata[b1.meta >> 16];
+    const RigidBodyMetadata m2 = P.objs.metadata[b2.meta >> 16];
+    Vector3 x1 = b1.x, x2 = b2.x;
+    Quat q1 = b1.q, q2 = b2.q;
+    float im1 = m1.invMass, im2 = m2.invMass;
+    Vector3 iI1 = m1.invInertiaTensor, iI2 = m2.invInertiaTensor;
+    if (isStaticBody(b1.meta)) { im1 = 0.f; iI1 = Vector3::zero(); }
+    if (isStaticBody(b2.meta)) { im2 = 0.f; iI2 = Vector3::zero(); }
+
+    Vector3 corr;
+    if (j.type == JointConstraint::Type::Fixed) {          // :580-615
+        const JointConstraint::Fixed f = j.fixed;
+        const Quat o1 = (q1 * f.attachRot1).normalize();  // applyJointOrientationConstraint
+        const Quat o2 = (q2 * f.attachRot2).normalize();
+        const Quat diff = o1 * o2.inv();
+        angularCorrection(q1, q2, 2.f * Vector3 { diff.x, diff.y, diff.z }, iI1, iI2);
+        const Vector3 r1w = q1.rotateVec(j.r1) + x1;
+        const Vector3 r2w = q2.rotateVec(j.r2) + x2;
+        const Vector3 dr = r2w - r1w;
+        const Quat axes = (q1 * f.attachRot1).normalize();
+        const Vector3 a1 = axes.rotateVec(math::fwd);
+        const Vector3 b1v = axes.rotateVec(math::right);
+        const Vector3 c1 = cross(a1, b1v);
+        corr = Vector3::zero();
+        const float as = dot(dr, a1);
+        corr -= (as - f.separation) * a1;
+        const float bs = dot(dr, b1v);
+        corr -= bs * b1v;
+        const float cs = dot(dr, c1);
+        corr -= cs * c1;
+    } else {                                               // Hinge, :616-627
+        const JointConstraint::Hinge hg = j.hinge;
+        // applyJointAxisConstraint (:507-535) without its debug printf
+        const Vector3 ax1 = q1.rotateVec(hg.a1Local);
+        const Vector3 ax2 = q2.rotateVec(hg.a2Local);
+        angularCorrection(q1, q2, cross(ax1, ax2), iI1, iI2);
+        const Vector3 r1w = q1.rotateVec(j.r1) + x1;
+        const Vector3 r2w = q2.rotateVec(j.r2) + x2;
+        corr = r2w - r1w;
+    }
+    const float cm = corr.length();
+    if (cm > 0.f) {
+        corr /= cm;
+        // applyPositionalUpdate overload with lever arms (:213-245)
+        const Vector3 nl1 = q1.inv().rotateVec(corr);
+        const Vector3 nl2 = q2.inv().rotateVec(corr);
+        const Vector3 ta1 = cross(j.r1, nl1);
+        const Vector3 ta2 = cross(j.r2, nl2);
+        const Vector3 ra1 = multDiag(iI1, ta1);
+        const Vector3 ra2 = multDiag(iI2, ta2);
+        const float dl = computePositionalLambda(ta1, ta2, ra1, ra2, im1, im2, cm, 0);
+        applyPositionalUpdate(x1, x2, q1, q2, ra1, ra2, im1, im2, corr, dl);
+    }
+    b1.x = x1; b2.x = x2;
+    b1.q = q1; b2.q = q2;
+}
+
 __device__ __forceinline__ Vector3 relVel(Vector3 v1, Vector3 v2, Vector3 o1, Vector3 o2,
                                           Vector3 d1, Vector3 d2)
 {
@@ -259,10 +342,13 @@ __device__ __forceinline__ bool staticInvariant(const SMut &b)
            __float_as_uint(nq.z) == __float_as_uint(b.q.z);
 }
 
-// Per-contact solver record: body slots of ref / alt and the contact's
-// level (1 + max level of earlier contacts sharing a non-invariant body).
+// Per-item solver record: body slots of ref / alt (e1 / e2 for a joint)
+// and the item's level (1 + max level of earlier items sharing a
+// non-invariant body).  Items are the world's contacts followed by its
+// joints, the reference's solvePositions order.
 struct CRec {
-    int16_t s1, s2, lvl, slot;   // slot: survivor slot holding the manifold
+    int16_t s1, s2, lvl, slot;   // slot: survivor slot holding the manifold;
+                                 // a joint: -1 - ConstraintData row
 };
 static_assert(sizeof(CRec) == 8);
 
@@ -388,6 +474,33 @@ __device__ __forceinline__ int32_t worldContactCount(const PhysArgs &P, int32_t 
     return K;
 }
 
+// ConstraintData rows the substep solves (collectConstraintsSystem copies
+// every row, physics.cpp:34-40), capped at maxJointConstraints.
+__device__ __forceinline__ int32_t worldJointCount(const PhysArgs &P, int32_t w, int32_t lane)
+{
+    int32_t J = P.numJointRows[w];
+    const int32_t cap = min(P.maxJoints, P.jointCapacity);
+    if (J > cap) {
+        if (lane == 0) atomicOr(P.errorFlags + w, kErrJointOverflow);
+        J = cap;
+    }
+    return J;
+}
+
+// Body slot of a joint's entity (ctx.getLoc + getDirect, physics.cpp:540-553).
+__device__ __forceinline__ int32_t jointBodySlot(const PhysArgs &P, int32_t w, Entity e)
+{
+    const Loc l = entityLoc(P, w, e);
+    int32_t slot = -1;
+    for (int i = 0; i < P.numBodyArchs; i++) {
+        if ((uint32_t)P.body[i].archetype == l.archetype && l.row >= 0 &&
+            l.row < P.body[i].numRows[w]) {
+            slot = P.body[i].slotBase + l.row;
+        }
+    }
+    return guardIndex(slot, P.maxBodiesPerWorld, P.errorFlags + w, kGuardSolverBody);
+}
+
 // Contact records in survivor order (== the reference's addManifoldToSolver
 // append order, narrowphase.cpp:1123-1162) and their dependency levels: a
 // contact waits only for the latest earlier contact on each of its bodies
@@ -395,8 +508,8 @@ __device__ __forceinline__ int32_t worldContactCount(const PhysArgs &P, int32_t 
 // predecessors), relaxed to its fixpoint.  One wave per world.
 template <typename RecPtr, typename PrevPtr>
 __device__ __forceinline__ int32_t orderAndLevel(const PhysArgs &P, int32_t w, SolverLDS &L,
-                                                 int32_t K, RecPtr recs, PrevPtr prevs,
-                                                 int32_t lane)
+                                                 int32_t K, int32_t J, RecPtr recs,
+                                                 PrevPtr prevs, int32_t lane)
 {
     const int32_t nb = P.maxBodiesPerWorld;
     const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
@@ -419,6 +532,13 @@ __device__ __forceinline__ int32_t orderAndLevel(const PhysArgs &P, int32_t w, S
         }
         k0 += __popcll(mask);
     }
+    const JointConstraint *jrows = P.joints + (size_t)w * P.jointCapacity;
+    for (int32_t j = lane; j < J; j += kSolverBlock) {
+        const JointConstraint &jc = jrows[j];
+        recs[K + j] = CRec { (int16_t)jointBodySlot(P, w, jc.e1), (int16_t)jointBodySlot(P, w, jc.e2),
+                             0, (int16_t)(-1 - j) };
+    }
+    K += J;
     waveSync();
     for (int32_t k = lane; k < K; k += kSolverBlock) {
         CRec r = recs[k];
@@ -454,7 +574,7 @@ __device__ __forceinline__ int32_t orderAndLevel(const PhysArgs &P, int32_t w, S
     for (int32_t k = lane; k < K; k += kSolverBlock) max_level = max(max_level, (int32_t)recs[k].lvl);
 #pragma unroll
     for (int32_t off = 32; off > 0; off >>= 1) max_level = max(max_level, __shfl_xor(max_level, off));
-    if (lane == 0) P.lastNumContacts[w] = K;
+    if (lane == 0) P.lastNumContacts[w] = K - J;
     return max_level;
 }
 
@@ -498,28 +618,41 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
     if (lane == 0) P.solver[w].numContacts = 0;           // physics.cpp:1007
 }
 
+// One positional item: a contact (solveContactPositions) or a joint.
+__device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w, SolverLDS &L,
+                                                   const CRec r)
+{
+    if (r.slot >= 0) {
+        Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
+        solveContactPositions(P, w, L.bodies[r.s1], r.s1, L.bodies[r.s2], r.s2, c);
+    } else {
+        const JointConstraint &j = P.joints[(size_t)w * P.jointCapacity + (-1 - r.slot)];
+        solveJoint(P, L.bodies[r.s1], L.bodies[r.s2], j);
+    }
+}
+
 // Fallback for a world whose contacts do not fit the LDS records: the whole
 // solve on its own wave, records in the global slab, level by level.
 __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, SolverLDS L,
-                                              int32_t K, int32_t lane)
+                                              int32_t K, int32_t J, int32_t lane)
 {
-    CRec *recs = (CRec *)(P.solverRecs + (size_t)w * P.candCapacity);
-    int32_t *prevs = P.solverPrevs + (size_t)w * P.candCapacity;
-    const int32_t max_level = orderAndLevel(P, w, L, K, recs, prevs, lane);
+    CRec *recs = (CRec *)(P.solverRecs + (size_t)w * P.recStride);
+    int32_t *prevs = P.solverPrevs + (size_t)w * P.recStride;
+    const int32_t max_level = orderAndLevel(P, w, L, K, J, recs, prevs, lane);
     const SolverData &sd = P.solver[w];
+    const int32_t N = K + J;
     for (int32_t l = 1; l <= max_level; l++) {
-        for (int32_t k = lane; k < K; k += kSolverBlock) {
+        for (int32_t k = lane; k < N; k += kSolverBlock) {
             const CRec r = recs[k];
             if (r.lvl != l) continue;
-            Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
-            solveContactPositions(P, w, L.bodies[r.s1], r.s1, L.bodies[r.s2], r.s2, c);
+            solveItemPositions(P, w, L, r);
         }
         waveSync();
     }
     setWorldVelocities(P, w, L, sd.h, lane);
     waveSync();
     for (int32_t l = 1; l <= max_level; l++) {
-        for (int32_t k = lane; k < K; k += kSolverBlock) {
+        for (int32_t k = lane; k < K; k += kSolverBlock) {   // joints sort last
             const CRec r = recs[k];
             if (r.lvl != l) continue;
             const Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
@@ -555,13 +688,14 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     SolverBlockLDS BL = solverBlockLDS(smem, nb);
 
     if (threadIdx.x == 0) { BL.scalars[0] = 0; BL.scalars[1] = 0; BL.scalars[2] = 0; }
-    int32_t K = 0;
+    int32_t K = 0, J = 0;
     if (live) {
         loadWorldBodies(P, w, L, lane);
         K = worldContactCount(P, w, lane);
+        J = worldJointCount(P, w, lane);
     }
     __syncthreads();
-    if (live && lane == 0) atomicMax(&BL.scalars[1], K);
+    if (live && lane == 0) atomicMax(&BL.scalars[1], K + J);
     __syncthreads();
     const bool fits = BL.scalars[1] <= kSolverLDSContacts;
 
@@ -569,14 +703,14 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
         // some world of the block overflows the LDS records: every world
         // of the block solves on its own wave with global records
         if (live) {
-            solveWorldGlobal(P, w, L, K, lane);
+            solveWorldGlobal(P, w, L, K, J, lane);
             writeWorldBodies(P, w, L, lane);
         }
         return;
     }
 
     int32_t my_levels = 0;
-    if (live) my_levels = orderAndLevel(P, w, L, K, L.recs, L.prevs, lane);
+    if (live) my_levels = orderAndLevel(P, w, L, K, J, L.recs, L.prevs, lane);
     if (live && lane == 0) atomicMax(&BL.scalars[2], my_levels);
     __syncthreads();
     const int32_t max_level = BL.scalars[2];
@@ -587,8 +721,9 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
         BL.levelCur[i] = 0;
     }
     __syncthreads();
+    const int32_t N = K + J;     // contacts, then joints
     if (live) {
-        for (int32_t k = lane; k < K; k += kSolverBlock) atomicAdd(&BL.levelOff[L.recs[k].lvl], 1);
+        for (int32_t k = lane; k < N; k += kSolverBlock) atomicAdd(&BL.levelOff[L.recs[k].lvl], 1);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -601,7 +736,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     }
     __syncthreads();
     if (live) {
-        for (int32_t k = lane; k < K; k += kSolverBlock) {
+        for (int32_t k = lane; k < N; k += kSolverBlock) {
             const int32_t l = L.recs[k].lvl;
             const int32_t pos = BL.levelOff[l] + atomicAdd(&BL.levelCur[l], 1);
             BL.items[pos] = ((uint32_t)wi << 16) | (uint32_t)k;
@@ -617,9 +752,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
             const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xffffu);
             const int32_t ww = blockIdx.x * kSolverWorlds + iw;
             SolverLDS LW = solverWorldLDS(smem, nb, iw);
-            const CRec r = LW.recs[k];
-            Contact &c = P.candContacts[(size_t)ww * P.candCapacity + r.slot];
-            solveContactPositions(P, ww, LW.bodies[r.s1], r.s1, LW.bodies[r.s2], r.s2, c);
+            solveItemPositions(P, ww, LW, LW.recs[k]);
         }
         __syncthreads();
     }
@@ -636,6 +769,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
             const int32_t ww = blockIdx.x * kSolverWorlds + iw;
             SolverLDS LW = solverWorldLDS(smem, nb, iw);
             const CRec r = LW.recs[k];
+            if (r.slot < 0) continue;                      // joints: positions only
             const Contact &c = P.candContacts[(size_t)ww * P.candCapacity + r.slot];
             const SolverData &sd = P.solver[ww];
             solveContactVelocities(P, ww, LW.bodies[r.s1], r.s1, LW.bodies[r.s2], r.s2, c,

@@ -151,6 +151,40 @@ struct JointConstraint {
     };
     math::Vector3 r1;
     math::Vector3 r2;
+
+    // reference include/madrona/physics.inl:151-190
+    static MW_HD inline JointConstraint setupFixed(Entity e1, Entity e2,
+                                                   math::Quat attach_rot1,
+                                                   math::Quat attach_rot2,
+                                                   math::Vector3 r1, math::Vector3 r2,
+                                                   float separation)
+    {
+        JointConstraint j {};
+        j.e1 = e1;
+        j.e2 = e2;
+        j.type = Type::Fixed;
+        j.fixed = Fixed { attach_rot1, attach_rot2, separation };
+        j.r1 = r1;
+        j.r2 = r2;
+        return j;
+    }
+
+    static MW_HD inline JointConstraint setupHinge(Entity e1, Entity e2,
+                                                   math::Vector3 a1_local,
+                                                   math::Vector3 a2_local,
+                                                   math::Vector3 b1_local,
+                                                   math::Vector3 b2_local,
+                                                   math::Vector3 r1, math::Vector3 r2)
+    {
+        JointConstraint j {};
+        j.e1 = e1;
+        j.e2 = e2;
+        j.type = Type::Hinge;
+        j.hinge = Hinge { a1_local, a2_local, b1_local, b2_local };
+        j.r1 = r1;
+        j.r2 = r2;
+        return j;
+    }
 };
 static_assert(sizeof(JointConstraint) == 92);
 

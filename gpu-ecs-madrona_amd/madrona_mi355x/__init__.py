@@ -61,7 +61,8 @@ class CollisionsConfig(ctypes.Structure):
                 ("delta_t", ctypes.c_float), ("gravity_z", ctypes.c_float),
                 ("max_contacts", ctypes.c_int32), ("max_candidates", ctypes.c_int32),
                 ("cube_inv_mass", ctypes.c_float), ("cube_inv_inertia", ctypes.c_float),
-                ("mu_s", ctypes.c_float), ("mu_d", ctypes.c_float)]
+                ("mu_s", ctypes.c_float), ("mu_d", ctypes.c_float),
+                ("num_joints", ctypes.c_int32), ("num_hinge_joints", ctypes.c_int32)]
 
 
 class FvsConfig(ctypes.Structure):
@@ -329,10 +330,14 @@ class Executor:
 
 
 def default_collisions_config(num_cubes=128, num_substeps=4, max_contacts=4096,
-                              max_candidates=4096):
-    """dt 1/60, S=4, g=-9.8, unit mass cubes."""
+                              max_candidates=4096, num_joints=0, num_hinge_joints=0):
+    """dt 1/60, S=4, g=-9.8, unit mass cubes.  num_joints
+    > 0 adds the joint workload: joint j ties cube 2j to 2j+1 with a fixed
+    joint, or a hinge for the last num_hinge_joints."""
+    if 2 * num_joints > num_cubes or not 0 <= num_hinge_joints <= num_joints:
+        raise ValueError("need 2 * num_joints <= num_cubes, 0 <= num_hinge_joints <= num_joints")
     return CollisionsConfig(num_cubes, num_substeps, 1.0 / 60.0, -9.8, max_contacts,
-                            max_candidates, 1.0, 1.5, 0.5, 0.5)
+                            max_candidates, 1.0, 1.5, 0.5, 0.5, num_joints, num_hinge_joints)
 
 
 class CollisionsSim(Executor):

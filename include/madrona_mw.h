@@ -56,6 +56,11 @@ typedef struct mw_collisions_config {
     float cube_inv_inertia;
     float mu_s;
     float mu_d;
+    int32_t num_joints;        /* ConstraintData rows per world: joint j ties
+                                  cube 2j to 2j+1 (fixed joint); 0 = none  */
+    int32_t num_hinge_joints;  /* the last num_hinge_joints joints are hinges
+                                  instead (the reference's hinge diverges,
+                                  DESIGN.md §4: short horizons only)       */
 } mw_collisions_config;
 
 /* Per-world init (reference InitT): host pointers to num_cubes x 3 positions

@@ -154,6 +154,8 @@ struct Config {
     float cubeInvInertia;
     float muS;
     float muD;
+    int32_t numJoints;      // joint pairs per world (jointSpec), 0 = none
+    int32_t numHingeJoints; // the last numHingeJoints of them are hinges
 };
 
 static constexpr uint32_t kBodyArchetype = 6;   // registration order, see DESIGN.md
@@ -161,6 +163,47 @@ static constexpr uint32_t kBodyArchetype = 6;   // registration order, see DESIG
 // registered where the collisions body archetype is, Agent right after it.
 static constexpr uint32_t kSphereArchetype = kBodyArchetype;
 static constexpr uint32_t kAgentArchetype = kBodyArchetype + 1;
+
+// JointConstraint (include/madrona/physics.hpp:196-238), 92 B.  The union
+// holds Fixed {attachRot1, attachRot2, separation} or Hinge {a1Local,
+// a2Local, b1Local, b2Local}.
+struct Joint {
+    Entity e1, e2;
+    uint32_t type;                    // 0 Fixed, 1 Hinge
+    float u[12];
+    V3 r1, r2;
+};
+static_assert(sizeof(Joint) == 92);
+
+// The joint workload shared with oracle/ref_harness.cpp and the collisions
+// environment: joint j ties cube 2j to cube 2j + 1; fixed, or hinge for the
+// last numHingeJoints (JointConstraint::setupFixed / setupHinge,
+// physics.inl:151-190).
+static Joint jointSpec(bool hinge, Entity e1, Entity e2)
+{
+    Joint jt {};
+    jt.e1 = e1;
+    jt.e2 = e2;
+    if (!hinge) {
+        jt.type = 0;
+        const float rot1[4] = { 1.f, 0.f, 0.f, 0.f };
+        const float rot2[4] = { 0.70710678f, 0.f, 0.f, 0.70710678f };
+        memcpy(jt.u, rot1, 16);
+        memcpy(jt.u + 4, rot2, 16);
+        jt.u[8] = 0.5f;
+        jt.r1 = V3 { 0.f, 1.5f, 0.f };
+        jt.r2 = V3 { 0.f, -1.5f, 0.f };
+    } else {
+        jt.type = 1;
+        const float axes[12] = { 1, 0, 0, 1, 0, 0, 0, 1, 0, 0, 1, 0 };
+        memcpy(jt.u, axes, 48);
+        jt.r1 = V3 { 0.f, 0.f, 1.5f };
+        jt.r2 = V3 { 0.f, 0.f, -1.5f };
+    }
+    return jt;
+}
+
+static constexpr uint32_t kConstraintArchetype = 5;
 
 struct World {
     IDMap ids;
@@ -182,6 +225,7 @@ struct World {
     // SolverData (src/physics/physics.cpp:15-32)
     std::vector<Contact> contacts;
     int32_t numContacts = 0;
+    std::vector<Joint> joints;        // ConstraintData rows, row order
     float h = 0, gMag = 0, restThresh = 0;
     V3 g;
 
@@ -285,6 +329,12 @@ static void initWorld(const Sim &sim, World &w, const float *pos, const float *r
              0, Response::Dynamic);
     }
     make(V3::zero(), Q { 1.f, 0.f, 0.f, 0.f }, 1, Response::Static);
+    for (int32_t j = 0; j < cfg.numJoints; j++) {         // ConstraintData entities
+        Entity e = w.ids.acquireID(w.worldCache);
+        w.ids.ref(e.id) = Loc { kConstraintArchetype, j };
+        const bool hinge = j >= cfg.numJoints - cfg.numHingeJoints;
+        w.joints.push_back(jointSpec(hinge, w.bodies[2 * j].e, w.bodies[2 * j + 1].e));
+    }
     w.forceRebuild = true;                               // rebuildOnUpdate
 }
 
@@ -1047,9 +1097,102 @@ static void handleContact(const Sim &sim, World &w, Contact &c)  // physics.cpp:
     b1.rot = q1; b2.rot = q2;
 }
 
+static std::pair<Q, Q> computeAngularUpdate(Q q1, Q q2, V3 iI1, V3 iI2, V3 n1, V3 n2,
+                                            float theta, float alpha)
+{                                                          // physics.cpp:247-271
+    V3 lra1 = multDiag(iI1, n1);
+    V3 lra2 = multDiag(iI2, n2);
+    float w1 = dot(n1, lra1);
+    float w2 = dot(n2, lra2);
+    float dl = -theta / (w1 + w2 + alpha);
+    float half = 0.5f * dl;
+    V3 u1 = half * lra1;
+    V3 u2 = half * lra2;
+    return { Q::fromAngularVec(q1.rotateVec(u1)), Q::fromAngularVec(q2.rotateVec(u2)) };
+}
+
+static void applyAngularUpdate(Q &q1, Q &q2, Q u1, Q u2)  // physics.cpp:273-279
+{
+    q1 = (q1 + u1 * q1).normalize();
+    q2 = (q2 - u2 * q2).normalize();
+}
+
+static void angularCorrection(Q &q1, Q &q2, V3 dq, V3 iI1, V3 iI2)
+{                                                          // physics.cpp:490-504, 522-534
+    float mag = dq.length();
+    if (mag > 0) {
+        dq /= mag;
+        V3 l1 = q1.inv().rotateVec(dq);
+        V3 l2 = q2.inv().rotateVec(dq);
+        auto [u1, u2] = computeAngularUpdate(q1, q2, iI1, iI2, l1, l2, mag, 0);
+        applyAngularUpdate(q1, q2, u1, u2);
+    }
+}
+
+static void handleJoint(const Sim &sim, World &w, const Joint &j)  // physics.cpp:537-648
+{
+    Loc l1 = w.ids.lookup(j.e1), l2 = w.ids.lookup(j.e2);
+    Body &b1 = w.bodies[bodyIndex(w, l1)];
+    Body &b2 = w.bodies[bodyIndex(w, l2)];
+    V3 x1 = b1.pos, x2 = b2.pos;
+    Q q1 = b1.rot, q2 = b2.rot;
+    const Metadata md1 = sim.objs.metadata[b1.objID];
+    const Metadata md2 = sim.objs.metadata[b2.objID];
+    float im1 = md1.invMass, im2 = md2.invMass;
+    V3 iI1 = md1.invInertia, iI2 = md2.invInertia;
+    if (b1.resp == Response::Static) { im1 = 0.f; iI1 = V3::zero(); }
+    if (b2.resp == Response::Static) { im2 = 0.f; iI2 = V3::zero(); }
+
+    V3 corr;
+    if (j.type == 0) {                                     // Fixed, :580-615
+        Q a1q { j.u[0], j.u[1], j.u[2], j.u[3] };
+        Q a2q { j.u[4], j.u[5], j.u[6], j.u[7] };
+        float separation = j.u[8];
+        Q o1 = (q1 * a1q).normalize();                     // applyJointOrientationConstraint
+        Q o2 = (q2 * a2q).normalize();
+        Q diff = o1 * o2.inv();
+        V3 dq = 2.f * V3 { diff.x, diff.y, diff.z };
+        angularCorrection(q1, q2, dq, iI1, iI2);
+
+        V3 r1w = q1.rotateVec(j.r1) + x1;
+        V3 r2w = q2.rotateVec(j.r2) + x2;
+        V3 dr = r2w - r1w;
+        Q axes = (q1 * a1q).normalize();
+        V3 a1 = axes.rotateVec(V3 { 0, 1, 0 });            // math::fwd
+        V3 b1v = axes.rotateVec(V3 { 1, 0, 0 });           // math::right
+        V3 c1 = cross(a1, b1v);
+        corr = V3::zero();
+        float as = dot(dr, a1);
+        corr -= (as - separation) * a1;
+        float bs = dot(dr, b1v);
+        corr -= bs * b1v;
+        float cs = dot(dr, c1);
+        corr -= cs * c1;
+    } else {                                               // Hinge, :616-627
+        V3 a1l { j.u[0], j.u[1], j.u[2] };
+        V3 a2l { j.u[3], j.u[4], j.u[5] };
+        V3 ax1 = q1.rotateVec(a1l);                        // applyJointAxisConstraint
+        V3 ax2 = q2.rotateVec(a2l);
+        angularCorrection(q1, q2, cross(ax1, ax2), iI1, iI2);
+        V3 r1w = q1.rotateVec(j.r1) + x1;
+        V3 r2w = q2.rotateVec(j.r2) + x2;
+        corr = r2w - r1w;
+    }
+    float cm = corr.length();
+    if (cm > 0.f) {
+        corr /= cm;
+        applyPositionalUpdateFull(x1, x2, q1, q2, j.r1, j.r2, im1, im2, iI1, iI2, corr, cm, 0);
+    }
+    b1.pos = x1; b2.pos = x2;
+    b1.rot = q1; b2.rot = q2;
+}
+
 static void solvePositions(const Sim &sim, World &w)      // physics.cpp:650-671
 {
     for (int32_t i = 0; i < w.numContacts; i++) handleContact(sim, w, w.contacts[i]);
+    // collectConstraintsSystem (physics.cpp:34-40) gathers the ConstraintData
+    // rows in row order every substep; they run after all contacts.
+    for (const Joint &j : w.joints) handleJoint(sim, w, j);
 }
 
 static void setVelocities(World &w)                       // physics.cpp:673-714

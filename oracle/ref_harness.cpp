@@ -66,6 +66,8 @@ struct RefPhysConfig {
     float cubeInvInertia;
     float muS;
     float muD;
+    int32_t numJoints;      // joint pairs per world, 0 = none
+    int32_t numHingeJoints; // the last numHingeJoints of them are hinges
 };
 
 struct WorldInit {
@@ -143,7 +145,7 @@ PhysWorld::PhysWorld(Engine &ctx, ObjectManager *mgr,
 {
     RigidBodyPhysicsSystem::init(ctx, mgr, cfg.deltaT, cfg.numSubsteps,
         Vector3 { 0.f, 0.f, cfg.gravityZ }, cfg.numCubes + (simple ? 2 : 1),
-        cfg.maxContacts, 16);
+        cfg.maxContacts, cfg.numJoints > 16 ? cfg.numJoints : 16);
 
     auto setup = [&](Entity e, Vector3 p, Quat q, int32_t obj,
                      ResponseType rt) {
@@ -182,17 +184,39 @@ PhysWorld::PhysWorld(Engine &ctx, ObjectManager *mgr,
         return;
     }
 
+    std::vector<Entity> cubes;
     for (int32_t i = 0; i < cfg.numCubes; i++) {
         Entity e = ctx.makeEntityNow<PhysicsBody>();
         Vector3 p { init.pos[3 * i], init.pos[3 * i + 1], init.pos[3 * i + 2] };
         Quat q { init.rot[4 * i], init.rot[4 * i + 1], init.rot[4 * i + 2],
                  init.rot[4 * i + 3] };
         setup(e, p, q, 0, ResponseType::Dynamic);
+        cubes.push_back(e);
     }
 
     Entity plane = ctx.makeEntityNow<PhysicsBody>();
     setup(plane, Vector3::zero(), Quat { 1.f, 0.f, 0.f, 0.f }, 1,
           ResponseType::Static);
+
+    // Joint workload (shared with the oracle and the collisions
+    // environment): joint j ties cube 2j to cube 2j + 1, fixed,
+    // or hinge for the last numHingeJoints, through the reference's own
+    // setup helpers.
+    for (int32_t j = 0; j < cfg.numJoints; j++) {
+        Entity e1 = cubes[2 * j], e2 = cubes[2 * j + 1];
+        Entity je = ctx.makeEntityNow<ConstraintData>();
+        if (j < cfg.numJoints - cfg.numHingeJoints) {
+            ctx.getUnsafe<JointConstraint>(je) = JointConstraint::setupFixed(
+                e1, e2, Quat { 1.f, 0.f, 0.f, 0.f },
+                Quat { 0.70710678f, 0.f, 0.f, 0.70710678f },
+                Vector3 { 0.f, 1.5f, 0.f }, Vector3 { 0.f, -1.5f, 0.f }, 0.5f);
+        } else {
+            ctx.getUnsafe<JointConstraint>(je) = JointConstraint::setupHinge(
+                e1, e2, Vector3 { 1, 0, 0 }, Vector3 { 1, 0, 0 },
+                Vector3 { 0, 1, 0 }, Vector3 { 0, 1, 0 },
+                Vector3 { 0.f, 0.f, 1.5f }, Vector3 { 0.f, 0.f, -1.5f });
+        }
+    }
 
     ctx.getSingleton<broadphase::BVH>().rebuildOnUpdate();
 }

@@ -26,6 +26,8 @@ class PhysConfig(ctypes.Structure):
         ("cubeInvInertia", ctypes.c_float),
         ("muS", ctypes.c_float),
         ("muD", ctypes.c_float),
+        ("numJoints", ctypes.c_int32),
+        ("numHingeJoints", ctypes.c_int32),
     ]
 
 
@@ -74,6 +76,46 @@ def gen_collisions_inits(num_worlds, num_cubes=128, seed=0):
 
 _ORC = None
 _REF = {}
+
+
+def _qmul(a, b):
+    w1, x1, y1, z1 = np.moveaxis(a, -1, 0)
+    w2, x2, y2, z2 = np.moveaxis(b, -1, 0)
+    return np.stack([w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2,
+                     w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2,
+                     w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
+                     w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2], axis=-1)
+
+
+def _qrot(q, v):
+    p = q[..., 1:]
+    v = np.broadcast_to(np.asarray(v, np.float64), p.shape)
+    return v + 2.0 * (np.cross(p, v) * q[..., :1] + np.cross(p, np.cross(p, v)))
+
+
+def joint_inits(pos, rot, num_joints, num_hinge_joints=0):
+    """Inputs for the joint workload (collisions config num_joints): cube
+    2j+1 starts where joint j (cube 2j -> 2j+1) is satisfied relative to cube
+    2j -- fixed: attachRot2 = 90 deg about z, r1 = (0, 1.5, 0), r2 = (0, -1.5, 0),
+    separation 0.5 along the fwd axis; hinge: same rotation, 3 apart along
+    local z.  Computed in float64, rounded once to float32 (an input, not a
+    parity-critical computation)."""
+    pos = pos.astype(np.float64).copy()
+    rot = rot.astype(np.float64).copy()
+    att2_inv = np.array([np.sqrt(0.5), 0.0, 0.0, -np.sqrt(0.5)])
+    for j in range(num_joints):
+        i1, i2 = 2 * j, 2 * j + 1
+        q1, x1 = rot[:, i1], pos[:, i1]
+        if j < num_joints - num_hinge_joints:
+            q2 = _qmul(q1, np.broadcast_to(att2_inv, q1.shape))
+            x2 = (x1 + _qrot(q1, [0, 1.5, 0]) + 0.5 * _qrot(q1, [0, 1, 0])
+                  - _qrot(q2, [0, -1.5, 0]))
+        else:
+            q2 = q1.copy()
+            x2 = x1 + _qrot(q1, [0, 0, 3.0])
+        rot[:, i2] = q2
+        pos[:, i2] = x2
+    return pos.astype(np.float32), rot.astype(np.float32)
 
 
 def load_orc():
