@@ -31,6 +31,7 @@ struct PhysicsBody : Archetype<
 struct Config {
     mw_collisions_config c;
     ObjectManager *objMgr;
+    int32_t numHulls;             // body i uses object i % numHulls
 };
 
 // Per-world episode return handed to a learner: the running
@@ -122,11 +123,11 @@ PhysWorld::PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &i
         Entity e = ctx.makeEntityNow<PhysicsBody>();
         Vector3 p { init.pos[3 * i], init.pos[3 * i + 1], init.pos[3 * i + 2] };
         Quat q { init.rot[4 * i], init.rot[4 * i + 1], init.rot[4 * i + 2], init.rot[4 * i + 3] };
-        setup(e, p, q, 0, ResponseType::Dynamic);
+        setup(e, p, q, i % cfg.numHulls, ResponseType::Dynamic);
         cubes.push_back(e);
     }
     Entity plane = ctx.makeEntityNow<PhysicsBody>();
-    setup(plane, Vector3::zero(), Quat { 1.f, 0.f, 0.f, 0.f }, 1, ResponseType::Static);
+    setup(plane, Vector3::zero(), Quat { 1.f, 0.f, 0.f, 0.f }, cfg.numHulls, ResponseType::Static);
 
     // Joint workload (mw_collisions_config::num_joints): joint j ties cube
     // 2j to cube 2j + 1, fixed, or hinge for the last num_hinge_joints --
@@ -166,7 +167,14 @@ static Executor *create(const ExecConfig &ecfg, const void *user_cfg, size_t cfg
         throw std::runtime_error("collisions: need 0 <= 2 * num_joints <= num_cubes and "
                                  "0 <= num_hinge_joints <= num_joints");
     }
-    cfg.objMgr = envs::makeCubeObjectManager(cfg.c);
+    const std::vector<std::string> hulls = envs::splitHullPaths(cfg.c.hull_paths);
+    if (hulls.empty()) {
+        cfg.objMgr = envs::makeCubeObjectManager(cfg.c);
+        cfg.numHulls = 1;
+    } else {
+        cfg.objMgr = envs::makeHullObjectManager(cfg.c, hulls);
+        cfg.numHulls = (int32_t)hulls.size();
+    }
     std::vector<mw_collisions_init> init_vec(ecfg.numWorlds);
     for (int32_t w = 0; w < ecfg.numWorlds; w++) {
         memcpy(&init_vec[w], (const char *)inits + (size_t)w * init_stride, sizeof(mw_collisions_init));

@@ -5,9 +5,12 @@
 #pragma once
 
 #include <madrona/physics.hpp>
+#include <madrona/physics_assets.hpp>
 #include "../../../include/madrona_mw.h"
 
 #include <cfloat>
+#include <string>
+#include <vector>
 
 namespace madrona::envs {
 
@@ -45,6 +48,53 @@ inline phys::ObjectManager *makeCubeObjectManager(const mw_collisions_config &c)
     mgr->metadata[1] = RigidBodyMetadata { { 0.f, 0.f, 0.f }, 0.f, c.mu_s, c.mu_d };
     mgr->aabbs[1] = AABB { { -FLT_MAX, -FLT_MAX, -FLT_MAX }, { FLT_MAX, FLT_MAX, 0.f } };
     return mgr;
+}
+
+inline std::vector<std::string> splitHullPaths(const char *paths)
+{
+    std::vector<std::string> out;
+    if (!paths) return out;
+    std::string cur;
+    for (const char *p = paths;; p++) {
+        if (*p == ';' || *p == '\0') {
+            if (!cur.empty()) out.push_back(cur);
+            cur.clear();
+            if (*p == '\0') break;
+        } else {
+            cur.push_back(*p);
+        }
+    }
+    return out;
+}
+
+// Object table from OBJ hulls through the asset path (PhysicsLoader, the
+// reference's physics_assets.cpp flow): objects 0..n-1 = the hulls (mass
+// properties from the config), object n = ground plane.  The loader (and
+// with it the table) lives as long as the process, like the cube table.
+inline phys::ObjectManager *makeHullObjectManager(const mw_collisions_config &c,
+                                                  const std::vector<std::string> &paths)
+{
+    using namespace phys;
+    using namespace math;
+    const CountT n = (CountT)paths.size();
+    auto *loader = new PhysicsLoader(PhysicsLoader::StorageType::HIP, n + 1);
+    std::vector<RigidBodyMetadata> meta;
+    std::vector<AABB> aabbs;
+    std::vector<CollisionPrimitive> prims(n + 1);
+    for (CountT i = 0; i < n; i++) {
+        PhysicsLoader::LoadedHull h = loader->loadHullFromDisk(paths[i].c_str());
+        prims[i].type = CollisionPrimitive::Type::Hull;
+        prims[i].hull.halfEdgeMesh = h.collisionMesh;
+        aabbs.push_back(h.aabb);
+        meta.push_back(RigidBodyMetadata {
+            { c.cube_inv_inertia, c.cube_inv_inertia, c.cube_inv_inertia }, c.cube_inv_mass,
+            c.mu_s, c.mu_d });
+    }
+    prims[n].type = CollisionPrimitive::Type::Plane;
+    meta.push_back(RigidBodyMetadata { { 0.f, 0.f, 0.f }, 0.f, c.mu_s, c.mu_d });
+    aabbs.push_back(AABB { { -FLT_MAX, -FLT_MAX, -FLT_MAX }, { FLT_MAX, FLT_MAX, 0.f } });
+    loader->loadObjects(meta.data(), aabbs.data(), prims.data(), n + 1);
+    return &loader->getObjectManager();
 }
 
 }

@@ -5,6 +5,7 @@
 #include "../physics/physics_impl.hpp"
 
 #include <madrona/mw_gpu.hpp>
+#include <madrona/physics_assets.hpp>
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -200,6 +201,32 @@ int mw_destroy(mw_exec *exec)
 }
 
 const char *mw_last_error(void) { return g_last_error.c_str(); }
+
+int mw_load_hull(const char *obj_path, int32_t *counts_out, float *aabb_out, float *verts_out,
+                 int32_t vert_cap, float *planes_out, int32_t face_cap, uint32_t *half_edges_out,
+                 int32_t half_edge_cap)
+{
+    MW_TRY({
+        if (!obj_path || !counts_out || !aabb_out) throw std::runtime_error("mw_load_hull: null argument");
+        madrona::phys::PhysicsLoader loader(madrona::phys::PhysicsLoader::StorageType::CPU, 1);
+        madrona::phys::PhysicsLoader::LoadedHull h = loader.loadHullFromDisk(obj_path);
+        const madrona::phys::geometry::HalfEdgeMesh &m = h.collisionMesh;
+        counts_out[0] = (int32_t)m.mVertexCount;
+        counts_out[1] = (int32_t)m.mPolygonCount;
+        counts_out[2] = (int32_t)m.mEdgeCount;
+        counts_out[3] = (int32_t)m.mHalfEdgeCount;
+        memcpy(aabb_out, &h.aabb.pMin, 12);
+        memcpy(aabb_out + 3, &h.aabb.pMax, 12);
+        if ((int64_t)m.mVertexCount > vert_cap || (int64_t)m.mPolygonCount > face_cap ||
+            (int64_t)m.mHalfEdgeCount > half_edge_cap) {
+            return -2;
+        }
+        if (verts_out) memcpy(verts_out, m.mVertices, 12 * (size_t)m.mVertexCount);
+        if (planes_out) memcpy(planes_out, m.mFacePlanes, 16 * (size_t)m.mPolygonCount);
+        if (half_edges_out) memcpy(half_edges_out, m.mHalfEdges, 16 * (size_t)m.mHalfEdgeCount);
+        return 0;
+    }, -1)
+}
 
 // ---------------------------------------------------------------------------
 // Training hand-off across world shards: RCCL over xGMI, issued on the

@@ -26,6 +26,11 @@ constexpr inline float pi_m2 { pi * 2.f };
 MW_INLINE float fminRef(float a, float b) { return (a < b || b != b) ? a : b; }
 MW_INLINE float fmaxRef(float a, float b) { return (a > b || b != b) ? a : b; }
 
+struct Vector2 {
+    float x;
+    float y;
+};
+
 struct Vector3 {
     float x;
     float y;

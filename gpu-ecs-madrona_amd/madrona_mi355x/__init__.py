@@ -62,7 +62,8 @@ class CollisionsConfig(ctypes.Structure):
                 ("max_contacts", ctypes.c_int32), ("max_candidates", ctypes.c_int32),
                 ("cube_inv_mass", ctypes.c_float), ("cube_inv_inertia", ctypes.c_float),
                 ("mu_s", ctypes.c_float), ("mu_d", ctypes.c_float),
-                ("num_joints", ctypes.c_int32), ("num_hinge_joints", ctypes.c_int32)]
+                ("num_joints", ctypes.c_int32), ("num_hinge_joints", ctypes.c_int32),
+                ("hull_paths", ctypes.c_char_p)]
 
 
 class FvsConfig(ctypes.Structure):
@@ -119,6 +120,9 @@ _lib.mw_device_alloc.restype = ctypes.c_void_p
 _lib.mw_device_alloc.argtypes = [ctypes.c_void_p, ctypes.c_int64]
 _lib.mw_device_free.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 RCCL_ID_BYTES = 128
+_lib.mw_load_hull.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                             ctypes.c_int32]
 _lib.mw_set_timed_node.restype = ctypes.c_int32
 _lib.mw_set_timed_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
 _lib.mw_timed_node_ms.restype = ctypes.c_double
@@ -132,7 +136,7 @@ C_ABI_SYMBOLS = (
     "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_copy_exported",
     "mw_gen_collisions_inits", "mw_set_timed_node", "mw_timed_node_ms",
     "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
-    "mw_device_free", "mw_gen_fvs_inits", "mw_stream_wait",
+    "mw_device_free", "mw_gen_fvs_inits", "mw_stream_wait", "mw_load_hull",
 )
 
 
@@ -157,6 +161,28 @@ def gen_collisions_inits(num_worlds, num_cubes=128, seed=0, first_world=0):
 ERR_BITS = {1: "id store full", 2: "table full", 4: "candidate overflow",
             8: "contact overflow", 16: "BVH stack overflow", 32: "solver body overflow",
             64: "index guard (site in bits 8..15)"}
+
+
+def load_hull(path):
+    """PhysicsLoader::loadHullFromDisk on the host (no device needed): the
+    half-edge hull of an .obj file as numpy arrays -- vertices [V,3], face
+    planes [F,4] (normal, d), half edges [H,4] (next, twin, root vertex,
+    polygon), num_edges and the AABB [2,3]."""
+    counts = np.zeros(4, np.int32)
+    aabb = np.zeros((2, 3), np.float32)
+    _lib.mw_load_hull(os.fspath(path).encode(), counts.ctypes.data, aabb.ctypes.data, None, 0,
+                      None, 0, None, 0)
+    if counts[0] == 0:
+        raise _err()
+    verts = np.zeros((counts[0], 3), np.float32)
+    planes = np.zeros((counts[1], 4), np.float32)
+    hes = np.zeros((counts[3], 4), np.uint32)
+    if _lib.mw_load_hull(os.fspath(path).encode(), counts.ctypes.data, aabb.ctypes.data,
+                         verts.ctypes.data, len(verts), planes.ctypes.data, len(planes),
+                         hes.ctypes.data, len(hes)) != 0:
+        raise _err()
+    return {"vertices": verts, "planes": planes, "half_edges": hes,
+            "num_edges": int(counts[2]), "aabb": aabb}
 
 
 class MadronaError(RuntimeError):
@@ -330,14 +356,21 @@ class Executor:
 
 
 def default_collisions_config(num_cubes=128, num_substeps=4, max_contacts=4096,
-                              max_candidates=4096, num_joints=0, num_hinge_joints=0):
+                              max_candidates=4096, num_joints=0, num_hinge_joints=0,
+                              hull_paths=None):
     """dt 1/60, S=4, g=-9.8, unit mass cubes.  num_joints
     > 0 adds the joint workload: joint j ties cube 2j to 2j+1 with a fixed
-    joint, or a hinge for the last num_hinge_joints."""
+    joint, or a hinge for the last num_hinge_joints.  hull_paths: .obj files
+    loaded as convex hulls through PhysicsLoader (reference
+    physics_assets.cpp:205-254); body i uses hull i % len(hull_paths)."""
     if 2 * num_joints > num_cubes or not 0 <= num_hinge_joints <= num_joints:
         raise ValueError("need 2 * num_joints <= num_cubes, 0 <= num_hinge_joints <= num_joints")
+    paths = None
+    if hull_paths:
+        paths = ";".join(os.fspath(p) for p in hull_paths).encode()
     return CollisionsConfig(num_cubes, num_substeps, 1.0 / 60.0, -9.8, max_contacts,
-                            max_candidates, 1.0, 1.5, 0.5, 0.5, num_joints, num_hinge_joints)
+                            max_candidates, 1.0, 1.5, 0.5, 0.5, num_joints, num_hinge_joints,
+                            paths)
 
 
 class CollisionsSim(Executor):

@@ -61,6 +61,11 @@ typedef struct mw_collisions_config {
     int32_t num_hinge_joints;  /* the last num_hinge_joints joints are hinges
                                   instead (the reference's hinge diverges,
                                   DESIGN.md §4: short horizons only)       */
+    const char *hull_paths;    /* NULL / "": every body is the built-in unit
+                                  cube.  Otherwise ';'-separated .obj files
+                                  loaded as convex hulls (PhysicsLoader);
+                                  body i uses hull i % count, the ground
+                                  plane comes after them                    */
 } mw_collisions_config;
 
 /* Per-world init (reference InitT): host pointers to num_cubes x 3 positions
@@ -75,6 +80,17 @@ typedef struct mw_collisions_init {
 void mw_gen_collisions_inits(int32_t first_world, int32_t num_worlds,
                              int32_t num_cubes, uint32_t seed,
                              float *pos_out, float *rot_out);
+
+/* Physics asset path without a device (replaces PhysicsLoader::
+ * loadHullFromDisk, src/physics/physics_assets.cpp:205-254): imports the
+ * .obj, builds the half-edge hull and writes counts_out = {vertices, faces,
+ * edges, half edges}, aabb_out = {min xyz, max xyz}, then up to the given
+ * capacities the hull's vertices (xyz), face planes (normal xyz, d) and half
+ * edges (next, twin, root vertex, polygon).  0 on success, -1 on a malformed
+ * file (mw_last_error), -2 when a capacity is too small (counts still set). */
+int mw_load_hull(const char *obj_path, int32_t *counts_out, float *aabb_out,
+                 float *verts_out, int32_t vert_cap, float *planes_out, int32_t face_cap,
+                 uint32_t *half_edges_out, int32_t half_edge_cap);
 
 /* Create an executor for environment `env`.  `inits` points at num_worlds
  * records of `init_stride` bytes each (reference: const InitT *user_inits). */

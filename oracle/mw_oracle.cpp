@@ -248,6 +248,7 @@ struct Sim {
     Objects objs;
     std::vector<World> worlds;
     bool simple = false;      // simple_taskgraph worlds: clamp node, two archetypes, no plane
+    int32_t numHulls = 1;     // body i uses object i % numHulls, the plane is object numHulls
 };
 
 static inline int32_t bodyIndex(const World &w, Loc l)
@@ -326,9 +327,9 @@ static void initWorld(const Sim &sim, World &w, const float *pos, const float *r
     for (int32_t i = 0; i < cfg.numCubes; i++) {
         make(V3 { pos[3 * i], pos[3 * i + 1], pos[3 * i + 2] },
              Q { rot[4 * i], rot[4 * i + 1], rot[4 * i + 2], rot[4 * i + 3] },
-             0, Response::Dynamic);
+             i % sim.numHulls, Response::Dynamic);
     }
-    make(V3::zero(), Q { 1.f, 0.f, 0.f, 0.f }, 1, Response::Static);
+    make(V3::zero(), Q { 1.f, 0.f, 0.f, 0.f }, sim.numHulls, Response::Static);
     for (int32_t j = 0; j < cfg.numJoints; j++) {         // ConstraintData entities
         Entity e = w.ids.acquireID(w.worldCache);
         w.ids.ref(e.id) = Loc { kConstraintArchetype, j };
@@ -1388,6 +1389,48 @@ static Objects makeObjects(const Config &cfg)
     return o;
 }
 
+// Object table of OBJ hulls (PhysicsLoader::loadHullFromDisk, reference
+// physics_assets.cpp:205-254: half-edge construction over the imported
+// polygons, AABB = point(v0) expanded by every vertex) + the ground plane.
+static Objects makeHullObjects(const Config &cfg, int32_t num_hulls, const int32_t *num_verts,
+                               const float *verts, const int32_t *num_faces,
+                               const int32_t *face_counts, const uint32_t *indices)
+{
+    Objects o;
+    const Metadata md { { cfg.cubeInvInertia, cfg.cubeInvInertia, cfg.cubeInvInertia },
+                        cfg.cubeInvMass, cfg.muS, cfg.muD };
+    for (int32_t h = 0; h < num_hulls; h++) {
+        std::vector<V3> vs;
+        for (int32_t v = 0; v < num_verts[h]; v++) {
+            vs.push_back(V3 { verts[0], verts[1], verts[2] });
+            verts += 3;
+        }
+        std::vector<std::vector<uint32_t>> faces;
+        for (int32_t f = 0; f < num_faces[h]; f++) {
+            faces.emplace_back(indices, indices + *face_counts);
+            indices += *face_counts;
+            face_counts++;
+        }
+        AABB box { vs[0], vs[0] };
+        for (size_t v = 1; v < vs.size(); v++) {           // AABB::expand, else-if kept
+            const V3 p = vs[v];
+            for (int a = 0; a < 3; a++) {
+                if (p[a] < box.pMin[a]) box.pMin[a] = p[a];
+                else if (p[a] > box.pMax[a]) box.pMax[a] = p[a];
+            }
+        }
+        o.hulls.push_back(constructHull(faces, vs));
+        o.types.push_back(PrimType::Hull);
+        o.metadata.push_back(md);
+        o.aabbs.push_back(box);
+    }
+    o.hulls.push_back(Hull {});
+    o.types.push_back(PrimType::Plane);
+    o.metadata.push_back(Metadata { { 0, 0, 0 }, 0.f, cfg.muS, cfg.muD });
+    o.aabbs.push_back(AABB { { -FLT_MAX, -FLT_MAX, -FLT_MAX }, { FLT_MAX, FLT_MAX, 0.f } });
+    return o;
+}
+
 }  // namespace orc
 
 using namespace orc;
@@ -1442,6 +1485,54 @@ void *orc_phys_create(int32_t num_worlds, const Config *cfg,
     auto *sim = new Sim {};
     sim->cfg = *cfg;
     sim->objs = makeObjects(*cfg);
+    sim->worlds.resize(num_worlds);
+    for (int32_t w = 0; w < num_worlds; w++) {
+        initWorld(*sim, sim->worlds[w], pos + (size_t)w * cfg->numCubes * 3,
+                  rot + (size_t)w * cfg->numCubes * 4);
+    }
+    return sim;
+}
+
+// One hull of the asset path, for pinning HalfEdgeMesh::construct and the
+// AABB against the reference (ref_build_hull) and the product's loader
+// (mw_load_hull): counts_out = {vertices, faces, edges, half edges}; outputs
+// sized by the caller (vertices num_verts, faces num_faces, half edges and
+// edges 2 * total face indices).
+__attribute__((visibility("default")))
+void orc_build_hull(int32_t num_verts, const float *verts, int32_t num_faces,
+                    const int32_t *face_counts, const uint32_t *indices, int32_t *counts_out,
+                    float *verts_out, float *planes_out, uint32_t *half_edges_out,
+                    uint32_t *polys_out, uint32_t *edges_out, float *aabb_out)
+{
+    Config cfg {};
+    Objects o = makeHullObjects(cfg, 1, &num_verts, verts, &num_faces, face_counts, indices);
+    const Hull &h = o.hulls[0];
+    counts_out[0] = (int32_t)h.vertices.size();
+    counts_out[1] = (int32_t)h.polygons.size();
+    counts_out[2] = (int32_t)h.edges.size();
+    counts_out[3] = (int32_t)h.halfEdges.size();
+    memcpy(verts_out, h.vertices.data(), 12 * h.vertices.size());
+    memcpy(planes_out, h.facePlanes.data(), 16 * h.facePlanes.size());
+    memcpy(half_edges_out, h.halfEdges.data(), 16 * h.halfEdges.size());
+    memcpy(polys_out, h.polygons.data(), 4 * h.polygons.size());
+    memcpy(edges_out, h.edges.data(), 4 * h.edges.size());
+    memcpy(aabb_out, &o.aabbs[0], 24);
+}
+
+// Collisions worlds over OBJ hulls: body i uses hull i % num_hulls.  Hull h
+// has num_verts[h] vertices (xyz, concatenated in verts) and num_faces[h]
+// polygons (vertex counts in face_counts, indices concatenated).
+__attribute__((visibility("default")))
+void *orc_phys_create_hulls(int32_t num_worlds, const Config *cfg, const float *pos,
+                            const float *rot, int32_t num_hulls, const int32_t *num_verts,
+                            const float *verts, const int32_t *num_faces,
+                            const int32_t *face_counts, const uint32_t *indices)
+{
+    auto *sim = new Sim {};
+    sim->cfg = *cfg;
+    sim->numHulls = num_hulls;
+    sim->objs = makeHullObjects(*cfg, num_hulls, num_verts, verts, num_faces, face_counts,
+                                indices);
     sim->worlds.resize(num_worlds);
     for (int32_t w = 0; w < num_worlds; w++) {
         initWorld(*sim, sim->worlds[w], pos + (size_t)w * cfg->numCubes * 3,

@@ -79,7 +79,7 @@ class Engine;
 
 struct PhysWorld : public WorldBase {
     PhysWorld(Engine &ctx, ObjectManager *mgr, const RefPhysConfig &cfg,
-              const WorldInit &init, bool simple = false);
+              const WorldInit &init, bool simple = false, int32_t num_hulls = 1);
 
     AABB worldBounds;
 };
@@ -139,7 +139,8 @@ static void clampSystem(Engine &ctx, Position &position)
 }
 
 PhysWorld::PhysWorld(Engine &ctx, ObjectManager *mgr,
-                     const RefPhysConfig &cfg, const WorldInit &init, bool simple)
+                     const RefPhysConfig &cfg, const WorldInit &init, bool simple,
+                     int32_t num_hulls)
     : WorldBase(ctx),
       worldBounds { { -10, -10, 0 }, { 10, 10, 10 } }
 {
@@ -190,12 +191,12 @@ PhysWorld::PhysWorld(Engine &ctx, ObjectManager *mgr,
         Vector3 p { init.pos[3 * i], init.pos[3 * i + 1], init.pos[3 * i + 2] };
         Quat q { init.rot[4 * i], init.rot[4 * i + 1], init.rot[4 * i + 2],
                  init.rot[4 * i + 3] };
-        setup(e, p, q, 0, ResponseType::Dynamic);
+        setup(e, p, q, i % num_hulls, ResponseType::Dynamic);
         cubes.push_back(e);
     }
 
     Entity plane = ctx.makeEntityNow<PhysicsBody>();
-    setup(plane, Vector3::zero(), Quat { 1.f, 0.f, 0.f, 0.f }, 1,
+    setup(plane, Vector3::zero(), Quat { 1.f, 0.f, 0.f, 0.f }, num_hulls,
           ResponseType::Static);
 
     // Joint workload (shared with the oracle and the collisions
@@ -267,6 +268,56 @@ static ObjectManager * makeObjectManager(const RefPhysConfig &cfg)
     return mgr;
 }
 
+// Object table of OBJ hulls, built the way PhysicsLoader::loadHullFromDisk
+// does after import (physics_assets.cpp:205-254): FastPolygonList of the
+// faces, HalfEdgeMesh::construct, AABB::point + AABB::expand; then the plane.
+static ObjectManager * makeHullObjectManager(const RefPhysConfig &cfg,
+    int32_t num_hulls, const int32_t *num_verts, const float *verts,
+    const int32_t *num_faces, const int32_t *face_counts,
+    const uint32_t *indices)
+{
+    auto *mgr = new ObjectManager {};
+    mgr->metadata = new RigidBodyMetadata[num_hulls + 1];
+    mgr->aabbs = new AABB[num_hulls + 1];
+    mgr->primitives = new CollisionPrimitive[num_hulls + 1];
+    for (int32_t h = 0; h < num_hulls; h++) {
+        auto *vs = new Vector3[num_verts[h]];
+        for (int32_t v = 0; v < num_verts[h]; v++) {
+            vs[v] = Vector3 { verts[0], verts[1], verts[2] };
+            verts += 3;
+        }
+        uint32_t space = 0;
+        for (int32_t f = 0; f < num_faces[h]; f++) space += face_counts[f] + 1;
+        geometry::FastPolygonList pl {};
+        pl.allocate(space);
+        pl.polygonCount = 0;
+        pl.edgeCount = 0;
+        for (int32_t f = 0; f < num_faces[h]; f++) {
+            pl.addPolygon(Span<const uint32_t>(indices, face_counts[f]));
+            indices += face_counts[f];
+        }
+        face_counts += num_faces[h];
+        mgr->primitives[h].type = CollisionPrimitive::Type::Hull;
+        mgr->primitives[h].hull.halfEdgeMesh.construct(pl, num_verts[h], vs);
+        AABB box = AABB::point(vs[0]);
+        for (int32_t v = 1; v < num_verts[h]; v++) box.expand(vs[v]);
+        mgr->aabbs[h] = box;
+        mgr->metadata[h] = RigidBodyMetadata {
+            { cfg.cubeInvInertia, cfg.cubeInvInertia, cfg.cubeInvInertia },
+            cfg.cubeInvMass, cfg.muS, cfg.muD,
+        };
+    }
+    mgr->primitives[num_hulls].type = CollisionPrimitive::Type::Plane;
+    mgr->metadata[num_hulls] = RigidBodyMetadata {
+        { 0.f, 0.f, 0.f }, 0.f, cfg.muS, cfg.muD,
+    };
+    mgr->aabbs[num_hulls] = AABB {
+        { -FLT_MAX, -FLT_MAX, -FLT_MAX },
+        { FLT_MAX, FLT_MAX, 0.f },
+    };
+    return mgr;
+}
+
 struct RefWorld {
     StateManager sm;
     StateCache sc;
@@ -327,11 +378,13 @@ struct RefBodyState {
 static void * createWorlds(bool simple, int32_t num_worlds,
                                       const RefPhysConfig *cfg,
                                       const float *init_pos,
-                                      const float *init_rot)
+                                      const float *init_rot,
+                                      ObjectManager *mgr = nullptr,
+                                      int32_t num_hulls = 1)
 {
     auto *h = new RefPhys {};
     h->cfg = *cfg;
-    h->mgr = makeObjectManager(*cfg);
+    h->mgr = mgr ? mgr : makeObjectManager(*cfg);
 
     for (int32_t w = 0; w < num_worlds; w++) {
         auto *rw = new RefWorld {};
@@ -345,7 +398,7 @@ static void * createWorlds(bool simple, int32_t num_worlds,
             init_pos + (size_t)w * cfg->numCubes * 3,
             init_rot + (size_t)w * cfg->numCubes * 4,
         };
-        new (rw->world) PhysWorld(*rw->ctx, h->mgr, *cfg, init, simple);
+        new (rw->world) PhysWorld(*rw->ctx, h->mgr, *cfg, init, simple, num_hulls);
 
         TaskGraph::Builder builder(*rw->ctx);
         if (simple) setupSimpleTasks(builder, cfg->numSubsteps);
@@ -363,6 +416,44 @@ MADRONA_EXPORT void * ref_phys_create(int32_t num_worlds,
                                       const float *init_rot)
 {
     return createWorlds(false, num_worlds, cfg, init_pos, init_rot);
+}
+
+// One hull through the reference's HalfEdgeMesh::construct + AABB (same
+// arguments as the oracle's orc_build_hull).
+MADRONA_EXPORT void ref_build_hull(int32_t num_verts, const float *verts,
+    int32_t num_faces, const int32_t *face_counts, const uint32_t *indices,
+    int32_t *counts_out, float *verts_out, float *planes_out,
+    uint32_t *half_edges_out, uint32_t *polys_out, uint32_t *edges_out,
+    float *aabb_out)
+{
+    RefPhysConfig cfg {};
+    ObjectManager *mgr = makeHullObjectManager(cfg, 1, &num_verts, verts,
+        &num_faces, face_counts, indices);
+    const geometry::HalfEdgeMesh &m = mgr->primitives[0].hull.halfEdgeMesh;
+    counts_out[0] = (int32_t)m.mVertexCount;
+    counts_out[1] = (int32_t)m.mPolygonCount;
+    counts_out[2] = (int32_t)m.mEdgeCount;
+    counts_out[3] = (int32_t)m.mHalfEdgeCount;
+    memcpy(verts_out, m.mVertices, 12 * (size_t)m.mVertexCount);
+    memcpy(planes_out, m.mFacePlanes, 16 * (size_t)m.mPolygonCount);
+    memcpy(half_edges_out, m.mHalfEdges, 16 * (size_t)m.mHalfEdgeCount);
+    memcpy(polys_out, m.mPolygons, 4 * (size_t)m.mPolygonCount);
+    memcpy(edges_out, m.mEdges, 4 * (size_t)m.mEdgeCount);
+    memcpy(aabb_out, &mgr->aabbs[0], 24);
+}
+
+// Collisions worlds over OBJ hulls (body i uses hull i % num_hulls); same
+// geometry arguments as the oracle's orc_phys_create_hulls.
+MADRONA_EXPORT void * ref_phys_create_hulls(int32_t num_worlds,
+    const RefPhysConfig *cfg, const float *init_pos, const float *init_rot,
+    int32_t num_hulls, const int32_t *num_verts, const float *verts,
+    const int32_t *num_faces, const int32_t *face_counts,
+    const uint32_t *indices)
+{
+    ObjectManager *mgr = makeHullObjectManager(*cfg, num_hulls, num_verts,
+        verts, num_faces, face_counts, indices);
+    return createWorlds(false, num_worlds, cfg, init_pos, init_rot, mgr,
+                        num_hulls);
 }
 
 // simple_taskgraph worlds: cfg->numCubes objects + agent + test object.

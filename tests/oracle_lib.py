@@ -74,6 +74,91 @@ def gen_collisions_inits(num_worlds, num_cubes=128, seed=0):
     return pos, rot
 
 
+def parse_obj(path):
+    """OBJ -> (positions f32[V,3], face_counts i32[F], indices u32[sum]) the way
+    the reference importer hands a mesh to PhysicsLoader::loadHullFromDisk
+    (src/common/importer.cpp:35-439): 'v'/'vn'/'vt' records, 'f' records of
+    pos[/uv[/normal]] 1-based indices; the mesh is un-indexed and re-indexed
+    by unique (position, normal, uv) bit patterns in order of first use, the
+    remap meshoptimizer's generateVertexRemapMulti computes (meshoptimizer is
+    an empty submodule in the reference, so this restates its published
+    algorithm).  Single-mesh files only, as loadHullFromDisk asserts."""
+    pos, nrm, uvs, idx, counts = [], [], [], [], []
+    with open(path) as f:
+        for line in f:
+            t = line.split()
+            if not t or t[0].startswith("#"):
+                continue
+            if t[0] == "v":
+                pos.append(np.array(t[1:4], np.float32))
+            elif t[0] == "vn":
+                nrm.append(np.array(t[1:4], np.float32))
+            elif t[0] == "vt":
+                uvs.append(np.array(t[1:3], np.float32))
+            elif t[0] == "f":
+                for c in t[1:]:
+                    p = (c.split("/") + ["", ""])[:3]
+                    idx.append(tuple(int(x) if x else 0 for x in (p[0], p[2], p[1])))
+                counts.append(len(t) - 1)
+    remap, verts, out_idx = {}, [], []
+    for p, n, u in idx:
+        key = pos[p - 1].tobytes() + (nrm[n - 1].tobytes() if n else b"") + \
+            (uvs[u - 1].tobytes() if u else b"")
+        if key not in remap:
+            remap[key] = len(verts)
+            verts.append(pos[p - 1])
+        out_idx.append(remap[key])
+    return (np.array(verts, np.float32).reshape(-1, 3), np.array(counts, np.int32),
+            np.array(out_idx, np.uint32))
+
+
+class HullSet:
+    """Packed geometry of several hulls, the argument block of
+    orc_phys_create_hulls / ref_phys_create_hulls."""
+
+    def __init__(self, meshes):
+        self.meshes = list(meshes)
+        self.num_verts = np.array([len(m[0]) for m in self.meshes], np.int32)
+        self.num_faces = np.array([len(m[1]) for m in self.meshes], np.int32)
+        self.verts = np.ascontiguousarray(np.concatenate([m[0] for m in self.meshes]), np.float32)
+        self.face_counts = np.ascontiguousarray(np.concatenate([m[1] for m in self.meshes]),
+                                                np.int32)
+        self.indices = np.ascontiguousarray(np.concatenate([m[2] for m in self.meshes]), np.uint32)
+
+    @classmethod
+    def from_files(cls, paths):
+        return cls(parse_obj(p) for p in paths)
+
+    def args(self):
+        return (len(self.meshes), _vp(self.num_verts), _vp(self.verts), _vp(self.num_faces),
+                _vp(self.face_counts), _vp(self.indices))
+
+
+def build_hull(mesh, lib=None):
+    """HalfEdgeMesh::construct + AABB of one parsed mesh on the oracle
+    (orc_build_hull) or, with lib=load_ref(), on the reference
+    (ref_build_hull)."""
+    lib = lib or load_orc()
+    fn = lib.orc_build_hull if hasattr(lib, "orc_build_hull") else lib.ref_build_hull
+    fn.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 9
+    verts, counts, idx = (np.ascontiguousarray(a) for a in mesh)
+    cap = 2 * int(counts.sum()) + 8
+    c = np.zeros(4, np.int32)
+    vo = np.zeros((len(verts), 3), np.float32)
+    po = np.zeros((len(counts), 4), np.float32)
+    he = np.zeros((cap, 4), np.uint32)
+    polys = np.zeros(len(counts), np.uint32)
+    edges = np.zeros(cap, np.uint32)
+    aabb = np.zeros((2, 3), np.float32)
+    fn(len(verts), _vp(verts), len(counts), _vp(counts), _vp(idx), _vp(c), _vp(vo), _vp(po),
+       _vp(he), _vp(polys), _vp(edges), _vp(aabb))
+    return {"vertices": vo[:c[0]], "planes": po[:c[1]], "half_edges": he[:c[3]],
+            "polygons": polys[:c[1]], "edges": edges[:c[2]], "aabb": aabb}
+
+
+_HULL_ARGTYPES = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_void_p]
+
 _ORC = None
 _REF = {}
 
@@ -135,6 +220,8 @@ def load_orc():
         lib.orc_phys_destroy.argtypes = [ctypes.c_void_p]
         lib.orc_simple_create.restype = ctypes.c_void_p
         lib.orc_simple_create.argtypes = lib.orc_phys_create.argtypes
+        lib.orc_phys_create_hulls.restype = ctypes.c_void_p
+        lib.orc_phys_create_hulls.argtypes = lib.orc_phys_create.argtypes + _HULL_ARGTYPES
         lib.orc_phys_ub_manifolds.restype = ctypes.c_int32
         lib.orc_phys_ub_manifolds.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         lib.orc_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
@@ -160,6 +247,9 @@ def load_ref(image="main"):
         lib.ref_phys_create.restype = ctypes.c_void_p
         lib.ref_phys_create.argtypes = [ctypes.c_int32, ctypes.POINTER(PhysConfig),
                                         ctypes.c_void_p, ctypes.c_void_p]
+        if hasattr(lib, "ref_phys_create_hulls"):
+            lib.ref_phys_create_hulls.restype = ctypes.c_void_p
+            lib.ref_phys_create_hulls.argtypes = lib.ref_phys_create.argtypes + _HULL_ARGTYPES
         lib.ref_phys_step.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         lib.ref_phys_read_bodies.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
         lib.ref_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 4
@@ -171,14 +261,21 @@ def load_ref(image="main"):
 class OraclePhys:
     """Restated CPU physics (oracle/mw_oracle.cpp)."""
 
-    def __init__(self, cfg, pos, rot):
+    def __init__(self, cfg, pos, rot, hulls=None):
+        """hulls: a HullSet -> body i uses hull i % len(hulls), the plane
+        follows them (orc_phys_create_hulls); None -> the built-in cube."""
         self.lib = load_orc()
         self.cfg = cfg
         self.num_worlds = pos.shape[0]
         self.nb = cfg.numCubes + 1
         pos = np.ascontiguousarray(pos, np.float32)
         rot = np.ascontiguousarray(rot, np.float32)
-        self.h = self.lib.orc_phys_create(self.num_worlds, ctypes.byref(cfg), _vp(pos), _vp(rot))
+        if hulls is None:
+            self.h = self.lib.orc_phys_create(self.num_worlds, ctypes.byref(cfg), _vp(pos),
+                                              _vp(rot))
+        else:
+            self.h = self.lib.orc_phys_create_hulls(self.num_worlds, ctypes.byref(cfg), _vp(pos),
+                                                    _vp(rot), *hulls.args())
 
     def step(self, n=1, threads=1):
         self.lib.orc_phys_step(self.h, n, threads)
@@ -236,15 +333,19 @@ class OracleSimple(OraclePhys):
 class ReferencePhys:
     """The reference itself (oracle/_ref/libmadrona_ref.so)."""
 
-    def __init__(self, cfg, pos, rot):
+    def __init__(self, cfg, pos, rot, hulls=None):
         self.lib = load_ref()
         self.cfg = cfg
         self.num_worlds = pos.shape[0]
         self.nb = cfg.numCubes + 1
         self._pos = np.ascontiguousarray(pos, np.float32)
         self._rot = np.ascontiguousarray(rot, np.float32)
-        self.h = self.lib.ref_phys_create(self.num_worlds, ctypes.byref(cfg),
-                                          _vp(self._pos), _vp(self._rot))
+        if hulls is None:
+            self.h = self.lib.ref_phys_create(self.num_worlds, ctypes.byref(cfg),
+                                              _vp(self._pos), _vp(self._rot))
+        else:
+            self.h = self.lib.ref_phys_create_hulls(self.num_worlds, ctypes.byref(cfg),
+                                                    _vp(self._pos), _vp(self._rot), *hulls.args())
 
     def step(self, n=1):
         self.lib.ref_phys_step(self.h, n)

@@ -57,8 +57,9 @@ def test_struct_layout_matches_header(tmp_path):
         int main(void) {
             printf("%zu %zu %zu\\n", sizeof(mw_config), sizeof(mw_collisions_config),
                    sizeof(mw_collisions_init));
-            printf("%zu %zu %zu\\n", offsetof(mw_collisions_config, max_contacts),
-                   offsetof(mw_collisions_config, mu_d), offsetof(mw_config, use_graph));
+            printf("%zu %zu %zu %zu\\n", offsetof(mw_collisions_config, max_contacts),
+                   offsetof(mw_collisions_config, mu_d), offsetof(mw_config, use_graph),
+                   offsetof(mw_collisions_config, hull_paths));
             return 0;
         }
     """))
@@ -72,7 +73,8 @@ def test_struct_layout_matches_header(tmp_path):
                                                 ctypes.sizeof(mw.CollisionsInit)]
     assert [int(x) for x in offs.split()] == [mw.CollisionsConfig.max_contacts.offset,
                                               mw.CollisionsConfig.mu_d.offset,
-                                              mw.MwConfig.use_graph.offset]
+                                              mw.MwConfig.use_graph.offset,
+                                              mw.CollisionsConfig.hull_paths.offset]
 
 
 def test_init_generator_matches_oracle_including_shard_offsets():
