@@ -25,6 +25,7 @@ __device__ __forceinline__ AABB expandAABBWithMotion(AABB aabb, const Vector3 &v
 // updateLeafPositionsEntry (broadphase.cpp:858-873, 461-480)
 __global__ void __launch_bounds__(256) leafUpdateKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     const BodyArch &B = P.body[blockIdx.y];
     RowIdx ri = rowIndex(P, B);
     if (!ri.valid) return;
@@ -85,6 +86,7 @@ __device__ int32_t midpointSplit(const AABB *aabbs, int32_t *sorted, int32_t bas
 
 __global__ void __launch_bounds__(64) bvhRebuildKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     const int32_t w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= P.numWorlds) return;
     broadphase::BVH &bvh = P.bvh[w];
@@ -234,6 +236,7 @@ size_t refitSharedBytes(const PhysArgs &P)
 
 __global__ void __launch_bounds__(kRefitBlock) refitKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     BVHNode *lnodes = (BVHNode *)smem;
     const int32_t w = blockIdx.x;
@@ -375,6 +378,7 @@ size_t findOverlapsSharedBytes(const PhysArgs &P)
 
 __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int32_t scan_scratch[kOverlapBlock / 64];
     const int32_t w = blockIdx.x;

@@ -13,6 +13,7 @@ namespace madrona::phys {
 
 __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     const BodyArch &B = P.body[blockIdx.y];
     RowIdx ri = rowIndex(P, B);
     if (!ri.valid) return;
@@ -534,6 +535,7 @@ __device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
 // (hull-hull from the front, hull-plane from the back).  No global atomics.
 __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     __shared__ int32_t s_scan[kNarrowBlock / 64];
     const int32_t w = blockIdx.x;
     const int32_t cap = P.candCapacity;
@@ -577,6 +579,7 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
 // hull-plane counts -> each world's offset in the flat lists, and totals.
 __global__ void __launch_bounds__(1024) narrowScanKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     // Each thread owns a contiguous run of worlds (counts held in registers):
     // one block scan of the run sums instead of one per 1024 worlds.
     __shared__ int32_t s_scan[1024 / 64];
@@ -628,6 +631,7 @@ __global__ void __launch_bounds__(1024) narrowScanKernel(PhysArgs P)
 // positions (hull-plane pairs become contact jobs directly).
 __global__ void __launch_bounds__(kNarrowBlock) narrowCompactKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     const int32_t w = blockIdx.x;
     const int32_t cap = P.candCapacity;
     const SatWork *stage = P.satStage + (size_t)w * cap;
@@ -699,6 +703,7 @@ __device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS
 #endif
 __global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int32_t group = threadIdx.x / kGroup;
     const int32_t lane = threadIdx.x % kGroup;
@@ -741,6 +746,7 @@ size_t contactSharedBytes(const PhysArgs &P)
 // (narrowphase.cpp:866-1121) for one job per lane.
 __global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const ObjDev &O = P.objs;
     const int32_t cap = P.clipCap;

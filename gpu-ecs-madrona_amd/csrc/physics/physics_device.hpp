@@ -6,6 +6,7 @@
 #include <madrona/physics.hpp>
 
 #include "physics_impl.hpp"
+#include <madrona/tracing.hpp>
 
 #include <hip/hip_runtime.h>
 

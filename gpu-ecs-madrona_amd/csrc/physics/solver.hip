@@ -678,6 +678,7 @@ __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, S
 __global__ void __launch_bounds__(kSolverThreads)
 __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(PhysArgs P)
 {
+    MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int32_t nb = P.maxBodiesPerWorld;
     const int32_t wi = threadIdx.x / kSolverBlock;

@@ -413,6 +413,38 @@ double mw_timed_node_ms(mw_exec *exec, int64_t *launches)
     MW_TRY({ return exec->exec->timedNodeMs(launches); }, -1.0)
 }
 
+int mw_trace_enable(mw_exec *exec, int64_t max_records)
+{
+    MW_TRY({
+        if (max_records < 0) throw std::runtime_error("mw_trace_enable: negative max_records");
+        exec->exec->enableTracing(max_records);
+        return 0;
+    }, -1)
+}
+
+int mw_trace_block_records(void)
+{
+#if defined(MW_TRACING)
+    return 1;
+#else
+    return 0;
+#endif
+}
+
+int64_t mw_trace_read(mw_exec *exec, void *dst, int64_t max_bytes, int64_t *dropped)
+{
+    MW_TRY({
+        const int64_t n = exec->exec->readTrace(dst, max_bytes, dropped);
+        if (n < 0) throw std::runtime_error("mw_trace_read: tracing is not enabled");
+        return n;
+    }, (int64_t)-1)
+}
+
+const char *mw_trace_func_name(mw_exec *exec, int32_t func_id)
+{
+    MW_TRY({ return exec->exec->traceFuncName(func_id); }, (const char *)nullptr)
+}
+
 }
 
 extern "C" int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *contacts_out)

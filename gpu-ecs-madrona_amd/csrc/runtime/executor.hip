@@ -3,6 +3,7 @@
 // Reference: src/core/taskgraph.cpp:18-122 (Builder/build/run),
 // src/mw/cuda_exec.cpp:1519-1815 (run graph, getExported, export kernels).
 #include <madrona/mw_gpu.hpp>
+#include <madrona/tracing.hpp>
 
 #include <hip/hip_runtime.h>
 
@@ -113,6 +114,7 @@ void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype,
 
 __global__ void clearRowsKernel(int32_t *num_rows, int32_t num_worlds)
 {
+    MW_TRACE_BLOCK(0);
     int32_t w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w < num_worlds) num_rows[w] = 0;
 }
@@ -132,6 +134,7 @@ void launchClearRows(LaunchCtx &lc, int32_t archetype)
 __global__ void __launch_bounds__(1024)
 exportScanKernel(const int32_t *num_rows, int32_t num_worlds, int64_t *offsets)
 {
+    MW_TRACE_BLOCK(0);
     __shared__ int64_t wave_sums[1024 / 64];
     const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int32_t per = (num_worlds + 1023) / 1024;
@@ -163,6 +166,7 @@ __global__ void __launch_bounds__(256)
 exportCopyKernel(const uint32_t *col, int32_t capacity, uint32_t words_per_row,
                  const int32_t *num_rows, const int64_t *offsets, uint32_t *out)
 {
+    MW_TRACE_BLOCK(0);
     const int32_t w = blockIdx.y;
     const int32_t n = num_rows[w] * (int32_t)words_per_row;
     const uint32_t *src = col + (size_t)w * capacity * words_per_row;
@@ -170,6 +174,50 @@ exportCopyKernel(const uint32_t *col, int32_t capacity, uint32_t words_per_row,
     for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         dst[i] = src[i];
     }
+}
+
+// ---------------------------------------------------------------------------
+// Device tracing (include/madrona/tracing.hpp)
+// ---------------------------------------------------------------------------
+namespace mwGPU {
+
+static std::vector<TraceSetter> &traceSetters()
+{
+    static std::vector<TraceSetter> v;
+    return v;
+}
+
+void registerTraceSetter(TraceSetter fn) { traceSetters().push_back(fn); }
+
+static void setTracePointer(TraceDev *p)
+{
+    for (TraceSetter fn : traceSetters()) fn(p);
+}
+
+// One lane: a step / node boundary record.  The calibration record opens a
+// step (logIndex 0: funcID = loggers per block, numInvocations = blocks per
+// CU accounted per record, nodeID = size of the SM id space -- the fields
+// parse_device_tracing.py reads from it); nodeStart also publishes the node
+// to the blocks of the kernels that follow it.
+__global__ void traceMarkerKernel(TraceDev *t, uint32_t ev, uint32_t func, uint32_t inv,
+                                  uint32_t node)
+{
+    if (ev == (uint32_t)DeviceEvent::calibration) {
+        const uint32_t i = atomicAdd(&t->next, 1u);
+        __hip_atomic_store(&t->stepBase, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t ts = (uint64_t)wall_clock64() * t->nsPerTick;
+        if (i >= t->capacity) {
+            atomicAdd(&t->dropped, 1u);
+            return;
+        }
+        t->logs[i] = DeviceLog { DeviceEvent::calibration, func, inv, node, 0, 0, traceSMID(), 0,
+                                 ts };
+        return;
+    }
+    if (ev == (uint32_t)DeviceEvent::nodeStart) t->curNode = node;
+    traceLog(t, (DeviceEvent)ev, func, inv, node, 0);
+}
+
 }
 
 // ---------------------------------------------------------------------------
@@ -208,6 +256,12 @@ struct Executor::Impl {
     double timedMs = 0.0;
     int64_t timedLaunches = 0;
     bool timedPending = false;
+
+    // Device tracing: null unless enabled (Executor::enableTracing).
+    mwGPU::TraceDev *trace = nullptr;
+    mwGPU::DeviceLog *traceLogs = nullptr;
+    std::vector<std::string> traceFuncs;      // funcID -> node kind
+    std::vector<uint32_t> nodeFunc;           // node -> funcID
 };
 
 Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
@@ -227,6 +281,12 @@ Executor::~Executor()
     for (auto &sg : impl_->segs) {
         if (sg.exec) (void)hipGraphExecDestroy(sg.exec);
         if (sg.graph) (void)hipGraphDestroy(sg.graph);
+    }
+    if (impl_->trace) {
+        (void)hipStreamSynchronize(impl_->stream);
+        mwGPU::setTracePointer(nullptr);
+        (void)hipFree(impl_->trace);
+        (void)hipFree(impl_->traceLogs);
     }
     for (auto &e : impl_->exports) {
         (void)hipFree(e.buf);
@@ -288,9 +348,21 @@ void Executor::uploadState()
     }
 }
 
+static void traceMarker(Executor::Impl &I, mwGPU::DeviceEvent ev, uint32_t func, uint32_t inv,
+                        uint32_t node);
+
+// With tracing on, each export gather is its own trace node (IDs after the
+// graph's nodes, funcID of the "ExportNode" kind).
 static void launchExports(Executor::Impl &I, const StateView &dv)
 {
-    for (ExportBuf &b : I.exports) {
+    for (size_t e = 0; e < I.exports.size(); e++) {
+        ExportBuf &b = I.exports[e];
+        const uint32_t trace_node = (uint32_t)(I.graph.numNodes() + e);
+        const uint32_t trace_func = (uint32_t)I.traceFuncs.size() - 1;
+        if (I.trace) {
+            traceMarker(I, mwGPU::DeviceEvent::nodeStart, trace_func, (uint32_t)dv.numWorlds,
+                        trace_node);
+        }
         const ArchetypeView &av = dv.arch[b.archetype];
         if (b.scanOwner) {
             hipLaunchKernelGGL(exportScanKernel, dim3(1), dim3(1024), 0, I.stream,
@@ -301,6 +373,10 @@ static void launchExports(Executor::Impl &I, const StateView &dv)
         hipLaunchKernelGGL(exportCopyKernel, dim3(bx, dv.numWorlds), dim3(256), 0, I.stream,
                            (const uint32_t *)av.cols[b.column], av.capacity, words, av.numRows,
                            b.offsets, (uint32_t *)b.buf);
+        if (I.trace) {
+            traceMarker(I, mwGPU::DeviceEvent::nodeFinish, trace_func, (uint32_t)dv.numWorlds,
+                        trace_node);
+        }
     }
 }
 
@@ -309,18 +385,55 @@ static bool isTimed(const Executor::Impl &I, int32_t node)
     return !I.timedName.empty() && I.timedName == I.graph.nodeName(node);
 }
 
+static void traceMarker(Executor::Impl &I, mwGPU::DeviceEvent ev, uint32_t func, uint32_t inv,
+                        uint32_t node)
+{
+    hipLaunchKernelGGL(mwGPU::traceMarkerKernel, dim3(1), dim3(1), 0, I.stream, I.trace,
+                       (uint32_t)ev, func, inv, node);
+}
+
+// A node's launches; with tracing on, bracketed by nodeStart / nodeFinish.
+static void launchNode(Executor::Impl &I, int32_t i, LaunchCtx &lc)
+{
+    if (!I.trace) {
+        I.graph.launchNode(i, lc);
+        return;
+    }
+    const uint32_t f = I.nodeFunc[i], n = (uint32_t)I.cfg.numWorlds;
+    traceMarker(I, mwGPU::DeviceEvent::nodeStart, f, n, (uint32_t)i);
+    I.graph.launchNode(i, lc);
+    traceMarker(I, mwGPU::DeviceEvent::nodeFinish, f, n, (uint32_t)i);
+}
+
+// Step boundaries of the trace (calibration record / blockExit record).
+static constexpr uint32_t kTraceSMIDs = 8 * 4 * 16;
+
+static void traceStepBegin(Executor::Impl &I)
+{
+    if (I.trace) traceMarker(I, mwGPU::DeviceEvent::calibration, 1, 1, kTraceSMIDs);
+}
+
+static void traceStepEnd(Executor::Impl &I)
+{
+    if (I.trace) {
+        traceMarker(I, mwGPU::DeviceEvent::blockExit, 0, 0, (uint32_t)I.graph.numNodes());
+    }
+}
+
 // One step's launch sequence: every node in sorted order, then the export
 // gathers.  Nodes of the timed kind are bracketed by their own event pair.
 static void launchStep(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
 {
     size_t ev = 0;
+    traceStepBegin(I);
     for (int32_t i = 0; i < I.graph.numNodes(); i++) {
         const bool timed = isTimed(I, i);
         if (timed) MW_HIP_CHECK(hipEventRecord(I.timedEvents[ev].first, I.stream));
-        I.graph.launchNode(i, lc);
+        launchNode(I, i, lc);
         if (timed) MW_HIP_CHECK(hipEventRecord(I.timedEvents[ev++].second, I.stream));
     }
     launchExports(I, dv);
+    traceStepEnd(I);
 }
 
 static void captureGraph(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
@@ -337,10 +450,14 @@ static void captureGraph(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
         if (!last && !isTimed(I, i)) continue;
         Executor::Impl::Segment sg;
         sg.timedNode = last ? -1 : i;
-        if (i > start || last) {
+        if (i > start || last || (start == 0 && I.trace)) {
             MW_HIP_CHECK(hipStreamBeginCapture(I.stream, hipStreamCaptureModeThreadLocal));
-            for (int32_t k = start; k < i; k++) I.graph.launchNode(k, lc);
-            if (last) launchExports(I, dv);
+            if (start == 0) traceStepBegin(I);
+            for (int32_t k = start; k < i; k++) launchNode(I, k, lc);
+            if (last) {
+                launchExports(I, dv);
+                traceStepEnd(I);
+            }
             MW_HIP_CHECK(hipStreamEndCapture(I.stream, &sg.graph));
             MW_HIP_CHECK(hipGraphInstantiate(&sg.exec, sg.graph, nullptr, nullptr, 0));
         }
@@ -367,7 +484,7 @@ void Executor::runAsync()
             if (sg.exec) MW_HIP_CHECK(hipGraphLaunch(sg.exec, impl_->stream));
             if (sg.timedNode >= 0) {
                 MW_HIP_CHECK(hipEventRecord(impl_->timedEvents[ev].first, impl_->stream));
-                impl_->graph.launchNode(sg.timedNode, lc);
+                launchNode(*impl_, sg.timedNode, lc);
                 MW_HIP_CHECK(hipEventRecord(impl_->timedEvents[ev].second, impl_->stream));
                 ev++;
             }
@@ -424,6 +541,71 @@ void Executor::setTimedNode(const char *name)
     const StateView &dv = impl_->mgr->deviceViewHost();
     LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
     if (impl_->cfg.useGraph) captureGraph(*impl_, lc, dv);
+}
+
+void Executor::enableTracing(int64_t max_records)
+{
+    Impl &I = *impl_;
+    sync();
+    if (I.trace) {
+        mwGPU::setTracePointer(nullptr);
+        MW_HIP_CHECK(hipFree(I.trace));
+        MW_HIP_CHECK(hipFree(I.traceLogs));
+        I.trace = nullptr;
+        I.traceLogs = nullptr;
+    }
+    if (max_records > 0) {
+        if (max_records > 0xffffffffll) throw std::runtime_error("tracing: too many records");
+        int rate_khz = 0;
+        MW_HIP_CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate,
+                                           I.cfg.gpuID));
+        if (rate_khz <= 0) rate_khz = 100000;
+        MW_HIP_CHECK(hipMalloc(&I.traceLogs, sizeof(mwGPU::DeviceLog) * (size_t)max_records));
+        MW_HIP_CHECK(hipMalloc(&I.trace, sizeof(mwGPU::TraceDev)));
+        mwGPU::TraceDev t {};
+        t.capacity = (uint32_t)max_records;
+        t.nsPerTick = (uint32_t)std::max(1, 1000000 / rate_khz);
+        t.logs = I.traceLogs;
+        MW_HIP_CHECK(hipMemcpy(I.trace, &t, sizeof(t), hipMemcpyHostToDevice));
+        mwGPU::setTracePointer(I.trace);
+        // funcID: node kind, numbered in first-appearance order
+        I.traceFuncs.clear();
+        I.nodeFunc.clear();
+        for (int32_t i = 0; i < I.graph.numNodes(); i++) {
+            const std::string name = I.graph.nodeName(i);
+            auto it = std::find(I.traceFuncs.begin(), I.traceFuncs.end(), name);
+            I.nodeFunc.push_back((uint32_t)(it - I.traceFuncs.begin()));
+            if (it == I.traceFuncs.end()) I.traceFuncs.push_back(name);
+        }
+        I.traceFuncs.push_back("ExportNode");
+    }
+    MW_HIP_CHECK(hipDeviceSynchronize());
+    const StateView &dv = I.mgr->deviceViewHost();
+    LaunchCtx lc { I.stream, I.mgr->deviceView(), &dv, I.cfg.numWorlds, this };
+    if (I.cfg.useGraph) captureGraph(I, lc, dv);
+}
+
+int64_t Executor::readTrace(void *dst, int64_t max_bytes, int64_t *dropped)
+{
+    Impl &I = *impl_;
+    sync();
+    if (!I.trace) return -1;
+    mwGPU::TraceDev t {};
+    MW_HIP_CHECK(hipMemcpy(&t, I.trace, sizeof(t), hipMemcpyDeviceToHost));
+    const int64_t n = std::min<int64_t>(t.next, t.capacity);
+    if (dropped) *dropped = t.dropped;
+    const int64_t bytes = n * (int64_t)sizeof(mwGPU::DeviceLog);
+    if (dst) {
+        MW_HIP_CHECK(hipMemcpy(dst, I.traceLogs, (size_t)std::min(bytes, std::max<int64_t>(0, max_bytes)),
+                               hipMemcpyDeviceToHost));
+    }
+    return bytes;
+}
+
+const char *Executor::traceFuncName(int32_t func_id)
+{
+    if (func_id < 0 || func_id >= (int32_t)impl_->traceFuncs.size()) return nullptr;
+    return impl_->traceFuncs[func_id].c_str();
 }
 
 double Executor::timedNodeMs(int64_t *launches)

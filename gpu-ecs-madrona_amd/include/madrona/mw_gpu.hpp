@@ -73,6 +73,15 @@ public:
     void setTimedNode(const char *name);
     double timedNodeMs(int64_t *launches);
 
+    // Device tracing (reference mw_gpu/tracing.hpp): records of every step
+    // run after this call, up to max_records 40-byte DeviceLogs in total (0
+    // disables); re-captures the step graph with the node markers.
+    void enableTracing(int64_t max_records);
+    // Copies the records so far (all traced steps, in log order) into dst;
+    // returns their byte size (-1 when tracing is off).
+    int64_t readTrace(void *dst, int64_t max_bytes, int64_t *dropped);
+    const char *traceFuncName(int32_t func_id);
+
     struct Impl;
 private:
     std::unique_ptr<Impl> impl_;

@@ -13,6 +13,7 @@
 #pragma once
 
 #include <madrona/context.hpp>
+#include <madrona/tracing.hpp>
 
 #include <initializer_list>
 #include <memory>
@@ -152,6 +153,7 @@ __global__ void __launch_bounds__(256)
 parallelForKernel(const StateView *__restrict__ st_in, int32_t arch,
                   ColArgs<sizeof...(ComponentTs)> cols)
 {
+    MW_TRACE_BLOCK(arch);
     // The StateView itself is read-only inside a node (only the slabs it
     // points to are written); const + restrict lets the backend treat the
     // column pointers loaded from it as global (no flat accesses).
@@ -223,6 +225,7 @@ void launchWorldKernel(const void *kernel, LaunchCtx &lc);
 template <typename ContextT, auto Fn>
 __global__ void __launch_bounds__(64) perWorldKernel(const StateView *__restrict__ st_in)
 {
+    MW_TRACE_BLOCK(0);
     StateView *st = const_cast<StateView *>(st_in);
     const int32_t w = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (w >= st->numWorlds) return;

@@ -123,6 +123,13 @@ RCCL_ID_BYTES = 128
 _lib.mw_load_hull.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                              ctypes.c_int32]
+_lib.mw_trace_enable.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+_lib.mw_trace_block_records.restype = ctypes.c_int
+_lib.mw_trace_read.restype = ctypes.c_int64
+_lib.mw_trace_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                               ctypes.POINTER(ctypes.c_int64)]
+_lib.mw_trace_func_name.restype = ctypes.c_char_p
+_lib.mw_trace_func_name.argtypes = [ctypes.c_void_p, ctypes.c_int32]
 _lib.mw_set_timed_node.restype = ctypes.c_int32
 _lib.mw_set_timed_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
 _lib.mw_timed_node_ms.restype = ctypes.c_double
@@ -137,6 +144,7 @@ C_ABI_SYMBOLS = (
     "mw_gen_collisions_inits", "mw_set_timed_node", "mw_timed_node_ms",
     "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
     "mw_device_free", "mw_gen_fvs_inits", "mw_stream_wait", "mw_load_hull",
+    "mw_trace_enable", "mw_trace_read", "mw_trace_func_name", "mw_trace_block_records",
 )
 
 
@@ -161,6 +169,14 @@ def gen_collisions_inits(num_worlds, num_cubes=128, seed=0, first_world=0):
 ERR_BITS = {1: "id store full", 2: "table full", 4: "candidate overflow",
             8: "contact overflow", 16: "BVH stack overflow", 32: "solver body overflow",
             64: "index guard (site in bits 8..15)"}
+
+
+# DeviceLog (include/madrona/tracing.hpp; reference mw_gpu/tracing.hpp:30-41).
+TRACE_DTYPE = np.dtype([("event", np.uint32), ("funcID", np.uint32),
+                        ("numInvocations", np.uint32), ("nodeID", np.uint32),
+                        ("warpID", np.uint32), ("blockID", np.uint32), ("smID", np.uint32),
+                        ("logIndex", np.uint32), ("cycleCount", np.uint64)])
+assert TRACE_DTYPE.itemsize == 40
 
 
 def load_hull(path):
@@ -345,6 +361,45 @@ class Executor:
         n = ctypes.c_int64(0)
         ms = _lib.mw_timed_node_ms(self.h, ctypes.byref(n))
         return ms, n.value
+
+    def enable_tracing(self, max_records=1 << 20):
+        """Device tracing (reference MADRONA_TRACING, mw_gpu/tracing.hpp): every
+        following step logs 40-byte DeviceLog records; 0 disables."""
+        if _lib.mw_trace_enable(self.h, int(max_records)) != 0:
+            raise _err()
+
+    @staticmethod
+    def trace_block_records():
+        """True for the tracing build (block records compiled in)."""
+        return bool(_lib.mw_trace_block_records())
+
+    def trace_records(self):
+        """(records as a TRACE_DTYPE array, number dropped to a full buffer)."""
+        dropped = ctypes.c_int64(0)
+        n = _lib.mw_trace_read(self.h, None, 0, ctypes.byref(dropped))
+        if n < 0:
+            raise _err()
+        out = np.zeros(n // TRACE_DTYPE.itemsize, TRACE_DTYPE)
+        if _lib.mw_trace_read(self.h, out.ctypes.data, n, ctypes.byref(dropped)) < 0:
+            raise _err()
+        return out, int(dropped.value)
+
+    def trace_func_names(self):
+        names, i = [], 0
+        while True:
+            s = _lib.mw_trace_func_name(self.h, i)
+            if s is None:
+                return names
+            names.append(s.decode())
+            i += 1
+
+    def dump_trace(self, path):
+        """Writes the records as the flat binary file
+        scripts/parse_device_tracing.py --trace_file reads."""
+        recs, _ = self.trace_records()
+        with open(path, "wb") as f:
+            f.write(recs.tobytes())
+        return len(recs)
 
     def close(self):
         if getattr(self, "h", None):

@@ -166,6 +166,26 @@ double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps
 int32_t mw_set_timed_node(mw_exec *exec, const char *node_name);
 double mw_timed_node_ms(mw_exec *exec, int64_t *launches);
 
+/* ---- device tracing (reference src/mw/device/include/madrona/mw_gpu/
+ * tracing.hpp:14-128, MADRONA_TRACING + DeviceTracingManager::
+ * transferLogToCPU, cuda_exec.cpp:1784) ----------------------------------
+ * mw_trace_enable: log every following step -- a calibration record per
+ * step, nodeStart / nodeFinish per node, blockStart / blockWait per block of
+ * every kernel, blockExit at the step's end -- as 40-byte DeviceLog records
+ * (event, funcID, numInvocations, nodeID, warpID, blockID, smID, logIndex,
+ * ns timestamp), the input format of scripts/parse_device_tracing.py, up to
+ * max_records in total (0 disables; re-captures the step graph).  One traced
+ * executor per process.  mw_trace_read copies the records so far into dst
+ * (up to max_bytes) and returns their total byte size (-1: tracing off);
+ * *dropped counts records lost to a full buffer.  mw_trace_func_name maps a
+ * funcID to its node kind ("SolverNode", ...), NULL past the last.        */
+int mw_trace_enable(mw_exec *exec, int64_t max_records);
+/* 1 when this library logs block records (the tracing build, -DMW_TRACING,
+ * like the reference's MADRONA_TRACING); 0: node / step records only.     */
+int mw_trace_block_records(void);
+int64_t mw_trace_read(mw_exec *exec, void *dst, int64_t max_bytes, int64_t *dropped);
+const char *mw_trace_func_name(mw_exec *exec, int32_t func_id);
+
 /* ---- "fantasy_vs" environment (BASELINE.json configs[4]) -----------------
  * per world num_dragons casters + num_knights archers; dead entities are
  * destroyed every tick (examples/fantasy_vs/fvs.cpp, restated onto the
