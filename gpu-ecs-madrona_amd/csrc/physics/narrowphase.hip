@@ -14,6 +14,12 @@ namespace madrona::phys {
 __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
+    // Zero the per-64-world survivor sums the narrowphase filter accumulates
+    // (the previous substep's compact kernel has finished reading them).
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+        const int32_t groups = (P.numWorlds + 63) >> 6;
+        for (int32_t g = threadIdx.x; g < groups; g += blockDim.x) P.groupCounts[g] = 0;
+    }
     const BodyArch &B = P.body[blockIdx.y];
     RowIdx ri = rowIndex(P, B);
     if (!ri.valid) return;
@@ -572,72 +578,49 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
         P.survCount[w] = S;
         P.hhCount[w] = nhh;
         P.planeCount[w] = npl;
+        // packed (hull-hull | hull-plane << 32) sum of this world's group of
+        // 64: the compact kernel's offsets need only these plus the <= 63
+        // counts before it in its group (no separate scan launch); 64 worlds
+        // share an address, so the atomics barely contend
+        atomicAdd(P.groupCounts + (w >> 6),
+                  (unsigned long long)(uint32_t)nhh | ((unsigned long long)(uint32_t)npl << 32));
     }
 }
 
-// Stage 2, one block: exclusive scans of the per-world hull-hull and
-// hull-plane counts -> each world's offset in the flat lists, and totals.
-__global__ void __launch_bounds__(1024) narrowScanKernel(PhysArgs P)
-{
-    MW_TRACE_BLOCK(0);
-    // Each thread owns a contiguous run of worlds (counts held in registers):
-    // one block scan of the run sums instead of one per 1024 worlds.
-    __shared__ int32_t s_scan[1024 / 64];
-    const int32_t W = P.numWorlds;
-    const int32_t per = (W + 1023) / 1024;
-    const int32_t w0 = threadIdx.x * per;
-    const int32_t w1 = min(w0 + per, W);
-    constexpr int32_t kRun = 16;
-    int32_t hc[kRun], pc[kRun];
-    int32_t hh = 0, pl = 0;
-#pragma unroll
-    for (int32_t i = 0; i < kRun; i++) {
-        const int32_t w = w0 + i;
-        hc[i] = (i < per && w < w1) ? P.hhCount[w] : 0;
-        pc[i] = (i < per && w < w1) ? P.planeCount[w] : 0;
-    }
-#pragma unroll
-    for (int32_t i = 0; i < kRun; i++) { hh += hc[i]; pl += pc[i]; }
-    for (int32_t w = w0 + kRun; w < w1; w++) {      // more than 16 K worlds
-        hh += P.hhCount[w];
-        pl += P.planeCount[w];
-    }
-    int32_t total_hh, total_pl;
-    int32_t off_hh = blockExclusiveScan(hh, s_scan, &total_hh);
-    int32_t off_pl = blockExclusiveScan(pl, s_scan, &total_pl);
-#pragma unroll
-    for (int32_t i = 0; i < kRun; i++) {
-        const int32_t w = w0 + i;
-        if (i < per && w < w1) {
-            P.hhOffset[w] = off_hh;
-            P.planeOffset[w] = off_pl;
-            off_hh += hc[i];
-            off_pl += pc[i];
-        }
-    }
-    for (int32_t w = w0 + kRun; w < w1; w++) {
-        P.hhOffset[w] = off_hh;
-        P.planeOffset[w] = off_pl;
-        off_hh += P.hhCount[w];
-        off_pl += P.planeCount[w];
-    }
-    if (threadIdx.x == 0) {
-        *P.satWorkCount = total_hh;
-        *P.jobCount = total_pl;
-    }
-}
-
-// Stage 3, block per world: move the world's staged pairs to their flat
-// positions (hull-plane pairs become contact jobs directly).
+// Stage 2, block per world: the world's offsets in the flat lists (sum of
+// the group sums before its group + the counts before it in its group, one
+// wave), then move its staged pairs there (hull-plane pairs become contact
+// jobs directly).  World order in the flat lists = world index.
 __global__ void __launch_bounds__(kNarrowBlock) narrowCompactKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
+    __shared__ unsigned long long s_off;
     const int32_t w = blockIdx.x;
     const int32_t cap = P.candCapacity;
     const SatWork *stage = P.satStage + (size_t)w * cap;
     const int32_t nhh = P.hhCount[w], npl = P.planeCount[w];
-    SatWork *hh_out = P.satWork + P.hhOffset[w];
-    ContactJob *pl_out = P.planeJobs + P.planeOffset[w];
+    if (threadIdx.x < 64) {
+        const int32_t g = w >> 6;
+        unsigned long long acc = 0;
+        for (int32_t j = threadIdx.x; j < g; j += 64) acc += P.groupCounts[j];
+        const int32_t wi = (g << 6) + threadIdx.x;
+        if (wi < w) {
+            acc += (unsigned long long)(uint32_t)P.hhCount[wi] |
+                   ((unsigned long long)(uint32_t)P.planeCount[wi] << 32);
+        }
+#pragma unroll
+        for (int32_t o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (threadIdx.x == 0) {
+            s_off = acc;
+            if (w == P.numWorlds - 1) {                    // list totals
+                *P.satWorkCount = (int32_t)(uint32_t)acc + nhh;
+                *P.jobCount = (int32_t)(acc >> 32) + npl;
+            }
+        }
+    }
+    __syncthreads();
+    SatWork *hh_out = P.satWork + (uint32_t)s_off;
+    ContactJob *pl_out = P.planeJobs + (uint32_t)(s_off >> 32);
     for (int32_t i = threadIdx.x; i < nhh; i += kNarrowBlock) hh_out[i] = stage[i];
     for (int32_t i = threadIdx.x; i < npl; i += kNarrowBlock) {
         ContactJob job;

@@ -322,8 +322,7 @@ void PhysicsModule::upload(void *stream_ptr)
     P.satStage = devAlloc<SatWork>((size_t)W * P.candCapacity, stream);
     P.hhCount = devAlloc<int32_t>(W, stream);
     P.planeCount = devAlloc<int32_t>(W, stream);
-    P.hhOffset = devAlloc<int32_t>(W, stream);
-    P.planeOffset = devAlloc<int32_t>(W, stream);
+    P.groupCounts = devAlloc<unsigned long long>((size_t)(W + 63) / 64, stream);
     P.planeJobs = devAlloc<ContactJob>((size_t)W * P.candCapacity, stream);
     P.hhJobs = devAlloc<ContactJob>((size_t)W * P.candCapacity, stream);
     P.candContacts = devAlloc<Contact>((size_t)W * P.candCapacity, stream);
@@ -432,7 +431,6 @@ MW_PHYS_NODE(SubstepRigidBodiesNode,
 // the per-survivor manifolds into the ordered contact list.
 MW_PHYS_NODE(NarrowphaseNode,
     hipLaunchKernelGGL(narrowFilterKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
-    hipLaunchKernelGGL(narrowScanKernel, dim3(1), dim3(1024), 0, stream, P);
     hipLaunchKernelGGL(narrowCompactKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
     hipLaunchKernelGGL(narrowSATKernel, dim3(P.satGrid), dim3(kNarrowBlock),
                        narrowphaseSharedBytes(P), stream, P);

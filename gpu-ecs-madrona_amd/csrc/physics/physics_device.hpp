@@ -142,7 +142,6 @@ __global__ void refitKernel(PhysArgs P);
 __global__ void findOverlapsKernel(PhysArgs P);
 __global__ void integrateKernel(PhysArgs P);
 __global__ void narrowFilterKernel(PhysArgs P);
-__global__ void narrowScanKernel(PhysArgs P);
 __global__ void narrowCompactKernel(PhysArgs P);
 __global__ void narrowSATKernel(PhysArgs P);
 __global__ void narrowContactKernel(PhysArgs P);

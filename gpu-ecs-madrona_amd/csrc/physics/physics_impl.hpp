@@ -133,7 +133,8 @@ struct PhysArgs {
     int32_t *satWorkCount;        // [1] entries in satWork this substep
     SatWork *satStage;            // [W][candCapacity] survivors per world (filter output)
     int32_t *hhCount, *planeCount;    // [W] hull-hull / hull-plane survivors
-    int32_t *hhOffset, *planeOffset;  // [W] world offsets in the flat lists
+    unsigned long long *groupCounts;  // [W/64] packed (hull-hull | hull-plane << 32)
+                                      // survivor sums per group of 64 worlds
     ContactJob *planeJobs;        // [W * candCapacity] flat hull-plane contact jobs
     ContactJob *hhJobs;           // [W * candCapacity] SAT verdict per satWork entry
     int32_t *jobCount;            // [1] hull-plane jobs this substep

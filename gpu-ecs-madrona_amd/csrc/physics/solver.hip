@@ -663,6 +663,22 @@ __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, S
     }
 }
 
+// Phase profile (experiments only, -DMW_SOLVER_PROFILE): per-phase sums of
+// block time in 10 ns device-clock ticks, read by mw_debug_solver_phases.
+#if defined(MW_SOLVER_PROFILE)
+static __device__ unsigned long long g_solverPhase[16];
+#define MW_SOLVER_MARK(i)                                                        \
+    do {                                                                         \
+        if (threadIdx.x == 0) {                                                  \
+            const long long t__ = wall_clock64();                                \
+            atomicAdd(&g_solverPhase[(i)], (unsigned long long)(t__ - prof_t));  \
+            prof_t = t__;                                                        \
+        }                                                                        \
+    } while (0)
+#else
+#define MW_SOLVER_MARK(i) ((void)0)
+#endif
+
 // Occupancy: latency bound (dependent LDS / column reads per contact), so
 // residency matters more than packed math; built without SLP vectorisation
 // (Makefile) it fits 3 waves per SIMD without spills.
@@ -688,6 +704,9 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     SolverLDS L = solverWorldLDS(smem, nb, wi);
     SolverBlockLDS BL = solverBlockLDS(smem, nb);
 
+#if defined(MW_SOLVER_PROFILE)
+    long long prof_t = wall_clock64();
+#endif
     if (threadIdx.x == 0) { BL.scalars[0] = 0; BL.scalars[1] = 0; BL.scalars[2] = 0; }
     int32_t K = 0, J = 0;
     if (live) {
@@ -699,6 +718,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     if (live && lane == 0) atomicMax(&BL.scalars[1], K + J);
     __syncthreads();
     const bool fits = BL.scalars[1] <= kSolverLDSContacts;
+    MW_SOLVER_MARK(0);
 
     if (!fits) {
         // some world of the block overflows the LDS records: every world
@@ -715,6 +735,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     if (live && lane == 0) atomicMax(&BL.scalars[2], my_levels);
     __syncthreads();
     const int32_t max_level = BL.scalars[2];
+    MW_SOLVER_MARK(1);
 
     // counting sort of the block's contacts by level
     for (int32_t i = threadIdx.x; i <= max_level + 1; i += kSolverThreads) {
@@ -744,6 +765,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
         }
     }
     __syncthreads();
+    MW_SOLVER_MARK(2);
 
     // solvePositions, level by level over the whole block
     for (int32_t l = 1; l <= max_level; l++) {
@@ -758,8 +780,10 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
         __syncthreads();
     }
 
+    MW_SOLVER_MARK(3);
     if (live) setWorldVelocities(P, w, L, P.solver[w].h, lane);
     __syncthreads();
+    MW_SOLVER_MARK(4);
 
     // solveVelocities, same schedule
     for (int32_t l = 1; l <= max_level; l++) {
@@ -779,8 +803,24 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
         __syncthreads();
     }
 
+    MW_SOLVER_MARK(5);
     if (live) writeWorldBodies(P, w, L, lane);
+    __syncthreads();
+    MW_SOLVER_MARK(6);
+#if defined(MW_SOLVER_PROFILE)
+    if (threadIdx.x == 0) atomicAdd(&g_solverPhase[7], 1ull);
+    if (threadIdx.x == 0) atomicAdd(&g_solverPhase[8], (unsigned long long)max_level);
+#endif
 }
+
+#if defined(MW_SOLVER_PROFILE)
+extern "C" int mw_debug_solver_phases(unsigned long long *out)
+{
+    unsigned long long z[16] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solverPhase), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_solverPhase), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t solverSharedBytes(const PhysArgs &P)
 {
