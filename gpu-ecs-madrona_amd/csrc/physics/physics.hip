@@ -425,17 +425,19 @@ MW_PHYS_NODE(SubstepRigidBodiesNode,
         hipLaunchKernelGGL(integrateKernel, rowGrid(P), dim3(256), 0, stream, P);)
 
 // Narrowphase = AABB recheck + survivor numbering (block per world), a
-// one-block scan and a per-world compaction into flat lists, a persistent
-// SAT kernel (16-lane group per hull-hull pair) and a persistent contact
-// kernel (lane per manifold); see narrowphase.hip.  The solver turns
+// per-world compaction into flat lists, a persistent SAT kernel (16-lane
+// group per hull-hull pair) and a persistent contact kernel (lane per
+// manifold); see narrowphase.hip.  The node's launch configuration (blocks
+// per CU) sizes the two persistent grids; by default they are exactly the
+// resident blocks.  The solver turns
 // the per-survivor manifolds into the ordered contact list.
 MW_PHYS_NODE(NarrowphaseNode,
     hipLaunchKernelGGL(narrowFilterKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
     hipLaunchKernelGGL(narrowCompactKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
-    hipLaunchKernelGGL(narrowSATKernel, dim3(P.satGrid), dim3(kNarrowBlock),
+    hipLaunchKernelGGL(narrowSATKernel, dim3(lc.persistentGrid(P.satGrid)), dim3(kNarrowBlock),
                        narrowphaseSharedBytes(P), stream, P);
-    hipLaunchKernelGGL(narrowContactKernel, dim3(P.contactGrid), dim3(kContactBlock),
-                       contactSharedBytes(P), stream, P);)
+    hipLaunchKernelGGL(narrowContactKernel, dim3(lc.persistentGrid(P.contactGrid)),
+                       dim3(kContactBlock), contactSharedBytes(P), stream, P);)
 
 MW_PHYS_NODE(SolverNode,
     hipLaunchKernelGGL(solverKernel, dim3((P.numWorlds + kSolverWorlds - 1) / kSolverWorlds),

@@ -5,6 +5,7 @@
 #include "../physics/physics_impl.hpp"
 
 #include <madrona/mw_gpu.hpp>
+#include <madrona/launch_config.hpp>
 #include <madrona/physics_assets.hpp>
 
 #include <hip/hip_runtime.h>
@@ -398,6 +399,54 @@ int32_t mw_phys_read_bvh(mw_exec *exec, int32_t world, void *nodes_out, float *l
 double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps)
 {
     MW_TRY({ return exec->exec->timeNode(node_name, num_steps); }, -1.0)
+}
+
+int32_t mw_num_nodes(mw_exec *exec)
+{
+    MW_TRY({ return exec->exec->numNodes(); }, -1)
+}
+
+const char *mw_node_name(mw_exec *exec, int32_t node)
+{
+    MW_TRY({ return exec->exec->nodeName(node); }, nullptr)
+}
+
+int32_t mw_node_blocks_per_cu(mw_exec *exec, int32_t node)
+{
+    MW_TRY({ return exec->exec->nodeBlocksPerCU(node); }, -1)
+}
+
+int mw_set_node_blocks_per_cu(mw_exec *exec, int32_t node, int32_t blocks_per_cu)
+{
+    MW_TRY({
+        exec->exec->setNodeBlocksPerCU(node, blocks_per_cu);
+        return 0;
+    }, -1)
+}
+
+int mw_parse_exec_config_override(const char *s, uint32_t *out)
+{
+    MW_TRY({
+        if (!s || !out) throw std::runtime_error("mw_parse_exec_config_override: null argument");
+        const madrona::ExecConfigOverride o = madrona::parseExecConfigOverride(s);
+        out[0] = o.numThreads;
+        out[1] = o.blocksPerCU;
+        out[2] = o.numCUs;
+        return 0;
+    }, -1)
+}
+
+int32_t mw_parse_exec_config_file(const char *json, int32_t *nodes, int32_t *blocks, int32_t cap)
+{
+    MW_TRY({
+        if (!json) throw std::runtime_error("mw_parse_exec_config_file: null argument");
+        const auto v = madrona::parseExecConfigFile(json);
+        for (int32_t i = 0; i < (int32_t)v.size() && i < cap; i++) {
+            if (nodes) nodes[i] = v[i].node;
+            if (blocks) blocks[i] = v[i].blocksPerCU;
+        }
+        return (int32_t)v.size();
+    }, -1)
 }
 
 int32_t mw_set_timed_node(mw_exec *exec, const char *node_name)

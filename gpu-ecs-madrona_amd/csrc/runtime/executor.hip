@@ -4,12 +4,16 @@
 // src/mw/cuda_exec.cpp:1519-1815 (run graph, getExported, export kernels).
 #include <madrona/mw_gpu.hpp>
 #include <madrona/tracing.hpp>
+#include <madrona/launch_config.hpp>
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <cstdio>
+#include <fstream>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -90,7 +94,7 @@ void launchWorldKernel(const void *kernel, LaunchCtx &lc)
 {
     StateView *st = lc.devState;
     void *args[] = { &st };
-    const uint32_t blocks = (uint32_t)((lc.numWorlds + 63) / 64);
+    const uint32_t blocks = lc.capGrid((uint32_t)((lc.numWorlds + 63) / 64));
     if (blocks == 0) return;
     MW_HIP_CHECK(hipLaunchKernel(kernel, dim3(blocks), dim3(64), args, 0,
                                  (hipStream_t)lc.stream));
@@ -103,7 +107,7 @@ void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype,
     const int64_t total = (int64_t)lc.numWorlds * cap;
     if (total == 0) return;
     dim3 block(256);
-    dim3 grid((unsigned)((total + 255) / 256));
+    dim3 grid(lc.capGrid((unsigned)((total + 255) / 256)));
     StateView *st = lc.devState;
     int32_t arch = archetype;
     void *kargs[] = { &st, &arch, const_cast<void *>(args) };
@@ -262,6 +266,13 @@ struct Executor::Impl {
     mwGPU::DeviceLog *traceLogs = nullptr;
     std::vector<std::string> traceFuncs;      // funcID -> node kind
     std::vector<uint32_t> nodeFunc;           // node -> funcID
+
+    // Launch configuration (reference MADRONA_MWGPU_EXEC_CONFIG_OVERRIDE /
+    // _FILE, src/mw/cuda_exec.cpp:1534-1560): blocks per CU per node, -1 =
+    // the default; numCUs = the CUs grids are sized for.
+    int32_t defaultBlocksPerCU = 0;
+    int32_t numCUs = 0;
+    std::vector<int32_t> nodeBlocksPerCU;
 };
 
 Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
@@ -395,6 +406,9 @@ static void traceMarker(Executor::Impl &I, mwGPU::DeviceEvent ev, uint32_t func,
 // A node's launches; with tracing on, bracketed by nodeStart / nodeFinish.
 static void launchNode(Executor::Impl &I, int32_t i, LaunchCtx &lc)
 {
+    const int32_t bpc = i < (int32_t)I.nodeBlocksPerCU.size() ? I.nodeBlocksPerCU[i] : -1;
+    lc.blocksPerCU = bpc >= 0 ? bpc : I.defaultBlocksPerCU;
+    lc.numCUs = I.numCUs;
     if (!I.trace) {
         I.graph.launchNode(i, lc);
         return;
@@ -466,9 +480,77 @@ static void captureGraph(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
     }
 }
 
+// The reference's launch-configuration environment (src/mw/cuda_exec.cpp:
+// 1534-1560): the override sets the default blocks per CU (and the CU
+// count), the file one value per node index; both are read when the step
+// graph is captured.  Node indices past the graph are an error here (the
+// reference silently grows its table).
+static void applyLaunchConfigEnv(Executor::Impl &I)
+{
+    int dev = 0, cus = 0;
+    MW_HIP_CHECK(hipGetDevice(&dev));
+    MW_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    I.numCUs = cus;
+    I.nodeBlocksPerCU.assign(I.graph.numNodes(), -1);
+    if (const char *ov = std::getenv("MADRONA_MWGPU_EXEC_CONFIG_OVERRIDE")) {
+        const ExecConfigOverride o = parseExecConfigOverride(ov);
+        I.defaultBlocksPerCU = (int32_t)o.blocksPerCU;
+        if (o.numCUs > 0) I.numCUs = (int32_t)o.numCUs;
+        std::fprintf(stderr, "Using %u %u %u as the default launch configuration\n",
+                     o.numThreads, o.blocksPerCU, (unsigned)I.numCUs);
+    }
+    if (const char *path = std::getenv("MADRONA_MWGPU_EXEC_CONFIG_FILE")) {
+        std::ifstream f(path);
+        if (!f) throw std::runtime_error(std::string("MADRONA_MWGPU_EXEC_CONFIG_FILE: cannot open ") + path);
+        std::stringstream ss;
+        ss << f.rdbuf();
+        for (const NodeBlocks &nb : parseExecConfigFile(ss.str())) {
+            if (nb.node >= I.graph.numNodes()) {
+                throw std::runtime_error("MADRONA_MWGPU_EXEC_CONFIG_FILE: node index past the graph");
+            }
+            I.nodeBlocksPerCU[nb.node] = nb.blocksPerCU;
+            std::fprintf(stderr, "Taskgraph node %d (%s): using %d blocks per CU\n", nb.node,
+                         I.graph.nodeName(nb.node), nb.blocksPerCU);
+        }
+    }
+}
+
+int32_t Executor::numNodes() const { return impl_->graph.numNodes(); }
+const char *Executor::nodeName(int32_t node) const
+{
+    if (node < 0 || node >= impl_->graph.numNodes()) return nullptr;
+    return impl_->graph.nodeName(node);
+}
+
+int32_t Executor::nodeBlocksPerCU(int32_t node) const
+{
+    if (node < 0) return impl_->defaultBlocksPerCU;
+    if (node >= impl_->graph.numNodes()) return -1;
+    const int32_t v = impl_->nodeBlocksPerCU[node];
+    return v >= 0 ? v : impl_->defaultBlocksPerCU;
+}
+
+void Executor::setNodeBlocksPerCU(int32_t node, int32_t blocks_per_cu)
+{
+    Impl &I = *impl_;
+    if (node >= I.graph.numNodes() || blocks_per_cu < -1 || (node < 0 && blocks_per_cu < 0)) {
+        throw std::runtime_error("setNodeBlocksPerCU: bad node index or block count");
+    }
+    sync();
+    if (node < 0) {
+        I.defaultBlocksPerCU = blocks_per_cu;
+    } else {
+        I.nodeBlocksPerCU[node] = blocks_per_cu;
+    }
+    const StateView &dv = I.mgr->deviceViewHost();
+    LaunchCtx lc { I.stream, I.mgr->deviceView(), &dv, I.cfg.numWorlds, this };
+    if (I.cfg.useGraph) captureGraph(I, lc, dv);
+}
+
 void Executor::setGraph(TaskGraph &&graph)
 {
     impl_->graph = std::move(graph);
+    applyLaunchConfigEnv(*impl_);
     const StateView &dv = impl_->mgr->deviceViewHost();
     LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
     if (impl_->cfg.useGraph) captureGraph(*impl_, lc, dv);
@@ -675,7 +757,7 @@ double Executor::timeNode(const char *name, int32_t num_steps)
                 MW_HIP_CHECK(hipEventCreate(&b));
                 MW_HIP_CHECK(hipEventRecord(a, impl_->stream));
             }
-            impl_->graph.launchNode(i, lc);
+            launchNode(*impl_, i, lc);
             if (match) {
                 MW_HIP_CHECK(hipEventRecord(b, impl_->stream));
                 evs.push_back({ a, b });

@@ -82,6 +82,16 @@ public:
     int64_t readTrace(void *dst, int64_t max_bytes, int64_t *dropped);
     const char *traceFuncName(int32_t func_id);
 
+    // Per-node launch configuration (reference MADRONA_MWGPU_EXEC_CONFIG_*,
+    // also read from the environment when the graph is set): blocks per CU
+    // for the node's grid-stride / persistent kernels, 0 = full grid;
+    // node -1 = the default of every node without its own value (-1 there:
+    // use the default).  Setting re-captures the step graph.
+    int32_t numNodes() const;
+    const char *nodeName(int32_t node) const;
+    int32_t nodeBlocksPerCU(int32_t node) const;
+    void setNodeBlocksPerCU(int32_t node, int32_t blocks_per_cu);
+
     struct Impl;
 private:
     std::unique_ptr<Impl> impl_;

@@ -47,6 +47,27 @@ struct LaunchCtx {
     const StateView *view;       // host copy of the device view
     int32_t numWorlds;
     Executor *exec;
+    // Per-node launch configuration (reference MegakernelConfig,
+    // src/mw/cuda_exec.cpp:216-222, 1460-1517): blocks per CU for the node's
+    // grid-stride / persistent kernels, 0 = the node's own full grid; numCUs
+    // = the CUs the grid is sized for.  Set by the executor for each node.
+    int32_t blocksPerCU = 0;
+    int32_t numCUs = 0;
+
+    // Grid for a grid-stride kernel that needs `blocks` blocks to cover its
+    // work in one pass: capped at numCUs x blocksPerCU when configured.
+    uint32_t capGrid(uint32_t blocks) const
+    {
+        if (blocksPerCU <= 0 || numCUs <= 0) return blocks;
+        const uint32_t cap = (uint32_t)numCUs * (uint32_t)blocksPerCU;
+        return blocks < cap ? blocks : cap;
+    }
+    // Grid for a persistent kernel whose default grid is `resident` blocks.
+    uint32_t persistentGrid(uint32_t resident) const
+    {
+        if (blocksPerCU <= 0 || numCUs <= 0) return resident;
+        return (uint32_t)numCUs * (uint32_t)blocksPerCU;
+    }
 };
 
 struct NodeBase {};
@@ -159,15 +180,20 @@ parallelForKernel(const StateView *__restrict__ st_in, int32_t arch,
     // column pointers loaded from it as global (no flat accesses).
     StateView *st = const_cast<StateView *>(st_in);
     const int32_t cap = st->arch[arch].capacity;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int32_t w = (int32_t)(t / cap);
-    const int32_t r = (int32_t)(t - (int64_t)w * cap);
-    if (w >= st->numWorlds || r >= st->arch[arch].numRows[w]) return;
-    using WorldT = typename WorldOf<ContextT>::type;
-    ContextT ctx((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
-                 WorkerInit { st, w, nullptr });
-    invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, r,
-                                            std::index_sequence_for<ComponentTs...> {});
+    const int64_t total = (int64_t)st->numWorlds * cap;
+    // grid-stride: one pass with the default grid, several when the node's
+    // launch configuration caps the grid (LaunchCtx::capGrid)
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t w = (int32_t)(t / cap);
+        const int32_t r = (int32_t)(t - (int64_t)w * cap);
+        if (r >= st->arch[arch].numRows[w]) continue;
+        using WorldT = typename WorldOf<ContextT>::type;
+        ContextT ctx((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
+                     WorkerInit { st, w, nullptr });
+        invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, r,
+                                                std::index_sequence_for<ComponentTs...> {});
+    }
 }
 #endif
 
@@ -227,12 +253,13 @@ __global__ void __launch_bounds__(64) perWorldKernel(const StateView *__restrict
 {
     MW_TRACE_BLOCK(0);
     StateView *st = const_cast<StateView *>(st_in);
-    const int32_t w = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (w >= st->numWorlds) return;
-    using WorldT = typename WorldOf<ContextT>::type;
-    ContextT ctx((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
-                 WorkerInit { st, w, nullptr });
-    Fn(ctx);
+    for (int32_t w = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); w < st->numWorlds;
+         w += (int32_t)(gridDim.x * blockDim.x)) {
+        using WorldT = typename WorldOf<ContextT>::type;
+        ContextT ctx((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
+                     WorkerInit { st, w, nullptr });
+        Fn(ctx);
+    }
 }
 #endif
 }

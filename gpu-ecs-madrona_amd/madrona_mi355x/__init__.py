@@ -134,6 +134,14 @@ _lib.mw_set_timed_node.restype = ctypes.c_int32
 _lib.mw_set_timed_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
 _lib.mw_timed_node_ms.restype = ctypes.c_double
 _lib.mw_timed_node_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+_lib.mw_num_nodes.argtypes = [ctypes.c_void_p]
+_lib.mw_node_name.restype = ctypes.c_char_p
+_lib.mw_node_name.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_node_blocks_per_cu.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_set_node_blocks_per_cu.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+_lib.mw_parse_exec_config_override.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+_lib.mw_parse_exec_config_file.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int32]
 
 # The symbols include/madrona_mw.h declares (checked by tests/test_capi_symbols.py).
 C_ABI_SYMBOLS = (
@@ -145,7 +153,29 @@ C_ABI_SYMBOLS = (
     "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
     "mw_device_free", "mw_gen_fvs_inits", "mw_stream_wait", "mw_load_hull",
     "mw_trace_enable", "mw_trace_read", "mw_trace_func_name", "mw_trace_block_records",
+    "mw_num_nodes", "mw_node_name", "mw_node_blocks_per_cu", "mw_set_node_blocks_per_cu",
+    "mw_parse_exec_config_override", "mw_parse_exec_config_file",
 )
+
+
+def parse_exec_config_override(s):
+    """MADRONA_MWGPU_EXEC_CONFIG_OVERRIDE "threads,blocksPerCU,numCUs" ->
+    (threads, blocks_per_cu, num_cus); MadronaError when malformed."""
+    out = np.zeros(3, np.uint32)
+    if _lib.mw_parse_exec_config_override(s.encode(), out.ctypes.data) != 0:
+        raise _err()
+    return tuple(int(v) for v in out)
+
+
+def parse_exec_config_file(text):
+    """MADRONA_MWGPU_EXEC_CONFIG_FILE contents -> [(node, blocks_per_cu)]."""
+    n = _lib.mw_parse_exec_config_file(text.encode(), None, None, 0)
+    if n < 0:
+        raise _err()
+    nodes = np.zeros(max(n, 1), np.int32)
+    blocks = np.zeros(max(n, 1), np.int32)
+    _lib.mw_parse_exec_config_file(text.encode(), nodes.ctypes.data, blocks.ctypes.data, n)
+    return [(int(a), int(b)) for a, b in zip(nodes[:n], blocks[:n])]
 
 
 def rccl_unique_id():
@@ -349,6 +379,21 @@ class Executor:
     def time_node(self, name, steps):
         """Eager timing of `steps` extra steps (advances the simulation)."""
         return _lib.mw_phys_time_node(self.h, name.encode(), steps)
+
+    def nodes(self):
+        """Node kinds of the sorted step graph, by node index."""
+        return [_lib.mw_node_name(self.h, i).decode() for i in range(_lib.mw_num_nodes(self.h))]
+
+    def node_blocks_per_cu(self, node=-1):
+        """Effective launch configuration (blocks per CU, 0 = full grid) of
+        `node`; node -1: the default."""
+        return _lib.mw_node_blocks_per_cu(self.h, node)
+
+    def set_node_blocks_per_cu(self, node, blocks_per_cu):
+        """Per-node launch configuration (node -1: the default; value -1 on a
+        node: back to the default).  Re-captures the step graph."""
+        if _lib.mw_set_node_blocks_per_cu(self.h, node, blocks_per_cu) != 0:
+            raise _err()
 
     def set_timed_node(self, name):
         """Bracket every launch of node kind `name` with HIP events inside the

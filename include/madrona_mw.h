@@ -166,6 +166,27 @@ double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps
 int32_t mw_set_timed_node(mw_exec *exec, const char *node_name);
 double mw_timed_node_ms(mw_exec *exec, int64_t *launches);
 
+/* ---- launch configuration (reference MADRONA_MWGPU_EXEC_CONFIG_OVERRIDE /
+ * MADRONA_MWGPU_EXEC_CONFIG_FILE, src/mw/cuda_exec.cpp:1401-1560) ---------
+ * Both environment variables are honoured when the step graph is built:
+ * the override "threads,blocksPerCU,numCUs" sets the default blocks per CU
+ * (threads: accepted, unused -- block sizes are per kernel here), the file
+ * is a JSON object {"<node index>": <blocks per CU>, ...}.  Blocks per CU
+ * caps the grid of a node's grid-stride kernels (ParallelForNode,
+ * PerWorldNode) and sizes its persistent kernels (NarrowphaseNode's SAT and
+ * contact kernels); 0 = the node's default grid.  Results do not depend on
+ * it.  mw_set_node_blocks_per_cu: node -1 sets the default, value -1 on a
+ * node reverts it to the default; re-captures the step graph.             */
+int32_t mw_num_nodes(mw_exec *exec);
+const char *mw_node_name(mw_exec *exec, int32_t node);
+int32_t mw_node_blocks_per_cu(mw_exec *exec, int32_t node);
+int mw_set_node_blocks_per_cu(mw_exec *exec, int32_t node, int32_t blocks_per_cu);
+/* host-only parsers of the two formats (no GPU needed): 0 / the number of
+ * entries on success, -1 on malformed input (mw_last_error says why).     */
+int mw_parse_exec_config_override(const char *s, uint32_t *threads_blocks_cus);
+int32_t mw_parse_exec_config_file(const char *json, int32_t *nodes, int32_t *blocks_per_cu,
+                                  int32_t cap);
+
 /* ---- device tracing (reference src/mw/device/include/madrona/mw_gpu/
  * tracing.hpp:14-128, MADRONA_TRACING + DeviceTracingManager::
  * transferLogToCPU, cuda_exec.cpp:1784) ----------------------------------
