@@ -49,6 +49,76 @@ struct Query {
     static Query resolve(const StateManager &mgr);
 };
 
+// ---------------------------------------------------------------------------
+// Job API (reference include/madrona/context.hpp:88-114, job.hpp:29-34,
+// query.hpp:60-105).  The reference snapshot's job system is dead code
+// (SURVEY.md Q2), but examples/collisions and examples/fantasy_vs are written
+// against it.  Here a job runs where it is submitted, on the lane that owns
+// the world: submit(fn) calls fn(ctx) and parallelFor(query, fn) walks the
+// world's matching rows in query order -- one valid schedule of the
+// reference's dependency graph, since every dependency names an earlier
+// submission.  A non-child job submitted from inside a job (the examples'
+// `submit(loop, false, currentJobID())` re-queue) is the next tick: it runs
+// at the next replay of the step graph, so it is dropped here.  The loop is
+// hosted by a PerWorldNode (csrc/envs/fvs_jobs.hip, collisions_jobs.hip).
+// ---------------------------------------------------------------------------
+struct JobID {
+    uint32_t gen;
+    int32_t id;
+    static constexpr JobID none() { return JobID { 0, -1 }; }
+};
+
+template <typename ComponentT>
+class ComponentRef {
+public:
+    MW_INLINE ComponentRef(ComponentT *col, const int32_t *num_rows) : col_(col), n_(num_rows) {}
+    MW_INLINE ComponentT &operator[](uint32_t row) const { return col_[row]; }
+    MW_INLINE ComponentT *data() const { return col_; }
+    MW_INLINE uint32_t size() const { return (uint32_t)*n_; }
+    MW_INLINE ComponentT *begin() const { return col_; }
+    MW_INLINE ComponentT *end() const { return col_ + size(); }
+private:
+    ComponentT *col_;
+    const int32_t *n_;      // live row count, as the reference reads tbl_->numRows()
+};
+
+template <typename ArchetypeT>
+class ArchetypeRef {
+public:
+    MW_INLINE ArchetypeRef(StateView *st, int32_t world)
+        : st_(st), arch_(st->findArchetype(typeKey<ArchetypeT>())), world_(world)
+    {}
+    template <typename ComponentT>
+    MW_INLINE ComponentRef<ComponentT> component() const
+    {
+        const int32_t col = st_->findColumn(arch_, typeKey<std::remove_const_t<ComponentT>>());
+        return ComponentRef<ComponentT>(
+            st_->column<std::remove_const_t<ComponentT>>(arch_, col, world_),
+            st_->arch[arch_].numRows + world_);
+    }
+    template <typename ComponentT>
+    MW_INLINE ComponentT &get(uint32_t idx) const { return component<ComponentT>()[idx]; }
+    MW_INLINE uint32_t size() const { return (uint32_t)st_->arch[arch_].numRows[world_]; }
+private:
+    StateView *st_;
+    int32_t arch_;
+    int32_t world_;
+};
+
+namespace detail {
+// The context type a job function takes first (Engine &ctx, ...).
+template <typename F>
+struct JobFnTraits : JobFnTraits<decltype(&std::remove_reference_t<F>::operator())> {};
+template <typename C, typename R, typename A0, typename... A>
+struct JobFnTraits<R (C::*)(A0, A...) const> {
+    using Ctx = std::remove_cv_t<std::remove_reference_t<A0>>;
+};
+template <typename C, typename R, typename A0, typename... A>
+struct JobFnTraits<R (C::*)(A0, A...)> {
+    using Ctx = std::remove_cv_t<std::remove_reference_t<A0>>;
+};
+}
+
 class Context {
 public:
     MW_INLINE Context(WorldBase *world_data, const WorkerInit &init)
@@ -92,6 +162,16 @@ public:
         return state_->arch[state_->findArchetype(typeKey<ArchetypeT>())].numRows[world_];
     }
 
+    // Job API (see above).
+    template <typename ArchetypeT>
+    MW_INLINE ArchetypeRef<ArchetypeT> archetype() { return ArchetypeRef<ArchetypeT>(state_, world_); }
+    template <typename Fn, typename... DepTs>
+    MW_INLINE JobID submit(Fn &&fn, bool is_child = true, DepTs &&...dependencies);
+    template <typename... ComponentTs, typename Fn, typename... DepTs>
+    MW_INLINE JobID parallelFor(const Query<ComponentTs...> &query, Fn &&fn, bool is_child = true,
+                                DepTs &&...dependencies);
+    MW_INLINE JobID currentJobID() const { return jobDepth_ > 0 ? JobID { 0, jobDepth_ } : JobID::none(); }
+
     MW_INLINE void *tmpAlloc(uint64_t) { return nullptr; }
     MW_INLINE void resetTmpAlloc() {}
 
@@ -110,6 +190,7 @@ protected:
     StateView *state_;
     int32_t world_;
     StateManager *mgr_;
+    int32_t jobDepth_ = 0;      // nesting of the job being run (0: none)
 };
 
 template <typename ContextT, typename DataT>
@@ -235,6 +316,36 @@ MW_INLINE void Context::forEachRows(int32_t arch, const int32_t *cols, int32_t n
     for (int32_t r = 0; r < n; r++) {
         fn(rowRef(std::get<Is>(ptrs), r)...);
     }
+}
+
+template <typename Fn, typename... DepTs>
+MW_INLINE JobID Context::submit(Fn &&fn, bool is_child, DepTs &&...)
+{
+    using CtxT = typename detail::JobFnTraits<Fn>::Ctx;
+    if (!is_child && jobDepth_ > 0) return JobID::none();    // the next tick's job
+    jobDepth_++;
+    fn(static_cast<CtxT &>(*this));
+    jobDepth_--;
+    return JobID { 0, jobDepth_ + 1 };
+}
+
+template <typename... ComponentTs, typename Fn, typename... DepTs>
+MW_INLINE JobID Context::parallelFor(const Query<ComponentTs...> &q, Fn &&fn, bool, DepTs &&...)
+{                                              // context.inl:172-289 (#if 0 in the snapshot)
+    using CtxT = typename detail::JobFnTraits<Fn>::Ctx;
+    jobDepth_++;
+    CtxT &ctx = static_cast<CtxT &>(*this);
+    for (int32_t a = 0; a < q.numArchetypes; a++) {
+        const int32_t arch = q.archetypes[a];
+        const int32_t n = state_->arch[arch].numRows[world_];   // rows at launch
+        [&]<size_t... Is>(std::index_sequence<Is...>) {
+            auto cols = std::make_tuple(
+                state_->column<std::remove_const_t<ComponentTs>>(arch, q.cols[a][Is], world_)...);
+            for (int32_t r = 0; r < n; r++) fn(ctx, rowRef(std::get<Is>(cols), r)...);
+        }(std::index_sequence_for<ComponentTs...> {});
+    }
+    jobDepth_--;
+    return JobID { 0, jobDepth_ + 1 };
 }
 
 template <typename... ComponentTs>

@@ -80,6 +80,15 @@ class CollisionsInit(ctypes.Structure):
     _fields_ = [("pos", ctypes.c_void_p), ("rot", ctypes.c_void_p)]
 
 
+class JobsCollisionsConfig(ctypes.Structure):
+    _fields_ = [("num_objects", ctypes.c_int32), ("max_candidates", ctypes.c_int32)]
+
+
+# collisions_jobs CubeObject row: Entity, Translation, Rotation (w, x, y, z), PhysicsAABB
+JC_ROW_DTYPE = np.dtype([("gen", np.uint32), ("id", np.int32), ("pos", np.float32, 3),
+                         ("rot", np.float32, 4), ("aabb", np.float32, 6)])
+
+
 _lib.mw_create.restype = ctypes.c_void_p
 _lib.mw_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(MwConfig), ctypes.c_void_p,
                            ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
@@ -573,7 +582,9 @@ class FvsSim(Executor):
     """The `fantasy_vs` environment: casters / archers, deaths destroy entities."""
     DRAGON, KNIGHT, TRACKER = 0, 1, 2
 
-    def __init__(self, num_worlds, inits, first_world=0, gpu_id=0, use_graph=True):
+    def __init__(self, num_worlds, inits, first_world=0, gpu_id=0, use_graph=True,
+                 env="fantasy_vs"):
+        # env "fantasy_vs_jobs": the same game written against the job API
         self._inits = {k: np.ascontiguousarray(v) for k, v in inits.items()}
         nd = self._inits["dragon_mana"].shape[1]
         nk = self._inits["knight_arrows"].shape[1]
@@ -587,7 +598,7 @@ class FvsSim(Executor):
             arr[w].knight_pos = base["knight_pos"] + w * nk * 12
             arr[w].knight_arrows = base["knight_arrows"] + w * nk * 4
             arr[w].world_index = first_world + w
-        super().__init__("fantasy_vs", num_worlds, self.cfg, arr, ctypes.sizeof(FvsInit),
+        super().__init__(env, num_worlds, self.cfg, arr, ctypes.sizeof(FvsInit),
                          gpu_id=gpu_id, default_capacity=64, use_graph=use_graph)
 
     def table(self, w, arch):
@@ -607,6 +618,41 @@ class FvsSim(Executor):
 
     def num_rows(self, w, arch):
         return len(self.read_column(arch, 0, w, np.uint64))
+
+
+class JobsCollisionsSim(Executor):
+    """`collisions_jobs`: examples/collisions' own job-API toy (brute-force
+    pairs, pass-through narrowphase, push-apart solver) on the Context job
+    API; pos [W, N, 3] / rot [W, N, 4] from gen_collisions_inits."""
+    CUBE, CANDIDATE, CONTACT = 0, 1, 2
+
+    def __init__(self, num_worlds, pos, rot, max_candidates=1024, gpu_id=0, use_graph=True):
+        self._pos = np.ascontiguousarray(pos, np.float32)
+        self._rot = np.ascontiguousarray(rot, np.float32)
+        n = self._pos.shape[1]
+        assert self._pos.shape[0] == num_worlds and self._rot.shape[:2] == (num_worlds, n)
+        self.num_objects = n
+        self.cfg = JobsCollisionsConfig(n, max_candidates)
+        arr = (CollisionsInit * num_worlds)()
+        for w in range(num_worlds):
+            arr[w].pos = self._pos.ctypes.data + w * n * 12
+            arr[w].rot = self._rot.ctypes.data + w * n * 16
+        super().__init__("collisions_jobs", num_worlds, self.cfg, arr, ctypes.sizeof(CollisionsInit),
+                         gpu_id=gpu_id, default_capacity=64, use_graph=use_graph)
+
+    def cubes(self, w):
+        """CubeObject rows of world w (JC_ROW_DTYPE), table order."""
+        ent = self.read_column(self.CUBE, 0, w, np.uint32).reshape(-1, 2)
+        n = len(ent)
+        out = np.zeros(n, JC_ROW_DTYPE)
+        if n == 0:
+            return out
+        out["gen"] = ent[:, 0]
+        out["id"] = ent[:, 1].view(np.int32)
+        out["pos"] = self.read_column(self.CUBE, 1, w, np.float32).reshape(n, 3)
+        out["rot"] = self.read_column(self.CUBE, 2, w, np.float32).reshape(n, 4)
+        out["aabb"] = self.read_column(self.CUBE, 3, w, np.float32).reshape(n, 6)
+        return out
 
 
 class SimpleSim(CollisionsSim):

@@ -166,6 +166,20 @@ double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps
 int32_t mw_set_timed_node(mw_exec *exec, const char *node_name);
 double mw_timed_node_ms(mw_exec *exec, int64_t *launches);
 
+/* ---- job-API environments -----------------------------
+ * The reference's examples written against its job API (ctx.submit /
+ * ctx.parallelFor / ctx.archetype / currentJobID), run through the Context
+ * job API: each world's jobs on the lane that owns it, in submission order.
+ * "fantasy_vs_jobs": examples/fantasy_vs/fvs.cpp (mw_fvs_config /
+ * mw_fvs_init, same game as "fantasy_vs").  "collisions_jobs":
+ * examples/collisions/collisions.cpp:88-227 (brute-force pairs, pass-through
+ * narrowphase, push-apart solver) with mw_collisions_init positions /
+ * rotations of num_objects cubes (mw_gen_collisions_inits).              */
+typedef struct mw_jobs_collisions_config {
+    int32_t num_objects;       /* 100 in the reference (collisions.cpp:73) */
+    int32_t max_candidates;    /* CollisionCandidate / Contact rows per world */
+} mw_jobs_collisions_config;
+
 /* ---- launch configuration (reference MADRONA_MWGPU_EXEC_CONFIG_OVERRIDE /
  * MADRONA_MWGPU_EXEC_CONFIG_FILE, src/mw/cuda_exec.cpp:1401-1560) ---------
  * Both environment variables are honoured when the step graph is built:

@@ -447,3 +447,47 @@ class ReferenceSimple(ReferencePhys):
         self._rot = np.ascontiguousarray(rot, np.float32)
         self.h = self.lib.ref_simple_create(self.num_worlds, ctypes.byref(cfg),
                                             _vp(self._pos), _vp(self._rot))
+
+
+# ---------------------------------------------------------------------------
+# collisions_jobs: examples/collisions' job-API toy (oracle/jobs_oracle.cpp)
+# ---------------------------------------------------------------------------
+JC_ROW_DTYPE = np.dtype([("gen", np.uint32), ("id", np.int32), ("pos", np.float32, 3),
+                         ("rot", np.float32, 4), ("aabb", np.float32, 6)])
+
+
+class OracleJobsCollisions:
+    def __init__(self, pos, rot, max_candidates=1024):
+        L = self.lib = load_orc()
+        L.orc_jc_create.restype = ctypes.c_void_p
+        L.orc_jc_create.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_jc_step.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        L.orc_jc_read.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+        L.orc_jc_last_counts.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                         ctypes.c_void_p]
+        L.orc_jc_destroy.argtypes = [ctypes.c_void_p]
+        self._pos = np.ascontiguousarray(pos, np.float32)
+        self._rot = np.ascontiguousarray(rot, np.float32)
+        self.num_worlds, self.n = self._pos.shape[:2]
+        self.h = L.orc_jc_create(self.num_worlds, self.n, max_candidates, _vp(self._pos),
+                                 _vp(self._rot))
+
+    def step(self, n=1):
+        self.lib.orc_jc_step(self.h, n)
+
+    def cubes(self, w):
+        out = np.zeros(self.n, JC_ROW_DTYPE)
+        k = self.lib.orc_jc_read(self.h, w, _vp(out), self.n)
+        return out[:k]
+
+    def last_counts(self, w):
+        """(candidates, contacts, overflowed) of world w's last tick."""
+        c = np.zeros(2, np.int32)
+        flag = self.lib.orc_jc_last_counts(self.h, w, c.ctypes.data, c.ctypes.data + 4)
+        return int(c[0]), int(c[1]), bool(flag)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.orc_jc_destroy(self.h)
+            self.h = None
