@@ -160,16 +160,9 @@ void *mw_get_exported(mw_exec *exec, int32_t slot, int64_t *num_rows)
 int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_bytes)
 {
     MW_TRY({
-        int64_t rows = 0;
-        void *src = exec->exec->getExported(slot, &rows);
-        if (!src) throw std::runtime_error("mw_copy_exported: no such export slot");
-        int32_t bytes_per_row = exec->exec->exportRowBytes(slot);
-        int64_t n = rows * bytes_per_row;
-        if (n > max_bytes) n = max_bytes;
         // dst may be device or host memory (unified addressing)
-        MW_HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDefault,
-                                 (hipStream_t)exec->exec->stream()));
-        exec->exec->sync();
+        const int64_t n = exec->exec->copyExported(slot, dst, max_bytes);
+        if (n < 0) throw std::runtime_error("mw_copy_exported: no such export slot");
         return n;
     }, (int64_t)-1)
 }

@@ -299,6 +299,7 @@ Executor::~Executor()
         (void)hipFree(impl_->trace);
         (void)hipFree(impl_->traceLogs);
     }
+    if (impl_->hostRowsTotal) (void)hipHostFree(impl_->hostRowsTotal);
     for (auto &e : impl_->exports) {
         (void)hipFree(e.buf);
         if (e.scanOwner) (void)hipFree(e.offsets);
@@ -697,20 +698,53 @@ double Executor::timedNodeMs(int64_t *launches)
     return impl_->timedMs;
 }
 
+// The packed row total is read on the executor stream (into pinned host
+// memory), so it is the total of the last enqueued step even after
+// runAsync(); a null-stream hipMemcpy would not wait for the non-blocking
+// executor stream.
+static int64_t *pinnedRowsTotal(Executor::Impl &I)
+{
+    if (!I.hostRowsTotal) MW_HIP_CHECK(hipHostMalloc(&I.hostRowsTotal, sizeof(int64_t)));
+    return I.hostRowsTotal;
+}
+
 void *Executor::getExported(int32_t slot, int64_t *num_rows)
 {
     for (ExportBuf &b : impl_->exports) {
         if (b.slot == slot) {
             if (num_rows) {
-                int64_t total = 0;
-                MW_HIP_CHECK(hipMemcpy(&total, b.offsets + impl_->cfg.numWorlds, sizeof(int64_t),
-                                       hipMemcpyDeviceToHost));
-                *num_rows = total;
+                int64_t *total = pinnedRowsTotal(*impl_);
+                MW_HIP_CHECK(hipMemcpyAsync(total, b.offsets + impl_->cfg.numWorlds, sizeof(int64_t),
+                                            hipMemcpyDeviceToHost, impl_->stream));
+                sync();
+                *num_rows = *total;
             }
             return b.buf;
         }
     }
     return nullptr;
+}
+
+// Stream-ordered copy of the packed rows into dst with one host sync: the
+// copy spans min(max_bytes, the export buffer) -- bytes of dst past the
+// returned count are unspecified -- and the row total travels with it.
+int64_t Executor::copyExported(int32_t slot, void *dst, int64_t max_bytes)
+{
+    for (ExportBuf &b : impl_->exports) {
+        if (b.slot != slot) continue;
+        const StateView &dv = impl_->mgr->deviceViewHost();
+        const int64_t buf_bytes = (int64_t)dv.numWorlds * dv.arch[b.archetype].capacity * b.bytes;
+        const int64_t span = std::min(std::max<int64_t>(max_bytes, 0), buf_bytes);
+        int64_t *total = pinnedRowsTotal(*impl_);
+        MW_HIP_CHECK(hipMemcpyAsync(total, b.offsets + impl_->cfg.numWorlds, sizeof(int64_t),
+                                    hipMemcpyDeviceToHost, impl_->stream));
+        if (span > 0) {
+            MW_HIP_CHECK(hipMemcpyAsync(dst, b.buf, (size_t)span, hipMemcpyDefault, impl_->stream));
+        }
+        sync();
+        return std::min(*total * (int64_t)b.bytes, span);
+    }
+    return -1;
 }
 
 int32_t Executor::exportRowBytes(int32_t slot)

@@ -54,6 +54,9 @@ public:
     // Packed export (reference getExported contract: rows of all worlds,
     // world-major).  Valid after run().
     void *getExported(int32_t slot, int64_t *num_rows = nullptr);
+    // Stream-ordered copy of export `slot` into dst (device or host), one
+    // sync; returns the bytes of packed rows copied (-1: no such slot).
+    int64_t copyExported(int32_t slot, void *dst, int64_t max_bytes);
     void copyOutExports();
     int32_t exportRowBytes(int32_t slot);
 

@@ -108,11 +108,14 @@ int mw_step_async(mw_exec *exec, int32_t num_steps);
 int mw_sync(mw_exec *exec);
 
 /* Device pointer of export slot `slot`: rows of all worlds packed
- * world-major (reference getExported).  *num_rows receives the row count. */
+ * world-major (reference getExported).  *num_rows receives the row count of
+ * the last enqueued step (waits for it).                                  */
 void *mw_get_exported(mw_exec *exec, int32_t slot, int64_t *num_rows);
 
-/* Copy up to max_bytes of export slot `slot` into device buffer `dst`
- * (ordered on the executor stream, then synchronised).  Returns bytes copied. */
+/* Copy up to max_bytes of export slot `slot` into buffer `dst` (device or
+ * host; ordered on the executor stream after every enqueued step, then one
+ * synchronisation).  Returns the bytes of packed rows copied; bytes of dst
+ * past that count (up to max_bytes) are unspecified.                      */
 int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_bytes);
 
 /* hipStream_t of the executor (device work ordering for callers). */

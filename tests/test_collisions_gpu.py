@@ -196,3 +196,26 @@ def test_episode_return_export_matches_oracle():
     got = sim.exported_array(2, np.float32)
     assert got.shape == (W,)
     assert got.tobytes() == ret.tobytes()
+
+
+def test_export_copy_is_ordered_after_async_steps():
+    # mw_copy_exported / mw_get_exported(&rows) read the packed rows and
+    # their total on the executor stream: right after step_async they see
+    # that step's export, with no host sync by the caller.
+    mw = _mw()
+    gcfg, _ = _cfg_pair()
+    pos, rot = gen_collisions_inits(64, 128, seed=6)
+    a = mw.CollisionsSim(64, pos, rot, gcfg)
+    b = mw.CollisionsSim(64, pos, rot, gcfg)
+    for _ in range(3):
+        a.step_async(1)
+        got = a.exported_array(2, np.float32)
+        b.step(1)
+        assert got.shape == (64,)
+        assert got.tobytes() == b.exported_array(2, np.float32).tobytes()
+    dst = np.full(64 * 2, -7.0, np.float32)
+    a.step_async(1)
+    n = a.copy_exported(2, dst.ctypes.data, dst.nbytes)
+    b.step(1)
+    assert n == 64 * 4
+    assert dst[:64].tobytes() == b.exported_array(2, np.float32).tobytes()
