@@ -67,8 +67,8 @@ def pmc_traffic(kernel_node):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--worlds", type=int, default=8192, help="worlds per GPU")
     p.add_argument("--settle", type=int, default=120,
                    help="untimed pre-roll steps so the timed window is the settled, "
@@ -76,8 +76,10 @@ def parse():
     p.add_argument("--cubes", type=int, default=128)
     p.add_argument("--substeps", type=int, default=4)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-worlds", type=int, default=256, help="worlds per CPU batch")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-worlds", type=int, default=0,
+                   help="worlds per CPU batch (0 = 16 per CPU thread, at least 256)")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="0 = every core this process may use (affinity, capped by the cgroup CPU quota)")
     p.add_argument("--cpu-steps", type=int, default=80, help="timed steps per CPU batch")
     p.add_argument("--cpu-target-s", type=float, default=10.0)
     p.add_argument("--cpu-max-batches", type=int, default=12)
@@ -119,6 +121,29 @@ def _cpu_child(args):
     print(json.dumps({"kind": kind, "seconds": dt, "env_steps": W * args.cpu_steps}))
 
 
+def usable_cores():
+    """Cores this process may run on: the affinity mask, capped by the cgroup
+    v2 CPU quota when one is set (a GPU box's share of a larger host)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args):
     """Reference CPU executor (oracle/_ref, built from the reference's own
     src/core + src/physics) on a bounded sample of the same workload and the
@@ -126,7 +151,9 @@ def cpu_baseline(args):
     consecutive world batches); falls back to the parity-pinned restatement
     (oracle/) when the reference build is absent."""
     import subprocess
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = args.cpu_threads if args.cpu_threads > 0 else usable_cores()
+    if args.cpu_worlds <= 0:
+        args.cpu_worlds = max(256, 16 * threads)
     total_s, total_steps, kind, batches = 0.0, 0, None, 0
     t_wall = time.perf_counter()
     while batches < args.cpu_max_batches and total_s < args.cpu_target_s:
@@ -149,12 +176,15 @@ def cpu_baseline(args):
         "value": round(total_steps / total_s, 1),
         "unit": "env-steps/s",
         "cores": threads,
+        "cpu_model": cpu_model(),
+        "host_cpus_visible": os.cpu_count(),
         "kind": kind,
         "sample": f"collisions {batches} batches x {args.cpu_worlds} worlds (worlds 0-"
                   f"{batches * args.cpu_worlds - 1}) x {args.cubes} cubes, S={args.substeps}; "
                   f"timed steps {args.settle + args.warmup + 1}-"
                   f"{args.settle + args.warmup + args.cpu_steps} (settled regime, GPU window starts "
-                  f"at the same step), {threads} host threads, {total_s:.2f} s timed / {wall:.1f} s wall",
+                  f"at the same step), {threads} host threads (one per usable core), "
+                  f"{total_s:.2f} s timed / {wall:.1f} s wall",
     }
 
 
@@ -210,17 +240,21 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    if args.settle:
-        sim.step(args.settle)
-
-    # Per-node breakdown (eager, untimed pre-roll): picks the dominant kernel,
-    # whose launches are then timed live inside the replayed graph.
+    # Per-node breakdown (eager, untimed, part of the settle pre-roll: each
+    # kind's 2 timed steps advance the simulation, so they count towards
+    # --settle and the timed window starts exactly at step settle+warmup+1):
+    # picks the dominant kernel, whose launches are then timed live inside
+    # the replayed graph.
     launches = {"SubstepRigidBodiesNode": args.substeps, "NarrowphaseNode": args.substeps,
                 "SolverNode": args.substeps, "FindOverlappingNode": 1,
                 "UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
                 "ParallelForNode": 1}
     node_table = {}
     dom = None
+    breakdown_steps = 0 if args.no_roofline else 2 * len(NODE_KINDS)
+    if args.settle < breakdown_steps:
+        raise SystemExit(f"--settle must be >= {breakdown_steps} (the per-node breakdown's steps)")
+    sim.step(args.settle - breakdown_steps)
     if not args.no_roofline:
         for name in NODE_KINDS:
             ms = sim.time_node(name, 2)

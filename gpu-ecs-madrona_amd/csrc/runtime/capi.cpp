@@ -261,6 +261,11 @@ int mw_allgather_exported(mw_exec *exec, int32_t slot, void *dst, int64_t bytes_
         if (!exec->comm) throw std::runtime_error("mw_allgather_exported: call mw_rccl_init first");
         void *src = exec->exec->getExported(slot, nullptr);
         if (!src) throw std::runtime_error("mw_allgather_exported: no such export slot");
+        const int64_t cap = exec->exec->exportBufferBytes(slot);
+        if (bytes_per_rank < 0 || bytes_per_rank > cap) {
+            throw std::runtime_error("mw_allgather_exported: bytes_per_rank exceeds the export buffer (" +
+                                     std::to_string(cap) + " bytes)");
+        }
         MW_NCCL_OK(rccl().allGather(src, dst, (size_t)bytes_per_rank, ncclChar, exec->comm,
                                  (hipStream_t)exec->exec->stream()));
         return 0;
@@ -287,6 +292,15 @@ int mw_device_free(mw_exec *exec, void *ptr)
 }
 
 int32_t mw_num_worlds(mw_exec *exec) { return exec->exec->numWorlds(); }
+
+int32_t mw_export_row_bytes(mw_exec *exec, int32_t slot)
+{
+    MW_TRY({
+        const int32_t b = exec->exec->exportRowBytes(slot);
+        if (b <= 0) throw std::runtime_error("mw_export_row_bytes: no such export slot");
+        return b;
+    }, -1)
+}
 
 int32_t mw_error_flags(mw_exec *exec)
 {

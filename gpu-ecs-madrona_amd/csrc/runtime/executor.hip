@@ -506,7 +506,7 @@ static void applyLaunchConfigEnv(Executor::Impl &I)
         std::stringstream ss;
         ss << f.rdbuf();
         for (const NodeBlocks &nb : parseExecConfigFile(ss.str())) {
-            if (nb.node >= I.graph.numNodes()) {
+            if (nb.node < 0 || nb.node >= I.graph.numNodes()) {
                 throw std::runtime_error("MADRONA_MWGPU_EXEC_CONFIG_FILE: node index past the graph");
             }
             I.nodeBlocksPerCU[nb.node] = nb.blocksPerCU;
@@ -534,7 +534,8 @@ int32_t Executor::nodeBlocksPerCU(int32_t node) const
 void Executor::setNodeBlocksPerCU(int32_t node, int32_t blocks_per_cu)
 {
     Impl &I = *impl_;
-    if (node >= I.graph.numNodes() || blocks_per_cu < -1 || (node < 0 && blocks_per_cu < 0)) {
+    if (node >= I.graph.numNodes() || node < -1 || blocks_per_cu < -1 ||
+        blocks_per_cu > kMaxBlocksPerCU || (node < 0 && blocks_per_cu < 0)) {
         throw std::runtime_error("setNodeBlocksPerCU: bad node index or block count");
     }
     sync();
@@ -755,6 +756,15 @@ int32_t Executor::exportRowBytes(int32_t slot)
     return 0;
 }
 
+int64_t Executor::exportBufferBytes(int32_t slot)
+{
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    for (ExportBuf &b : impl_->exports) {
+        if (b.slot == slot) return (int64_t)dv.numWorlds * dv.arch[b.archetype].capacity * b.bytes;
+    }
+    return -1;
+}
+
 void Executor::copyOutExports() { launchExports(*impl_, impl_->mgr->deviceViewHost()); }
 
 void *Executor::columnBase(int32_t archetype, int32_t column, int32_t *capacity, uint32_t *bytes)
@@ -814,12 +824,15 @@ double Executor::timeNode(const char *name, int32_t num_steps)
 void Executor::downloadState() { impl_->mgr->downloadFromDevice(impl_->stream); }
 const StateView &Executor::hostView() { return impl_->mgr->hostView(); }
 
+// Ordered on the executor stream behind every enqueued step (the stream is
+// non-blocking, so a null-stream copy could read flags from before them).
 int32_t Executor::errorFlags()
 {
     const StateView &dv = impl_->mgr->deviceViewHost();
     std::vector<int32_t> f(dv.numWorlds);
-    MW_HIP_CHECK(hipMemcpy(f.data(), dv.errorFlags, sizeof(int32_t) * dv.numWorlds,
-                           hipMemcpyDeviceToHost));
+    MW_HIP_CHECK(hipMemcpyAsync(f.data(), dv.errorFlags, sizeof(int32_t) * dv.numWorlds,
+                                hipMemcpyDeviceToHost, impl_->stream));
+    sync();
     int32_t r = 0;
     for (int32_t v : f) r |= v;
     return r;

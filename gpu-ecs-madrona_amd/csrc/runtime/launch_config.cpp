@@ -15,6 +15,7 @@
 
 #include <cctype>
 #include <charconv>
+#include <climits>
 #include <cstring>
 #include <stdexcept>
 
@@ -43,6 +44,10 @@ ExecConfigOverride parseExecConfigOverride(const char *s)
     if (!parseU32(s, c1, o.numThreads) || !parseU32(c1 + 1, c2, o.blocksPerCU) ||
         !parseU32(c2 + 1, s + std::strlen(s), o.numCUs)) {
         return err();
+    }
+    if (o.blocksPerCU > (uint32_t)kMaxBlocksPerCU || o.numCUs > (uint32_t)kMaxLaunchCUs) {
+        throw std::runtime_error("MADRONA_MWGPU_EXEC_CONFIG_OVERRIDE out of range "
+                                 "(blocksPerCU <= 64, numCUs <= 65536)");
     }
     return o;
 }
@@ -76,6 +81,7 @@ std::vector<NodeBlocks> parseExecConfigFile(const std::string &text)
             if (i >= n) err("unterminated key");
             uint32_t node = 0;
             if (!parseU32(text.data() + kb, text.data() + i, node)) err("key is not a node index");
+            if (node > (uint32_t)INT32_MAX) err("node index out of range");
             i++;
             skip();
             if (i >= n || text[i] != ':') err("expected ':'");
@@ -85,6 +91,7 @@ std::vector<NodeBlocks> parseExecConfigFile(const std::string &text)
             while (i < n && std::isdigit((unsigned char)text[i])) i++;
             uint32_t blocks = 0;
             if (!parseU32(text.data() + vb, text.data() + i, blocks)) err("value is not a block count");
+            if (blocks > (uint32_t)kMaxBlocksPerCU) err("block count out of range (at most 64 per CU)");
             out.push_back(NodeBlocks { (int32_t)node, (int32_t)blocks });
             skip();
             if (i < n && text[i] == ',') {

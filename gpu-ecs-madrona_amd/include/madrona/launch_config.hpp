@@ -8,6 +8,11 @@
 
 namespace madrona {
 
+// Bounds of every blocks-per-CU value (parsers, setNodeBlocksPerCU) and of
+// the CU count a grid is sized for: grids stay far below 2^31 blocks.
+inline constexpr int32_t kMaxBlocksPerCU = 64;
+inline constexpr int32_t kMaxLaunchCUs = 65536;
+
 struct ExecConfigOverride {
     uint32_t numThreads;     // accepted for format compatibility
     uint32_t blocksPerCU;    // default blocks per CU of every node

@@ -59,6 +59,7 @@ public:
     int64_t copyExported(int32_t slot, void *dst, int64_t max_bytes);
     void copyOutExports();
     int32_t exportRowBytes(int32_t slot);
+    int64_t exportBufferBytes(int32_t slot);  // capacity of the packed buffer
 
     // Raw column access (device pointer of a [world][capacity] slab).
     void *columnBase(int32_t archetype, int32_t column, int32_t *capacity, uint32_t *bytes);

@@ -56,17 +56,20 @@ struct LaunchCtx {
 
     // Grid for a grid-stride kernel that needs `blocks` blocks to cover its
     // work in one pass: capped at numCUs x blocksPerCU when configured.
+    // The product is formed in 64 bits and is at least one block (the
+    // parsers bound blocksPerCU and numCUs, launch_config.hpp).
     uint32_t capGrid(uint32_t blocks) const
     {
         if (blocksPerCU <= 0 || numCUs <= 0) return blocks;
-        const uint32_t cap = (uint32_t)numCUs * (uint32_t)blocksPerCU;
-        return blocks < cap ? blocks : cap;
+        const uint64_t cap = (uint64_t)numCUs * (uint64_t)blocksPerCU;
+        return (uint64_t)blocks < cap ? blocks : (uint32_t)(cap < 0x7fffffffu ? cap : 0x7fffffffu);
     }
     // Grid for a persistent kernel whose default grid is `resident` blocks.
     uint32_t persistentGrid(uint32_t resident) const
     {
-        if (blocksPerCU <= 0 || numCUs <= 0) return resident;
-        return (uint32_t)numCUs * (uint32_t)blocksPerCU;
+        if (blocksPerCU <= 0 || numCUs <= 0) return resident > 0 ? resident : 1;
+        const uint64_t g = (uint64_t)numCUs * (uint64_t)blocksPerCU;
+        return (uint32_t)(g < 0x7fffffffu ? g : 0x7fffffffu);
     }
 };
 

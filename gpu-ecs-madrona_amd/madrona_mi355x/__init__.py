@@ -103,6 +103,7 @@ _lib.mw_stream_wait.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 _lib.mw_destroy.argtypes = [ctypes.c_void_p]
 _lib.mw_last_error.restype = ctypes.c_char_p
 _lib.mw_num_worlds.argtypes = [ctypes.c_void_p]
+_lib.mw_export_row_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int32]
 _lib.mw_error_flags.argtypes = [ctypes.c_void_p]
 _lib.mw_num_archetypes.argtypes = [ctypes.c_void_p]
 _lib.mw_read_column.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -164,6 +165,7 @@ C_ABI_SYMBOLS = (
     "mw_trace_enable", "mw_trace_read", "mw_trace_func_name", "mw_trace_block_records",
     "mw_num_nodes", "mw_node_name", "mw_node_blocks_per_cu", "mw_set_node_blocks_per_cu",
     "mw_parse_exec_config_override", "mw_parse_exec_config_file",
+    "mw_export_row_bytes",
 )
 
 
@@ -338,7 +340,10 @@ class Executor:
         """Host copy of export `slot` (packed [world-major, row] rows)."""
         dtype = np.dtype(dtype)
         _, rows = self.exported(slot)
-        out = np.empty(max(rows, 1) * 256, np.uint8)       # >= rows * row bytes
+        row_bytes = _lib.mw_export_row_bytes(self.h, slot)
+        if row_bytes <= 0:
+            raise _err()
+        out = np.empty(max(rows, 1) * row_bytes, np.uint8)
         n = self.copy_exported(slot, out.ctypes.data, out.nbytes)
         return out[:n].view(dtype)
 

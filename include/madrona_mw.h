@@ -118,6 +118,9 @@ void *mw_get_exported(mw_exec *exec, int32_t slot, int64_t *num_rows);
  * past that count (up to max_bytes) are unspecified.                      */
 int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_bytes);
 
+/* Bytes of one packed row of export slot `slot` (-1: no such slot). */
+int32_t mw_export_row_bytes(mw_exec *exec, int32_t slot);
+
 /* hipStream_t of the executor (device work ordering for callers). */
 void *mw_stream(mw_exec *exec);
 
@@ -253,7 +256,9 @@ void mw_gen_fvs_inits(int32_t first_world, int32_t num_worlds, int32_t num_drago
  * 128 bytes (e.g. over the torch.distributed TCP store), every rank calls
  * mw_rccl_init.  mw_allgather_exported enqueues an all-gather of the slot's
  * packed export buffer on the executor stream (after the step that wrote
- * it): dst receives nranks * bytes_per_rank bytes in rank order.  Replaces
+ * it): dst receives nranks * bytes_per_rank bytes in rank order;
+ * bytes_per_rank may not exceed the slot's export buffer (num_worlds x rows
+ * per world x row bytes), else -1.  Replaces
  * the reference's host-side getExported gather for multi-GPU learners
  * (include/madrona/mw_gpu.hpp:71).                                         */
 #define MW_RCCL_ID_BYTES 128

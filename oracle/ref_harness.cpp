@@ -26,6 +26,9 @@
 #include <cstring>
 #include <new>
 #include <thread>
+
+#include <pthread.h>
+#include <sched.h>
 #include <vector>
 
 using namespace madrona;
@@ -488,9 +491,25 @@ MADRONA_EXPORT void ref_phys_step_mt(void *handle, int32_t num_steps,
 {
     auto *h = (RefPhys *)handle;
     int32_t W = (int32_t)h->worlds.size();
+    // One worker pinned per usable core, as ThreadPoolExecutor pins its
+    // workers (src/mw/cpu_exec.cpp:56-93): the t-th CPU of this process's
+    // affinity mask.
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    sched_getaffinity(0, sizeof(allowed), &allowed);
+    std::vector<int> cpus;
+    for (int c = 0; c < CPU_SETSIZE; c++) {
+        if (CPU_ISSET(c, &allowed)) cpus.push_back(c);
+    }
     std::vector<std::thread> pool;
     for (int32_t t = 0; t < num_threads; t++) {
-        pool.emplace_back([=]() {
+        pool.emplace_back([=, &cpus]() {
+            if (!cpus.empty()) {
+                cpu_set_t one;
+                CPU_ZERO(&one);
+                CPU_SET(cpus[t % cpus.size()], &one);
+                pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+            }
             for (int32_t w = t; w < W; w += num_threads) {
                 RefWorld *rw = h->worlds[w];
                 for (int32_t s = 0; s < num_steps; s++) {

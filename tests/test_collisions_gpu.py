@@ -137,21 +137,34 @@ def test_collisions_bit_exact_long_horizon_contacts():
 
 
 def test_collisions_full_size_sampled_worlds():
-    # BASELINE.json configs[2] size (8192 worlds); the oracle replays a sample
-    # of worlds (first, middle, last) from the same per-world seeds.
+    # BASELINE.json configs[2] size (8192 worlds) through bench.py's whole
+    # window (settle 120 + warmup 10 + 200 timed steps): the oracle replays a
+    # sample of worlds (first, middle, last) from the same per-world seeds;
+    # bodies, candidate pairs and contacts are compared at the start and the
+    # end of the timed window.
     mw = _mw()
     gcfg, ocfg = _cfg_pair(max_contacts=4096)
-    W, steps = 8192, 40
+    W = 8192
     pos, rot = mw.gen_collisions_inits(W, 128, seed=0)
     sim = mw.CollisionsSim(W, pos, rot, gcfg)
     sample = [0, 1, W // 2, W - 1]
     orc = OraclePhys(ocfg, np.ascontiguousarray(pos[sample]), np.ascontiguousarray(rot[sample]))
-    sim.step(steps)
-    orc.step(steps, 4)
-    assert sim.error_flags() == 0, mw.ERR_BITS
-    for i, w in enumerate(sample):
-        d = _diff(sim.bodies(w), orc.bodies(i))
-        assert d is None, f"world {w}: {d}"
+    done = 0
+    for checkpoint in (130, 330):
+        sim.step(checkpoint - done)
+        orc.step(checkpoint - done, 4)
+        done = checkpoint
+        assert sim.error_flags() == 0, mw.ERR_BITS
+        cands, contacts = sim.counts()
+        assert cands.mean() > 100 and contacts.mean() > 10, (cands.mean(), contacts.mean())
+        for i, w in enumerate(sample):
+            d = _diff(sim.bodies(w), orc.bodies(i))
+            assert d is None, f"step {checkpoint} world {w}: {d}"
+            assert sim.candidates(w).tobytes() == orc.candidates(i).tobytes(), (checkpoint, w)
+            ka, kb = sim.contacts(w), orc.contacts(i)
+            assert len(ka) == len(kb), (checkpoint, w)
+            for k in range(len(ka)):
+                assert _contacts_equal(ka[k], kb[k]), f"step {checkpoint} world {w}: contact {k}"
 
 
 def test_live_node_timing_does_not_perturb_state():

@@ -24,7 +24,8 @@ def test_override_format():
     import madrona_mi355x as mw
     assert mw.parse_exec_config_override("256,2,256") == (256, 2, 256)
     assert mw.parse_exec_config_override(" 64 , 0 ,0") == (64, 0, 0)
-    for bad in ("", "256", "256,2", "a,2,3", "1,2,3,4", "-1,2,3", "1,,3"):
+    for bad in ("", "256", "256,2", "a,2,3", "1,2,3,4", "-1,2,3", "1,,3",
+                "256,65,256", "256,4294967295,256", "256,2,70000"):
         with pytest.raises(mw.MadronaError):
             mw.parse_exec_config_override(bad)
 
@@ -35,7 +36,9 @@ def test_config_file_format():
     assert mw.parse_exec_config_file(json.dumps({"3": 4}, indent=2)) == [(3, 4)]
     assert mw.parse_exec_config_file(" { } ") == []
     for bad in ("", "[]", '{"a": 1}', '{"1": -2}', '{"1": 2,}', '{"1" 2}', '{"1": 2} x',
-                '{"1": 2.5}', '{1: 2}'):
+                '{"1": 2.5}', '{1: 2}',
+                # out of range: keys past INT32_MAX, block counts past 64 per CU
+                '{"4294967295": 1}', '{"2147483648": 1}', '{"0": 65}', '{"0": 4294967295}'):
         with pytest.raises(mw.MadronaError):
             mw.parse_exec_config_file(bad)
 

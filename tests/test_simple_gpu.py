@@ -74,15 +74,26 @@ def test_simple_taskgraph_matches_oracle_and_reference(nsub, seed):
     assert not all(live), "no world reached an undefined manifold: UB path not covered"
 
 
-def test_simple_taskgraph_full_size_runs_clean():
+def test_simple_taskgraph_full_size_sampled_worlds():
     # BASELINE.json configs[1] size (8192 worlds): no error flags, agents
-    # exported through getExported slot 0 (one row per world).
+    # exported through getExported slot 0 (one row per world), and sampled
+    # worlds (first, middle, last) bit-exact against the oracle replaying
+    # them from the same per-world seeds.
     mw = _mw()
-    gcfg, _ = _cfg_pair(num_cubes=100, max_contacts=4096)
-    W = 8192
+    gcfg, ocfg = _cfg_pair(num_cubes=100, max_contacts=4096)
+    W, STEPS = 8192, 60
     pos, rot = mw.gen_collisions_inits(W, 100, seed=0)
     sim = mw.SimpleSim(W, pos, rot, gcfg)
-    sim.step(30)
+    sample = [0, 1, W // 2, W - 1]
+    orc = ol.OracleSimple(ocfg, np.ascontiguousarray(pos[sample]), np.ascontiguousarray(rot[sample]))
+    sim.step(STEPS)
+    orc.step(STEPS, 4)
     assert sim.error_flags() == 0, mw.ERR_BITS
+    for i, w in enumerate(sample):
+        d = _diff(sim.bodies(w), orc.bodies(i))
+        assert d is None, f"world {w}: {d}"
     agents = sim.exported_array(0, np.float32).reshape(-1, 3)
     assert agents.shape == (W, 3) and np.all(np.isfinite(agents))
+    for i, w in enumerate(sample):
+        b = orc.bodies(i)
+        assert agents[w].tobytes() == b["pos"][-1].tobytes(), w
