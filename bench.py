@@ -80,7 +80,8 @@ def parse():
                    help="worlds per CPU batch (0 = 16 per CPU thread, at least 256)")
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="0 = every core this process may use (affinity, capped by the cgroup CPU quota)")
-    p.add_argument("--cpu-steps", type=int, default=80, help="timed steps per CPU batch")
+    p.add_argument("--cpu-steps", type=int, default=0,
+                   help="timed steps per CPU batch (0 = --steps: the GPU's timed window)")
     p.add_argument("--cpu-target-s", type=float, default=10.0)
     p.add_argument("--cpu-max-batches", type=int, default=12)
     p.add_argument("--cpu-port", action="store_true", help="time oracle/ instead of oracle/_ref")
@@ -154,6 +155,8 @@ def cpu_baseline(args):
     threads = args.cpu_threads if args.cpu_threads > 0 else usable_cores()
     if args.cpu_worlds <= 0:
         args.cpu_worlds = max(256, 16 * threads)
+    if args.cpu_steps <= 0:
+        args.cpu_steps = args.steps
     total_s, total_steps, kind, batches = 0.0, 0, None, 0
     t_wall = time.perf_counter()
     while batches < args.cpu_max_batches and total_s < args.cpu_target_s:
@@ -182,8 +185,10 @@ def cpu_baseline(args):
         "sample": f"collisions {batches} batches x {args.cpu_worlds} worlds (worlds 0-"
                   f"{batches * args.cpu_worlds - 1}) x {args.cubes} cubes, S={args.substeps}; "
                   f"timed steps {args.settle + args.warmup + 1}-"
-                  f"{args.settle + args.warmup + args.cpu_steps} (settled regime, GPU window starts "
-                  f"at the same step), {threads} host threads (one per usable core), "
+                  f"{args.settle + args.warmup + args.cpu_steps} ("
+                  + ("the GPU's timed window" if args.cpu_steps == args.steps
+                     else "starts where the GPU's timed window starts")
+                  + f"), {threads} host threads pinned one per usable core, "
                   f"{total_s:.2f} s timed / {wall:.1f} s wall",
     }
 

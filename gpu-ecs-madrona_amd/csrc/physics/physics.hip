@@ -468,9 +468,11 @@ void RigidBodyPhysicsSystem::registerTypes(ECSRegistry &registry)
     registry.registerComponent<CollisionEvent>();
     registry.registerArchetype<CollisionEventTemporary>();
     mgr.setTemporary(typeKey<CollisionEventTemporary>());
+    mgr.setModuleRows(typeKey<CollisionEventTemporary>());
     registry.registerComponent<CandidateCollision>();
     registry.registerArchetype<CandidateTemporary>();
     mgr.setTemporary(typeKey<CandidateTemporary>());
+    mgr.setModuleRows(typeKey<CandidateTemporary>());
     registry.registerComponent<JointConstraint>();
     registry.registerArchetype<ConstraintData>();
     registry.registerSingleton<SolverData>();

@@ -64,7 +64,16 @@ static std::map<std::string, EnvFactory> &envTable()
 
 EnvRegistration::EnvRegistration(const char *name, EnvFactory factory)
 {
-    envTable()[name] = factory;
+    // A name registered twice (two loaded objects defining one world) keeps
+    // the first factory; the C ABI reports the clash at load time.
+    envTable().emplace(name, factory);
+}
+
+static std::vector<std::string> envNames()
+{
+    std::vector<std::string> v;
+    for (auto &e : envTable()) v.push_back(e.first);
+    return v;
 }
 
 EnvFactory findEnv(const char *name)
@@ -125,9 +134,40 @@ mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
         ec.defaultCapacity = cfg->default_capacity > 0 ? cfg->default_capacity : 64;
         ec.numExportedBuffers = 0;
         ec.useGraph = cfg->use_graph;
+        ec.tmpAllocBytesPerWorld = cfg->tmp_alloc_bytes;
+        ec.maxDeferredPerWorld = cfg->max_deferred_destroys;
+        if (cfg->tmp_alloc_bytes < -1 || cfg->max_deferred_destroys < 0 ||
+            cfg->max_deferred_destroys > 65536) {
+            throw std::runtime_error("mw_create: tmp_alloc_bytes >= -1 and 0 <= max_deferred_destroys <= 65536");
+        }
         Executor *e = f(ec, user_cfg, user_cfg_bytes, inits, init_stride);
         return new mw_exec { e };
     }, nullptr)
+}
+
+int32_t mw_load_env(const char *so_path)
+{
+    MW_TRY({
+        if (!so_path) throw std::runtime_error("mw_load_env: null path");
+        const size_t before = envTable().size();
+        // RTLD_NOW: unresolved symbols fail here, not at the first step.
+        // The object's DT_NEEDED libmadrona_mw.so resolves to this loaded
+        // library by its soname, so the world registers into this table.
+        void *h = dlopen(so_path, RTLD_NOW | RTLD_LOCAL);
+        if (!h) throw std::runtime_error(std::string("mw_load_env: ") + dlerror());
+        return (int32_t)(envTable().size() - before);
+    }, -1)
+}
+
+int32_t mw_num_envs(void) { return (int32_t)envTable().size(); }
+
+const char *mw_env_name(int32_t i)
+{
+    static thread_local std::string name;
+    const std::vector<std::string> v = envNames();
+    if (i < 0 || i >= (int32_t)v.size()) return nullptr;
+    name = v[i];
+    return name.c_str();
 }
 
 int mw_step(mw_exec *exec, int32_t num_steps)
@@ -321,6 +361,18 @@ int32_t mw_column_info(mw_exec *exec, int32_t archetype, int32_t column, int32_t
     if (bytes) *bytes = (int32_t)b;
     if (capacity) *capacity = cap;
     return 0;
+}
+
+int32_t mw_entity_loc(mw_exec *exec, int32_t world, int32_t id, uint32_t gen, int32_t *archetype,
+                      int32_t *row)
+{
+    MW_TRY({
+        Loc l;
+        if (!exec->exec->entityLoc(world, Entity { gen, id }, &l)) return 1;
+        if (archetype) *archetype = (int32_t)l.archetype;
+        if (row) *row = l.row;
+        return 0;
+    }, -1)
 }
 
 int32_t mw_read_column(mw_exec *exec, int32_t archetype, int32_t column, int32_t world, void *out,

@@ -58,7 +58,11 @@ TaskGraph TaskGraph::Builder::build()
 {                                               // taskgraph.cpp:46-109
     TaskGraph g;
     const size_t n = staged_.size();
-    if (n == 0) return g;                       // the reference segfaults here
+    if (n == 0) {                               // the reference segfaults here
+        g.datas_ = datas_;
+        g.dataIsNodeBase_ = dataIsNodeBase_;
+        return g;
+    }
     std::vector<bool> queued(n, false);
     if (!staged_[0].deps.empty()) throw std::runtime_error("first node has dependencies");
     g.nodes_.push_back(Node { staged_[0].data, staged_[0].fn, staged_[0].name });
@@ -77,6 +81,8 @@ TaskGraph TaskGraph::Builder::build()
         g.nodes_.push_back(Node { staged_[cur].data, staged_[cur].fn, staged_[cur].name });
         remaining--;
     }
+    g.datas_ = datas_;
+    g.dataIsNodeBase_ = dataIsNodeBase_;
     return g;
 }
 
@@ -100,18 +106,278 @@ void launchWorldKernel(const void *kernel, LaunchCtx &lc)
                                  (hipStream_t)lc.stream));
 }
 
-void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype,
-                     const void *args, size_t)
+// Row-parallel kernels: numWorlds x ceil(capacity / items) invocations of
+// `threads` lanes each, 256-lane blocks (grid-stride past capGrid).
+void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype, int32_t query_arch,
+                     int32_t threads, int32_t items, const void *cols, size_t)
 {
     const int32_t cap = lc.view->arch[archetype].capacity;
-    const int64_t total = (int64_t)lc.numWorlds * cap;
-    if (total == 0) return;
+    const int64_t lanes = (int64_t)lc.numWorlds * ((cap + items - 1) / items) * threads;
+    if (lanes == 0) return;
     dim3 block(256);
-    dim3 grid(lc.capGrid((unsigned)((total + 255) / 256)));
+    const int64_t blocks = std::min<int64_t>((lanes + 255) / 256, 0x7fffffff);
+    dim3 grid(lc.capGrid((uint32_t)blocks));
     StateView *st = lc.devState;
-    int32_t arch = archetype;
-    void *kargs[] = { &st, &arch, const_cast<void *>(args) };
+    int32_t arch = archetype, qa = query_arch;
+    void *kargs[] = { &st, &arch, &qa, const_cast<void *>(cols) };
     MW_HIP_CHECK(hipLaunchKernel(kernel, grid, block, kargs, 0, (hipStream_t)lc.stream));
+}
+
+// addNodeFn nodes: a fixed count per world sizes the grid; a dynamic count
+// is only known on the device, so its grid is persistent (grid-stride).
+void launchNodeFnKernel(const void *kernel, LaunchCtx &lc, void *node_dev, uint32_t fixed_count,
+                        uint32_t threads)
+{
+    uint32_t blocks;
+    if (fixed_count == 0xFFFF'FFFFu) {
+        blocks = 1;
+    } else if (fixed_count > 0) {
+        const int64_t lanes = (int64_t)lc.numWorlds * fixed_count * threads;
+        blocks = lc.capGrid((uint32_t)std::min<int64_t>((lanes + 255) / 256, 0x7fffffff));
+    } else {
+        blocks = lc.persistentGrid((uint32_t)std::max(1, lc.numCUs) * 4);
+    }
+    if (blocks == 0) return;
+    void *kargs[] = { &node_dev, &fixed_count, &threads };
+    MW_HIP_CHECK(hipLaunchKernel(kernel, dim3(blocks), dim3(256), kargs, 0,
+                                 (hipStream_t)lc.stream));
+}
+
+}
+
+// ---------------------------------------------------------------------------
+// Ordered structural commit of a row-parallel node (Context, row-parallel
+// mode).  One block per world with work (others exit on two loads):
+//   1. the world's deferred destroys are sorted by append key (LDS bitonic
+//      sort) and their targets looked up (before anything moves);
+//   2. per touched archetype: the rows appended past the (unchanged) row
+//      count are sorted by key; one lane replays appends and
+//      swap-removes in key order on row INDICES only (slot[final position]
+//      = source row, where[source row] = position: O(1) per event in LDS),
+//      which is the reference's serial order (state.inl:398-472,
+//      src/core/state.cpp:181-202); then all lanes move the rows that
+//      changed position, column by column through a per-block scratch
+//      (wave-parallel compaction: coalesced copies), remap moved entities
+//      and clear the keys;
+//   3. one lane releases the destroyed IDs in key order (IDMap::releaseID).
+// ---------------------------------------------------------------------------
+struct CommitArgs {
+    StateView *st;
+    char *scratch;                 // [gridDim.x][scratchPerBlock]
+    uint64_t scratchPerBlock;
+    int32_t capMax;                // rows per world the LDS index arrays hold
+    int32_t sortA;                 // pow2 >= capMax
+    int32_t sortO;                 // pow2 >= deferCap
+};
+
+static constexpr uint64_t kAppliedOp = 0xFFFF'FFFE'FFFF'FFFFull;
+
+__device__ static inline void bitonicSortLDS(uint64_t *keys, int32_t n)
+{
+    for (int32_t k = 2; k <= n; k <<= 1) {
+        for (int32_t j = k >> 1; j > 0; j >>= 1) {
+            for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                const int32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = keys[i], b = keys[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) {
+                        keys[i] = b;
+                        keys[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ static inline int32_t pow2Ceil(int32_t n)
+{
+    int32_t p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+__global__ void __launch_bounds__(256) structuralCommitKernel(CommitArgs A)
+{
+    MW_TRACE_BLOCK(0);
+    extern __shared__ __align__(16) char commit_lds[];
+    int32_t *slot = (int32_t *)commit_lds;
+    int32_t *where = slot + A.capMax;
+    uint64_t *akeys = (uint64_t *)(where + A.capMax);
+    uint64_t *okeys = akeys + A.sortA;
+    __shared__ unsigned long long arch_mask;
+    __shared__ int32_t n_final;
+
+    StateView &st = *A.st;
+    char *scratch = A.scratch + (size_t)blockIdx.x * A.scratchPerBlock;
+    const int32_t tid = threadIdx.x;
+
+    for (int32_t w = blockIdx.x; w < st.numWorlds; w += gridDim.x) {
+        const uint64_t dirty = st.appendDirty[w];
+        int32_t nops = st.deferCount[w];
+        if (dirty == 0 && nops == 0) continue;
+        nops = min(nops, st.deferCap);
+        DeferredDestroy *log = st.deferLog + (size_t)w * st.deferCap;
+        IDMapView ids = st.ids(w);
+
+        // 1. deferred destroys: sort by key, resolve targets
+        const int32_t so = pow2Ceil(max(nops, 1));
+        for (int32_t i = tid; i < so; i += blockDim.x) {
+            okeys[i] = i < nops ? ((log[i].key & ~0xFFFFull) | (uint64_t)i) : ~0ull;
+        }
+        if (tid == 0) arch_mask = dirty;
+        __syncthreads();
+        bitonicSortLDS(okeys, so);
+        for (int32_t i = tid; i < nops; i += blockDim.x) {
+            const Loc l = ids.lookup(log[i].e);
+            log[i].key = l.valid() ? (((uint64_t)l.archetype << 32) | (uint32_t)l.row) : ~0ull;
+            if (l.valid()) atomicOr(&arch_mask, 1ull << l.archetype);
+        }
+        __syncthreads();
+        const uint64_t mask = arch_mask;
+
+        // 2. per archetype, in index order
+        for (int32_t a = 0; a < st.numArchetypes; a++) {
+            if (!(mask & (1ull << a))) continue;
+            ArchetypeView &av = st.arch[a];
+            const int32_t cap = av.capacity;
+            if (cap > A.capMax) {
+                if (tid == 0) atomicOr(st.errorFlags + w, kErrFlagCommitLimit);
+                __syncthreads();
+                continue;
+            }
+            uint64_t *keys = av.appendKeys ? av.appendKeys + (size_t)w * cap : nullptr;
+            // rows appended by the node: [numRows, numRows + pending), the
+            // ones past the capacity were refused (kErrTableFull)
+            const int32_t n0 = min(av.numRows[w], cap);
+            const int32_t m = keys ? min(av.pendingRows[w], cap - n0) : 0;
+            const int32_t n_end = n0 + m;
+            const int32_t sa = pow2Ceil(max(m, 1));
+            for (int32_t j = tid; j < sa; j += blockDim.x) {
+                akeys[j] = j < m ? ((keys[n0 + j] & ~0xFFFFull) | (uint64_t)j) : ~0ull;
+            }
+            for (int32_t p = tid; p < n_end; p += blockDim.x) {
+                slot[p] = p < n0 ? p : -1;
+                where[p] = p < n0 ? p : -1;
+            }
+            __syncthreads();
+            bitonicSortLDS(akeys, sa);
+
+            const bool temporary = (av.flags & kArchTemporary) != 0;
+            const Entity *ecol = (const Entity *)(av.cols[0] + (size_t)w * cap * sizeof(Entity));
+            if (tid == 0) {
+                int32_t n = n0, ia = 0, io = 0;
+                for (;;) {
+                    while (io < so && okeys[io] != ~0ull &&
+                           (log[okeys[io] & 0xFFFF].key == ~0ull ||
+                            (int32_t)(log[okeys[io] & 0xFFFF].key >> 32) != a)) {
+                        io++;
+                    }
+                    const uint64_t ka = ia < m ? akeys[ia] : ~0ull;
+                    const uint64_t ko = io < so ? okeys[io] : ~0ull;
+                    if (ka == ~0ull && ko == ~0ull) break;
+                    if (ka < ko) {
+                        const int32_t r = n0 + (int32_t)(ka & 0xFFFF);
+                        ia++;
+                        if (!temporary && ecol[r].id < 0) continue;   // ID store was full
+                        slot[n] = r;
+                        where[r] = n;
+                        n++;
+                    } else {
+                        const int32_t i = (int32_t)(ko & 0xFFFF);
+                        const int32_t r = (int32_t)(uint32_t)log[i].key;
+                        io++;
+                        if (r < 0 || r >= n_end || where[r] < 0) continue;
+                        const int32_t p = where[r];
+                        const int32_t q = slot[n - 1];
+                        slot[p] = q;
+                        where[q] = p;
+                        where[r] = -1;
+                        n--;
+                        log[i].key = kAppliedOp;
+                    }
+                }
+                n_final = n;
+            }
+            __syncthreads();
+            const int32_t nf = n_final;
+
+            // move rows that changed position, column by column
+            for (int32_t c = 0; c < av.numColumns; c++) {
+                const uint32_t nb = av.colBytes[c];
+                char *base = av.cols[c] + (size_t)w * cap * nb;
+                if (nb % 4 == 0) {
+                    const uint32_t words = nb / 4;
+                    const int64_t total = (int64_t)nf * words;
+                    for (int64_t t = tid; t < total; t += blockDim.x) {
+                        const int32_t p = (int32_t)(t / words), k = (int32_t)(t - (int64_t)p * words);
+                        const int32_t src = slot[p];
+                        if (src != p) ((uint32_t *)scratch)[t] = ((const uint32_t *)(base + (size_t)src * nb))[k];
+                    }
+                    __syncthreads();
+                    for (int64_t t = tid; t < total; t += blockDim.x) {
+                        const int32_t p = (int32_t)(t / words), k = (int32_t)(t - (int64_t)p * words);
+                        if (slot[p] != p) ((uint32_t *)(base + (size_t)p * nb))[k] = ((const uint32_t *)scratch)[t];
+                    }
+                } else {
+                    const int64_t total = (int64_t)nf * nb;
+                    for (int64_t t = tid; t < total; t += blockDim.x) {
+                        const int32_t p = (int32_t)(t / nb), k = (int32_t)(t - (int64_t)p * nb);
+                        const int32_t src = slot[p];
+                        if (src != p) scratch[t] = base[(size_t)src * nb + k];
+                    }
+                    __syncthreads();
+                    for (int64_t t = tid; t < total; t += blockDim.x) {
+                        const int32_t p = (int32_t)(t / nb), k = (int32_t)(t - (int64_t)p * nb);
+                        if (slot[p] != p) base[(size_t)p * nb + k] = scratch[t];
+                    }
+                }
+                __syncthreads();
+            }
+            // remap moved / appended entities, settle the keys and the count
+            if (!temporary) {
+                for (int32_t p = tid; p < nf; p += blockDim.x) {
+                    if (slot[p] != p || p >= n0) {
+                        const Entity e = ecol[p];
+                        ids.nodes[e.id].val = Loc { (uint32_t)a, p };
+                    }
+                }
+            }
+            if (keys) {
+                for (int32_t r = n0 + tid; r < n_end; r += blockDim.x) keys[r] = kNoAppendKey;
+            }
+            if (tid == 0) {
+                av.numRows[w] = nf;
+                if (av.pendingRows) av.pendingRows[w] = 0;
+            }
+            __syncthreads();
+        }
+
+        // 3. ID releases of the applied destroys, in key order
+        if (tid == 0) {
+            for (int32_t s = 0; s < nops; s++) {
+                const int32_t i = (int32_t)(okeys[s] & 0xFFFF);
+                if (log[i].key == kAppliedOp) ids.release(ids.st->worldCache, log[i].e.id);
+            }
+            st.appendDirty[w] = 0;
+            st.deferCount[w] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+namespace detail {
+
+void launchStructuralCommit(LaunchCtx &lc)
+{
+    const CommitArgs *A = lc.exec ? (const CommitArgs *)lc.exec->commitArgs() : nullptr;
+    if (!A || A->capMax <= 0) return;
+    const uint32_t blocks = (uint32_t)std::min<int64_t>(lc.numWorlds, 512);
+    const size_t lds = (size_t)A->capMax * 8 + (size_t)(A->sortA + A->sortO) * 8;
+    hipLaunchKernelGGL(structuralCommitKernel, dim3(blocks), dim3(256), lds,
+                       (hipStream_t)lc.stream, *A);
 }
 
 }
@@ -128,6 +394,13 @@ void launchClearRows(LaunchCtx &lc, int32_t archetype)
     int32_t *rows = lc.view->arch[archetype].numRows;
     hipLaunchKernelGGL(clearRowsKernel, dim3((lc.numWorlds + 255) / 256), dim3(256), 0,
                        (hipStream_t)lc.stream, rows, lc.numWorlds);
+}
+
+void launchResetTmpAlloc(LaunchCtx &lc)
+{
+    if (!lc.view->tmpOffset) return;
+    MW_HIP_CHECK(hipMemsetAsync(lc.view->tmpOffset, 0, sizeof(uint32_t) * lc.numWorlds,
+                                (hipStream_t)lc.stream));
 }
 
 // Packed export: world w's rows land at offset prefix(numRows)[w]
@@ -273,14 +546,32 @@ struct Executor::Impl {
     int32_t defaultBlocksPerCU = 0;
     int32_t numCUs = 0;
     std::vector<int32_t> nodeBlocksPerCU;
+
+    // Device copies of the graph's node data (TaskGraph::NodeData blocks).
+    char *nodeDataDev = nullptr;
+    // Ordered structural commit of row-parallel nodes.
+    CommitArgs commit {};
 };
+
+static LaunchCtx makeLaunchCtx(Executor::Impl &I, Executor *exec)
+{
+    const StateView &dv = I.mgr->deviceViewHost();
+    LaunchCtx lc { I.stream, I.mgr->deviceView(), &dv, I.cfg.numWorlds, exec };
+    lc.nodeData = I.nodeDataDev;
+    return lc;
+}
+
+const void *Executor::commitArgs() const { return &impl_->commit; }
 
 Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
 {
     impl_->cfg = cfg;
     MW_HIP_CHECK(hipSetDevice(cfg.gpuID));
     MW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
-    impl_->mgr.reset(new StateManager(StateManager::Config { cfg.numWorlds, cfg.defaultCapacity }));
+    impl_->mgr.reset(new StateManager(StateManager::Config {
+        cfg.numWorlds, cfg.defaultCapacity,
+        cfg.tmpAllocBytesPerWorld >= 0 ? cfg.tmpAllocBytesPerWorld : kDefaultTmpAllocBytes,
+        cfg.maxDeferredPerWorld > 0 ? cfg.maxDeferredPerWorld : kDefaultDeferredPerWorld }));
 }
 
 Executor::~Executor()
@@ -300,6 +591,8 @@ Executor::~Executor()
         (void)hipFree(impl_->traceLogs);
     }
     if (impl_->hostRowsTotal) (void)hipHostFree(impl_->hostRowsTotal);
+    if (impl_->nodeDataDev) (void)hipFree(impl_->nodeDataDev);
+    if (impl_->commit.scratch) (void)hipFree(impl_->commit.scratch);
     for (auto &e : impl_->exports) {
         (void)hipFree(e.buf);
         if (e.scanOwner) (void)hipFree(e.offsets);
@@ -333,6 +626,35 @@ char *Executor::hostWorldData(int32_t world)
 void Executor::uploadState()
 {
     impl_->mgr->uploadToDevice(impl_->stream);
+
+    // Ordered-commit sizing: the LDS index arrays hold the largest table
+    // that takes entity rows or row-parallel appends (at most 4096 rows per
+    // world; larger tables raise kErrFlagCommitLimit if a row-parallel node
+    // mutates them); one scratch slab per commit block holds a column of it.
+    {
+        const StateView &dv = impl_->mgr->deviceViewHost();
+        int32_t cap_max = 0;
+        uint32_t col_max = 4;
+        for (int32_t a = 0; a < dv.numArchetypes; a++) {
+            const ArchetypeView &av = dv.arch[a];
+            if (av.flags & kArchModuleRows) continue;
+            if (av.capacity > kCommitMaxRows) continue;
+            cap_max = std::max(cap_max, av.capacity);
+            for (int32_t c = 0; c < av.numColumns; c++) col_max = std::max(col_max, av.colBytes[c]);
+        }
+        CommitArgs &A = impl_->commit;
+        A.st = impl_->mgr->deviceView();
+        A.capMax = (cap_max + 63) / 64 * 64;
+        A.sortA = 1;
+        while (A.sortA < A.capMax) A.sortA <<= 1;
+        A.sortO = 1;
+        while (A.sortO < dv.deferCap) A.sortO <<= 1;
+        A.scratchPerBlock = ((uint64_t)A.capMax * col_max + 255) / 256 * 256;
+        const int64_t blocks = std::min<int64_t>(dv.numWorlds, 512);
+        if (A.capMax > 0) {
+            MW_HIP_CHECK(hipMalloc(&A.scratch, std::max<size_t>(A.scratchPerBlock * blocks, 256)));
+        }
+    }
 
     int32_t num_exports = 0;
     const StateManager::ExportDesc *ex = impl_->mgr->exports(&num_exports);
@@ -545,23 +867,41 @@ void Executor::setNodeBlocksPerCU(int32_t node, int32_t blocks_per_cu)
         I.nodeBlocksPerCU[node] = blocks_per_cu;
     }
     const StateView &dv = I.mgr->deviceViewHost();
-    LaunchCtx lc { I.stream, I.mgr->deviceView(), &dv, I.cfg.numWorlds, this };
+    LaunchCtx lc = makeLaunchCtx(I, this);
     if (I.cfg.useGraph) captureGraph(I, lc, dv);
 }
 
 void Executor::setGraph(TaskGraph &&graph)
 {
     impl_->graph = std::move(graph);
+    // Node data blocks to the device; NodeBase-derived blocks learn the
+    // device state first (NodeBase::makeContext).
+    {
+        const TaskGraph &g = impl_->graph;
+        const int32_t nd = g.numNodeDatas();
+        if (nd > 0) {
+            std::vector<TaskGraph::NodeData> blocks(g.nodeDatas(), g.nodeDatas() + nd);
+            for (int32_t i = 0; i < nd; i++) {
+                if (!g.nodeDataIsNodeBase(i)) continue;
+                NodeBase *nb = (NodeBase *)blocks[i].userData;
+                nb->mwState = impl_->mgr->deviceView();
+                nb->mwNumWorlds = impl_->cfg.numWorlds;
+            }
+            const size_t bytes = sizeof(TaskGraph::NodeData) * nd;
+            MW_HIP_CHECK(hipMalloc(&impl_->nodeDataDev, bytes));
+            MW_HIP_CHECK(hipMemcpy(impl_->nodeDataDev, blocks.data(), bytes, hipMemcpyHostToDevice));
+        }
+    }
     applyLaunchConfigEnv(*impl_);
     const StateView &dv = impl_->mgr->deviceViewHost();
-    LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
+    LaunchCtx lc = makeLaunchCtx(*impl_, this);
     if (impl_->cfg.useGraph) captureGraph(*impl_, lc, dv);
 }
 
 void Executor::runAsync()
 {
     const StateView &dv = impl_->mgr->deviceViewHost();
-    LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
+    LaunchCtx lc = makeLaunchCtx(*impl_, this);
     if (!impl_->segs.empty()) {
         size_t ev = 0;
         for (auto &sg : impl_->segs) {
@@ -623,7 +963,7 @@ void Executor::setTimedNode(const char *name)
         }
     }
     const StateView &dv = impl_->mgr->deviceViewHost();
-    LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
+    LaunchCtx lc = makeLaunchCtx(*impl_, this);
     if (impl_->cfg.useGraph) captureGraph(*impl_, lc, dv);
 }
 
@@ -665,7 +1005,7 @@ void Executor::enableTracing(int64_t max_records)
     }
     MW_HIP_CHECK(hipDeviceSynchronize());
     const StateView &dv = I.mgr->deviceViewHost();
-    LaunchCtx lc { I.stream, I.mgr->deviceView(), &dv, I.cfg.numWorlds, this };
+    LaunchCtx lc = makeLaunchCtx(I, this);
     if (I.cfg.useGraph) captureGraph(I, lc, dv);
 }
 
@@ -790,7 +1130,7 @@ int32_t Executor::numRows(int32_t archetype, int32_t world)
 double Executor::timeNode(const char *name, int32_t num_steps)
 {
     const StateView &dv = impl_->mgr->deviceViewHost();
-    LaunchCtx lc { impl_->stream, impl_->mgr->deviceView(), &dv, impl_->cfg.numWorlds, this };
+    LaunchCtx lc = makeLaunchCtx(*impl_, this);
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
     for (int32_t s = 0; s < num_steps; s++) {
         for (int32_t i = 0; i < impl_->graph.numNodes(); i++) {
@@ -819,6 +1159,22 @@ double Executor::timeNode(const char *name, int32_t num_steps)
         (void)hipEventDestroy(e.second);
     }
     return evs.empty() ? -1.0 : total / (double)evs.size();
+}
+
+bool Executor::entityLoc(int32_t world, Entity e, Loc *out)
+{
+    sync();
+    const StateView &dv = impl_->mgr->deviceViewHost();
+    if (world < 0 || world >= dv.numWorlds) return false;
+    IDMapState st {};
+    MW_HIP_CHECK(hipMemcpy(&st, dv.idState + world, sizeof(st), hipMemcpyDeviceToHost));
+    if (e.id < 0 || e.id >= st.numIDs) return false;
+    IDNode n {};
+    MW_HIP_CHECK(hipMemcpy(&n, dv.idNodes + (size_t)world * dv.idsPerWorld + e.id, sizeof(n),
+                           hipMemcpyDeviceToHost));
+    if (n.gen != e.gen) return false;
+    *out = n.val;
+    return true;
 }
 
 void Executor::downloadState() { impl_->mgr->downloadFromDevice(impl_->stream); }

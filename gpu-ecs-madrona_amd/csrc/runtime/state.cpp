@@ -35,6 +35,7 @@ struct ArchetypeInfo {
     std::vector<TypeDesc> cols;     // col 0 = Entity
     int32_t capacity;
     bool temporary;
+    bool moduleRows = false;
 };
 
 struct StateManager::Impl {
@@ -115,6 +116,13 @@ void StateManager::setTemporary(uint64_t key)
 {
     for (auto &a : impl_->archetypes) {
         if (a.key == key) a.temporary = true;
+    }
+}
+
+void StateManager::setModuleRows(uint64_t key)
+{
+    for (auto &a : impl_->archetypes) {
+        if (a.key == key) a.moduleRows = true;
     }
 }
 
@@ -204,7 +212,7 @@ void StateManager::finalizeLayout(uint32_t world_data_bytes, uint32_t world_data
         v.archKeys[a] = ai.key;
         av.numColumns = (int32_t)ai.cols.size();
         av.capacity = ai.capacity;
-        av.flags = ai.temporary ? 1u : 0u;
+        av.flags = (ai.temporary ? kArchTemporary : 0u) | (ai.moduleRows ? kArchModuleRows : 0u);
         av.numRows = (int32_t *)hostAlloc(I, sizeof(int32_t) * W);
         for (int32_t c = 0; c < av.numColumns; c++) {
             size_t bytes = (size_t)W * ai.capacity * ai.cols[c].numBytes;
@@ -234,6 +242,13 @@ void StateManager::finalizeLayout(uint32_t world_data_bytes, uint32_t world_data
     v.worldDataStride = (std::max<uint32_t>(world_data_bytes, 16) + align - 1) / align * align;
     v.worldData = hostAlloc(I, (size_t)v.worldDataStride * W);
     v.errorFlags = (int32_t *)hostAlloc(I, sizeof(int32_t) * W);
+    // Per-world tmpAlloc arena (also used by world constructors on the host).
+    v.tmpBytesPerWorld = (uint32_t)std::max(0, I.cfg.tmpAllocBytesPerWorld) / 256 * 256;
+    if (v.tmpBytesPerWorld > 0) {
+        v.tmpArena = hostAlloc(I, (size_t)v.tmpBytesPerWorld * W);
+        v.tmpOffset = (uint32_t *)hostAlloc(I, sizeof(uint32_t) * W);
+    }
+    v.deferCap = std::max(1, I.cfg.deferCap);
 
     // Singleton entities, per world in registration order, from the init
     // cache (state.inl:171-187).  Single-world semantics: each world's IDs
@@ -293,6 +308,35 @@ void StateManager::uploadToDevice(void *stream_ptr)
     copy(d.worldData, I.host.worldData, (size_t)d.worldDataStride * W);
     d.errorFlags = (int32_t *)devAlloc(sizeof(int32_t) * W);
     copy(d.errorFlags, I.host.errorFlags, sizeof(int32_t) * W);
+
+    // Row-parallel structural mutation (Context): append keys for every
+    // table a lane may append to (not singletons, not module-written rows,
+    // at most 4096 rows: the ordered commit's LDS index arrays), all keys
+    // settled (kNoAppendKey = all ones); the deferred destroy log.
+    for (int32_t a = 0; a < d.numArchetypes; a++) {
+        ArchetypeView &av = d.arch[a];
+        av.appendKeys = nullptr;
+        av.pendingRows = nullptr;
+        const bool singleton = std::find(I.singletons.begin(), I.singletons.end(),
+                                         I.archetypes[a].key) != I.singletons.end();
+        if (singleton || (av.flags & kArchModuleRows) || av.capacity > 4096) continue;
+        const size_t bytes = sizeof(uint64_t) * (size_t)W * av.capacity;
+        av.appendKeys = (uint64_t *)devAlloc(bytes);
+        MW_HIP_CHECK(hipMemsetAsync(av.appendKeys, 0xFF, bytes, stream));
+        av.pendingRows = (int32_t *)devAlloc(sizeof(int32_t) * W);
+        MW_HIP_CHECK(hipMemsetAsync(av.pendingRows, 0, sizeof(int32_t) * W, stream));
+    }
+    d.appendDirty = (uint64_t *)devAlloc(sizeof(uint64_t) * W);
+    MW_HIP_CHECK(hipMemsetAsync(d.appendDirty, 0, sizeof(uint64_t) * W, stream));
+    d.deferCount = (int32_t *)devAlloc(sizeof(int32_t) * W);
+    MW_HIP_CHECK(hipMemsetAsync(d.deferCount, 0, sizeof(int32_t) * W, stream));
+    d.deferLog = (DeferredDestroy *)devAlloc(sizeof(DeferredDestroy) * (size_t)W * d.deferCap);
+    if (d.tmpBytesPerWorld > 0) {
+        d.tmpArena = devAlloc((size_t)d.tmpBytesPerWorld * W);
+        copy(d.tmpArena, I.host.tmpArena, (size_t)d.tmpBytesPerWorld * W);
+        d.tmpOffset = (uint32_t *)devAlloc(sizeof(uint32_t) * W);
+        copy(d.tmpOffset, I.host.tmpOffset, sizeof(uint32_t) * W);
+    }
 
     MW_HIP_CHECK(hipMalloc(&I.devView, sizeof(StateView)));
     copy(I.devView, &d, sizeof(StateView));

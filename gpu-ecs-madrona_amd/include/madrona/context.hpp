@@ -4,10 +4,22 @@
 //     arena's host mirror (IDs are computed exactly as the reference's
 //     single-world executor would, SURVEY.md §8c entity-ID rule);
 //   * device, inside every kernel, one Context per (world, lane).
-// Structural mutation on the device (makeEntityNow / destroyEntityNow /
-// clear) is only legal from a node that owns the world serially (see
-// taskgraph.hpp SerialWorldNode); row-parallel nodes use makeTemporary's
-// ordered append instead.
+// Structural mutation has two modes on the device:
+//   * world-serial (one lane owns the world: PerWorldNode, one-off nodes,
+//     the host): makeEntityNow / destroyEntityNow / makeTemporary / clear act
+//     immediately, exactly as the reference's StateManager does;
+//   * row-parallel (ParallelForNode / CustomParallelForNode lanes, where the
+//     reference walks the world's rows serially, taskgraph.inl:63-71): a
+//     lane's makeTemporary / makeEntityNow appends its row atomically and
+//     tags it with an append key (the lane's row, then its call count); a
+//     destroyEntityNow is logged with its key.  After the node the executor's
+//     ordered commit (csrc/runtime/executor.hip) sorts each world's appended
+//     rows and deferred destroys by key and replays them in that order --
+//     rows land where the reference's serial walk puts them, swap-removes
+//     happen in its order, moved entities are remapped.  Entity IDs made by
+//     row-parallel lanes come from the world's ID store under a per-world
+//     lock, so they match the reference up to a relabelling (SURVEY.md §8c
+//     rule for in-step churn); clearArchetype is world-serial only.
 #pragma once
 
 #include <madrona/state.hpp>
@@ -57,16 +69,24 @@ struct Query {
 // the world: submit(fn) calls fn(ctx) and parallelFor(query, fn) walks the
 // world's matching rows in query order -- one valid schedule of the
 // reference's dependency graph, since every dependency names an earlier
-// submission.  A non-child job submitted from inside a job (the examples'
-// `submit(loop, false, currentJobID())` re-queue) is the next tick: it runs
-// at the next replay of the step graph, so it is dropped here.  The loop is
-// hosted by a PerWorldNode (csrc/envs/fvs_jobs.hip, collisions_jobs.hip).
+// submission.  A non-child job submitted from inside a job runs after the
+// outermost running job returns, except a job re-queueing itself while it
+// runs (the examples' `submit(loop, false, currentJobID())`): that is the
+// next tick, i.e. the next replay of the step graph.  The loop is hosted by
+// a PerWorldNode (csrc/envs/fvs_jobs.hip, collisions_jobs.hip).
 // ---------------------------------------------------------------------------
 struct JobID {
     uint32_t gen;
     int32_t id;
     static constexpr JobID none() { return JobID { 0, -1 }; }
 };
+
+// A non-child job submitted from inside a job runs after the outermost job
+// of the lane returns (the reference runs it once its parent finishes); its
+// closure is kept by value in the submitting context.
+inline constexpr int32_t kMaxDeferredJobs = 4;
+inline constexpr int32_t kDeferredJobBytes = 64;
+inline constexpr int32_t kMaxJobDepth = 8;
 
 template <typename ComponentT>
 class ComponentRef {
@@ -125,6 +145,11 @@ public:
         : data_(world_data), state_(init.state), world_(init.worldIdx), mgr_(init.mgr)
     {}
 
+    // Row-parallel mode (set by the row-parallel node kernels): the lane's
+    // position in the reference's serial walk, (query archetype << 24) | row.
+    MW_INLINE void setRowParallel(uint32_t row_key) { rowKey_ = row_key; seq_ = 0; }
+    MW_INLINE bool rowParallel() const { return rowKey_ != kSerialRowKey; }
+
     template <typename ArchetypeT, typename... Args>
     MW_INLINE Entity makeEntityNow(Args &&...args);
     MW_INLINE void destroyEntityNow(Entity e);
@@ -172,8 +197,8 @@ public:
                                 DepTs &&...dependencies);
     MW_INLINE JobID currentJobID() const { return jobDepth_ > 0 ? JobID { 0, jobDepth_ } : JobID::none(); }
 
-    MW_INLINE void *tmpAlloc(uint64_t) { return nullptr; }
-    MW_INLINE void resetTmpAlloc() {}
+    MW_INLINE void *tmpAlloc(uint64_t num_bytes);
+    MW_INLINE void resetTmpAlloc();
 
     MW_INLINE WorldID worldID() const { return WorldID { world_ }; }
     MW_INLINE WorldBase &data() { return rowRef(data_, 0); }
@@ -185,12 +210,32 @@ public:
 
 protected:
     MW_INLINE void clear(int32_t archetype, bool is_temporary);
+    MW_INLINE uint64_t nextAppendKey() { return ((uint64_t)rowKey_ << 32) | ((uint64_t)(seq_++ & 0xFFFFu) << 16); }
+    MW_INLINE Entity lockedAcquire(int32_t arch, int32_t row);
+    template <typename Fn> MW_INLINE void runJob(Fn &fn);
+    MW_INLINE void drainDeferredJobs();
+    MW_INLINE bool jobRunning(uint64_t key) const
+    {
+        for (int32_t i = 0; i < jobDepth_ && i < kMaxJobDepth; i++) {
+            if (jobKeys_[i] == key) return true;
+        }
+        return false;
+    }
 
     WorldBase *data_;
     StateView *state_;
     int32_t world_;
     StateManager *mgr_;
+    uint32_t rowKey_ = kSerialRowKey;
+    uint32_t seq_ = 0;
     int32_t jobDepth_ = 0;      // nesting of the job being run (0: none)
+    // Job API bookkeeping (only touched by job-API worlds).
+    uint64_t jobKeys_[kMaxJobDepth];
+    int32_t numDeferredJobs_ = 0;
+    struct DeferredJob {
+        void (*run)(Context &, void *);
+        alignas(16) char bytes[kDeferredJobBytes];
+    } deferredJobs_[kMaxDeferredJobs];
 };
 
 template <typename ContextT, typename DataT>
@@ -205,28 +250,84 @@ public:
 };
 
 // ---------------------------------------------------------------------------
+// Row-parallel makeEntityNow: the world's ID store is serial
+// (id_map_impl.inl:69-182), so lanes take it one at a time -- the lanes of a
+// wave in lane order (no two lanes of one wave contend for the lock), waves
+// through a per-world spin lock with agent-scope fences (a world's rows may
+// run on several XCDs).
+MW_INLINE Entity Context::lockedAcquire(int32_t arch, int32_t row)
+{
+    IDMapView ids = state_->ids(world_);
+#if defined(__HIP_DEVICE_COMPILE__)
+    Entity e = Entity::none();
+    const uint32_t lane = __lane_id();
+    uint64_t pending = __ballot(1);
+    while (pending) {
+        const uint32_t leader = (uint32_t)__builtin_ctzll(pending);
+        if (lane == leader) {
+            while (atomicCAS(&ids.st->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
+            __threadfence();
+            e = ids.acquire(ids.st->worldCache);
+            if (e.id >= 0) ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
+            __threadfence();
+            atomicExch(&ids.st->lock, 0);
+        }
+        pending &= pending - 1;
+    }
+    return e;
+#else
+    Entity e = ids.acquire(ids.st->worldCache);
+    if (e.id >= 0) ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
+    return e;
+#endif
+}
+
 template <typename ArchetypeT, typename... Args>
 MW_INLINE Entity Context::makeEntityNow(Args &&...args)
 {                                              // state.inl:398-449
     int32_t arch = state_->findArchetype(typeKey<ArchetypeT>());
+    auto construct_row = [&](int32_t row) {
+        int32_t col = 1;
+        auto construct = [&](auto &&arg) {
+            using T = std::remove_cv_t<std::remove_reference_t<decltype(arg)>>;
+            new (&rowRef(state_->column<T>(arch, col, world_), row)) T(std::forward<decltype(arg)>(arg));
+            col++;
+        };
+        (construct(std::forward<Args>(args)), ...);
+    };
+    if (rowParallel()) {
+        const int32_t row = state_->appendRowParallel(arch, world_, nextAppendKey());
+        if (row < 0) return Entity::none();
+        Entity e = lockedAcquire(arch, row);
+        // a row whose ID could not be acquired keeps Entity::none(); the
+        // commit drops it
+        rowRef(state_->column<Entity>(arch, 0, world_), row) = e;
+        if (e.id >= 0) construct_row(row);
+        return e;
+    }
     IDMapView ids = state_->ids(world_);
     Entity e = ids.acquire(ids.st->worldCache);
     int32_t row = state_->addRow(arch, world_);
     if (row < 0 || e.id < 0) return Entity::none();
     rowRef(state_->column<Entity>(arch, 0, world_), row) = e;
-    int32_t col = 1;
-    auto construct = [&](auto &&arg) {
-        using T = std::remove_cv_t<std::remove_reference_t<decltype(arg)>>;
-        new (&rowRef(state_->column<T>(arch, col, world_), row)) T(std::forward<decltype(arg)>(arg));
-        col++;
-    };
-    (construct(std::forward<Args>(args)), ...);
+    construct_row(row);
     ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
     return e;
 }
 
 MW_INLINE void Context::destroyEntityNow(Entity e)
 {                                              // src/core/state.cpp:181-202
+    if (rowParallel()) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const int32_t i = atomicAdd(state_->deferCount + world_, 1);
+        if (i >= state_->deferCap) {
+            atomicOr(state_->errorFlags + world_, kErrFlagDeferredFull);
+            return;
+        }
+        state_->deferLog[(size_t)world_ * state_->deferCap + i] = DeferredDestroy { nextAppendKey(), e };
+        return;
+#endif
+    }
     IDMapView ids = state_->ids(world_);
     Loc loc = ids.lookup(e);
     if (!loc.valid()) return;
@@ -242,18 +343,64 @@ template <typename ArchetypeT>
 MW_INLINE Loc Context::makeTemporary()
 {                                              // state.inl:451-463
     int32_t arch = state_->findArchetype(typeKey<ArchetypeT>());
-    int32_t row = state_->addRow(arch, world_);
+    int32_t row = rowParallel() ? state_->appendRowParallel(arch, world_, nextAppendKey())
+                                : state_->addRow(arch, world_);
+    if (row < 0) return Loc::none();
     return Loc { (uint32_t)arch, row };
 }
 
 MW_INLINE void Context::clear(int32_t arch, bool is_temporary)
 {                                              // src/core/state.cpp:565-581
+    if (rowParallel()) {
+        // a clear inside a row walk has no per-row order to keep: use a
+        // ClearTmpNode or a world-serial node
+        state_->errorFlags[world_] |= kErrFlagRowParallelOp;
+        return;
+    }
     if (!is_temporary) {
         IDMapView ids = state_->ids(world_);
         ids.bulkRelease(ids.st->worldCache, state_->column<Entity>(arch, 0, world_),
                         state_->arch[arch].numRows[world_]);
     }
     state_->arch[arch].numRows[world_] = 0;
+}
+
+// Per-world bump allocator (reference TmpAllocator::alloc,
+// src/core/state.cpp:95-114: 256-byte granules); row-parallel lanes bump
+// the world's offset atomically.  Exhaustion returns null and raises
+// kErrFlagTmpAllocFull (the reference chains another block).
+MW_INLINE void *Context::tmpAlloc(uint64_t num_bytes)
+{
+    const uint64_t bytes = (num_bytes + 255) & ~uint64_t(255);
+    if (bytes == 0) return nullptr;
+    if (bytes > state_->tmpBytesPerWorld || !state_->tmpArena) {
+        state_->errorFlags[world_] |= kErrFlagTmpAllocFull;
+        return nullptr;
+    }
+    uint32_t off;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (rowParallel()) {
+        off = atomicAdd(state_->tmpOffset + world_, (uint32_t)bytes);
+    } else
+#endif
+    {
+        off = state_->tmpOffset[world_];
+        if ((uint64_t)off + bytes <= state_->tmpBytesPerWorld) state_->tmpOffset[world_] = off + (uint32_t)bytes;
+    }
+    if ((uint64_t)off + bytes > state_->tmpBytesPerWorld) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        atomicOr(state_->errorFlags + world_, kErrFlagTmpAllocFull);
+#else
+        state_->errorFlags[world_] |= kErrFlagTmpAllocFull;
+#endif
+        return nullptr;
+    }
+    return state_->tmpArena + (size_t)world_ * state_->tmpBytesPerWorld + off;
+}
+
+MW_INLINE void Context::resetTmpAlloc()
+{                                              // src/core/state.cpp:116-127
+    if (state_->tmpOffset) state_->tmpOffset[world_] = 0;
 }
 
 template <typename ComponentT>
@@ -318,14 +465,56 @@ MW_INLINE void Context::forEachRows(int32_t arch, const int32_t *cols, int32_t n
     }
 }
 
-template <typename Fn, typename... DepTs>
-MW_INLINE JobID Context::submit(Fn &&fn, bool is_child, DepTs &&...)
+template <typename Fn>
+MW_INLINE void Context::runJob(Fn &fn)
 {
     using CtxT = typename detail::JobFnTraits<Fn>::Ctx;
-    if (!is_child && jobDepth_ > 0) return JobID::none();    // the next tick's job
+    if (jobDepth_ < kMaxJobDepth) jobKeys_[jobDepth_] = typeKey<Fn>();
     jobDepth_++;
     fn(static_cast<CtxT &>(*this));
     jobDepth_--;
+    if (jobDepth_ == 0) drainDeferredJobs();
+}
+
+MW_INLINE void Context::drainDeferredJobs()
+{
+    // FIFO; a drained job may defer more (it runs at depth 0, so those run
+    // when it returns)
+    for (int32_t i = 0; i < numDeferredJobs_; i++) {
+        DeferredJob job = deferredJobs_[i];
+        deferredJobs_[i].run = nullptr;
+        job.run(*this, job.bytes);
+    }
+    numDeferredJobs_ = 0;
+}
+
+template <typename Fn, typename... DepTs>
+MW_INLINE JobID Context::submit(Fn &&fn, bool is_child, DepTs &&...)
+{
+    using FnT = std::remove_cv_t<std::remove_reference_t<Fn>>;
+    if (!is_child && jobDepth_ > 0) {
+        // The examples' loop re-queues itself behind the running job
+        // (`submit(loop, false, currentJobID())`): that is the next tick,
+        // i.e. the next replay of the step graph.
+        if (jobRunning(typeKey<FnT>())) return JobID::none();
+        // Any other non-child job runs after the outermost job returns.
+        if constexpr (sizeof(FnT) <= kDeferredJobBytes && alignof(FnT) <= 16 &&
+                      std::is_trivially_copyable_v<FnT>) {
+            if (numDeferredJobs_ < kMaxDeferredJobs) {
+                DeferredJob &d = deferredJobs_[numDeferredJobs_++];
+                memcpy(d.bytes, &fn, sizeof(FnT));
+                d.run = [](Context &c, void *bytes) {
+                    alignas(FnT) char copy[sizeof(FnT)];
+                    memcpy(copy, bytes, sizeof(FnT));
+                    c.runJob(*reinterpret_cast<FnT *>(copy));
+                };
+                return JobID { 0, jobDepth_ + 1 };
+            }
+        }
+        state_->errorFlags[world_] |= kErrFlagJobDropped;
+        return JobID::none();
+    }
+    runJob(fn);
     return JobID { 0, jobDepth_ + 1 };
 }
 
@@ -333,6 +522,7 @@ template <typename... ComponentTs, typename Fn, typename... DepTs>
 MW_INLINE JobID Context::parallelFor(const Query<ComponentTs...> &q, Fn &&fn, bool, DepTs &&...)
 {                                              // context.inl:172-289 (#if 0 in the snapshot)
     using CtxT = typename detail::JobFnTraits<Fn>::Ctx;
+    if (jobDepth_ < kMaxJobDepth) jobKeys_[jobDepth_] = 0;
     jobDepth_++;
     CtxT &ctx = static_cast<CtxT &>(*this);
     for (int32_t a = 0; a < q.numArchetypes; a++) {
@@ -345,6 +535,7 @@ MW_INLINE JobID Context::parallelFor(const Query<ComponentTs...> &q, Fn &&fn, bo
         }(std::index_sequence_for<ComponentTs...> {});
     }
     jobDepth_--;
+    if (jobDepth_ == 0) drainDeferredJobs();
     return JobID { 0, jobDepth_ + 1 };
 }
 

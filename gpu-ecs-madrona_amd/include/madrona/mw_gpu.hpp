@@ -22,12 +22,18 @@
 
 namespace madrona {
 
+inline constexpr int32_t kDefaultTmpAllocBytes = 16 * 1024;    // Context::tmpAlloc per world
+inline constexpr int32_t kDefaultDeferredPerWorld = 256;        // deferred destroys per node per world
+inline constexpr int32_t kCommitMaxRows = 4096;                 // ordered-commit table limit
+
 struct ExecConfig {
     int32_t numWorlds;
     int32_t gpuID;
     int32_t defaultCapacity;        // rows per world per archetype
     int32_t numExportedBuffers;
     int32_t useGraph;               // capture the step into a hipGraph
+    int32_t tmpAllocBytesPerWorld = -1;   // -1: kDefaultTmpAllocBytes, 0: no arena
+    int32_t maxDeferredPerWorld = 0;      // 0: kDefaultDeferredPerWorld
 };
 
 // Non-template core (csrc/runtime/executor.cpp).
@@ -65,6 +71,8 @@ public:
     void *columnBase(int32_t archetype, int32_t column, int32_t *capacity, uint32_t *bytes);
     int32_t numRows(int32_t archetype, int32_t world);
     void downloadState();
+    // IDMap lookup of a live entity (false: not alive).
+    bool entityLoc(int32_t world, Entity e, Loc *out);
     const StateView &hostView();
     int32_t numWorlds() const;
     int32_t errorFlags();                     // OR of per-world error flags
@@ -91,6 +99,9 @@ public:
     // for the node's grid-stride / persistent kernels, 0 = full grid;
     // node -1 = the default of every node without its own value (-1 there:
     // use the default).  Setting re-captures the step graph.
+    // Device-side arguments of the ordered structural commit (executor.hip).
+    const void *commitArgs() const;
+
     int32_t numNodes() const;
     const char *nodeName(int32_t node) const;
     int32_t nodeBlocksPerCU(int32_t node) const;

@@ -80,6 +80,8 @@ struct IDMapState {
     int32_t numIDs;
     IDCache worldCache;
     IDCache initCache;
+    int32_t lock;         // row-parallel makeEntityNow (Context::lockedAcquire)
+    int32_t pad;
 };
 
 struct IDMapView {
@@ -227,13 +229,43 @@ struct IDMapView {
 };
 
 // ---------------------------------------------------------------------------
+// Per-world error bits raised by the engine (StateView::errorFlags; the
+// physics module's bits live in csrc/physics/physics_impl.hpp, bits 0..15).
+// ---------------------------------------------------------------------------
+inline constexpr int32_t kErrFlagJobDropped = 1 << 16;     // deferred job queue full / closure too big
+inline constexpr int32_t kErrFlagTmpAllocFull = 1 << 17;   // per-world tmpAlloc arena exhausted
+inline constexpr int32_t kErrFlagDeferredFull = 1 << 18;   // deferred destroy log full
+inline constexpr int32_t kErrFlagRowParallelOp = 1 << 19;  // op not available in a row-parallel node
+inline constexpr int32_t kErrFlagCommitLimit = 1 << 20;    // archetype too large for the ordered commit
+
+// Ordered structural commit (see Context, row-parallel mode): an append key
+// orders a row made by a row-parallel lane exactly where the reference's
+// world-serial row walk would have made it: [63:32] the lane's row key
+// (query archetype << 24 | row), [31:16] the lane's per-row sequence number,
+// [15:0] free for the commit's sort.  kNoAppendKey marks settled rows.
+inline constexpr uint64_t kNoAppendKey = ~0ull;
+inline constexpr uint32_t kSerialRowKey = 0xFFFF'FFFFu;
+
+// Destroy requested by a row-parallel lane; applied by the commit after the
+// node, in key order (= the reference's serial destroy order).
+struct DeferredDestroy {
+    uint64_t key;
+    Entity e;
+};
+
+// ---------------------------------------------------------------------------
 // Arena view (host mirror and device arena share this layout)
 // ---------------------------------------------------------------------------
+inline constexpr uint32_t kArchTemporary = 1;     // rows have no entity IDs
+inline constexpr uint32_t kArchModuleRows = 2;    // rows written by a module's own kernels
+
 struct ArchetypeView {
     int32_t numColumns;
     int32_t capacity;          // rows per world
-    uint32_t flags;            // 1 = temporary
+    uint32_t flags;            // kArchTemporary | kArchModuleRows
     int32_t *numRows;          // [numWorlds]
+    uint64_t *appendKeys;      // [numWorlds][capacity] device only (null: no row-parallel appends)
+    int32_t *pendingRows;      // [numWorlds] rows appended by the running row-parallel node
     char *cols[kMaxColumns];
     uint32_t colBytes[kMaxColumns];
     uint64_t colKeys[kMaxColumns];
@@ -247,7 +279,19 @@ struct StateView {
     IDNode *idNodes;            // [numWorlds][idsPerWorld]
     IDMapState *idState;        // [numWorlds]
     char *worldData;            // [numWorlds][worldDataStride]
-    int32_t *errorFlags;        // [numWorlds]  bit0 ID store full, bit1 table full
+    int32_t *errorFlags;        // [numWorlds]  bit0 ID store full, bit1 table full, kErrFlag*
+    // Ordered structural commit of row-parallel nodes (device only; null
+    // on the host mirror, whose contexts are world-serial).
+    uint64_t *appendDirty;      // [numWorlds] archetypes appended to by the running node
+    int32_t *deferCount;        // [numWorlds] deferred destroys of the running node
+    DeferredDestroy *deferLog;  // [numWorlds][deferCap]
+    int32_t deferCap;
+    // Per-world bump allocator (Context::tmpAlloc, reference
+    // StateManager::tmpAlloc, src/core/state.cpp:584-602): 256-byte
+    // granules, reset by ResetTmpAllocNode.
+    uint32_t tmpBytesPerWorld;
+    char *tmpArena;             // [numWorlds][tmpBytesPerWorld]
+    uint32_t *tmpOffset;        // [numWorlds]
     uint64_t archKeys[kMaxArchetypes];
     ArchetypeView arch[kMaxArchetypes];
 
@@ -285,8 +329,40 @@ struct StateView {
         return -1;
     }
 
-    // Append a row (no entity).  Single writer per world assumed by callers;
-    // kernels that append concurrently use their own ordered scheme.
+    // Row-parallel append (device): a row at the end of the world's table,
+    // tagged with the caller's append key; the node's commit moves it to its
+    // serial position.  -1 when the table is full or the archetype takes no
+    // row-parallel appends.
+    MW_INLINE int32_t appendRowParallel(uint32_t archetype, int32_t world, uint64_t key)
+    {
+#if defined(__HIP_DEVICE_COMPILE__)
+        ArchetypeView &a = arch[archetype];
+        if (!a.appendKeys) {
+            atomicOr(errorFlags + world, kErrFlagRowParallelOp);
+            return -1;
+        }
+        const unsigned long long bit = 1ull << archetype;
+        if (!(appendDirty[world] & bit)) {
+            atomicOr((unsigned long long *)(appendDirty + world), bit);
+        }
+        // The row count itself stays put until the commit, so every lane of
+        // the node sees the tables as they were when it started (rows made
+        // by other lanes are not visible, as destroyed rows stay visible).
+        const int32_t row = a.numRows[world] + atomicAdd(a.pendingRows + world, 1);
+        if (row >= a.capacity) {
+            atomicOr(errorFlags + world, 2);
+            return -1;
+        }
+        a.appendKeys[(size_t)world * a.capacity + row] = key;
+        return row;
+#else
+        (void)key;
+        return addRow(archetype, world);
+#endif
+    }
+
+    // Append a row (no entity) from a world-serial context (host, or one
+    // lane owning the world).
     MW_INLINE int32_t addRow(uint32_t archetype, int32_t world)
     {
         ArchetypeView &a = arch[archetype];
@@ -375,6 +451,8 @@ public:
     struct Config {
         int32_t numWorlds;
         int32_t defaultCapacity;     // rows per world for registerArchetype
+        int32_t tmpAllocBytesPerWorld = 0;   // Context::tmpAlloc arena per world
+        int32_t deferCap = 256;              // deferred destroys per world per node
     };
 
     explicit StateManager(const Config &cfg);
@@ -388,6 +466,9 @@ public:
     void setCapacityHint(uint64_t archetype_key, int32_t capacity);
     int32_t capacityHint(uint64_t archetype_key) const;
     void setTemporary(uint64_t archetype_key);
+    // Rows of this archetype are written by a module's own kernels (e.g. the
+    // physics candidate list): no row-parallel append keys are kept for it.
+    void setModuleRows(uint64_t archetype_key);
 
     template <typename ComponentT>
     uint32_t registerComponent()

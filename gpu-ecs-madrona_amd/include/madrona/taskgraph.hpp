@@ -13,10 +13,14 @@
 #pragma once
 
 #include <madrona/context.hpp>
+#include <madrona/optional.hpp>
 #include <madrona/tracing.hpp>
 
+#include <functional>
 #include <initializer_list>
 #include <memory>
+#include <stdexcept>
+#include <type_traits>
 #include <vector>
 
 namespace madrona {
@@ -53,6 +57,9 @@ struct LaunchCtx {
     // = the CUs the grid is sized for.  Set by the executor for each node.
     int32_t blocksPerCU = 0;
     int32_t numCUs = 0;
+    // Device copies of the graph's node data blocks (TaskGraph::NodeData,
+    // constructNodeData), uploaded once when the graph is set.
+    char *nodeData = nullptr;
 
     // Grid for a grid-stride kernel that needs `blocks` blocks to cover its
     // work in one pass: capped at numCUs x blocksPerCU when configured.
@@ -73,12 +80,39 @@ struct LaunchCtx {
     }
 };
 
-struct NodeBase {};
+// Base of every node's data (reference device NodeBase,
+// src/mw/device/include/madrona/taskgraph.hpp:23-25).  For nodes whose run()
+// executes on the device (addNodeFn / addOneOffNode / addDynamicCountNode)
+// the executor fills in the device state before uploading the node data, so
+// run() can build a world's context: makeContext<ContextT>(WorldID), the
+// analogue of the reference's static TaskGraph::makeContext.
+struct NodeBase {
+    uint32_t numDynamicInvocations = 0;
+    int32_t mwNumWorlds = 0;
+    StateView *mwState = nullptr;
+
+#if defined(__HIPCC__)
+    template <typename ContextT>
+    __device__ inline ContextT makeContext(WorldID world) const;
+#endif
+};
 
 class TaskGraph {
 public:
     struct NodeID {
         uint32_t id;
+    };
+    struct DataID {
+        int32_t id;
+    };
+    template <typename NodeT>
+    struct TypedDataID : DataID {};
+
+    // Node data: at most 128 bytes, trivially copyable (the reference
+    // memcpy's it into the built graph, src/core/taskgraph.cpp:104-106).
+    static inline constexpr uint32_t maxNodeDataBytes = 128;
+    struct alignas(maxNodeDataBytes) NodeData {
+        char userData[maxNodeDataBytes];
     };
 
     using LaunchFn = void (*)(void *node, LaunchCtx &lc);
@@ -87,27 +121,113 @@ public:
     public:
         explicit Builder(Context &ctx);
 
+        // Node data constructed in place in the graph (reference
+        // taskgraph.inl:5-19); shared by every node that names it.
         template <typename NodeT, typename... Args>
-        NodeID addDefaultNode(Span<const NodeID> dependencies, Args &&...args)
+        TypedDataID<NodeT> constructNodeData(Args &&...args)
         {
-            auto data = std::make_shared<NodeT>(std::forward<Args>(args)...);
-            return registerNode(std::static_pointer_cast<void>(data),
-                                [](void *n, LaunchCtx &lc) { NodeT::launch((NodeT *)n, lc); },
-                                dependencies, NodeT::nodeName());
+            static_assert(sizeof(NodeT) <= maxNodeDataBytes);
+            static_assert(alignof(NodeT) <= maxNodeDataBytes);
+            static_assert(std::is_trivially_copyable_v<NodeT>,
+                          "node data is copied to the device: it must be trivially copyable");
+            datas_.emplace_back();
+            new (datas_.back().userData) NodeT(std::forward<Args>(args)...);
+            dataIsNodeBase_.push_back(std::is_base_of_v<NodeBase, NodeT>);
+            return TypedDataID<NodeT> { DataID { (int32_t)datas_.size() - 1 } };
         }
 
         template <typename NodeT>
+        NodeT &getDataRef(TypedDataID<NodeT> data_id)
+        {
+            return *(NodeT *)datas_[data_id.id].userData;
+        }
+
+        // A node that runs `fn(NodeT *, int32_t invocation_idx)` on the
+        // device (reference device taskgraph.inl:41-59).  fixed_num_invocations
+        // > 0: that many invocations per world, invocation_idx = world *
+        // count + k (count 1: invocation_idx is the world, as every node of
+        // the reference snapshot is invoked, megakernel_impl.inl:29-40).
+        // 0: node->numDynamicInvocations invocations in total, read on the
+        // device when the node runs (set by an earlier node, e.g.
+        // addDynamicCountNode's count node).  num_threads_per_invocation
+        // lanes call fn for each invocation (a power of two <= 64).
+        // Contexts made in run() are world-serial: with more than one
+        // invocation per world, at most one of them may mutate the world's
+        // structure.
+        template <auto fn, typename NodeT>
+        NodeID addNodeFn(TypedDataID<NodeT> data, Span<const NodeID> dependencies,
+                         Optional<NodeID> parent_node = Optional<NodeID>::none(),
+                         uint32_t fixed_num_invocations = 0,
+                         uint32_t num_threads_per_invocation = 1);
+
+        // Reference device taskgraph.inl:61-70: NodeT::run(int32_t) over
+        // `count` invocations per world.
+        template <typename NodeT, int32_t count = 1, typename... Args>
+        NodeID addOneOffNode(Span<const NodeID> dependencies, Args &&...args)
+        {
+            auto data_id = constructNodeData<NodeT>(std::forward<Args>(args)...);
+            return addNodeFn<&NodeT::run>(data_id, dependencies, Optional<NodeID>::none(),
+                                          (uint32_t)count);
+        }
+
+        // Reference device taskgraph.inl:72-95: a one-invocation node stores
+        // NodeT::numInvocations() in the node data, then NodeT::run runs over
+        // that many invocations (num_threads_per_invocation lanes each).
+        template <typename NodeT, typename... Args>
+        NodeID addDynamicCountNode(Span<const NodeID> dependencies,
+                                   uint32_t num_threads_per_invocation, Args &&...args)
+        {
+            auto data_id = constructNodeData<NodeT>(std::forward<Args>(args)...);
+            NodeID count_node = addNodeFn<&Builder::dynamicCountWrapper<NodeT>>(
+                data_id, dependencies, Optional<NodeID>::none(), 0xFFFF'FFFFu);
+            return addNodeFn<&NodeT::run>(data_id, { count_node }, Optional<NodeID>::none(), 0,
+                                          num_threads_per_invocation);
+        }
+
+        // Framework nodes (static launch(NodeT *, LaunchCtx &): their own
+        // kernels over all worlds) keep their data on the host; any other
+        // NodeT is a device node: constructNodeData + addNodeFn<&NodeT::run>
+        // with one invocation per world (reference taskgraph.inl:33-43).
+        template <typename NodeT, typename... Args>
+        NodeID addDefaultNode(Span<const NodeID> dependencies, Args &&...args)
+        {
+            if constexpr (requires(NodeT *n, LaunchCtx &lc) { NodeT::launch(n, lc); }) {
+                auto data = std::make_shared<NodeT>(std::forward<Args>(args)...);
+                return registerNode(std::static_pointer_cast<void>(data),
+                                    [](void *n, LaunchCtx &lc) { NodeT::launch((NodeT *)n, lc); },
+                                    dependencies, NodeT::nodeName());
+            } else {
+                auto data_id = constructNodeData<NodeT>(std::forward<Args>(args)...);
+                return addNodeFn<&NodeT::run>(data_id, dependencies, Optional<NodeID>::none(), 1);
+            }
+        }
+
+        // NodeT::addToGraph in either reference form: (Context &, Builder &,
+        // deps) (CPU, include/madrona/taskgraph.hpp) or (Builder &, deps)
+        // (device, src/mw/device/include/madrona/taskgraph.hpp).
+        template <typename NodeT>
         NodeID addToGraph(Span<const NodeID> dependencies)
         {
-            return NodeT::addToGraph(*ctx_, *this, dependencies);
+            if constexpr (requires(Builder &b) { NodeT::addToGraph(b, dependencies); }) {
+                return NodeT::addToGraph(*this, dependencies);
+            } else {
+                return NodeT::addToGraph(*ctx_, *this, dependencies);
+            }
         }
 
         Context &context() { return *ctx_; }
         StateManager &stateManager();
+        int32_t worldIDX() const { return 0; }
 
         TaskGraph build();
 
     private:
+        template <typename NodeT>
+        MW_HD static void dynamicCountWrapper(NodeT *node, int32_t)
+        {
+            node->numDynamicInvocations = (uint32_t)node->numInvocations();
+        }
+
         NodeID registerNode(std::shared_ptr<void> data, LaunchFn fn,
                             Span<const NodeID> deps, const char *name);
 
@@ -120,6 +240,8 @@ public:
 
         Context *ctx_;
         std::vector<Staged> staged_;
+        std::vector<NodeData> datas_;
+        std::vector<uint8_t> dataIsNodeBase_;
     };
 
     TaskGraph() = default;
@@ -128,6 +250,12 @@ public:
     int32_t numNodes() const { return (int32_t)nodes_.size(); }
     const char *nodeName(int32_t i) const { return nodes_[i].name; }
 
+    // Node data blocks, for the executor to upload (NodeBase-derived blocks
+    // get the device state filled in first).
+    int32_t numNodeDatas() const { return (int32_t)datas_.size(); }
+    const NodeData *nodeDatas() const { return datas_.data(); }
+    bool nodeDataIsNodeBase(int32_t i) const { return dataIsNodeBase_[i] != 0; }
+
 private:
     struct Node {
         std::shared_ptr<void> data;
@@ -135,15 +263,12 @@ private:
         const char *name;
     };
     std::vector<Node> nodes_;
+    std::vector<NodeData> datas_;
+    std::vector<uint8_t> dataIsNodeBase_;
 
     friend class Builder;
 };
 
-// ---------------------------------------------------------------------------
-// Generic row-parallel node: one lane per (world, row) of every archetype the
-// query matches; all worlds in one launch.  Rows of one world are contiguous
-// in every column slab, so lanes read columns fully coalesced.
-// ---------------------------------------------------------------------------
 namespace detail {
 
 template <typename C, typename = void>
@@ -160,8 +285,61 @@ struct ColArgs {
     int32_t c[N > 0 ? N : 1];
 };
 
-void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype,
-                     const void *args, size_t args_bytes);
+// Launch helpers (csrc/runtime/executor.hip).
+void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype, int32_t query_arch,
+                     int32_t threads_per_invocation, int32_t items_per_invocation,
+                     const void *cols, size_t cols_bytes);
+void launchWorldKernel(const void *kernel, LaunchCtx &lc);
+void launchNodeFnKernel(const void *kernel, LaunchCtx &lc, void *node_dev, uint32_t fixed_count,
+                        uint32_t threads_per_invocation);
+// The ordered structural commit of a row-parallel node (see Context): a
+// no-op for worlds whose lanes made / destroyed nothing.
+void launchStructuralCommit(LaunchCtx &lc);
+
+#if defined(__HIPCC__)
+template <typename ContextT>
+__device__ inline ContextT worldContext(StateView *st, int32_t w)
+{
+    using WorldT = typename WorldOf<ContextT>::type;
+    return ContextT((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
+                    WorkerInit { st, w, nullptr });
+}
+#endif
+
+}
+
+#if defined(__HIPCC__)
+template <typename ContextT>
+__device__ inline ContextT NodeBase::makeContext(WorldID world) const
+{
+    return detail::worldContext<ContextT>(mwState, world.idx);
+}
+
+namespace mwGPU {
+// Lane within the invocation of a CustomParallelForNode / multi-thread
+// node (invocations are aligned groups of threads_per_invocation lanes).
+template <int32_t threads_per_invocation>
+__device__ inline int32_t invocationLane()
+{
+    return (int32_t)(threadIdx.x & (threads_per_invocation - 1));
+}
+}
+#endif
+
+// ---------------------------------------------------------------------------
+// Row-parallel node (reference device CustomParallelForNode, taskgraph.hpp:
+// 166-182; CPU ParallelForNode, taskgraph.inl:58-71): Fn(ctx, components...)
+// for every row of every archetype the query matches, all worlds in one
+// launch.  An invocation is a group of threads_per_invocation lanes (a power
+// of two <= 64, aligned within the wave) that all call Fn for the same row
+// -- a cooperative Fn splits the row's work by mwGPU::invocationLane() --
+// and walks items_per_invocation consecutive rows.  Rows of one world are
+// contiguous in every column slab, so the lanes read columns coalesced.
+// Structural mutation from Fn follows the reference's serial row order
+// through the ordered commit (Context, row-parallel mode); with several
+// threads per invocation only one lane of the group may mutate.
+// ---------------------------------------------------------------------------
+namespace detail {
 
 #if defined(__HIPCC__)
 template <typename ContextT, auto Fn, typename... ComponentTs, size_t... Is>
@@ -172,9 +350,9 @@ __device__ inline void invokeRow(ContextT &ctx, StateView *st, int32_t arch,
     Fn(ctx, rowRef(st->column<std::remove_const_t<ComponentTs>>(arch, cols.c[Is], w), r)...);
 }
 
-template <typename ContextT, auto Fn, typename... ComponentTs>
+template <typename ContextT, auto Fn, int32_t threads, int32_t items, typename... ComponentTs>
 __global__ void __launch_bounds__(256)
-parallelForKernel(const StateView *__restrict__ st_in, int32_t arch,
+parallelForKernel(const StateView *__restrict__ st_in, int32_t arch, int32_t query_arch,
                   ColArgs<sizeof...(ComponentTs)> cols)
 {
     MW_TRACE_BLOCK(arch);
@@ -183,37 +361,52 @@ parallelForKernel(const StateView *__restrict__ st_in, int32_t arch,
     // column pointers loaded from it as global (no flat accesses).
     StateView *st = const_cast<StateView *>(st_in);
     const int32_t cap = st->arch[arch].capacity;
-    const int64_t total = (int64_t)st->numWorlds * cap;
+    const int32_t inv_per_world = (cap + items - 1) / items;
+    const int64_t total = (int64_t)st->numWorlds * inv_per_world * threads;
     // grid-stride: one pass with the default grid, several when the node's
     // launch configuration caps the grid (LaunchCtx::capGrid)
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
-        const int32_t w = (int32_t)(t / cap);
-        const int32_t r = (int32_t)(t - (int64_t)w * cap);
-        if (r >= st->arch[arch].numRows[w]) continue;
-        using WorldT = typename WorldOf<ContextT>::type;
-        ContextT ctx((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
-                     WorkerInit { st, w, nullptr });
-        invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, r,
-                                                std::index_sequence_for<ComponentTs...> {});
+        const int64_t inv = t / threads;
+        const int32_t w = (int32_t)(inv / inv_per_world);
+        const int32_t first = (int32_t)(inv - (int64_t)w * inv_per_world) * items;
+        const int32_t n = st->arch[arch].numRows[w];
+        if (first >= n) continue;
+        ContextT ctx = worldContext<ContextT>(st, w);
+#pragma unroll 1
+        for (int32_t k = 0; k < items && first + k < n; k++) {
+            ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k));
+            invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, first + k,
+                                                    std::index_sequence_for<ComponentTs...> {});
+        }
     }
 }
 #endif
 
 }
 
-template <typename ContextT, auto Fn, typename... ComponentTs>
-class ParallelForNode : public NodeBase {
+template <typename ContextT, auto Fn, int32_t threads_per_invocation, int32_t items_per_invocation,
+          typename... ComponentTs>
+class CustomParallelForNode : public NodeBase {
+    static_assert(threads_per_invocation >= 1 && threads_per_invocation <= 64 &&
+                  (threads_per_invocation & (threads_per_invocation - 1)) == 0,
+                  "threads_per_invocation: a power of two <= 64 (one wave)");
+    static_assert(items_per_invocation >= 1);
 public:
-    explicit ParallelForNode(Context &ctx);
+    explicit CustomParallelForNode(Context &ctx) : query_(ctx.query<ComponentTs...>()) {}
 
     static TaskGraph::NodeID addToGraph(Context &ctx, TaskGraph::Builder &builder,
                                         Span<const TaskGraph::NodeID> deps)
     {
-        return builder.addDefaultNode<ParallelForNode>(deps, ctx);
+        return builder.addDefaultNode<CustomParallelForNode>(deps, ctx);
+    }
+    static TaskGraph::NodeID addToGraph(TaskGraph::Builder &builder,
+                                        Span<const TaskGraph::NodeID> deps)
+    {
+        return builder.addDefaultNode<CustomParallelForNode>(deps, builder.context());
     }
 
-    static void launch(ParallelForNode *self, LaunchCtx &lc)
+    static void launch(CustomParallelForNode *self, LaunchCtx &lc)
     {
 #if defined(__HIPCC__)
         for (int32_t a = 0; a < self->query_.numArchetypes; a++) {
@@ -222,34 +415,106 @@ public:
                 cols.c[c] = self->query_.cols[a][c];
             }
             detail::launchRowKernel(
-                (const void *)&detail::parallelForKernel<ContextT, Fn, ComponentTs...>,
-                lc, self->query_.archetypes[a], &cols, sizeof(cols));
+                (const void *)&detail::parallelForKernel<ContextT, Fn, threads_per_invocation,
+                                                         items_per_invocation, ComponentTs...>,
+                lc, self->query_.archetypes[a], a, threads_per_invocation, items_per_invocation,
+                &cols, sizeof(cols));
         }
+        detail::launchStructuralCommit(lc);
 #else
         (void)self; (void)lc;
 #endif
     }
 
-    static const char *nodeName() { return "ParallelForNode"; }
+    static const char *nodeName()
+    {
+        return threads_per_invocation == 1 && items_per_invocation == 1 ? "ParallelForNode"
+                                                                        : "CustomParallelForNode";
+    }
 
     Query<ComponentTs...> query_;
 };
 
+// Reference device taskgraph.hpp:184-186 (the CPU class of the same name
+// walks rows serially; the commit keeps its order).
 template <typename ContextT, auto Fn, typename... ComponentTs>
-ParallelForNode<ContextT, Fn, ComponentTs...>::ParallelForNode(Context &ctx)
-    : query_(ctx.query<ComponentTs...>())
-{}
+using ParallelForNode = CustomParallelForNode<ContextT, Fn, 1, 1, ComponentTs...>;
+
+// ---------------------------------------------------------------------------
+// Device nodes of addNodeFn (run(int32_t invocation_idx) on the device).
+// ---------------------------------------------------------------------------
+namespace detail {
+
+#if defined(__HIPCC__)
+// fixed_count > 0: fixed_count invocations per world; 0: the node's
+// numDynamicInvocations in total; 0xFFFFFFFF: one invocation (the dynamic
+// count node).
+template <typename NodeT, auto fn>
+__global__ void __launch_bounds__(256)
+nodeFnKernel(NodeT *node, uint32_t fixed_count, uint32_t threads)
+{
+    MW_TRACE_BLOCK(0);
+    int64_t total;
+    if (fixed_count == 0xFFFF'FFFFu) {
+        total = 1;
+    } else if (fixed_count > 0) {
+        total = (int64_t)node->mwNumWorlds * fixed_count;
+    } else {
+        total = (int64_t)__hip_atomic_load(&node->numDynamicInvocations, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    total *= threads;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        std::invoke(fn, node, (int32_t)(t / threads));
+    }
+}
+#endif
+
+}
+
+template <auto fn, typename NodeT>
+TaskGraph::NodeID TaskGraph::Builder::addNodeFn(TypedDataID<NodeT> data,
+                                                Span<const NodeID> dependencies,
+                                                Optional<NodeID> parent_node,
+                                                uint32_t fixed_num_invocations,
+                                                uint32_t num_threads_per_invocation)
+{
+    static_assert(std::is_base_of_v<NodeBase, NodeT>, "device nodes derive from NodeBase");
+    (void)parent_node;   // children run as ordinary nodes, in dependency order
+    if (num_threads_per_invocation == 0 || num_threads_per_invocation > 64 ||
+        (num_threads_per_invocation & (num_threads_per_invocation - 1)) != 0) {
+        throw std::runtime_error("addNodeFn: num_threads_per_invocation must be a power of two <= 64");
+    }
+    struct Desc {
+        int32_t dataIdx;
+        uint32_t fixedCount;
+        uint32_t threads;
+    };
+    auto desc = std::make_shared<Desc>(Desc { data.id, fixed_num_invocations,
+                                              num_threads_per_invocation });
+    return registerNode(std::static_pointer_cast<void>(desc),
+                        [](void *d, LaunchCtx &lc) {
+#if defined(__HIPCC__)
+                            const Desc &dd = *(const Desc *)d;
+                            void *node = lc.nodeData + (size_t)dd.dataIdx * maxNodeDataBytes;
+                            detail::launchNodeFnKernel(
+                                (const void *)&detail::nodeFnKernel<NodeT, fn>, lc, node,
+                                dd.fixedCount, dd.threads);
+#else
+                            (void)d; (void)lc;
+#endif
+                        },
+                        dependencies, "NodeFn");
+}
 
 // ---------------------------------------------------------------------------
 // Per-world node: Fn(ContextT &) once per world, worlds in parallel (one lane
 // each).  The reference runs every node once per world (taskgraph.cpp:
-// 111-122); this is its general custom-node form, and the place for
-// structural mutation (makeEntityNow / destroyEntityNow / clearArchetype),
-// which must not race with other lanes of the same world.
+// 111-122); this is its general custom-node form: the lane owns its world, so
+// structural mutation acts immediately (world-serial mode).
 // ---------------------------------------------------------------------------
 namespace detail {
-void launchWorldKernel(const void *kernel, LaunchCtx &lc);
-
 #if defined(__HIPCC__)
 template <typename ContextT, auto Fn>
 __global__ void __launch_bounds__(64) perWorldKernel(const StateView *__restrict__ st_in)
@@ -258,9 +523,7 @@ __global__ void __launch_bounds__(64) perWorldKernel(const StateView *__restrict
     StateView *st = const_cast<StateView *>(st_in);
     for (int32_t w = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); w < st->numWorlds;
          w += (int32_t)(gridDim.x * blockDim.x)) {
-        using WorldT = typename WorldOf<ContextT>::type;
-        ContextT ctx((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
-                     WorkerInit { st, w, nullptr });
+        ContextT ctx = worldContext<ContextT>(st, w);
         Fn(ctx);
     }
 }
@@ -290,6 +553,8 @@ public:
 
 // Clear a temporary archetype in every world (taskgraph.inl:94-104).
 void launchClearRows(LaunchCtx &lc, int32_t archetype);
+// Reset every world's tmpAlloc arena (taskgraph.inl:83-86).
+void launchResetTmpAlloc(LaunchCtx &lc);
 
 template <typename ArchetypeT>
 class ClearTmpNode : public NodeBase {
@@ -302,14 +567,17 @@ public:
     {
         return builder.addDefaultNode<ClearTmpNode>(deps, ctx);
     }
+    static TaskGraph::NodeID addToGraph(TaskGraph::Builder &builder,
+                                        Span<const TaskGraph::NodeID> deps)
+    {
+        return builder.addDefaultNode<ClearTmpNode>(deps, builder.context());
+    }
     static void launch(ClearTmpNode *self, LaunchCtx &lc) { launchClearRows(lc, self->archetype_); }
     static const char *nodeName() { return "ClearTmpNode"; }
 
     int32_t archetype_;
 };
 
-// The per-world bump allocator has no device state in this design (physics
-// scratch lives in module-owned slabs), so the node is a scheduling marker.
 class ResetTmpAllocNode : public NodeBase {
 public:
     static TaskGraph::NodeID addToGraph(Context &, TaskGraph::Builder &builder,
@@ -317,7 +585,12 @@ public:
     {
         return builder.addDefaultNode<ResetTmpAllocNode>(deps);
     }
-    static void launch(ResetTmpAllocNode *, LaunchCtx &) {}
+    static TaskGraph::NodeID addToGraph(TaskGraph::Builder &builder,
+                                        Span<const TaskGraph::NodeID> deps)
+    {
+        return builder.addDefaultNode<ResetTmpAllocNode>(deps);
+    }
+    static void launch(ResetTmpAllocNode *, LaunchCtx &lc) { launchResetTmpAlloc(lc); }
     static const char *nodeName() { return "ResetTmpAllocNode"; }
 };
 

@@ -53,7 +53,8 @@ if len(_mapped_hip_runtimes()) > 1:
 
 class MwConfig(ctypes.Structure):
     _fields_ = [("num_worlds", ctypes.c_int32), ("gpu_id", ctypes.c_int32),
-                ("default_capacity", ctypes.c_int32), ("use_graph", ctypes.c_int32)]
+                ("default_capacity", ctypes.c_int32), ("use_graph", ctypes.c_int32),
+                ("tmp_alloc_bytes", ctypes.c_int32), ("max_deferred_destroys", ctypes.c_int32)]
 
 
 class CollisionsConfig(ctypes.Structure):
@@ -104,6 +105,11 @@ _lib.mw_destroy.argtypes = [ctypes.c_void_p]
 _lib.mw_last_error.restype = ctypes.c_char_p
 _lib.mw_num_worlds.argtypes = [ctypes.c_void_p]
 _lib.mw_export_row_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+_lib.mw_load_env.argtypes = [ctypes.c_char_p]
+_lib.mw_entity_loc.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
+                               ctypes.c_void_p, ctypes.c_void_p]
+_lib.mw_env_name.restype = ctypes.c_char_p
+_lib.mw_env_name.argtypes = [ctypes.c_int32]
 _lib.mw_error_flags.argtypes = [ctypes.c_void_p]
 _lib.mw_num_archetypes.argtypes = [ctypes.c_void_p]
 _lib.mw_read_column.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -165,7 +171,8 @@ C_ABI_SYMBOLS = (
     "mw_trace_enable", "mw_trace_read", "mw_trace_func_name", "mw_trace_block_records",
     "mw_num_nodes", "mw_node_name", "mw_node_blocks_per_cu", "mw_set_node_blocks_per_cu",
     "mw_parse_exec_config_override", "mw_parse_exec_config_file",
-    "mw_export_row_bytes",
+    "mw_export_row_bytes", "mw_load_env", "mw_num_envs", "mw_env_name",
+    "mw_entity_loc",
 )
 
 
@@ -187,6 +194,21 @@ def parse_exec_config_file(text):
     blocks = np.zeros(max(n, 1), np.int32)
     _lib.mw_parse_exec_config_file(text.encode(), nodes.ctypes.data, blocks.ctypes.data, n)
     return [(int(a), int(b)) for a, b in zip(nodes[:n], blocks[:n])]
+
+
+def load_env(so_path):
+    """Load an out-of-tree world (a shared object built against
+    include/madrona that registers itself with MADRONA_BUILD_MWGPU_ENTRY);
+    returns the number of environments it registered."""
+    n = _lib.mw_load_env(os.fsencode(so_path))
+    if n < 0:
+        raise _err()
+    return n
+
+
+def env_names():
+    """Every registered environment name (built-in and loaded)."""
+    return [_lib.mw_env_name(i).decode() for i in range(_lib.mw_num_envs())]
 
 
 def rccl_unique_id():
@@ -287,8 +309,10 @@ class Executor:
     """A batch of worlds of one environment on one GPU."""
 
     def __init__(self, env, num_worlds, user_cfg, inits, init_stride, gpu_id=0,
-                 default_capacity=64, use_graph=True):
-        cfg = MwConfig(num_worlds, gpu_id, default_capacity, 1 if use_graph else 0)
+                 default_capacity=64, use_graph=True, tmp_alloc_bytes=-1,
+                 max_deferred_destroys=0):
+        cfg = MwConfig(num_worlds, gpu_id, default_capacity, 1 if use_graph else 0,
+                       tmp_alloc_bytes, max_deferred_destroys)
         self._keep = (user_cfg, inits)
         self.h = _lib.mw_create(env.encode(), ctypes.byref(cfg), ctypes.byref(user_cfg),
                                 ctypes.sizeof(user_cfg), ctypes.cast(inits, ctypes.c_void_p),
@@ -349,6 +373,14 @@ class Executor:
 
     def error_flags(self):
         return _lib.mw_error_flags(self.h)
+
+    def entity_loc(self, world, entity_id, gen):
+        """(archetype, row) of a live entity, None when it is not alive."""
+        a, r = ctypes.c_int32(), ctypes.c_int32()
+        rc = _lib.mw_entity_loc(self.h, world, entity_id, gen, ctypes.byref(a), ctypes.byref(r))
+        if rc < 0:
+            raise _err()
+        return None if rc else (a.value, r.value)
 
     def read_column(self, archetype, column, world, dtype, max_rows=4096):
         b = ctypes.c_int32()

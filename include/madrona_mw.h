@@ -41,6 +41,11 @@ typedef struct mw_config {
     int32_t gpu_id;            /* HIP device ordinal                         */
     int32_t default_capacity;  /* rows per world for archetypes w/o a size   */
     int32_t use_graph;         /* 1: replay the step as one hipGraph         */
+    int32_t tmp_alloc_bytes;   /* Context::tmpAlloc arena per world (reference
+                                  StateManager::tmpAlloc); -1: 16 KiB, 0: none */
+    int32_t max_deferred_destroys; /* destroyEntityNow calls per world per
+                                  row-parallel node (applied in the reference's
+                                  order after the node); 0: 256              */
 } mw_config;
 
 /* "collisions": rigid-body workload of SURVEY.md §8(d) C3/C4 (128 unit cube
@@ -98,6 +103,17 @@ mw_exec *mw_create(const char *env, const mw_config *cfg,
                    const void *user_cfg, size_t user_cfg_bytes,
                    const void *inits, size_t init_stride);
 
+/* Load an environment compiled outside this library (reference: user
+ * sources of CompileConfig, src/mw/cuda_exec.cpp:444-831, compiled ahead of
+ * time here): a shared object built with hipcc against include/madrona,
+ * linked to libmadrona_mw.so, whose worlds register themselves with
+ * MADRONA_BUILD_MWGPU_ENTRY (include/madrona/mw_gpu_entry.hpp).  Returns the
+ * number of environments it registered (-1 on error); mw_create then takes
+ * their names.  mw_num_envs / mw_env_name list every registered name.     */
+int32_t mw_load_env(const char *so_path);
+int32_t mw_num_envs(void);
+const char *mw_env_name(int32_t i);
+
 /* Step every world `num_steps` times; blocks until done. */
 int mw_step(mw_exec *exec, int32_t num_steps);
 
@@ -143,6 +159,10 @@ int32_t mw_num_archetypes(mw_exec *exec);
  * max_rows); returns the world's row count or -1. */
 int32_t mw_read_column(mw_exec *exec, int32_t archetype, int32_t column,
                        int32_t world, void *out, int32_t max_rows);
+/* Entity lookup in world `world`'s ID store (reference getLoc): 0 and the
+ * entity's (archetype, row) when (id, gen) is alive, 1 when it is not.   */
+int32_t mw_entity_loc(mw_exec *exec, int32_t world, int32_t id, uint32_t gen,
+                      int32_t *archetype, int32_t *row);
 /* Column byte width and rows-per-world capacity. */
 int32_t mw_column_info(mw_exec *exec, int32_t archetype, int32_t column,
                        int32_t *bytes, int32_t *capacity);
