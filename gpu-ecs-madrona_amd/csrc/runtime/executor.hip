@@ -396,11 +396,21 @@ void launchClearRows(LaunchCtx &lc, int32_t archetype)
                        (hipStream_t)lc.stream, rows, lc.numWorlds);
 }
 
+// A kernel rather than a memset node: measured on the MI355X box, a
+// hipMemsetAsync captured into the step graph left every other world's
+// offset unreset once host hipMemcpy calls ran between graph replays.
+__global__ void resetTmpAllocKernel(uint32_t *offsets, int32_t num_worlds)
+{
+    MW_TRACE_BLOCK(0);
+    const int32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < num_worlds) offsets[w] = 0;
+}
+
 void launchResetTmpAlloc(LaunchCtx &lc)
 {
     if (!lc.view->tmpOffset) return;
-    MW_HIP_CHECK(hipMemsetAsync(lc.view->tmpOffset, 0, sizeof(uint32_t) * lc.numWorlds,
-                                (hipStream_t)lc.stream));
+    hipLaunchKernelGGL(resetTmpAllocKernel, dim3((lc.numWorlds + 255) / 256), dim3(256), 0,
+                       (hipStream_t)lc.stream, lc.view->tmpOffset, lc.numWorlds);
 }
 
 // Packed export: world w's rows land at offset prefix(numRows)[w]

@@ -72,6 +72,8 @@ class EcsOpsSim:
     def agents(self, w):
         parts = self._cols(ARCH_AGENT, w, (0, 1, 2, 3))
         n = len(parts[0]) // 8
+        if n == 0:
+            return np.zeros(0, AGENT_DTYPE)
         rows = np.hstack([p.reshape(n, -1) for p in parts])
         return rows.view(AGENT_DTYPE).reshape(n)
 
@@ -82,6 +84,8 @@ class EcsOpsSim:
     def spawns(self, w):
         parts = self._cols(ARCH_SPAWN, w, (0, 1))
         n = len(parts[0]) // 8
+        if n == 0:
+            return np.zeros(0, SPAWN_DTYPE)
         rows = np.hstack([p.reshape(n, -1) for p in parts])
         return rows.view(SPAWN_DTYPE).reshape(n)
 
