@@ -6,8 +6,10 @@
 //   actionSelect  ParallelForNode<Entity, Position, Action>   (fvs.cpp:111-151)
 //   caster        ParallelForNode<Entity, Action, Mana>       (fvs.cpp:153-190)
 //   archer        ParallelForNode<Entity, Action, Quiver>     (fvs.cpp:192-214)
-//   cleanup       ParallelForNode<Entity, Health> marks the dead, then a
-//                 PerWorldNode replays fvs.cpp:224-239 on them  (see below)
+//   cleanup       ParallelForNode<Entity, Health> marks the dead, a
+//                 PerWorldNode makes their trackers, a ParallelForNode over
+//                 the trackers destroys them (ordered commit), a PerWorldNode
+//                 clears the trackers -- fvs.cpp:224-239 (see below)
 // The reference draws from a racy thread_local mt19937 inside systems; here
 // every draw is a counter-based hash of (world, entity id, tick, draw index)
 // (SURVEY.md §8d), so any executor (this one, oracle/fvs_oracle.cpp,
@@ -86,7 +88,10 @@ struct Game : public WorldBase {
             ParallelForNode<Engine, archerSystem, Entity, Action, Quiver>>({ act });
         auto mark = builder.addToGraph<
             ParallelForNode<Engine, markDeadSystem, Entity, Health>>({ cast, shoot });
-        builder.addToGraph<PerWorldNode<Engine, cleanupSystem>>({ mark });
+        auto track = builder.addToGraph<PerWorldNode<Engine, trackDeadSystem>>({ mark });
+        auto kill = builder.addToGraph<
+            ParallelForNode<Engine, destroyTrackedSystem, CleanupEntity>>({ track });
+        builder.addToGraph<PerWorldNode<Engine, finishTickSystem>>({ kill });
     }
 
     Game(Engine &ctx, const Config &cfg, const mw_fvs_init &init);
@@ -95,10 +100,12 @@ struct Game : public WorldBase {
     static MW_HD void casterSystem(Engine &ctx, Entity &e, Action &action, Mana &mana);
     static MW_HD void archerSystem(Engine &ctx, Entity &e, Action &action, Quiver &quiver);
     static MW_HD void markDeadSystem(Engine &ctx, Entity &e, Health &h);
-    static MW_HD void cleanupSystem(Engine &ctx);
+    static MW_HD void trackDeadSystem(Engine &ctx);
+    static MW_HD void destroyTrackedSystem(Engine &ctx, CleanupEntity &c);
+    static MW_HD void finishTickSystem(Engine &ctx);
 
     // Entities found dead by markDeadSystem this tick, in arbitrary order;
-    // cleanupSystem restores the reference's query order (archetype, row).
+    // trackDeadSystem restores the reference's query order (archetype, row).
     static constexpr int32_t kMaxDead = 512;
     struct Dead {
         Entity e;
@@ -189,10 +196,19 @@ MW_HD void Game::archerSystem(Engine &ctx, Entity &e, Action &action, Quiver &qu
 }
 
 // The reference's cleanup (fvs.cpp:224-239) walks cleanupQuery serially and
-// makes a CleanupTracker for every entity with hp <= 0, then destroys them
-// all.  The walk is split: every row checks itself in parallel (this node),
-// and the per-world node below sorts the (few) hits back into the walk's
-// order -- query archetype order, then row -- before the serial part.
+// makes a CleanupTracker for every entity with hp <= 0, destroys every
+// tracked entity in tracker order, then clears the trackers.  Here:
+//   markDead     every row checks itself in parallel (atomics into a list);
+//   trackDead    one lane per world sorts the (few) hits back into the
+//                walk's order -- query archetype, then row -- and makes the
+//                trackers (the same IDs as the reference's serial walk);
+//   destroy      a row-parallel node over the trackers: each lane's
+//                destroyEntityNow is deferred and the executor's ordered
+//                commit replays them in tracker order -- the reference's
+//                swap-remove sequence on row indices in LDS, the row moves
+//                of every column spread over the world's block, ID releases
+//                in order (wave-parallel compaction);
+//   finishTick   clears the trackers (bulk ID release) and ticks.
 MW_HD void Game::markDeadSystem(Engine &ctx, Entity &e, Health &h)
 {
     if (h.hp > 0) return;
@@ -205,8 +221,8 @@ MW_HD void Game::markDeadSystem(Engine &ctx, Entity &e, Health &h)
     if (slot < kMaxDead) g.dead[slot] = Dead { e, ctx.getLoc(e) };
 }
 
-MW_HD void Game::cleanupSystem(Engine &ctx)
-{                                                          // fvs.cpp:224-239
+MW_HD void Game::trackDeadSystem(Engine &ctx)
+{
     Game &g = ctx.data();
     const int32_t n = g.numDead < kMaxDead ? g.numDead : kMaxDead;
     if (g.numDead > kMaxDead) ctx.state().errorFlags[ctx.worldID().idx] |= 2;
@@ -222,15 +238,18 @@ MW_HD void Game::cleanupSystem(Engine &ctx)
         g.dead[j + 1] = d;
     }
     for (int32_t i = 0; i < n; i++) ctx.makeEntityNow<CleanupTracker>(CleanupEntity { g.dead[i].e });
-    StateView &st = ctx.state();
-    const int32_t w = ctx.worldID().idx;
-    const int32_t tracker = st.findArchetype(typeKey<CleanupTracker>());
-    const int32_t m = st.arch[tracker].numRows[w];
-    const CleanupEntity *dead = st.column<CleanupEntity>(tracker, 1, w);
-    for (int32_t i = 0; i < m; i++) ctx.destroyEntityNow(dead[i]);
-    ctx.clearArchetype<CleanupTracker>();
     g.numDead = 0;
-    g.tickCount += 1;
+}
+
+MW_HD void Game::destroyTrackedSystem(Engine &ctx, CleanupEntity &c)
+{
+    ctx.destroyEntityNow(c);
+}
+
+MW_HD void Game::finishTickSystem(Engine &ctx)
+{
+    ctx.clearArchetype<CleanupTracker>();
+    ctx.data().tickCount += 1;
 }
 
 Game::Game(Engine &ctx, const Config &cfg, const mw_fvs_init &init)

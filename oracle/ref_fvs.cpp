@@ -20,6 +20,9 @@
 #include <cstring>
 #include <new>
 #include <thread>
+
+#include <pthread.h>
+#include <sched.h>
 #include <vector>
 
 using namespace madrona;
@@ -238,9 +241,23 @@ MADRONA_EXPORT void ref_fvs_step_mt(void *handle, int32_t num_ticks, int32_t num
 {
     auto *v = (std::vector<RefWorld *> *)handle;
     const int32_t W = (int32_t)v->size();
+    // one worker pinned per usable core (src/mw/cpu_exec.cpp:56-93)
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    sched_getaffinity(0, sizeof(allowed), &allowed);
+    std::vector<int> cpus;
+    for (int c = 0; c < CPU_SETSIZE; c++) {
+        if (CPU_ISSET(c, &allowed)) cpus.push_back(c);
+    }
     std::vector<std::thread> pool;
     for (int32_t t = 0; t < num_threads; t++) {
-        pool.emplace_back([=]() {
+        pool.emplace_back([=, &cpus]() {
+            if (!cpus.empty()) {
+                cpu_set_t one;
+                CPU_ZERO(&one);
+                CPU_SET(cpus[t % cpus.size()], &one);
+                pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+            }
             for (int32_t w = t; w < W; w += num_threads) {
                 RefWorld *rw = (*v)[w];
                 for (int32_t s = 0; s < num_ticks; s++) rw->graph->run(rw->ctx);

@@ -3,10 +3,16 @@
 worlds x 50 dragons + 200 knights, deaths destroy entities) on one MI355X.
 Same JSON contract as bench.py; a step = one tick of every world (action
 select, casters, archers, cleanup with device-side destroy / ID release).
-Timed window: ticks warmup+1 .. warmup+K from the reference init, which
-covers the dragons' deaths when K + warmup >= ~1500.
+Timed window: the CHURN window, ticks preroll+1 .. preroll+K (default
+751-1500): the dragons of the reference init start dying at tick ~550 and
+about 90 % of them die between ticks 750 and 1500 (oracle/_ref run of the
+same init), so every timed tick destroys entities, releases IDs and
+compacts rows (the ordered commit's wave-parallel swap-removes).  The CPU
+baseline is the reference's own ECS (oracle/_ref) on the same tick window,
+one pinned worker per usable core, batches of 2048 worlds (the reference
+reserves 48 GiB of address space per world) until ~4 s is timed.
 
-    python tools/bench_fvs.py [--worlds 16384 --steps 1500 --warmup 5]
+    python tools/bench_fvs.py [--worlds 16384 --preroll 750 --steps 750]
 """
 import argparse
 import ctypes
@@ -35,12 +41,17 @@ def world_bytes(node, nd, nk):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--worlds", type=int, default=16384)
-    p.add_argument("--steps", type=int, default=1500)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=750)
+    p.add_argument("--preroll", type=int, default=750,
+                   help="untimed ticks before the window (the warmup)")
     p.add_argument("--dragons", type=int, default=50)
     p.add_argument("--knights", type=int, default=200)
-    p.add_argument("--cpu-worlds", type=int, default=2048)
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-worlds", type=int, default=2048,
+                   help="worlds per CPU batch (the reference reserves address space per world)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = every usable core")
+    p.add_argument("--cpu-target-s", type=float, default=4.0)
+    p.add_argument("--cpu-max-batches", type=int, default=48)
+    p.add_argument("--cpu-first-world", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--chunk", type=int, default=50,
                    help="ticks launched back-to-back per host sync (the reference "
@@ -51,26 +62,46 @@ def parse():
 
 def cpu_child(args):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib as ol
-    inits = ol.gen_fvs_inits(args.cpu_worlds, args.dragons, args.knights, seed=0)
+    import oracle_lib as ol                      # no torch import in the child
+    first = args.cpu_first_world
+    inits = {k: v[first:] for k, v in
+             ol.gen_fvs_inits(first + args.cpu_worlds, args.dragons, args.knights, seed=0).items()}
     threads = max(1, args.cpu_threads)
-    if ol.ref_available():
-        ref = ol.ReferenceFvs(inits)
-        ref.lib.ref_fvs_step_mt.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
-        ref.lib.ref_fvs_step_mt(ref.h, args.warmup, threads)
-        t0 = time.perf_counter()
-        ref.lib.ref_fvs_step_mt(ref.h, args.steps, threads)
-        dt = time.perf_counter() - t0
-        kind = "reference"
-    else:
-        orc = ol.OracleFvs(inits)
-        orc.step(args.warmup)
-        t0 = time.perf_counter()
-        orc.step(args.steps)
-        dt = time.perf_counter() - t0
-        kind = "port"
-        threads = 1
-    print(json.dumps({"kind": kind, "seconds": dt, "threads": threads}))
+    ref = ol.ReferenceFvs(inits, first_world_index=args.cpu_first_world)
+    ref.lib.ref_fvs_step_mt.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+    ref.lib.ref_fvs_step_mt(ref.h, args.preroll, threads)
+    t0 = time.perf_counter()
+    ref.lib.ref_fvs_step_mt(ref.h, args.steps, threads)
+    dt = time.perf_counter() - t0
+    alive = sum(len(ref.table(w, 0)) for w in range(0, args.cpu_worlds, max(1, args.cpu_worlds // 64)))
+    print(json.dumps({"kind": "reference", "seconds": dt, "threads": threads, "alive": alive}))
+
+
+def cpu_baseline(args):
+    sys.path.insert(0, ROOT)
+    from bench import cpu_model, usable_cores
+    threads = args.cpu_threads if args.cpu_threads > 0 else usable_cores()
+    total_s, batches, t_wall = 0.0, 0, time.perf_counter()
+    while batches < args.cpu_max_batches and total_s < args.cpu_target_s:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child",
+                            "--cpu-worlds", str(args.cpu_worlds), "--cpu-threads", str(threads),
+                            "--cpu-first-world", str(batches * args.cpu_worlds),
+                            "--steps", str(args.steps), "--preroll", str(args.preroll),
+                            "--dragons", str(args.dragons), "--knights", str(args.knights)],
+                           capture_output=True, text=True, timeout=1200)
+        if r.returncode != 0:
+            raise RuntimeError(f"cpu baseline child failed: {r.stderr[-2000:]}")
+        res = json.loads(r.stdout.strip().splitlines()[-1])
+        total_s += res["seconds"]
+        batches += 1
+    worlds = batches * args.cpu_worlds
+    return {"value": round(worlds * args.steps / total_s, 1), "unit": "env-steps/s",
+            "cores": threads, "cpu_model": cpu_model(), "kind": "reference",
+            "sample": f"fantasy_vs {batches} batches x {args.cpu_worlds} worlds (worlds 0-{worlds - 1}) "
+                      f"x ({args.dragons} dragons + {args.knights} knights), ticks "
+                      f"{args.preroll + 1}-{args.preroll + args.steps} (the GPU's timed window), "
+                      f"{threads} host threads pinned one per usable core, {total_s:.2f} s timed / "
+                      f"{time.perf_counter() - t_wall:.1f} s wall"}
 
 
 def main():
@@ -89,9 +120,13 @@ def main():
     sim.close()
     sim = mw.FvsSim(W, inits)
     dom = max(node_ms, key=lambda n: node_ms[n] * (4 if n == "ParallelForNode" else 1))
-    for _ in range(args.warmup):
-        sim.step(1)
+    left = args.preroll
+    while left > 0:
+        n = min(args.chunk, left)
+        sim.step(n)
+        left -= n
     sim.sync()
+    alive0 = sum(sim.num_rows(w, 0) for w in range(0, W, max(1, W // 64)))
     # throughput: the plain step graph, chunks of ticks per host sync
     t0 = time.perf_counter()
     left = args.steps
@@ -101,6 +136,7 @@ def main():
         left -= n
     sim.sync()
     elapsed = time.perf_counter() - t0
+    alive = sum(sim.num_rows(w, 0) for w in range(0, W, max(1, W // 64)))
     # per-launch kernel time: HIP events around every launch of the dominant
     # node kind (graph split at that node), one tick per sync, 100 ticks
     sim.set_timed_node(dom)
@@ -110,35 +146,21 @@ def main():
     ms0, n0 = 0.0, 0
     sim.set_timed_node(None)
     flags = sim.error_flags()
-    alive = sum(sim.num_rows(w, 0) for w in range(0, W, max(1, W // 64)))
 
     launch_ms = (ms1 - ms0) / max(1, n1 - n0)
     nbytes = W * world_bytes(dom, args.dragons, args.knights)
     achieved = nbytes / (launch_ms * 1e-3) / 1e9
-    cpu = None
-    if not args.no_cpu_baseline:
-        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child",
-                            "--cpu-worlds", str(args.cpu_worlds), "--cpu-threads",
-                            str(args.cpu_threads), "--steps", str(args.steps), "--warmup",
-                            str(args.warmup), "--dragons", str(args.dragons), "--knights",
-                            str(args.knights)], capture_output=True, text=True, timeout=1200)
-        if r.returncode == 0:
-            res = json.loads(r.stdout.strip().splitlines()[-1])
-            cpu = {"value": round(args.cpu_worlds * args.steps / res["seconds"], 1),
-                   "unit": "env-steps/s", "cores": res["threads"], "kind": res["kind"],
-                   "sample": f"fantasy_vs {args.cpu_worlds} worlds x ({args.dragons} dragons + "
-                             f"{args.knights} knights), ticks {args.warmup + 1}-"
-                             f"{args.warmup + args.steps}, {res['threads']} host threads, "
-                             f"{res['seconds']:.2f} s"}
+    cpu = None if args.no_cpu_baseline else cpu_baseline(args)
     out = {
         "metric": "env-steps/sec (summed worlds)", "value": round(W * args.steps / elapsed, 1),
-        "unit": "env-steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "unit": "env-steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.preroll,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "warmup_note": "warmup = the untimed preroll ticks",
         "scaling": "weak", "vs_baseline": None, "dtype": "f32+i32",
         "data": "synthetic (reference example init, mt19937 seed 0; counter-based in-tick draws)",
         "config": {"workload": f"examples/fantasy_vs restated: {W} worlds x ({args.dragons} "
                                f"dragons + {args.knights} knights), Game::tick with cleanup",
-                   "timed_ticks": f"{args.warmup + 1}-{args.warmup + args.steps}"},
+                   "timed_ticks": f"{args.preroll + 1}-{args.preroll + args.steps}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": None, "ms_per_launch": round(launch_ms, 4),
@@ -147,7 +169,9 @@ def main():
                      "bytes_per_launch": int(nbytes)},
         "cpu_baseline": cpu, "error_flags": flags,
         "nodes_ms_per_launch_preroll": {k: round(v, 4) for k, v in node_ms.items()},
-        "dragons_alive_sampled_worlds": int(alive),
+        "dragons_alive_sampled_worlds": {"window_start": int(alive0), "window_end": int(alive),
+                                          "sampled_worlds": len(range(0, W, max(1, W // 64))),
+                                          "at_init": args.dragons * len(range(0, W, max(1, W // 64)))},
     }
     print(json.dumps(out))
     sim.close()
