@@ -8,8 +8,10 @@ dt=1/60) on MI355X.
 A "step" = one taskgraph step of every world (broadphase, 4 XPBD substeps of
 integrate / narrowphase / solve, cleanup, episode-return node) replayed as one
 hipGraph, followed by the training hand-off: the per-world episode returns are
-copied into a device buffer and, for N > 1, all-gathered over RCCL (xGMI) by
-the framework on its step stream.
+copied into a torch tensor on the device and, for N > 1, all-gathered over
+RCCL (xGMI) into it, by the framework on its step stream.  Steps and
+hand-offs are enqueued back to back (no host round trip per step); the timed
+region is closed by a device sync.
 Worlds are sharded contiguously across ranks (weak scaling: 8192 per GPU;
 N = 8 is BASELINE.json configs[3], 65 536 worlds).
 
@@ -230,16 +232,17 @@ def main():
     returns = torch.empty(W * world_size, dtype=torch.float32, device=f"cuda:{local_rank}")
     handoff = returns.data_ptr()
 
+    # Every step is enqueued without a host round trip: the step graph, then
+    # the hand-off (D2D copy / RCCL all-gather of the returns into the torch
+    # tensor) on the same stream; the timed region ends with a device sync.
     def step():
-        if args.no_handoff:
-            sim.step(1)
-            return
         sim.step_async(1)
+        if args.no_handoff:
+            return
         if dist is not None:
             sim.allgather_exported(2, handoff, 4 * W)
-            sim.sync()
         else:
-            sim.copy_exported(2, handoff, 4 * W)     # D2D on the step stream + sync
+            sim.copy_exported_async(2, handoff, 4 * W)
 
     def barrier():
         if dist is not None:

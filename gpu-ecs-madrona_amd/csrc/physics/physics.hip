@@ -395,6 +395,7 @@ struct PhysNodeBase : NodeBase {
             return b.addDefaultNode<NAME>(deps, ctx);                                \
         }                                                                            \
         static const char *nodeName() { return #NAME; }                             \
+        static constexpr bool kNoTmpAlloc = true;                                    \
         static void launch(NAME *self, LaunchCtx &lc)                                \
         {                                                                            \
             const PhysArgs &P = self->mod->args;                                     \

@@ -207,6 +207,15 @@ int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_byt
     }, (int64_t)-1)
 }
 
+int64_t mw_copy_exported_async(mw_exec *exec, int32_t slot, void *dst, int64_t max_bytes)
+{
+    MW_TRY({
+        const int64_t n = exec->exec->copyExportedAsync(slot, dst, max_bytes);
+        if (n < 0) throw std::runtime_error("mw_copy_exported_async: no such export slot");
+        return n;
+    }, (int64_t)-1)
+}
+
 void *mw_stream(mw_exec *exec) { return exec ? exec->exec->stream() : nullptr; }
 
 int mw_stream_wait(mw_exec *exec, void *stream)

@@ -43,12 +43,14 @@ StateManager &TaskGraph::Builder::stateManager()
 }
 
 TaskGraph::NodeID TaskGraph::Builder::registerNode(std::shared_ptr<void> data, LaunchFn fn,
-                                                   Span<const NodeID> deps, const char *name)
+                                                   Span<const NodeID> deps, const char *name,
+                                                   uint32_t flags)
 {                                               // taskgraph.cpp:18-44
     Staged s;
     s.data = std::move(data);
     s.fn = fn;
     s.name = name;
+    s.flags = flags;
     for (const NodeID &d : deps) s.deps.push_back(d.id);
     staged_.push_back(std::move(s));
     return NodeID { (uint32_t)staged_.size() - 1 };
@@ -65,7 +67,7 @@ TaskGraph TaskGraph::Builder::build()
     }
     std::vector<bool> queued(n, false);
     if (!staged_[0].deps.empty()) throw std::runtime_error("first node has dependencies");
-    g.nodes_.push_back(Node { staged_[0].data, staged_[0].fn, staged_[0].name });
+    g.nodes_.push_back(Node { staged_[0].data, staged_[0].fn, staged_[0].name, staged_[0].flags });
     queued[0] = true;
     size_t remaining = n - 1;
     while (remaining > 0) {
@@ -78,7 +80,8 @@ TaskGraph TaskGraph::Builder::build()
         // The reference spins forever here; report the bad dependency instead.
         if (!ok) throw std::runtime_error("taskgraph: node depends on a later node");
         queued[cur] = true;
-        g.nodes_.push_back(Node { staged_[cur].data, staged_[cur].fn, staged_[cur].name });
+        g.nodes_.push_back(Node { staged_[cur].data, staged_[cur].fn, staged_[cur].name,
+                                  staged_[cur].flags });
         remaining--;
     }
     g.datas_ = datas_;
@@ -214,10 +217,25 @@ __global__ void __launch_bounds__(256) structuralCommitKernel(CommitArgs A)
     char *scratch = A.scratch + (size_t)blockIdx.x * A.scratchPerBlock;
     const int32_t tid = threadIdx.x;
 
-    for (int32_t w = blockIdx.x; w < st.numWorlds; w += gridDim.x) {
+    // Most nodes mutate nothing: every lane checks one world, and only the
+    // worlds with work are walked (one block each).
+    __shared__ int32_t work[256];
+    __shared__ int32_t num_work;
+    for (int32_t chunk = blockIdx.x * 256; chunk < st.numWorlds; chunk += gridDim.x * 256) {
+    if (tid == 0) num_work = 0;
+    __syncthreads();
+    {
+        const int32_t cw = chunk + tid;
+        if (cw < st.numWorlds && (st.appendDirty[cw] != 0 || st.deferCount[cw] != 0)) {
+            work[atomicAdd(&num_work, 1)] = cw;
+        }
+    }
+    __syncthreads();
+    const int32_t nwork = num_work;
+    for (int32_t wi = 0; wi < nwork; wi++) {
+        const int32_t w = work[wi];
         const uint64_t dirty = st.appendDirty[w];
         int32_t nops = st.deferCount[w];
-        if (dirty == 0 && nops == 0) continue;
         nops = min(nops, st.deferCap);
         DeferredDestroy *log = st.deferLog + (size_t)w * st.deferCap;
         IDMapView ids = st.ids(w);
@@ -366,6 +384,8 @@ __global__ void __launch_bounds__(256) structuralCommitKernel(CommitArgs A)
         }
         __syncthreads();
     }
+    __syncthreads();
+    }
 }
 
 namespace detail {
@@ -374,7 +394,7 @@ void launchStructuralCommit(LaunchCtx &lc)
 {
     const CommitArgs *A = lc.exec ? (const CommitArgs *)lc.exec->commitArgs() : nullptr;
     if (!A || A->capMax <= 0) return;
-    const uint32_t blocks = (uint32_t)std::min<int64_t>(lc.numWorlds, 512);
+    const uint32_t blocks = (uint32_t)std::min<int64_t>((lc.numWorlds + 255) / 256, 512);
     const size_t lds = (size_t)A->capMax * 8 + (size_t)(A->sortA + A->sortO) * 8;
     hipLaunchKernelGGL(structuralCommitKernel, dim3(blocks), dim3(256), lds,
                        (hipStream_t)lc.stream, *A);
@@ -539,10 +559,13 @@ struct Executor::Impl {
     // Live per-node timing: HIP events recorded around every launch of one
     // node kind inside each step, accumulated at each sync.
     std::string timedName;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> timedEvents;
+    // One event pair per timed launch per enqueued step: a burst of
+    // runAsync steps keeps every step's pairs until the next sync.
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timedPool;
+    int32_t timedPerStep = 0;       // timed launches in one step
+    int32_t pendingSteps = 0;       // steps enqueued since the last sync
     double timedMs = 0.0;
     int64_t timedLaunches = 0;
-    bool timedPending = false;
 
     // Device tracing: null unless enabled (Executor::enableTracing).
     mwGPU::TraceDev *trace = nullptr;
@@ -556,6 +579,10 @@ struct Executor::Impl {
     int32_t defaultBlocksPerCU = 0;
     int32_t numCUs = 0;
     std::vector<int32_t> nodeBlocksPerCU;
+    // ResetTmpAllocNodes with no possibly-allocating node since the previous
+    // launched reset (the start of a step counts as one: the previous
+    // step's tail) are no-ops: not launched.
+    std::vector<uint8_t> nodeSkip;
 
     // Device copies of the graph's node data (TaskGraph::NodeData blocks).
     char *nodeDataDev = nullptr;
@@ -586,7 +613,7 @@ Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
 
 Executor::~Executor()
 {
-    for (auto &e : impl_->timedEvents) {
+    for (auto &e : impl_->timedPool) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
@@ -739,6 +766,14 @@ static void traceMarker(Executor::Impl &I, mwGPU::DeviceEvent ev, uint32_t func,
 // A node's launches; with tracing on, bracketed by nodeStart / nodeFinish.
 static void launchNode(Executor::Impl &I, int32_t i, LaunchCtx &lc)
 {
+    if (i < (int32_t)I.nodeSkip.size() && I.nodeSkip[i]) {
+        if (I.trace) {              // an elided node still appears in the trace, empty
+            const uint32_t f = I.nodeFunc[i], n = (uint32_t)I.cfg.numWorlds;
+            traceMarker(I, mwGPU::DeviceEvent::nodeStart, f, n, (uint32_t)i);
+            traceMarker(I, mwGPU::DeviceEvent::nodeFinish, f, n, (uint32_t)i);
+        }
+        return;
+    }
     const int32_t bpc = i < (int32_t)I.nodeBlocksPerCU.size() ? I.nodeBlocksPerCU[i] : -1;
     lc.blocksPerCU = bpc >= 0 ? bpc : I.defaultBlocksPerCU;
     lc.numCUs = I.numCUs;
@@ -767,17 +802,30 @@ static void traceStepEnd(Executor::Impl &I)
     }
 }
 
+// Event pair `ev` of the step being enqueued (created on first use).
+static std::pair<hipEvent_t, hipEvent_t> &timedPair(Executor::Impl &I, int32_t ev)
+{
+    const size_t i = (size_t)I.pendingSteps * I.timedPerStep + ev;
+    while (I.timedPool.size() <= i) {
+        hipEvent_t a, b;
+        MW_HIP_CHECK(hipEventCreate(&a));
+        MW_HIP_CHECK(hipEventCreate(&b));
+        I.timedPool.push_back({ a, b });
+    }
+    return I.timedPool[i];
+}
+
 // One step's launch sequence: every node in sorted order, then the export
 // gathers.  Nodes of the timed kind are bracketed by their own event pair.
 static void launchStep(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
 {
-    size_t ev = 0;
+    int32_t ev = 0;
     traceStepBegin(I);
     for (int32_t i = 0; i < I.graph.numNodes(); i++) {
         const bool timed = isTimed(I, i);
-        if (timed) MW_HIP_CHECK(hipEventRecord(I.timedEvents[ev].first, I.stream));
+        if (timed) MW_HIP_CHECK(hipEventRecord(timedPair(I, ev).first, I.stream));
         launchNode(I, i, lc);
-        if (timed) MW_HIP_CHECK(hipEventRecord(I.timedEvents[ev++].second, I.stream));
+        if (timed) MW_HIP_CHECK(hipEventRecord(timedPair(I, ev++).second, I.stream));
     }
     launchExports(I, dv);
     traceStepEnd(I);
@@ -791,6 +839,12 @@ static void captureGraph(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
     }
     I.segs.clear();
     const int32_t n = I.graph.numNodes();
+    // Live node timing splits the step graph at each launch of the timed
+    // kind, which runs on the stream between segments bracketed by events:
+    // HIP here refuses event records captured into a graph for timing
+    // (hipEventRecordWithFlags(..., hipEventRecordExternal) during capture:
+    // "invalid argument" on the MI355X box).  Cost measured there: +2 % per
+    // step with SolverNode timed (4 splits).
     int32_t start = 0;
     for (int32_t i = 0; i <= n; i++) {
         const bool last = i == n;
@@ -884,6 +938,20 @@ void Executor::setNodeBlocksPerCU(int32_t node, int32_t blocks_per_cu)
 void Executor::setGraph(TaskGraph &&graph)
 {
     impl_->graph = std::move(graph);
+    {
+        const TaskGraph &g = impl_->graph;
+        impl_->nodeSkip.assign(g.numNodes(), 0);
+        bool alloc_since = true;
+        for (int32_t i = 0; i < g.numNodes(); i++) {
+            const uint32_t f = g.nodeFlags(i);
+            if (f & TaskGraph::kNodeTmpAllocReset) {
+                impl_->nodeSkip[i] = alloc_since ? 0 : 1;
+                alloc_since = false;
+            } else if (!(f & TaskGraph::kNodeNoTmpAlloc)) {
+                alloc_since = true;
+            }
+        }
+    }
     // Node data blocks to the device; NodeBase-derived blocks learn the
     // device state first (NodeBase::makeContext).
     {
@@ -910,39 +978,39 @@ void Executor::setGraph(TaskGraph &&graph)
 
 void Executor::runAsync()
 {
-    const StateView &dv = impl_->mgr->deviceViewHost();
-    LaunchCtx lc = makeLaunchCtx(*impl_, this);
-    if (!impl_->segs.empty()) {
-        size_t ev = 0;
-        for (auto &sg : impl_->segs) {
-            if (sg.exec) MW_HIP_CHECK(hipGraphLaunch(sg.exec, impl_->stream));
+    Impl &I = *impl_;
+    const StateView &dv = I.mgr->deviceViewHost();
+    LaunchCtx lc = makeLaunchCtx(I, this);
+    if (!I.segs.empty()) {
+        int32_t ev = 0;
+        for (auto &sg : I.segs) {
+            if (sg.exec) MW_HIP_CHECK(hipGraphLaunch(sg.exec, I.stream));
             if (sg.timedNode >= 0) {
-                MW_HIP_CHECK(hipEventRecord(impl_->timedEvents[ev].first, impl_->stream));
-                launchNode(*impl_, sg.timedNode, lc);
-                MW_HIP_CHECK(hipEventRecord(impl_->timedEvents[ev].second, impl_->stream));
+                MW_HIP_CHECK(hipEventRecord(timedPair(I, ev).first, I.stream));
+                launchNode(I, sg.timedNode, lc);
+                MW_HIP_CHECK(hipEventRecord(timedPair(I, ev).second, I.stream));
                 ev++;
             }
         }
     } else {
-        launchStep(*impl_, lc, dv);
+        launchStep(I, lc, dv);
     }
-    impl_->timedPending = !impl_->timedEvents.empty();
+    if (I.timedPerStep > 0) I.pendingSteps++;
 }
 
 void Executor::sync()
 {
-    MW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
-    if (impl_->timedPending) {
-        // Events hold the most recent step's launches (earlier unsynced steps
-        // of a runAsync burst are not double counted).
-        for (auto &e : impl_->timedEvents) {
-            float ms = 0;
-            MW_HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
-            impl_->timedMs += ms;
-            impl_->timedLaunches++;
-        }
-        impl_->timedPending = false;
+    Impl &I = *impl_;
+    MW_HIP_CHECK(hipStreamSynchronize(I.stream));
+    // every enqueued step's timed launches since the last sync
+    const size_t n = (size_t)I.pendingSteps * I.timedPerStep;
+    for (size_t i = 0; i < n; i++) {
+        float ms = 0;
+        MW_HIP_CHECK(hipEventElapsedTime(&ms, I.timedPool[i].first, I.timedPool[i].second));
+        I.timedMs += ms;
+        I.timedLaunches++;
     }
+    I.pendingSteps = 0;
 }
 
 void Executor::run()
@@ -955,21 +1023,12 @@ void Executor::setTimedNode(const char *name)
 {
     sync();
     impl_->timedName = name ? name : "";
-    for (auto &e : impl_->timedEvents) {
-        MW_HIP_CHECK(hipEventDestroy(e.first));
-        MW_HIP_CHECK(hipEventDestroy(e.second));
-    }
-    impl_->timedEvents.clear();
     impl_->timedMs = 0.0;
     impl_->timedLaunches = 0;
+    impl_->timedPerStep = 0;
     if (!impl_->timedName.empty()) {
         for (int32_t i = 0; i < impl_->graph.numNodes(); i++) {
-            if (impl_->timedName == impl_->graph.nodeName(i)) {
-                hipEvent_t a, b;
-                MW_HIP_CHECK(hipEventCreate(&a));
-                MW_HIP_CHECK(hipEventCreate(&b));
-                impl_->timedEvents.push_back({ a, b });
-            }
+            if (impl_->timedName == impl_->graph.nodeName(i)) impl_->timedPerStep++;
         }
     }
     const StateView &dv = impl_->mgr->deviceViewHost();
@@ -1094,6 +1153,26 @@ int64_t Executor::copyExported(int32_t slot, void *dst, int64_t max_bytes)
         }
         sync();
         return std::min(*total * (int64_t)b.bytes, span);
+    }
+    return -1;
+}
+
+// Device-side hand-off: the copy is enqueued on the executor stream behind
+// the steps enqueued so far and the host does not wait (the learner orders
+// its stream after it with mw_stream_wait).  dst receives min(max_bytes, the
+// export buffer) bytes; bytes past the packed rows are unspecified.
+int64_t Executor::copyExportedAsync(int32_t slot, void *dst, int64_t max_bytes)
+{
+    for (ExportBuf &b : impl_->exports) {
+        if (b.slot != slot) continue;
+        const StateView &dv = impl_->mgr->deviceViewHost();
+        const int64_t buf_bytes = (int64_t)dv.numWorlds * dv.arch[b.archetype].capacity * b.bytes;
+        const int64_t span = std::min(std::max<int64_t>(max_bytes, 0), buf_bytes);
+        if (span > 0) {
+            MW_HIP_CHECK(hipMemcpyAsync(dst, b.buf, (size_t)span, hipMemcpyDeviceToDevice,
+                                        impl_->stream));
+        }
+        return span;
     }
     return -1;
 }

@@ -63,6 +63,8 @@ public:
     // Stream-ordered copy of export `slot` into dst (device or host), one
     // sync; returns the bytes of packed rows copied (-1: no such slot).
     int64_t copyExported(int32_t slot, void *dst, int64_t max_bytes);
+    // Same copy (device destination), enqueued without a host wait.
+    int64_t copyExportedAsync(int32_t slot, void *dst, int64_t max_bytes);
     void copyOutExports();
     int32_t exportRowBytes(int32_t slot);
     int64_t exportBufferBytes(int32_t slot);  // capacity of the packed buffer

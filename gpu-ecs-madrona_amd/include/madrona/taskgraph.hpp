@@ -117,6 +117,13 @@ public:
 
     using LaunchFn = void (*)(void *node, LaunchCtx &lc);
 
+    // Node flags: a framework node whose kernels never call Context::tmpAlloc
+    // (static constexpr bool kNoTmpAlloc), and ResetTmpAllocNode itself.  A
+    // reset with no possibly-allocating node since the previous one is a
+    // no-op and is not launched (the physics substeps reset twice each).
+    static constexpr uint32_t kNodeNoTmpAlloc = 1;
+    static constexpr uint32_t kNodeTmpAllocReset = 2;
+
     class Builder {
     public:
         explicit Builder(Context &ctx);
@@ -193,9 +200,12 @@ public:
         {
             if constexpr (requires(NodeT *n, LaunchCtx &lc) { NodeT::launch(n, lc); }) {
                 auto data = std::make_shared<NodeT>(std::forward<Args>(args)...);
+                uint32_t flags = 0;
+                if constexpr (requires { NodeT::kNoTmpAlloc; }) flags |= kNodeNoTmpAlloc;
+                if constexpr (requires { NodeT::kTmpAllocReset; }) flags |= kNodeTmpAllocReset;
                 return registerNode(std::static_pointer_cast<void>(data),
                                     [](void *n, LaunchCtx &lc) { NodeT::launch((NodeT *)n, lc); },
-                                    dependencies, NodeT::nodeName());
+                                    dependencies, NodeT::nodeName(), flags);
             } else {
                 auto data_id = constructNodeData<NodeT>(std::forward<Args>(args)...);
                 return addNodeFn<&NodeT::run>(data_id, dependencies, Optional<NodeID>::none(), 1);
@@ -229,13 +239,14 @@ public:
         }
 
         NodeID registerNode(std::shared_ptr<void> data, LaunchFn fn,
-                            Span<const NodeID> deps, const char *name);
+                            Span<const NodeID> deps, const char *name, uint32_t flags = 0);
 
         struct Staged {
             std::shared_ptr<void> data;
             LaunchFn fn;
             std::vector<uint32_t> deps;
             const char *name;
+            uint32_t flags;
         };
 
         Context *ctx_;
@@ -249,6 +260,7 @@ public:
     void launchNode(int32_t i, LaunchCtx &lc) const { nodes_[i].fn(nodes_[i].data.get(), lc); }
     int32_t numNodes() const { return (int32_t)nodes_.size(); }
     const char *nodeName(int32_t i) const { return nodes_[i].name; }
+    uint32_t nodeFlags(int32_t i) const { return nodes_[i].flags; }
 
     // Node data blocks, for the executor to upload (NodeBase-derived blocks
     // get the device state filled in first).
@@ -261,6 +273,7 @@ private:
         std::shared_ptr<void> data;
         LaunchFn fn;
         const char *name;
+        uint32_t flags;
     };
     std::vector<Node> nodes_;
     std::vector<NodeData> datas_;
@@ -574,6 +587,7 @@ public:
     }
     static void launch(ClearTmpNode *self, LaunchCtx &lc) { launchClearRows(lc, self->archetype_); }
     static const char *nodeName() { return "ClearTmpNode"; }
+    static constexpr bool kNoTmpAlloc = true;
 
     int32_t archetype_;
 };
@@ -592,6 +606,8 @@ public:
     }
     static void launch(ResetTmpAllocNode *, LaunchCtx &lc) { launchResetTmpAlloc(lc); }
     static const char *nodeName() { return "ResetTmpAllocNode"; }
+    static constexpr bool kNoTmpAlloc = true;
+    static constexpr bool kTmpAllocReset = true;
 };
 
 }

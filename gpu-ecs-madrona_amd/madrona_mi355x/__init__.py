@@ -123,6 +123,9 @@ _lib.mw_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void
 _lib.mw_phys_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 _lib.mw_copy_exported.restype = ctypes.c_int64
 _lib.mw_copy_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
+_lib.mw_copy_exported_async.restype = ctypes.c_int64
+_lib.mw_copy_exported_async.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                        ctypes.c_int64]
 _lib.mw_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
 _lib.mw_gen_fvs_inits.argtypes = [ctypes.c_int32] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
@@ -172,7 +175,7 @@ C_ABI_SYMBOLS = (
     "mw_num_nodes", "mw_node_name", "mw_node_blocks_per_cu", "mw_set_node_blocks_per_cu",
     "mw_parse_exec_config_override", "mw_parse_exec_config_file",
     "mw_export_row_bytes", "mw_load_env", "mw_num_envs", "mw_env_name",
-    "mw_entity_loc",
+    "mw_entity_loc", "mw_copy_exported_async",
 )
 
 
@@ -396,6 +399,14 @@ class Executor:
 
     def copy_exported(self, slot, dst_ptr, max_bytes):
         n = _lib.mw_copy_exported(self.h, slot, ctypes.c_void_p(dst_ptr), max_bytes)
+        if n < 0:
+            raise _err()
+        return n
+
+    def copy_exported_async(self, slot, dst_ptr, max_bytes):
+        """Enqueue the hand-off copy of export `slot` into device memory
+        dst_ptr on the executor stream (no host wait)."""
+        n = _lib.mw_copy_exported_async(self.h, slot, ctypes.c_void_p(dst_ptr), max_bytes)
         if n < 0:
             raise _err()
         return n

@@ -134,6 +134,14 @@ void *mw_get_exported(mw_exec *exec, int32_t slot, int64_t *num_rows);
  * past that count (up to max_bytes) are unspecified.                      */
 int64_t mw_copy_exported(mw_exec *exec, int32_t slot, void *dst, int64_t max_bytes);
 
+/* The training hand-off without a host round trip: a device-to-device copy
+ * of min(max_bytes, the slot's buffer) bytes of export slot `slot` into
+ * device memory `dst`, enqueued on the executor stream behind every step
+ * enqueued so far; returns the bytes enqueued and does not wait (order a
+ * consumer's stream after it with mw_stream_wait).  Bytes past the packed
+ * rows are unspecified.                                                    */
+int64_t mw_copy_exported_async(mw_exec *exec, int32_t slot, void *dst, int64_t max_bytes);
+
 /* Bytes of one packed row of export slot `slot` (-1: no such slot). */
 int32_t mw_export_row_bytes(mw_exec *exec, int32_t slot);
 
