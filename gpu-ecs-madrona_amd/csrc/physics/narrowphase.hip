@@ -567,6 +567,7 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
         if (keep) {
             wk.slot = S + (off & 1023);
             slots[wk.slot].numPoints = 0;
+            P.survInfo[(size_t)w * cap + wk.slot] = kNoManifold;
             if (hh) stage[nhh + ((off >> 10) & 1023)] = wk;
             if (pl) stage[cap - 1 - (npl + (off >> 20))] = wk;
         }
@@ -725,6 +726,20 @@ size_t contactSharedBytes(const PhysArgs &P)
     return contactLDSBytes(P.clipCap);
 }
 
+// Body slot (the solver's per-world body index) of a pair member.
+__device__ __forceinline__ int32_t slotOf(const PhysArgs &P, int32_t arch_idx, Loc l)
+{
+    return P.body[arch_idx].slotBase + l.row;
+}
+
+// The survivor's compact solver record: ref / alt body slots.
+__device__ __forceinline__ void recordManifold(const PhysArgs &P, int32_t w, int32_t slot,
+                                               int32_t ref_slot, int32_t alt_slot)
+{
+    P.survInfo[(size_t)w * P.candCapacity + slot] =
+        (uint32_t)(ref_slot & 0xffff) | ((uint32_t)(alt_slot & 0xffff) << 16);
+}
+
 // createFaceContact / createFacePlaneContact / createEdgeContact
 // (narrowphase.cpp:866-1121) for one job per lane.
 __global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
@@ -791,6 +806,7 @@ __global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
                 }
             } while (hidx != start && ++steps <= ha.numHedges);
             storeFaceManifold(out, plane.normal, clip0, depths, n, wk.b, wk.a);
+            if (n > 0) recordManifold(P, w, wk.slot, slotOf(P, wk.bArch, wk.b), slotOf(P, wk.aArch, wk.a));
         } else if (job.kind == kJobFace) {
             const bool a_is_ref = job.refIsA != 0;
             const HullDev hb = O.hulls[wk.bObj];
@@ -856,6 +872,10 @@ __global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
             }
             storeFaceManifold(out, ref_plane.normal, cin, depths, n_below,
                               a_is_ref ? wk.a : wk.b, a_is_ref ? wk.b : wk.a);
+            if (n_below > 0) {
+                const int32_t sa = slotOf(P, wk.aArch, wk.a), sb = slotOf(P, wk.bArch, wk.b);
+                recordManifold(P, w, wk.slot, a_is_ref ? sa : sb, a_is_ref ? sb : sa);
+            }
         } else {
             const HullDev hb = O.hulls[wk.bObj];
             const HullXform xa = hullXform(P, w, P.body[wk.aArch], wk.a.row);
@@ -875,6 +895,7 @@ __global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
             out.numPoints = 1;
             out.normal = ident.rotateVec(job.plane.normal);
             for (int k = 0; k < 4; k++) out.lambdaN[k] = 0.f;
+            recordManifold(P, w, wk.slot, slotOf(P, wk.aArch, wk.a), slotOf(P, wk.bArch, wk.b));
         }
     }
 }

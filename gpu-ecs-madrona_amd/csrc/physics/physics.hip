@@ -314,7 +314,7 @@ void PhysicsModule::upload(void *stream_ptr)
     O.polygons = devUpload(polygons, stream);
 
     P.bodyAABBs = devAlloc<AABB>((size_t)W * std::max(P.maxBodiesPerWorld, 1), stream);
-    P.survivors = devAlloc<int32_t>((size_t)W * P.candCapacity, stream);
+    P.survInfo = devAlloc<uint32_t>((size_t)W * P.candCapacity, stream);
     P.survCount = devAlloc<int32_t>(W, stream);
     P.satWork = devAlloc<SatWork>((size_t)W * P.candCapacity, stream);
     P.satWorkCount = devAlloc<int32_t>(2, stream);

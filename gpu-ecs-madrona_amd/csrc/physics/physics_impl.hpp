@@ -127,7 +127,9 @@ struct PhysArgs {
 
 
     math::AABB *bodyAABBs;        // [W][maxBodiesPerWorld] world AABB per body slot (substep)
-    int32_t *survivors;           // [W][candCapacity] candidates passing the AABB recheck
+    uint32_t *survInfo;           // [W][candCapacity] per survivor slot: the body slots of
+                                  // its manifold's ref | alt << 16, kNoManifold without one
+                                  // (the solver reads this instead of the Contact records)
     int32_t *survCount;           // [W] survivors per world
     struct SatWork *satWork;      // [W * candCapacity] SAT work list (one per survivor)
     int32_t *satWorkCount;        // [1] entries in satWork this substep
@@ -161,6 +163,8 @@ struct PhysArgs {
 
     ObjDev objs;
 };
+
+inline constexpr uint32_t kNoManifold = 0xFFFF'FFFFu;
 
 // Error flag bits (StateView::errorFlags)
 inline constexpr int32_t kErrIDStoreFull = 1;

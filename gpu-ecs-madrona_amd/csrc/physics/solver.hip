@@ -457,15 +457,25 @@ __device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, So
 }
 
 // Number of survivors with a manifold (the world's contact count), capped at
-// maxContacts like the reference's assert (narrowphase.cpp:1130).
+// maxContacts like the reference's assert (narrowphase.cpp:1130).  Reads the
+// compact per-survivor records (4 B, coalesced) with 8 chunks' loads in
+// flight, instead of the 112-B Contact records.
+constexpr int32_t kInfoUnroll = 8;
+
 __device__ __forceinline__ int32_t worldContactCount(const PhysArgs &P, int32_t w, int32_t lane)
 {
-    const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
+    const uint32_t *info = P.survInfo + (size_t)w * P.candCapacity;
     const int32_t S = P.survCount[w];
     int32_t K = 0;
-    for (int32_t chunk = 0; chunk < S; chunk += kSolverBlock) {
-        const int32_t s = chunk + lane;
-        K += __popcll(__ballot(s < S && cslots[s].numPoints > 0));
+    for (int32_t chunk = 0; chunk < S; chunk += kSolverBlock * kInfoUnroll) {
+        uint32_t v[kInfoUnroll];
+#pragma unroll
+        for (int32_t u = 0; u < kInfoUnroll; u++) {
+            const int32_t s = chunk + u * kSolverBlock + lane;
+            v[u] = s < S ? info[s] : kNoManifold;
+        }
+#pragma unroll
+        for (int32_t u = 0; u < kInfoUnroll; u++) K += __popcll(__ballot(v[u] != kNoManifold));
     }
     if (K > P.maxContacts) {
         if (lane == 0) atomicOr(P.errorFlags + w, kErrContactOverflow);
@@ -512,25 +522,33 @@ __device__ __forceinline__ int32_t orderAndLevel(const PhysArgs &P, int32_t w, S
                                                  PrevPtr prevs, int32_t lane)
 {
     const int32_t nb = P.maxBodiesPerWorld;
-    const Contact *cslots = P.candContacts + (size_t)w * P.candCapacity;
+    const uint32_t *info = P.survInfo + (size_t)w * P.candCapacity;
     int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
     const int32_t S = P.survCount[w];
     const uint64_t lt_mask = (1ull << lane) - 1;
+    int32_t *flags = P.errorFlags + w;
     int32_t k0 = 0;
-    for (int32_t chunk = 0; chunk < S && k0 < K; chunk += kSolverBlock) {
-        const int32_t s = chunk + lane;
-        const bool has = s < S && cslots[s].numPoints > 0;
-        const uint64_t mask = __ballot(has);
-        const int32_t k = k0 + __popcll(mask & lt_mask);
-        if (has && k < K) {
-            const Contact &c = cslots[s];
-            int32_t *flags = P.errorFlags + w;
-            recs[k] = CRec { (int16_t)guardIndex(bodySlot(P, c.ref), nb, flags, kGuardSolverBody),
-                             (int16_t)guardIndex(bodySlot(P, c.alt), nb, flags, kGuardSolverBody),
-                             0, (int16_t)s };
-            order[k] = s;
+    for (int32_t chunk = 0; chunk < S && k0 < K; chunk += kSolverBlock * kInfoUnroll) {
+        uint32_t v[kInfoUnroll];
+#pragma unroll
+        for (int32_t u = 0; u < kInfoUnroll; u++) {
+            const int32_t s = chunk + u * kSolverBlock + lane;
+            v[u] = s < S ? info[s] : kNoManifold;
         }
-        k0 += __popcll(mask);
+#pragma unroll
+        for (int32_t u = 0; u < kInfoUnroll; u++) {
+            const int32_t s = chunk + u * kSolverBlock + lane;
+            const bool has = v[u] != kNoManifold;
+            const uint64_t mask = __ballot(has);
+            const int32_t k = k0 + __popcll(mask & lt_mask);
+            if (has && k < K) {
+                recs[k] = CRec { (int16_t)guardIndex((int32_t)(v[u] & 0xffffu), nb, flags, kGuardSolverBody),
+                                 (int16_t)guardIndex((int32_t)(v[u] >> 16), nb, flags, kGuardSolverBody),
+                                 0, (int16_t)s };
+                order[k] = s;
+            }
+            k0 += __popcll(mask);
+        }
     }
     const JointConstraint *jrows = P.joints + (size_t)w * P.jointCapacity;
     for (int32_t j = lane; j < J; j += kSolverBlock) {
