@@ -421,9 +421,27 @@ MW_PHYS_NODE(FindOverlappingNode,
     hipLaunchKernelGGL(findOverlapsKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
                        findOverlapsSharedBytes(P), stream, P);)
 
-MW_PHYS_NODE(SubstepRigidBodiesNode,
-    if (P.numBodyArchs > 0)
-        hipLaunchKernelGGL(integrateKernel, rowGrid(P), dim3(256), 0, stream, P);)
+// substepRigidBodies.  Substeps after the first are integrated by the
+// previous substep's solver kernel as it writes its bodies back (fused: the
+// bodies are already in its LDS); their nodes keep the graph shape.
+struct SubstepRigidBodiesNode : PhysNodeBase {
+    bool fused;
+    SubstepRigidBodiesNode(Context &ctx, bool fused_into_solver)
+        : PhysNodeBase(ctx), fused(fused_into_solver) {}
+    static TaskGraph::NodeID addToGraph(Context &ctx, TaskGraph::Builder &b,
+                                        Span<const TaskGraph::NodeID> deps)
+    {
+        return b.addDefaultNode<SubstepRigidBodiesNode>(deps, ctx, false);
+    }
+    static const char *nodeName() { return "SubstepRigidBodiesNode"; }
+    static constexpr bool kNoTmpAlloc = true;
+    static void launch(SubstepRigidBodiesNode *self, LaunchCtx &lc)
+    {
+        const PhysArgs &P = self->mod->args;
+        if (self->fused || P.numBodyArchs == 0) return;
+        hipLaunchKernelGGL(integrateKernel, rowGrid(P), dim3(256), 0, (hipStream_t)lc.stream, P);
+    }
+};
 
 // Narrowphase = AABB recheck + survivor numbering (block per world), a
 // per-world compaction into flat lists, a persistent SAT kernel (16-lane
@@ -440,9 +458,27 @@ MW_PHYS_NODE(NarrowphaseNode,
     hipLaunchKernelGGL(narrowContactKernel, dim3(lc.persistentGrid(P.contactGrid)),
                        dim3(kContactBlock), contactSharedBytes(P), stream, P);)
 
-MW_PHYS_NODE(SolverNode,
-    hipLaunchKernelGGL(solverKernel, dim3((P.numWorlds + kSolverWorlds - 1) / kSolverWorlds),
-                       dim3(kSolverThreads), solverSharedBytes(P), stream, P);)
+// solvePositions + setVelocities + solveVelocities (one per-world kernel);
+// integrate_next: also substepRigidBodies of the next substep.
+struct SolverNode : PhysNodeBase {
+    int32_t integrateNext;
+    SolverNode(Context &ctx, bool integrate_next)
+        : PhysNodeBase(ctx), integrateNext(integrate_next ? 1 : 0) {}
+    static TaskGraph::NodeID addToGraph(Context &ctx, TaskGraph::Builder &b,
+                                        Span<const TaskGraph::NodeID> deps)
+    {
+        return b.addDefaultNode<SolverNode>(deps, ctx, false);
+    }
+    static const char *nodeName() { return "SolverNode"; }
+    static constexpr bool kNoTmpAlloc = true;
+    static void launch(SolverNode *self, LaunchCtx &lc)
+    {
+        const PhysArgs &P = self->mod->args;
+        hipLaunchKernelGGL(solverKernel, dim3((P.numWorlds + kSolverWorlds - 1) / kSolverWorlds),
+                           dim3(kSolverThreads), solverSharedBytes(P), (hipStream_t)lc.stream, P,
+                           self->integrateNext);
+    }
+};
 
 // Joint constraints are collected per substep in the reference
 // (collectConstraintsSystem, physics.cpp:34-40: ConstraintData rows copied
@@ -610,12 +646,14 @@ TaskGraph::NodeID RigidBodyPhysicsSystem::setupSubstepTasks(TaskGraph::Builder &
     auto cur = builder.addToGraph<FindOverlappingNode>(deps);
     for (CountT i = 0; i < num_substeps; i++) {
         auto collect = builder.addToGraph<CollectConstraintsNode>({ cur });
-        auto integrate = builder.addToGraph<SubstepRigidBodiesNode>({ cur });
+        auto integrate = builder.addDefaultNode<SubstepRigidBodiesNode>({ cur }, builder.context(),
+                                                                        i > 0);
         auto narrow = builder.addToGraph<NarrowphaseNode>({ integrate });
         auto reset1 = builder.addToGraph<ResetTmpAllocNode>({ narrow });
         // solvePositions + setVelocities + solveVelocities: one per-world
         // kernel (the three reference nodes are consecutive per world).
-        auto solve = builder.addToGraph<SolverNode>({ reset1, collect });
+        auto solve = builder.addDefaultNode<SolverNode>({ reset1, collect }, builder.context(),
+                                                        i + 1 < num_substeps);
         cur = builder.addToGraph<ResetTmpAllocNode>({ solve });
     }
     auto clear = builder.addToGraph<ClearTmpNode<CandidateTemporary>>({ cur });

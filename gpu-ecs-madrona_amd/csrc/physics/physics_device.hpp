@@ -145,7 +145,81 @@ __global__ void narrowFilterKernel(PhysArgs P);
 __global__ void narrowCompactKernel(PhysArgs P);
 __global__ void narrowSATKernel(PhysArgs P);
 __global__ void narrowContactKernel(PhysArgs P);
-__global__ void solverKernel(PhysArgs P);
+__global__ void solverKernel(PhysArgs P, int32_t integrate_next);
+
+// substepRigidBodies (physics.cpp:79-164) for one body row, from its
+// current pose and velocity (the integrate kernel reads them from the
+// columns; the solver's fused tail passes the values it is about to write
+// back -- the same inputs, so the same bits), plus the world AABB the
+// narrowphase recheck uses (narrowphase.cpp:1590-1594), indexed by body slot.
+__device__ __forceinline__ void integrateBody(const PhysArgs &P, const BodyArch &B, int32_t w,
+                                              int32_t r, Vector3 x, Quat q, Vector3 v_in,
+                                              Vector3 omega_in)
+{
+    Vector3 &pos = bcol<Vector3>(B, Cols::Position, w, r);
+    Quat &rot = bcol<Quat>(B, Cols::Rotation, w, r);
+    const int32_t obj = bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
+    const ResponseType rt = bcol<ResponseType>(B, Cols::ResponseType, w, r);
+    auto &prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
+    auto &ps_pos = bcol<solver::PreSolvePositional>(B, Cols::PreSolvePositional, w, r);
+    auto &ps_vel = bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
+
+    if (rt == ResponseType::Static) {
+        prev.prevPosition = x;
+        prev.prevRotation = q;
+        ps_pos.x = x;
+        ps_pos.q = q;
+        ps_vel.v = Vector3::zero();
+        ps_vel.omega = Vector3::zero();
+        pos = x;
+        rot = q;
+    } else {
+        Vector3 v = v_in;
+        Vector3 omega = omega_in;
+        prev.prevPosition = x;
+        prev.prevRotation = q;
+        const SolverData &solver = P.solver[w];
+        const RigidBodyMetadata md = P.objs.metadata[obj];
+        const float inv_m = md.invMass;
+        const Vector3 inv_I = md.invInertiaTensor;
+        const float h = solver.h;
+        const Vector3 ext_force = bcol<Vector3>(B, Cols::ExternalForce, w, r);
+        const Vector3 ext_torque = bcol<Vector3>(B, Cols::ExternalTorque, w, r);
+        if (rt == ResponseType::Dynamic) v += h * solver.g;
+        v += h * inv_m * ext_force;
+        x += h * v;
+        Vector3 I {
+            (inv_I.x == 0) ? 0.0f : 1.0f / inv_I.x,
+            (inv_I.y == 0) ? 0.0f : 1.0f / inv_I.y,
+            (inv_I.z == 0) ? 0.0f : 1.0f / inv_I.z,
+        };
+        Quat to_local = q.inv();
+        Vector3 tau_ext_local = to_local.rotateVec(ext_torque);
+        Vector3 omega_local = to_local.rotateVec(omega);
+        Vector3 I_omega_local = multDiag(I, omega_local);
+        omega_local += h * multDiag(inv_I, tau_ext_local - cross(omega_local, I_omega_local));
+        omega = q.rotateVec(omega_local);
+        Quat apply_omega = Quat::fromAngularVec(0.5f * h * omega);
+        q += apply_omega * q;
+        q = q.normalize();
+        pos = x;
+        rot = q;
+        ps_pos.x = x;
+        ps_pos.q = q;
+        ps_vel.v = v;
+        ps_vel.omega = omega;
+    }
+    const Diag3x3 scale = bcol<Diag3x3>(B, Cols::Scale, w, r);
+    P.bodyAABBs[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r] =
+        P.objs.aabbs[obj].applyTRS(x, q, scale);
+}
+
+// Zero the per-64-world survivor sums the narrowphase filter accumulates.
+__device__ __forceinline__ void zeroGroupCounts(const PhysArgs &P, int32_t tid, int32_t nthreads)
+{
+    const int32_t groups = (P.numWorlds + 63) >> 6;
+    for (int32_t g = tid; g < groups; g += nthreads) P.groupCounts[g] = 0;
+}
 
 size_t findOverlapsSharedBytes(const PhysArgs &P);
 size_t refitSharedBytes(const PhysArgs &P);

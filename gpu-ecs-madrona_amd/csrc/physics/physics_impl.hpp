@@ -179,5 +179,9 @@ inline constexpr int32_t kErrIndexGuard = 64;
 // More ConstraintData rows than SolverData::maxJointConstraints (the
 // reference writes past its buffer, physics.cpp:34-40); the excess is dropped.
 inline constexpr int32_t kErrJointOverflow = 128;
+// A solve that the solver's level schedule treated as leaving an invariant
+// static body untouched wrote it after all (a non-finite lambda): the
+// world's contact order is no longer guaranteed to be the reference's.
+inline constexpr int32_t kErrStaticSchedule = 1 << 21;
 
 }

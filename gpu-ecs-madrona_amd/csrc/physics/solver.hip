@@ -70,28 +70,118 @@ __device__ __forceinline__ void applyPositionalUpdate(Vector3 &x1, Vector3 &x2, 
     q2 = q2.normalize();
 }
 
-__device__ void solveContactPositions(const PhysArgs &P, int32_t w, SMut &b1, int32_t s1,
-                                      SMut &b2, int32_t s2, Contact &c)
+struct PairConst {
+    float im1, im2;
+    Vector3 iI1, iI2;
+    Vector3 n;
+    float mu;             // avg mu_s (positions) / avg mu_d (velocities)
+};
+
+__device__ __forceinline__ PairConst pairConst(const PhysArgs &P, const SMut &b1, const SMut &b2,
+                                               Vector3 n, bool velocities)
+{
+    const RigidBodyMetadata m1 = P.objs.metadata[b1.meta >> 16], m2 = P.objs.metadata[b2.meta >> 16];
+    PairConst k;
+    k.im1 = m1.invMass;
+    k.im2 = m2.invMass;
+    k.iI1 = m1.invInertiaTensor;
+    k.iI2 = m2.invInertiaTensor;
+    if (isStaticBody(b1.meta)) { k.im1 = 0.f; k.iI1 = Vector3::zero(); }
+    if (isStaticBody(b2.meta)) { k.im2 = 0.f; k.iI2 = Vector3::zero(); }
+    k.n = n;
+    k.mu = velocities ? 0.5f * (m1.muD + m2.muD) : 0.5f * (m1.muS + m2.muS);
+    return k;
+}
+
+// ---------------------------------------------------------------------------
+// Skipping an invariant static body (staticInvariant below: static, finite,
+// no -0 component, normalize() idempotent, previous pose == pose, pre-solve
+// velocity +0).  Every solver write to such a body is an exact no-op, and
+// its terms in the other body's update are exact zeros:
+//   ra_s = 0 * ta_s has the sign of ta_s, so ta_s . ra_s = +0 and
+//   w_s = 0 + (+0) = +0: the lambdas  -c / ((w1 + w2) + 0)  are computed
+//   with w_s the constant +0 (the same IEEE additions);
+//   x_s +- (dl * 0) * n and q_s +- (+-0 quaternion) keep their bits, and
+//   normalize() returns q_s itself;
+//   p_s - p_s_hat = +0 (pose == previous pose, same operations);
+//   v_s = omega_s = +0 after setVelocities, so v_s + cross(omega_s, r) = +0.
+// This holds while the lever arms and lambdas are finite: the contact's
+// input bound (boundedInput) guarantees it for ta_s, and a non-finite lambda
+// / velocity magnitude abandons the skipping solve before anything of the
+// bodies is written; the full solve then runs (it writes the static body,
+// which the level schedule treated as untouched, so the world is flagged).
+// sk1 / sk2: skip the ref / alt body.  With both false the functions are the
+// reference's op sequence verbatim.  Skipping cuts ~1/3 of a point's VALU;
+// the kind-sorted schedule keeps a wave's lanes on the same side.
+// ---------------------------------------------------------------------------
+enum : int32_t { kSolveDone = 0, kSolveNonFinite = 1 };
+
+// A contact's solver inputs, loaded with one batch of independent 16-B
+// loads when its item starts (the point loop would otherwise wait on a
+// global load per point): all four point slots, normal, count, lambdas.
+struct ContactIn {
+    Vector4 pts[4];
+    Vector3 n;
+    int32_t np;
+    float lam[4];
+};
+
+__device__ __forceinline__ ContactIn loadContact(const Contact &c)
+{
+    static_assert(offsetof(Contact, points) == 16 && offsetof(Contact, numPoints) == 80 &&
+                  offsetof(Contact, normal) == 84 && offsetof(Contact, lambdaN) == 96);
+    const float4 *v = (const float4 *)((const char *)&c + 16);
+    const float4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3], a4 = v[4], a5 = v[5];
+    ContactIn ci;
+    ci.pts[0] = Vector4 { a0.x, a0.y, a0.z, a0.w };
+    ci.pts[1] = Vector4 { a1.x, a1.y, a1.z, a1.w };
+    ci.pts[2] = Vector4 { a2.x, a2.y, a2.z, a2.w };
+    ci.pts[3] = Vector4 { a3.x, a3.y, a3.z, a3.w };
+    ci.np = __float_as_int(a4.x);
+    ci.n = Vector3 { a4.y, a4.z, a4.w };
+    ci.lam[0] = a5.x; ci.lam[1] = a5.y; ci.lam[2] = a5.z; ci.lam[3] = a5.w;
+    return ci;
+}
+
+__device__ __forceinline__ bool finiteF(float f) { return __builtin_isfinite(f); }
+
+__device__ __forceinline__ bool boundedInput(const ContactIn &c)
+{
+    constexpr float kBound = 1e18f;
+    bool ok = fabsf(c.n.x) <= kBound && fabsf(c.n.y) <= kBound &&
+              fabsf(c.n.z) <= kBound;   // false for NaN
+    for (int i = 0; i < 4; i++) {
+        if (i >= c.np) break;
+        const Vector4 p = c.pts[i];
+        ok = ok && fabsf(p.x) <= kBound && fabsf(p.y) <= kBound && fabsf(p.z) <= kBound &&
+             fabsf(p.w) <= kBound;
+    }
+    return ok;
+}
+
+__device__ int32_t solveContactPositions(const PhysArgs &P, int32_t w, SMut &b1, int32_t s1,
+                                         SMut &b2, int32_t s2, const ContactIn &c,
+                                         float *lambda_out, bool sk1, bool sk2)
 {                                                          // physics.cpp:281-476
     const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
     const auto ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
     const auto ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
-    const auto pv1 = bcol<solver::SubstepPrevState>(P.body[o1.arch], Cols::SubstepPrevState, w, o1.row);
-    const auto pv2 = bcol<solver::SubstepPrevState>(P.body[o2.arch], Cols::SubstepPrevState, w, o2.row);
-    const RigidBodyMetadata m1 = P.objs.metadata[o1.obj], m2 = P.objs.metadata[o2.obj];
+    solver::SubstepPrevState pv1 {}, pv2 {};
+    if (!sk1) pv1 = bcol<solver::SubstepPrevState>(P.body[o1.arch], Cols::SubstepPrevState, w, o1.row);
+    if (!sk2) pv2 = bcol<solver::SubstepPrevState>(P.body[o2.arch], Cols::SubstepPrevState, w, o2.row);
+    const PairConst k = pairConst(P, b1, b2, c.n, false);
+    const bool sk = sk1 || sk2;
+    const Vector3 n = k.n;
     Vector3 x1 = b1.x, x2 = b2.x;
     Quat q1 = b1.q, q2 = b2.q;
-    float im1 = m1.invMass, im2 = m2.invMass;
-    Vector3 iI1 = m1.invInertiaTensor, iI2 = m2.invInertiaTensor;
-    if (isStaticBody(b1.meta)) { im1 = 0.f; iI1 = Vector3::zero(); }
-    if (isStaticBody(b2.meta)) { im2 = 0.f; iI2 = Vector3::zero(); }
-    const float avg_mu_s = 0.5f * (m1.muS + m2.muS);
-    const Vector3 n = c.normal;
-    const int32_t np = c.numPoints;
+    const int32_t np = c.np;
+    Vector4 pa = c.pts[0], pb = c.pts[1], pc = c.pts[2], pd = c.pts[3];
 #pragma unroll 1
-    for (int i = 0; i < np; i++) {
-        Vector3 c1 = c.points[i].xyz();
-        float depth = c.points[i].w;
+    for (int i = 0; i < np; i++) {                         // :400-474
+        const Vector4 pt = pa;                             // point i (registers shift)
+        pa = pb; pb = pc; pc = pd;
+        Vector3 c1 = pt.xyz();
+        float depth = pt.w;
         Vector3 c2 = c1 - n * depth;
         Vector3 r1 = ps1.q.inv().rotateVec(c1 - ps1.x);
         Vector3 r2 = ps2.q.inv().rotateVec(c2 - ps2.x);
@@ -100,41 +190,89 @@ __device__ void solveContactPositions(const PhysArgs &P, int32_t w, SMut &b1, in
         Vector3 p2 = q2.rotateVec(r2) + x2;
         float d = dot(p1 - p2, n);
         if (d > 0) {
-            Vector3 nl1 = q1.inv().rotateVec(n);
-            Vector3 nl2 = q2.inv().rotateVec(n);
-            Vector3 ta1 = cross(r1, nl1);
-            Vector3 ta2 = cross(r2, nl2);
-            Vector3 ra1 = multDiag(iI1, ta1);
-            Vector3 ra2 = multDiag(iI2, ta2);
-            lambda_n = computePositionalLambda(ta1, ta2, ra1, ra2, im1, im2, d, 0);
-            applyPositionalUpdate(x1, x2, q1, q2, ra1, ra2, im1, im2, n, lambda_n);
+            Vector3 ra1 = Vector3::zero(), ra2 = Vector3::zero();
+            float w1 = 0.f, w2 = 0.f;
+            if (!sk1) {
+                Vector3 nl1 = q1.inv().rotateVec(n);
+                Vector3 ta1 = cross(r1, nl1);
+                ra1 = multDiag(k.iI1, ta1);
+                w1 = k.im1 + dot(ta1, ra1);
+            }
+            if (!sk2) {
+                Vector3 nl2 = q2.inv().rotateVec(n);
+                Vector3 ta2 = cross(r2, nl2);
+                ra2 = multDiag(k.iI2, ta2);
+                w2 = k.im2 + dot(ta2, ra2);
+            }
+            lambda_n = -d / (w1 + w2 + 0.f);               // computePositionalLambda
+            if (sk && !finiteF(lambda_n)) return kSolveNonFinite;
+            float half = 0.5f * lambda_n;                  // applyPositionalUpdate
+            if (!sk1) {
+                x1 += lambda_n * k.im1 * n;
+                Vector3 q1u = q1.rotateVec(half * ra1);
+                q1 += Quat::fromAngularVec(q1u) * q1;
+                q1 = q1.normalize();
+            }
+            if (!sk2) {
+                x2 -= lambda_n * k.im2 * n;
+                Vector3 q2u = q2.rotateVec(half * ra2);
+                q2 -= Quat::fromAngularVec(q2u) * q2;
+                q2 = q2.normalize();
+            }
 
-            Vector3 p1_hat = pv1.prevRotation.rotateVec(r1) + pv1.prevPosition;
-            Vector3 p2_hat = pv2.prevRotation.rotateVec(r2) + pv2.prevPosition;
-            p1 = q1.rotateVec(r1) + x1;
-            p2 = q2.rotateVec(r2) + x2;
-            Vector3 dp = (p1 - p1_hat) - (p2 - p2_hat);
+            Vector3 e1 = Vector3::zero(), e2 = Vector3::zero();   // p - p_hat
+            if (!sk1) {
+                Vector3 p1_hat = pv1.prevRotation.rotateVec(r1) + pv1.prevPosition;
+                e1 = (q1.rotateVec(r1) + x1) - p1_hat;
+            }
+            if (!sk2) {
+                Vector3 p2_hat = pv2.prevRotation.rotateVec(r2) + pv2.prevPosition;
+                e2 = (q2.rotateVec(r2) + x2) - p2_hat;
+            }
+            Vector3 dp = e1 - e2;
             Vector3 dpt = dp - dot(dp, n) * n;
             float tmag = dpt.length();
             if (tmag > 0.f) {
                 Vector3 tw = dpt / tmag;
-                Vector3 tl1 = q1.inv().rotateVec(tw);
-                Vector3 tl2 = q2.inv().rotateVec(tw);
-                Vector3 fta1 = cross(r1, tl1);
-                Vector3 fta2 = cross(r2, tl2);
-                Vector3 fra1 = multDiag(iI1, fta1);
-                Vector3 fra2 = multDiag(iI2, fta2);
-                float lambda_t = computePositionalLambda(fta1, fta2, fra1, fra2, im1, im2, tmag, 0);
-                float thresh = lambda_n * avg_mu_s;
+                Vector3 fra1 = Vector3::zero(), fra2 = Vector3::zero();
+                float wt1 = 0.f, wt2 = 0.f;
+                if (!sk1) {
+                    Vector3 tl1 = q1.inv().rotateVec(tw);
+                    Vector3 fta1 = cross(r1, tl1);
+                    fra1 = multDiag(k.iI1, fta1);
+                    wt1 = k.im1 + dot(fta1, fra1);
+                }
+                if (!sk2) {
+                    Vector3 tl2 = q2.inv().rotateVec(tw);
+                    Vector3 fta2 = cross(r2, tl2);
+                    fra2 = multDiag(k.iI2, fta2);
+                    wt2 = k.im2 + dot(fta2, fra2);
+                }
+                float lambda_t = -tmag / (wt1 + wt2 + 0.f);
+                if (sk && !finiteF(lambda_t)) return kSolveNonFinite;
+                float thresh = lambda_n * k.mu;
                 if (lambda_t > thresh) {
-                    applyPositionalUpdate(x1, x2, q1, q2, fra1, fra2, im1, im2, tw, lambda_t);
+                    float half_t = 0.5f * lambda_t;
+                    if (!sk1) {
+                        x1 += lambda_t * k.im1 * tw;
+                        Vector3 q1u = q1.rotateVec(half_t * fra1);
+                        q1 += Quat::fromAngularVec(q1u) * q1;
+                        q1 = q1.normalize();
+                    }
+                    if (!sk2) {
+                        x2 -= lambda_t * k.im2 * tw;
+                        Vector3 q2u = q2.rotateVec(half_t * fra2);
+                        q2 -= Quat::fromAngularVec(q2u) * q2;
+                        q2 = q2.normalize();
+                    }
                 }
             }
         }
-        c.lambdaN[i] = lambda_n;
+        lambda_out[i] = lambda_n;
     }
-    b1.x = x1; b2.x = x2;
-    b1.q = q1; b2.q = q2;
+    if (!sk1) { b1.x = x1; b1.q = q1; }
+    if (!sk2) { b2.x = x2; b2.q = q2; }
+    return kSolveDone;
 }
 
 // Joint constraints (physics.cpp:247-279, 478-648), run after the contacts
@@ -245,24 +383,53 @@ __device__ __forceinline__ void applyVelocityUpdate(Vector3 &v1, Vector3 &v2, Ve
     o2 -= q2.rotateVec(o2u);
 }
 
-__device__ void solveContactVelocities(const PhysArgs &P, int32_t w, SMut &b1, int32_t s1,
-                                       SMut &b2, int32_t s2, const Contact &c, float h,
-                                       float rest_thresh)
+__device__ int32_t solveContactVelocities(const PhysArgs &P, int32_t w, SMut &b1, int32_t s1,
+                                          SMut &b2, int32_t s2, const ContactIn &c, float h,
+                                          float rest_thresh, bool sk1, bool sk2)
 {                                                          // physics.cpp:865-993
     const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
-    const auto ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
-    const auto ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
-    const auto pv1 = bcol<solver::PreSolveVelocity>(P.body[o1.arch], Cols::PreSolveVelocity, w, o1.row);
-    const auto pv2 = bcol<solver::PreSolveVelocity>(P.body[o2.arch], Cols::PreSolveVelocity, w, o2.row);
-    const RigidBodyMetadata m1 = P.objs.metadata[o1.obj], m2 = P.objs.metadata[o2.obj];
+    solver::PreSolvePositional ps1 {}, ps2 {};
+    solver::PreSolveVelocity pv1 {}, pv2 {};
+    if (!sk1) {
+        ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
+        pv1 = bcol<solver::PreSolveVelocity>(P.body[o1.arch], Cols::PreSolveVelocity, w, o1.row);
+    }
+    if (!sk2) {
+        ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
+        pv2 = bcol<solver::PreSolveVelocity>(P.body[o2.arch], Cols::PreSolveVelocity, w, o2.row);
+    }
+    const PairConst k = pairConst(P, b1, b2, c.n, true);
+    const bool sk = sk1 || sk2;
     const Quat q1 = b1.q, q2 = b2.q;
     Vector3 v1 = b1.v, o1v = b1.omega, v2 = b2.v, o2v = b2.omega;
-    float im1 = m1.invMass, im2 = m2.invMass;
-    Vector3 iI1 = m1.invInertiaTensor, iI2 = m2.invInertiaTensor;
-    if (isStaticBody(b1.meta)) { im1 = 0.f; iI1 = Vector3::zero(); }
-    if (isStaticBody(b2.meta)) { im2 = 0.f; iI2 = Vector3::zero(); }
-    const float mu_d = 0.5f * (m1.muD + m2.muD);
-    const Vector3 n = c.normal;
+    const Vector3 n = k.n;
+
+    // relVel (physics.cpp:716-722) as t1 - t2, a skipped side's term = +0
+    auto rel = [&](int32_t, Vector3 r1l, Vector3 r2l) {
+        Vector3 t1 = Vector3::zero(), t2 = Vector3::zero();
+        if (!sk1) t1 = v1 + cross(o1v, q1.rotateVec(r1l));
+        if (!sk2) t2 = v2 + cross(o2v, q2.rotateVec(r2l));
+        return t1 - t2;
+    };
+    // applyVelocityUpdate (physics.cpp:724-750), false on a non-finite
+    // magnitude when a side is skipped (nothing is written then)
+    auto apply = [&](Vector3 ta1, Vector3 ta2, Vector3 dv, float mag) {
+        Vector3 ra1 = Vector3::zero(), ra2 = Vector3::zero();
+        float w1 = 0.f, w2 = 0.f;
+        if (!sk1) { ra1 = multDiag(k.iI1, ta1); w1 = k.im1 + dot(ta1, ra1); }
+        if (!sk2) { ra2 = multDiag(k.iI2, ta2); w2 = k.im2 + dot(ta2, ra2); }
+        mag *= 1.f / (w1 + w2);
+        if (sk && !finiteF(mag)) return false;
+        if (!sk1) {
+            v1 += mag * k.im1 * dv;
+            o1v += q1.rotateVec(mag * ra1);
+        }
+        if (!sk2) {
+            v2 -= mag * k.im2 * dv;
+            o2v -= q2.rotateVec(mag * ra2);
+        }
+        return true;
+    };
 
     // Per point only the body-local lever arms and the pre-solve normal
     // velocity stay live; the world-space arms (q fixed during this phase)
@@ -270,76 +437,92 @@ __device__ void solveContactVelocities(const PhysArgs &P, int32_t w, SMut &b1, i
     // on the same inputs, so bit-identical, at a third of the registers.
     Vector3 r1l[4], r2l[4];
     float vn_bars[4];
-    const Vector3 nl1 = q1.inv().rotateVec(n);
-    const Vector3 nl2 = q2.inv().rotateVec(n);
+    Vector3 nl1 = Vector3::zero(), nl2 = Vector3::zero();
+    if (!sk1) nl1 = q1.inv().rotateVec(n);
+    if (!sk2) nl2 = q2.inv().rotateVec(n);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        if (i >= c.numPoints) continue;
-        Vector3 c1 = c.points[i].xyz();
-        float depth = c.points[i].w;
+        if (i >= c.np) continue;
+        Vector3 c1 = c.pts[i].xyz();
+        float depth = c.pts[i].w;
         Vector3 c2 = c1 - n * depth;
-        Vector3 r1 = ps1.q.inv().rotateVec(c1 - ps1.x);
-        Vector3 r2 = ps2.q.inv().rotateVec(c2 - ps2.x);
-        Vector3 r1p = ps1.q.rotateVec(r1);
-        Vector3 r2p = ps2.q.rotateVec(r2);
-        Vector3 vbar = relVel(pv1.v, pv2.v, pv1.omega, pv2.omega, r1p, r2p);
-        vn_bars[i] = dot(n, vbar);
-        r1l[i] = r1;
-        r2l[i] = r2;
+        Vector3 t1 = Vector3::zero(), t2 = Vector3::zero();
+        r1l[i] = Vector3::zero();
+        r2l[i] = Vector3::zero();
+        if (!sk1) {
+            r1l[i] = ps1.q.inv().rotateVec(c1 - ps1.x);
+            t1 = pv1.v + cross(pv1.omega, ps1.q.rotateVec(r1l[i]));
+        }
+        if (!sk2) {
+            r2l[i] = ps2.q.inv().rotateVec(c2 - ps2.x);
+            t2 = pv2.v + cross(pv2.omega, ps2.q.rotateVec(r2l[i]));
+        }
+        vn_bars[i] = dot(n, t1 - t2);
     }
     for (int it = 0; it < 2; it++) {                       // :813-863
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            if (i >= c.numPoints) continue;
-            Vector3 v = relVel(v1, v2, o1v, o2v, q1.rotateVec(r1l[i]), q2.rotateVec(r2l[i]));
-            float vn = dot(n, v);
+            if (i >= c.np) continue;
+            float vn = dot(n, rel(i, r1l[i], r2l[i]));
             float vn_bar = vn_bars[i];
             float e = 0.3f;
             if (fabsf(vn_bar) <= rest_thresh) e = 0.f;
             float mag = fminRef(-e * vn_bar, 0) - vn;
-            applyVelocityUpdate(v1, v2, o1v, o2v, q1, q2, cross(r1l[i], nl1), cross(r2l[i], nl2),
-                                im1, im2, iI1, iI2, n, mag);
+            if (!apply(cross(r1l[i], nl1), cross(r2l[i], nl2), n, mag)) return kSolveNonFinite;
         }
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) {                          // :752-811
-        if (i >= c.numPoints) continue;
-        Vector3 v = relVel(v1, v2, o1v, o2v, q1.rotateVec(r1l[i]), q2.rotateVec(r2l[i]));
-        float dfm = mu_d * fabsf(c.lambdaN[i]) / h;
+        if (i >= c.np) continue;
+        Vector3 v = rel(i, r1l[i], r2l[i]);
+        float dfm = k.mu * fabsf(c.lam[i]) / h;
         float vn = dot(n, v);
         Vector3 vt = v - n * vn;
         float vt_len = vt.length();
         if (vt_len != 0 && dfm != 0.f) {
             float corrected = -fminRef(dfm, vt_len);
             Vector3 dw = vt / vt_len;
-            Vector3 d1l = q1.inv().rotateVec(dw);
-            Vector3 d2l = q2.inv().rotateVec(dw);
-            Vector3 fta1 = cross(r1l[i], d1l);
-            Vector3 fta2 = cross(r2l[i], d2l);
-            applyVelocityUpdate(v1, v2, o1v, o2v, q1, q2, fta1, fta2, im1, im2, iI1, iI2, dw,
-                                corrected);
+            Vector3 fta1 = Vector3::zero(), fta2 = Vector3::zero();
+            if (!sk1) fta1 = cross(r1l[i], q1.inv().rotateVec(dw));
+            if (!sk2) fta2 = cross(r2l[i], q2.inv().rotateVec(dw));
+            if (!apply(fta1, fta2, dw, corrected)) return kSolveNonFinite;
         }
     }
-    b1.v = v1; b1.omega = o1v;
-    b2.v = v2; b2.omega = o2v;
+    if (!sk1) { b1.v = v1; b1.omega = o1v; }
+    if (!sk2) { b2.v = v2; b2.omega = o2v; }
+    return kSolveDone;
 }
 
 __device__ __forceinline__ bool isNegZero(float f) { return __float_as_uint(f) == 0x80000000u; }
+__device__ __forceinline__ bool sameBits(float a, float b) { return __float_as_uint(a) == __float_as_uint(b); }
 
 // A static body is never written through if every solver write to it is an
 // exact no-op: x +- (+-0) and q +- (+-0) keep bits when no component is -0,
 // and normalize() must be idempotent on its rotation (static velocities are
-// always +0 after setVelocities).  Such bodies add no ordering edge.
-__device__ __forceinline__ bool staticInvariant(const SMut &b)
+// always +0 after setVelocities).  Such bodies add no ordering edge.  The
+// specialised contact solves (solveContact*Static) further use that its
+// previous pose equals its pose, that its pre-solve velocity is +0 and that
+// its position is finite and bounded; integrateKernel establishes all three
+// for every static body, and they are checked here.
+__device__ __forceinline__ bool staticInvariant(const SMut &b, Vector3 prev_x, Quat prev_q,
+                                                Vector3 ps_v, Vector3 ps_om)
 {
     if (!isStaticBody(b.meta)) return false;
     if (isNegZero(b.x.x) || isNegZero(b.x.y) || isNegZero(b.x.z)) return false;
     if (isNegZero(b.q.w) || isNegZero(b.q.x) || isNegZero(b.q.y) || isNegZero(b.q.z)) return false;
+    constexpr float kBound = 1e18f;
+    if (!(fabsf(b.x.x) <= kBound && fabsf(b.x.y) <= kBound && fabsf(b.x.z) <= kBound)) return false;
+    if (!(finiteF(b.q.w) && finiteF(b.q.x) && finiteF(b.q.y) && finiteF(b.q.z))) return false;
+    if (!(sameBits(prev_x.x, b.x.x) && sameBits(prev_x.y, b.x.y) && sameBits(prev_x.z, b.x.z) &&
+          sameBits(prev_q.w, b.q.w) && sameBits(prev_q.x, b.q.x) && sameBits(prev_q.y, b.q.y) &&
+          sameBits(prev_q.z, b.q.z))) return false;
+    const uint32_t vbits = __float_as_uint(ps_v.x) | __float_as_uint(ps_v.y) |
+                           __float_as_uint(ps_v.z) | __float_as_uint(ps_om.x) |
+                           __float_as_uint(ps_om.y) | __float_as_uint(ps_om.z);
+    if (vbits != 0) return false;
     Quat nq = b.q.normalize();
-    return __float_as_uint(nq.w) == __float_as_uint(b.q.w) &&
-           __float_as_uint(nq.x) == __float_as_uint(b.q.x) &&
-           __float_as_uint(nq.y) == __float_as_uint(b.q.y) &&
-           __float_as_uint(nq.z) == __float_as_uint(b.q.z);
+    return sameBits(nq.w, b.q.w) && sameBits(nq.x, b.q.x) && sameBits(nq.y, b.q.y) &&
+           sameBits(nq.z, b.q.z);
 }
 
 // Per-item solver record: body slots of ref / alt (e1 / e2 for a joint)
@@ -360,40 +543,50 @@ static_assert(sizeof(CRec) == 8);
 #endif
 constexpr int32_t kSolverLDSContacts = MW_SOLVER_LDS_CONTACTS;
 
-// Per-world LDS image: bodies, ordering flags, contact records.
+// Item kinds, in schedule order within a level: contacts whose ref (1) or
+// alt (2) body is an invariant static body take the specialised solves, the
+// rest (and joints) the general ones.  Sorting a level by kind keeps a
+// wave's lanes on one code path.
+enum : int32_t { kKindStaticRef = 0, kKindStaticAlt = 1, kKindGeneral = 2, kNumKinds = 3 };
+
+// Per-world LDS image: bodies, ordering state, contact records.
 struct SolverLDS {
     SMut *bodies;         // [nb]
-    int16_t *lastLevel;   // [nb] -1: invariant static body (no ordering edges)
+    uint64_t *touch;      // [nb] lanes of the current 64-item chunk touching the body
+    int16_t *flag;        // [nb] -1: invariant static body (no ordering edges), else 0
+    int16_t *lastItem;    // [nb] latest item of the earlier chunks touching the body
     CRec *recs;           // [kSolverLDSContacts]
-    int32_t *prevs;       // [kSolverLDSContacts] (prev contact on s1, on s2) as 2 x int16
+    int32_t *prevs;       // [kSolverLDSContacts] (prev item on s1, on s2) as 2 x int16
 };
 
 __host__ __device__ inline size_t solverA16(size_t b) { return (b + 15) & ~size_t(15); }
 
 __host__ __device__ inline size_t solverWorldLDSBytes(int32_t nb)
 {
-    return solverA16(sizeof(SMut) * nb) + solverA16(sizeof(int16_t) * nb) +
+    return solverA16(sizeof(SMut) * nb) + solverA16(sizeof(uint64_t) * nb) +
+           2 * solverA16(sizeof(int16_t) * nb) +
            (sizeof(CRec) + sizeof(int32_t)) * kSolverLDSContacts;
 }
 
-// Block-shared level schedule: every (world, contact) of the block sorted
-// by level, so one pass over a level keeps all of the block's lanes on that
-// level's contacts from all of its worlds.
+// Block-shared schedule: every (world, item) of the block sorted by (level,
+// kind), so one pass over a level keeps all of the block's lanes on that
+// level's items from all of its worlds.
 constexpr int32_t kSolverItems = kSolverWorlds * kSolverLDSContacts;
+constexpr int32_t kSolverBuckets = kNumKinds * (kSolverLDSContacts + 2);
 
 __host__ __device__ inline size_t solverBlockLDSBytes(int32_t nb)
 {
     return kSolverWorlds * solverWorldLDSBytes(nb) +
-           sizeof(uint32_t) * kSolverItems +               // items (world << 16 | k)
-           sizeof(int32_t) * 2 * (kSolverItems + 2) +      // level offsets / cursors
+           sizeof(uint32_t) * kSolverItems +               // items (world << 16 | kind << 12 | k)
+           sizeof(int32_t) * 2 * kSolverBuckets +          // bucket offsets / cursors
            sizeof(int32_t) * 4;                            // block scalars
 }
 
 struct SolverBlockLDS {
     uint32_t *items;
-    int32_t *levelOff;    // [Lmax + 2]
-    int32_t *levelCur;    // [Lmax + 2]
-    int32_t *scalars;     // [0] sum K, [1] max K, [2] max level
+    int32_t *bucketOff;   // [(Lmax + 2) * kNumKinds]
+    int32_t *bucketCur;
+    int32_t *scalars;     // [1] max items, [2] max level
 };
 
 __device__ __forceinline__ SolverLDS solverWorldLDS(char *smem, int32_t nb, int32_t wi)
@@ -402,7 +595,11 @@ __device__ __forceinline__ SolverLDS solverWorldLDS(char *smem, int32_t nb, int3
     char *p = smem + (size_t)wi * solverWorldLDSBytes(nb);
     L.bodies = (SMut *)p;
     p += solverA16(sizeof(SMut) * nb);
-    L.lastLevel = (int16_t *)p;
+    L.touch = (uint64_t *)p;
+    p += solverA16(sizeof(uint64_t) * nb);
+    L.flag = (int16_t *)p;
+    p += solverA16(sizeof(int16_t) * nb);
+    L.lastItem = (int16_t *)p;
     p += solverA16(sizeof(int16_t) * nb);
     L.recs = (CRec *)p;
     p += sizeof(CRec) * kSolverLDSContacts;
@@ -416,10 +613,10 @@ __device__ __forceinline__ SolverBlockLDS solverBlockLDS(char *smem, int32_t nb)
     char *p = smem + kSolverWorlds * solverWorldLDSBytes(nb);
     B.items = (uint32_t *)p;
     p += sizeof(uint32_t) * kSolverItems;
-    B.levelOff = (int32_t *)p;
-    p += sizeof(int32_t) * (kSolverItems + 2);
-    B.levelCur = (int32_t *)p;
-    p += sizeof(int32_t) * (kSolverItems + 2);
+    B.bucketOff = (int32_t *)p;
+    p += sizeof(int32_t) * kSolverBuckets;
+    B.bucketCur = (int32_t *)p;
+    p += sizeof(int32_t) * kSolverBuckets;
     B.scalars = (int32_t *)p;
     return B;
 }
@@ -433,7 +630,30 @@ __device__ __forceinline__ void waveSync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Load one world's bodies into its LDS image (wave `lane` 0..63).
+// Column reads as plain floats (no aggregate copies through scratch).
+__device__ __forceinline__ Vector3 ldV3(const void *p)
+{
+    const float *f = (const float *)p;
+    return Vector3 { f[0], f[1], f[2] };
+}
+__device__ __forceinline__ Quat ldQ(const void *p)
+{
+    const float *f = (const float *)p;
+    return Quat { f[0], f[1], f[2], f[3] };
+}
+__device__ __forceinline__ void stV3(void *p, Vector3 v)
+{
+    float *f = (float *)p;
+    f[0] = v.x; f[1] = v.y; f[2] = v.z;
+}
+__device__ __forceinline__ void stQ(void *p, Quat q)
+{
+    float *f = (float *)p;
+    f[0] = q.w; f[1] = q.x; f[2] = q.y; f[3] = q.z;
+}
+
+// Load one world's bodies into its LDS image (wave `lane` 0..63) and reset
+// its ordering state.
 __device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, SolverLDS &L,
                                                 int32_t lane)
 {
@@ -442,31 +662,67 @@ __device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, So
         const int32_t rows = B.numRows[w];
         for (int32_t r = lane; r < rows; r += kSolverBlock) {
             SMut s;
-            s.x = bcol<Vector3>(B, Cols::Position, w, r);
-            s.q = bcol<Quat>(B, Cols::Rotation, w, r);
-            const Velocity vel = bcol<Velocity>(B, Cols::Velocity, w, r);
-            s.v = vel.linear;
-            s.omega = vel.angular;
+            s.x = ldV3(&bcol<Vector3>(B, Cols::Position, w, r));
+            s.q = ldQ(&bcol<Quat>(B, Cols::Rotation, w, r));
+            const Velocity &vel = bcol<Velocity>(B, Cols::Velocity, w, r);
+            s.v = ldV3(&vel.linear);
+            s.omega = ldV3(&vel.angular);
             const uint32_t obj = (uint32_t)bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
-            s.meta = ((uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r) & 0xffu) |
-                     ((uint32_t)ba << 8) | (obj << 16);
-            L.bodies[B.slotBase + r] = s;
-            L.lastLevel[B.slotBase + r] = staticInvariant(s) ? (int16_t)-1 : (int16_t)0;
+            const uint32_t rt = (uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r) & 0xffu;
+            s.meta = rt | ((uint32_t)ba << 8) | (obj << 16);
+            bool inv = false;
+            if (rt == (uint32_t)ResponseType::Static) {
+                const auto &pv = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
+                const auto &psv = bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
+                inv = staticInvariant(s, ldV3(&pv.prevPosition), ldQ(&pv.prevRotation),
+                                      ldV3(&psv.v), ldV3(&psv.omega));
+            }
+            const int32_t slot = B.slotBase + r;
+            SMut *d = L.bodies + slot;
+            stV3(&d->x, s.x);
+            stQ(&d->q, s.q);
+            stV3(&d->v, s.v);
+            stV3(&d->omega, s.omega);
+            d->meta = s.meta;
+            L.flag[slot] = inv ? (int16_t)-1 : (int16_t)0;
+            L.lastItem[slot] = -1;
+            L.touch[slot] = 0;
         }
     }
 }
 
-// Number of survivors with a manifold (the world's contact count), capped at
-// maxContacts like the reference's assert (narrowphase.cpp:1130).  Reads the
-// compact per-survivor records (4 B, coalesced) with 8 chunks' loads in
-// flight, instead of the 112-B Contact records.
+__device__ __forceinline__ SMut ldBody(const SMut *p)
+{
+    SMut s;
+    s.x = ldV3(&p->x);
+    s.q = ldQ(&p->q);
+    s.v = ldV3(&p->v);
+    s.omega = ldV3(&p->omega);
+    s.meta = p->meta;
+    return s;
+}
+
+// The world's contacts: survivors with a manifold in survivor order (==
+// the reference's addManifoldToSolver append order, narrowphase.cpp:
+// 1123-1162), capped at maxContacts like the reference's assert
+// (narrowphase.cpp:1130).  One pass over the compact per-survivor records
+// (4 B, coalesced, 8 chunks' loads in flight): records k < rec_cap are
+// written, the count covers all of them.
 constexpr int32_t kInfoUnroll = 8;
 
-__device__ __forceinline__ int32_t worldContactCount(const PhysArgs &P, int32_t w, int32_t lane)
+template <typename RecPtr>
+__device__ __forceinline__ int32_t gatherContacts(const PhysArgs &P, int32_t w, RecPtr recs,
+                                                  int32_t rec_cap, int32_t lane)
 {
+    const int32_t nb = P.maxBodiesPerWorld;
     const uint32_t *info = P.survInfo + (size_t)w * P.candCapacity;
+    int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
+    int32_t *flags = P.errorFlags + w;
     const int32_t S = P.survCount[w];
-    int32_t K = 0;
+    const int32_t maxK = P.maxContacts;
+    const int32_t cap = min(rec_cap, maxK);
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    int32_t k0 = 0;
     for (int32_t chunk = 0; chunk < S; chunk += kSolverBlock * kInfoUnroll) {
         uint32_t v[kInfoUnroll];
 #pragma unroll
@@ -475,13 +731,26 @@ __device__ __forceinline__ int32_t worldContactCount(const PhysArgs &P, int32_t 
             v[u] = s < S ? info[s] : kNoManifold;
         }
 #pragma unroll
-        for (int32_t u = 0; u < kInfoUnroll; u++) K += __popcll(__ballot(v[u] != kNoManifold));
+        for (int32_t u = 0; u < kInfoUnroll; u++) {
+            const int32_t s = chunk + u * kSolverBlock + lane;
+            const bool has = v[u] != kNoManifold;
+            const uint64_t mask = __ballot(has);
+            const int32_t k = k0 + __popcll(mask & lt_mask);
+            if (has && k < maxK) order[k] = s;
+            if (has && k < cap) {
+                recs[k] = CRec { (int16_t)guardIndex((int32_t)(v[u] & 0xffffu), nb, flags, kGuardSolverBody),
+                                 (int16_t)guardIndex((int32_t)(v[u] >> 16), nb, flags, kGuardSolverBody),
+                                 0, (int16_t)s };
+            }
+            k0 += __popcll(mask);
+        }
     }
-    if (K > P.maxContacts) {
-        if (lane == 0) atomicOr(P.errorFlags + w, kErrContactOverflow);
-        K = P.maxContacts;
+    if (k0 > maxK) {
+        if (lane == 0) atomicOr(flags, kErrContactOverflow);
+        k0 = maxK;
     }
-    return K;
+    if (lane == 0) P.lastNumContacts[w] = k0;
+    return k0;
 }
 
 // ConstraintData rows the substep solves (collectConstraintsSystem copies
@@ -511,70 +780,67 @@ __device__ __forceinline__ int32_t jointBodySlot(const PhysArgs &P, int32_t w, E
     return guardIndex(slot, P.maxBodiesPerWorld, P.errorFlags + w, kGuardSolverBody);
 }
 
-// Contact records in survivor order (== the reference's addManifoldToSolver
-// append order, narrowphase.cpp:1123-1162) and their dependency levels: a
-// contact waits only for the latest earlier contact on each of its bodies
-// (invariant static bodies excepted); level = 1 + max(levels of those
-// predecessors), relaxed to its fixpoint.  One wave per world.
-template <typename RecPtr, typename PrevPtr>
-__device__ __forceinline__ int32_t orderAndLevel(const PhysArgs &P, int32_t w, SolverLDS &L,
-                                                 int32_t K, int32_t J, RecPtr recs,
-                                                 PrevPtr prevs, int32_t lane)
+// Joint items K .. K+J-1 (the reference solves joints after contacts).
+template <typename RecPtr>
+__device__ __forceinline__ void appendJoints(const PhysArgs &P, int32_t w, RecPtr recs, int32_t K,
+                                             int32_t J, int32_t lane)
 {
-    const int32_t nb = P.maxBodiesPerWorld;
-    const uint32_t *info = P.survInfo + (size_t)w * P.candCapacity;
-    int32_t *order = P.contactOrder + (size_t)w * P.candCapacity;
-    const int32_t S = P.survCount[w];
-    const uint64_t lt_mask = (1ull << lane) - 1;
-    int32_t *flags = P.errorFlags + w;
-    int32_t k0 = 0;
-    for (int32_t chunk = 0; chunk < S && k0 < K; chunk += kSolverBlock * kInfoUnroll) {
-        uint32_t v[kInfoUnroll];
-#pragma unroll
-        for (int32_t u = 0; u < kInfoUnroll; u++) {
-            const int32_t s = chunk + u * kSolverBlock + lane;
-            v[u] = s < S ? info[s] : kNoManifold;
-        }
-#pragma unroll
-        for (int32_t u = 0; u < kInfoUnroll; u++) {
-            const int32_t s = chunk + u * kSolverBlock + lane;
-            const bool has = v[u] != kNoManifold;
-            const uint64_t mask = __ballot(has);
-            const int32_t k = k0 + __popcll(mask & lt_mask);
-            if (has && k < K) {
-                recs[k] = CRec { (int16_t)guardIndex((int32_t)(v[u] & 0xffffu), nb, flags, kGuardSolverBody),
-                                 (int16_t)guardIndex((int32_t)(v[u] >> 16), nb, flags, kGuardSolverBody),
-                                 0, (int16_t)s };
-                order[k] = s;
-            }
-            k0 += __popcll(mask);
-        }
-    }
     const JointConstraint *jrows = P.joints + (size_t)w * P.jointCapacity;
     for (int32_t j = lane; j < J; j += kSolverBlock) {
         const JointConstraint &jc = jrows[j];
         recs[K + j] = CRec { (int16_t)jointBodySlot(P, w, jc.e1), (int16_t)jointBodySlot(P, w, jc.e2),
                              0, (int16_t)(-1 - j) };
     }
-    K += J;
-    waveSync();
-    for (int32_t k = lane; k < K; k += kSolverBlock) {
-        CRec r = recs[k];
-        const bool on1 = L.lastLevel[r.s1] >= 0, on2 = L.lastLevel[r.s2] >= 0;
+}
+
+// Dependency levels of the world's N items: an item waits only for the
+// latest earlier item on each of its bodies (invariant static bodies
+// excepted); level = 1 + max(levels of those predecessors), relaxed to its
+// fixpoint.  Predecessors chunk by chunk (64 items, one per lane): each
+// body's touch mask holds the chunk's lanes touching it, so an item's
+// predecessor is the highest lower lane in that mask, else the body's latest
+// item of the earlier chunks.  One wave per world.
+template <typename RecPtr, typename PrevPtr>
+__device__ __forceinline__ int32_t scheduleLevels(SolverLDS &L, int32_t N, RecPtr recs,
+                                                  PrevPtr prevs, int32_t lane)
+{
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    for (int32_t base = 0; base < N; base += kSolverBlock) {
+        const int32_t k = base + lane;
+        const bool valid = k < N;
+        const CRec r = valid ? recs[k] : CRec { 0, 0, 0, 0 };
+        const bool on1 = valid && L.flag[r.s1] >= 0;
+        const bool on2 = valid && L.flag[r.s2] >= 0 && r.s2 != r.s1;
+        if (on1) atomicOr((unsigned long long *)&L.touch[r.s1], 1ull << lane);
+        if (on2) atomicOr((unsigned long long *)&L.touch[r.s2], 1ull << lane);
+        waveSync();
         int32_t p1 = -1, p2 = -1;
-        for (int32_t j = k - 1; j >= 0 && ((on1 && p1 < 0) || (on2 && p2 < 0)); j--) {
-            const CRec q = recs[j];
-            if (on1 && p1 < 0 && (q.s1 == r.s1 || q.s2 == r.s1)) p1 = j;
-            if (on2 && p2 < 0 && (q.s1 == r.s2 || q.s2 == r.s2)) p2 = j;
+        uint64_t m1 = 0, m2 = 0;
+        if (on1) {
+            m1 = L.touch[r.s1];
+            const uint64_t lo = m1 & lt_mask;
+            p1 = lo ? base + 63 - __clzll(lo) : L.lastItem[r.s1];
         }
-        prevs[k] = (p1 & 0xffff) | (p2 << 16);
-        r.lvl = 1;
-        recs[k] = r;
+        if (on2) {
+            m2 = L.touch[r.s2];
+            const uint64_t lo = m2 & lt_mask;
+            p2 = lo ? base + 63 - __clzll(lo) : L.lastItem[r.s2];
+        }
+        waveSync();
+        // the chunk's last item on each body becomes the body's latest
+        if (on1 && 63 - __clzll(m1) == lane) L.lastItem[r.s1] = (int16_t)k;
+        if (on2 && 63 - __clzll(m2) == lane) L.lastItem[r.s2] = (int16_t)k;
+        if (on1) L.touch[r.s1] = 0;
+        if (on2) L.touch[r.s2] = 0;
+        if (valid) {
+            prevs[k] = (p1 & 0xffff) | (p2 << 16);
+            recs[k].lvl = 1;
+        }
+        waveSync();
     }
-    waveSync();
     for (;;) {
         bool changed = false;
-        for (int32_t k = lane; k < K; k += kSolverBlock) {
+        for (int32_t k = lane; k < N; k += kSolverBlock) {
             const int32_t pv = prevs[k];
             const int32_t p1 = (int16_t)(pv & 0xffff), p2 = pv >> 16;
             const int32_t l1 = p1 >= 0 ? recs[p1].lvl : 0;
@@ -589,11 +855,19 @@ __device__ __forceinline__ int32_t orderAndLevel(const PhysArgs &P, int32_t w, S
         if (!__any(changed)) break;
     }
     int32_t max_level = 0;
-    for (int32_t k = lane; k < K; k += kSolverBlock) max_level = max(max_level, (int32_t)recs[k].lvl);
+    for (int32_t k = lane; k < N; k += kSolverBlock) max_level = max(max_level, (int32_t)recs[k].lvl);
 #pragma unroll
     for (int32_t off = 32; off > 0; off >>= 1) max_level = max(max_level, __shfl_xor(max_level, off));
-    if (lane == 0) P.lastNumContacts[w] = K - J;
     return max_level;
+}
+
+__device__ __forceinline__ int32_t itemKind(const SolverLDS &L, const CRec r)
+{
+    if (r.slot < 0) return kKindGeneral;
+    const bool i1 = L.flag[r.s1] < 0, i2 = L.flag[r.s2] < 0;
+    if (i1 && !i2) return kKindStaticRef;
+    if (i2 && !i1) return kKindStaticAlt;
+    return kKindGeneral;
 }
 
 // setVelocities (physics.cpp:673-714) for one world, one wave.
@@ -604,9 +878,12 @@ __device__ __forceinline__ void setWorldVelocities(const PhysArgs &P, int32_t w,
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
         for (int32_t r = lane; r < rows; r += kSolverBlock) {
-            SMut &s = L.bodies[B.slotBase + r];
-            const auto prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
-            const Quat q = s.q, qp = prev.prevRotation;
+            SMut *s = L.bodies + B.slotBase + r;
+            const auto &prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
+            const Vector3 px = ldV3(&prev.prevPosition);
+            const Quat qp = ldQ(&prev.prevRotation);
+            const Vector3 x = ldV3(&s->x);
+            const Quat q = ldQ(&s->q);
             Quat dq;
             if (q.w != qp.w || q.x != qp.x || q.y != qp.y || q.z != qp.z) {
                 dq = q * qp.inv();
@@ -614,56 +891,108 @@ __device__ __forceinline__ void setWorldVelocities(const PhysArgs &P, int32_t w,
                 dq = Quat { 1, 0, 0, 0 };
             }
             Vector3 new_omega = 2.f / h * Vector3 { dq.x, dq.y, dq.z };
-            s.v = (s.x - prev.prevPosition) / h;
-            s.omega = dq.w > 0.f ? new_omega : -new_omega;
+            stV3(&s->v, (x - px) / h);
+            stV3(&s->omega, dq.w > 0.f ? new_omega : -new_omega);
         }
     }
 }
 
+// Write the solved bodies back; integrate_next: then run the next
+// substep's substepRigidBodies on them (integrateBody writes the pose).
 __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, SolverLDS &L,
-                                                 int32_t lane)
+                                                 int32_t lane, bool integrate_next)
 {
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
         for (int32_t r = lane; r < rows; r += kSolverBlock) {
-            const SMut &s = L.bodies[B.slotBase + r];
-            bcol<Vector3>(B, Cols::Position, w, r) = s.x;
-            bcol<Quat>(B, Cols::Rotation, w, r) = s.q;
-            bcol<Velocity>(B, Cols::Velocity, w, r) = Velocity { s.v, s.omega };
+            const SMut *s = L.bodies + B.slotBase + r;
+            const Vector3 x = ldV3(&s->x), v = ldV3(&s->v), om = ldV3(&s->omega);
+            const Quat q = ldQ(&s->q);
+            Velocity &vel = bcol<Velocity>(B, Cols::Velocity, w, r);
+            stV3(&vel.linear, v);
+            stV3(&vel.angular, om);
+            if (integrate_next) {
+                integrateBody(P, B, w, r, x, q, v, om);
+            } else {
+                stV3(&bcol<Vector3>(B, Cols::Position, w, r), x);
+                stQ(&bcol<Quat>(B, Cols::Rotation, w, r), q);
+            }
         }
     }
     if (lane == 0) P.solver[w].numContacts = 0;           // physics.cpp:1007
 }
 
-// One positional item: a contact (solveContactPositions) or a joint.
+#if defined(MW_SOLVER_PROFILE)
+static __device__ unsigned long long g_solverPhase[16];
+static __device__ unsigned long long g_solverBlockT[2 * 16384];   // start, end per block (last launch)
+#endif
+
+// One positional item: a contact (solveContactPositions) or a joint.  A
+// contact against an invariant static body skips that body's side; if the
+// skipping solve meets a non-finite lambda it is redone in full, which
+// writes the static body the level schedule treated as untouched: the world
+// is flagged.
+__device__ __forceinline__ void skipSides(int32_t kind, const ContactIn &c, bool &sk1, bool &sk2)
+{
+    sk1 = kind == kKindStaticRef;
+    sk2 = kind == kKindStaticAlt;
+    if ((sk1 || sk2) && !boundedInput(c)) sk1 = sk2 = false;
+}
+
 __device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w, SolverLDS &L,
-                                                   const CRec r)
+                                                   const CRec r, int32_t kind)
 {
     if (r.slot >= 0) {
-        Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
-        solveContactPositions(P, w, L.bodies[r.s1], r.s1, L.bodies[r.s2], r.s2, c);
+        Contact &cr = P.candContacts[(size_t)w * P.candCapacity + r.slot];
+        const ContactIn c = loadContact(cr);
+        SMut &b1 = L.bodies[r.s1], &b2 = L.bodies[r.s2];
+        bool sk1, sk2;
+        skipSides(kind, c, sk1, sk2);
+        while (solveContactPositions(P, w, b1, r.s1, b2, r.s2, c, cr.lambdaN, sk1, sk2) != kSolveDone) {
+            atomicOr(P.errorFlags + w, kErrStaticSchedule);
+            sk1 = sk2 = false;
+        }
     } else {
         const JointConstraint &j = P.joints[(size_t)w * P.jointCapacity + (-1 - r.slot)];
         solveJoint(P, L.bodies[r.s1], L.bodies[r.s2], j);
     }
 }
 
-// Fallback for a world whose contacts do not fit the LDS records: the whole
+__device__ __forceinline__ void solveItemVelocities(const PhysArgs &P, int32_t w, SolverLDS &L,
+                                                    const CRec r, int32_t kind)
+{
+    if (r.slot < 0) return;                                // joints: positions only
+    const ContactIn c = loadContact(P.candContacts[(size_t)w * P.candCapacity + r.slot]);
+    const SolverData &sd = P.solver[w];
+    SMut &b1 = L.bodies[r.s1], &b2 = L.bodies[r.s2];
+    bool sk1, sk2;
+    skipSides(kind, c, sk1, sk2);
+    while (solveContactVelocities(P, w, b1, r.s1, b2, r.s2, c, sd.h, sd.restitutionThreshold,
+                                  sk1, sk2) != kSolveDone) {
+        atomicOr(P.errorFlags + w, kErrStaticSchedule);
+        sk1 = sk2 = false;
+    }
+}
+
+// Fallback for a world whose items do not fit the LDS records: the whole
 // solve on its own wave, records in the global slab, level by level.
 __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, SolverLDS L,
-                                              int32_t K, int32_t J, int32_t lane)
+                                                 int32_t J, int32_t lane)
 {
     CRec *recs = (CRec *)(P.solverRecs + (size_t)w * P.recStride);
     int32_t *prevs = P.solverPrevs + (size_t)w * P.recStride;
-    const int32_t max_level = orderAndLevel(P, w, L, K, J, recs, prevs, lane);
-    const SolverData &sd = P.solver[w];
+    const int32_t K = gatherContacts(P, w, recs, INT32_MAX, lane);
+    appendJoints(P, w, recs, K, J, lane);
+    waveSync();
     const int32_t N = K + J;
+    const int32_t max_level = scheduleLevels(L, N, recs, prevs, lane);
+    const SolverData &sd = P.solver[w];
     for (int32_t l = 1; l <= max_level; l++) {
         for (int32_t k = lane; k < N; k += kSolverBlock) {
             const CRec r = recs[k];
             if (r.lvl != l) continue;
-            solveItemPositions(P, w, L, r);
+            solveItemPositions(P, w, L, r, itemKind(L, r));
         }
         waveSync();
     }
@@ -673,9 +1002,7 @@ __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, S
         for (int32_t k = lane; k < K; k += kSolverBlock) {   // joints sort last
             const CRec r = recs[k];
             if (r.lvl != l) continue;
-            const Contact &c = P.candContacts[(size_t)w * P.candCapacity + r.slot];
-            solveContactVelocities(P, w, L.bodies[r.s1], r.s1, L.bodies[r.s2], r.s2, c, sd.h,
-                                   sd.restitutionThreshold);
+            solveItemVelocities(P, w, L, r, itemKind(L, r));
         }
         waveSync();
     }
@@ -684,7 +1011,6 @@ __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, S
 // Phase profile (experiments only, -DMW_SOLVER_PROFILE): per-phase sums of
 // block time in 10 ns device-clock ticks, read by mw_debug_solver_phases.
 #if defined(MW_SOLVER_PROFILE)
-static __device__ unsigned long long g_solverPhase[16];
 #define MW_SOLVER_MARK(i)                                                        \
     do {                                                                         \
         if (threadIdx.x == 0) {                                                  \
@@ -705,12 +1031,13 @@ static __device__ unsigned long long g_solverPhase[16];
 #endif
 
 // XPBD solver, kSolverWorlds worlds per block (one wave each for the
-// per-world phases).  The Gauss-Seidel contact passes run level by level
-// over the block's level-sorted (world, contact) list, so a level's
-// contacts from all of the block's worlds share the lanes: sparse deep
-// levels no longer cost a full wave pass per world.
+// per-world phases).  The Gauss-Seidel passes run level by level over the
+// block's (level, kind)-sorted (world, item) list, so a level's items from
+// all of the block's worlds share the lanes and a wave's lanes mostly share
+// a code path.
 __global__ void __launch_bounds__(kSolverThreads)
-__attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(PhysArgs P)
+__attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(PhysArgs P,
+                                                                            int32_t integrate_next)
 {
     MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -724,13 +1051,14 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
 
 #if defined(MW_SOLVER_PROFILE)
     long long prof_t = wall_clock64();
+    if (threadIdx.x == 0 && blockIdx.x < 16384) g_solverBlockT[2 * blockIdx.x] = (unsigned long long)prof_t;
 #endif
-    if (threadIdx.x == 0) { BL.scalars[0] = 0; BL.scalars[1] = 0; BL.scalars[2] = 0; }
+    if (threadIdx.x == 0) { BL.scalars[1] = 0; BL.scalars[2] = 0; }
     int32_t K = 0, J = 0;
     if (live) {
         loadWorldBodies(P, w, L, lane);
-        K = worldContactCount(P, w, lane);
         J = worldJointCount(P, w, lane);
+        K = gatherContacts(P, w, L.recs, kSolverLDSContacts, lane);
     }
     __syncthreads();
     if (live && lane == 0) atomicMax(&BL.scalars[1], K + J);
@@ -741,45 +1069,56 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     if (!fits) {
         // some world of the block overflows the LDS records: every world
         // of the block solves on its own wave with global records
+        if (integrate_next && blockIdx.x == 0) zeroGroupCounts(P, threadIdx.x, kSolverThreads);
         if (live) {
-            solveWorldGlobal(P, w, L, K, J, lane);
-            writeWorldBodies(P, w, L, lane);
+            solveWorldGlobal(P, w, L, J, lane);
+            writeWorldBodies(P, w, L, lane, integrate_next != 0);
         }
         return;
     }
 
+    const int32_t N = K + J;     // contacts, then joints
     int32_t my_levels = 0;
-    if (live) my_levels = orderAndLevel(P, w, L, K, J, L.recs, L.prevs, lane);
+    if (live) {
+        appendJoints(P, w, L.recs, K, J, lane);
+        waveSync();
+        my_levels = scheduleLevels(L, N, L.recs, L.prevs, lane);
+    }
     if (live && lane == 0) atomicMax(&BL.scalars[2], my_levels);
     __syncthreads();
     const int32_t max_level = BL.scalars[2];
     MW_SOLVER_MARK(1);
 
-    // counting sort of the block's contacts by level
-    for (int32_t i = threadIdx.x; i <= max_level + 1; i += kSolverThreads) {
-        BL.levelOff[i] = 0;
-        BL.levelCur[i] = 0;
+    // counting sort of the block's items by (level, kind)
+    const int32_t nbk = (max_level + 2) * kNumKinds;
+    for (int32_t i = threadIdx.x; i < nbk; i += kSolverThreads) {
+        BL.bucketOff[i] = 0;
+        BL.bucketCur[i] = 0;
     }
     __syncthreads();
-    const int32_t N = K + J;     // contacts, then joints
     if (live) {
-        for (int32_t k = lane; k < N; k += kSolverBlock) atomicAdd(&BL.levelOff[L.recs[k].lvl], 1);
+        for (int32_t k = lane; k < N; k += kSolverBlock) {
+            const CRec r = L.recs[k];
+            atomicAdd(&BL.bucketOff[r.lvl * kNumKinds + itemKind(L, r)], 1);
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         int32_t run = 0;
-        for (int32_t l = 0; l <= max_level + 1; l++) {
-            const int32_t c = BL.levelOff[l];
-            BL.levelOff[l] = run;
+        for (int32_t b = 0; b < nbk; b++) {
+            const int32_t c = BL.bucketOff[b];
+            BL.bucketOff[b] = run;
             run += c;
         }
     }
     __syncthreads();
     if (live) {
         for (int32_t k = lane; k < N; k += kSolverBlock) {
-            const int32_t l = L.recs[k].lvl;
-            const int32_t pos = BL.levelOff[l] + atomicAdd(&BL.levelCur[l], 1);
-            BL.items[pos] = ((uint32_t)wi << 16) | (uint32_t)k;
+            const CRec r = L.recs[k];
+            const int32_t kind = itemKind(L, r);
+            const int32_t b = r.lvl * kNumKinds + kind;
+            const int32_t pos = BL.bucketOff[b] + atomicAdd(&BL.bucketCur[b], 1);
+            BL.items[pos] = ((uint32_t)wi << 16) | ((uint32_t)kind << 12) | (uint32_t)k;
         }
     }
     __syncthreads();
@@ -787,13 +1126,13 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
 
     // solvePositions, level by level over the whole block
     for (int32_t l = 1; l <= max_level; l++) {
-        const int32_t beg = BL.levelOff[l], end = BL.levelOff[l + 1];
+        const int32_t beg = BL.bucketOff[l * kNumKinds], end = BL.bucketOff[(l + 1) * kNumKinds];
         for (int32_t t = beg + threadIdx.x; t < end; t += kSolverThreads) {
             const uint32_t it = BL.items[t];
-            const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xffffu);
+            const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xfffu);
             const int32_t ww = blockIdx.x * kSolverWorlds + iw;
             SolverLDS LW = solverWorldLDS(smem, nb, iw);
-            solveItemPositions(P, ww, LW, LW.recs[k]);
+            solveItemPositions(P, ww, LW, LW.recs[k], (int32_t)((it >> 12) & 0xfu));
         }
         __syncthreads();
     }
@@ -805,33 +1144,35 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
 
     // solveVelocities, same schedule
     for (int32_t l = 1; l <= max_level; l++) {
-        const int32_t beg = BL.levelOff[l], end = BL.levelOff[l + 1];
+        const int32_t beg = BL.bucketOff[l * kNumKinds], end = BL.bucketOff[(l + 1) * kNumKinds];
         for (int32_t t = beg + threadIdx.x; t < end; t += kSolverThreads) {
             const uint32_t it = BL.items[t];
-            const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xffffu);
+            const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xfffu);
             const int32_t ww = blockIdx.x * kSolverWorlds + iw;
             SolverLDS LW = solverWorldLDS(smem, nb, iw);
-            const CRec r = LW.recs[k];
-            if (r.slot < 0) continue;                      // joints: positions only
-            const Contact &c = P.candContacts[(size_t)ww * P.candCapacity + r.slot];
-            const SolverData &sd = P.solver[ww];
-            solveContactVelocities(P, ww, LW.bodies[r.s1], r.s1, LW.bodies[r.s2], r.s2, c,
-                                   sd.h, sd.restitutionThreshold);
+            solveItemVelocities(P, ww, LW, LW.recs[k], (int32_t)((it >> 12) & 0xfu));
         }
         __syncthreads();
     }
 
     MW_SOLVER_MARK(5);
-    if (live) writeWorldBodies(P, w, L, lane);
+    if (integrate_next && blockIdx.x == 0) zeroGroupCounts(P, threadIdx.x, kSolverThreads);
+    if (live) writeWorldBodies(P, w, L, lane, integrate_next != 0);
     __syncthreads();
     MW_SOLVER_MARK(6);
 #if defined(MW_SOLVER_PROFILE)
+    if (threadIdx.x == 0 && blockIdx.x < 16384) g_solverBlockT[2 * blockIdx.x + 1] = (unsigned long long)wall_clock64();
     if (threadIdx.x == 0) atomicAdd(&g_solverPhase[7], 1ull);
     if (threadIdx.x == 0) atomicAdd(&g_solverPhase[8], (unsigned long long)max_level);
 #endif
 }
 
 #if defined(MW_SOLVER_PROFILE)
+extern "C" int mw_debug_solver_block_times(unsigned long long *out, int n)
+{
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solverBlockT), sizeof(unsigned long long) * 2 * n) == hipSuccess ? 0 : -1;
+}
+
 extern "C" int mw_debug_solver_phases(unsigned long long *out)
 {
     unsigned long long z[16] = {};

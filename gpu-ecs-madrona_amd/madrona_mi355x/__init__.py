@@ -234,7 +234,10 @@ def gen_collisions_inits(num_worlds, num_cubes=128, seed=0, first_world=0):
 
 ERR_BITS = {1: "id store full", 2: "table full", 4: "candidate overflow",
             8: "contact overflow", 16: "BVH stack overflow", 32: "solver body overflow",
-            64: "index guard (site in bits 8..15)"}
+            64: "index guard (site in bits 8..15)", 128: "joint overflow",
+            1 << 16: "job dropped", 1 << 17: "tmpAlloc arena full", 1 << 18: "deferred log full",
+            1 << 19: "op not available in a row-parallel node", 1 << 20: "commit limit",
+            1 << 21: "static body written by a non-finite solve"}
 
 
 # DeviceLog (include/madrona/tracing.hpp; reference mw_gpu/tracing.hpp:30-41).

@@ -24,7 +24,7 @@ def main():
     sim = mw.CollisionsSim(W, pos, rot, cfg)
     lib = mw.library()
     out = np.zeros(16, np.uint64)
-    sim.step(120)
+    sim.step(int(os.environ.get('SETTLE', '220')))
     lib.mw_debug_solver_phases(out.ctypes.data_as(ctypes.c_void_p))
     sim.step(10)
     lib.mw_debug_solver_phases(out.ctypes.data_as(ctypes.c_void_p))
@@ -34,6 +34,21 @@ def main():
     for i, n in enumerate(PHASES):
         print(f"{n:14s} {out[i] * 10 / 1e3 / blocks:8.2f} us/block  {100 * out[i] / tot:5.1f} %")
     print(f"{'total':14s} {tot * 10 / 1e3 / blocks:8.2f} us/block")
+    nblk = W // 2
+    bt = np.zeros(2 * nblk, np.uint64)
+    lib.mw_debug_solver_block_times(bt.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(nblk))
+    st = bt[0::2].astype(np.int64)
+    en = bt[1::2].astype(np.int64)
+    t0 = st.min()
+    st, en = (st - t0) * 10 / 1e3, (en - t0) * 10 / 1e3
+    dur = en - st
+    print(f"last launch: span {en.max():.1f} us; block duration mean {dur.mean():.1f} p50 {np.median(dur):.1f} "
+          f"p99 {np.percentile(dur, 99):.1f} max {dur.max():.1f}; last start {st.max():.1f}")
+    for q in (0.25, 0.5, 0.75, 0.9, 1.0):
+        print(f"  blocks started by {q * en.max():6.1f} us: {(st <= q * en.max()).mean() * 100:5.1f} %  "
+              f"finished: {(en <= q * en.max()).mean() * 100:5.1f} %")
+    print("position items: skip ref", int(out[9]), "skip alt", int(out[10]), "general", int(out[11]),
+          "| numPoints 4/1/2/3:", [int(x) for x in out[12:16]])
 
 
 if __name__ == "__main__":
