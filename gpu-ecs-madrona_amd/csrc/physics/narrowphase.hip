@@ -14,9 +14,7 @@ namespace madrona::phys {
 __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
-    // Zero the per-64-world survivor sums the narrowphase filter accumulates
-    // (the previous substep's compact kernel has finished reading them).
-    if (blockIdx.x == 0 && blockIdx.y == 0) zeroGroupCounts(P, threadIdx.x, blockDim.x);
+    if (blockIdx.x == 0 && blockIdx.y == 0) resetNarrowLists(P, threadIdx.x, blockDim.x);
     const BodyArch &B = P.body[blockIdx.y];
     RowIdx ri = rowIndex(P, B);
     if (!ri.valid) return;
@@ -473,104 +471,233 @@ __device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
     return true;
 }
 
-// Stage 1, block per world: AABB recheck + type ordering of every candidate.
-// One block scan numbers the survivors in candidate order (survivor slot ==
-// contact slot) and, packed in the same scan, numbers the hull-hull and
-// hull-plane survivors separately; both go to the world's staging row
-// (hull-hull from the front, hull-plane from the back).  No global atomics.
+// buildFaceContactManifold (narrowphase.cpp:790-864) written straight into
+// the contact slot from up to four chosen points (storeFaceManifold's tail).
+__device__ __forceinline__ void writeFaceManifold(Contact &c, Vector3 n, const Vector3 *cp,
+                                                  const float *depth, int32_t m, Loc ref, Loc alt)
+{
+    const Quat ident { 1, 0, 0, 0 };
+    c.ref = ref;
+    c.alt = alt;
+    for (int i = 0; i < 4; i++) {
+        Vector3 p = (i < m) ? ident.rotateVec(cp[i]) + Vector3::zero() : cp[i];
+        c.points[i] = Vector4::fromVector3(p, depth[i]);
+    }
+    c.numPoints = m;
+    c.normal = ident.rotateVec(n);
+    for (int i = 0; i < 4; i++) c.lambdaN[i] = 0.f;
+}
+
+// Hull a against the plane of body b: doSATPlane (narrowphase.cpp:760-788)
+// + createFacePlaneContact (:974-1017) + buildFaceContactManifold (:790-864)
+// with O(1) state: the incident face's loop is walked once to count the
+// points below the plane and keep the first four, and -- only for a face
+// with more than four such points -- again for each of the reference's
+// point choices (farthest from p0, then the last positive and the last
+// negative area against the p0-p1 line, each over the point list with the
+// earlier choices replaced by p0).  Every walk recomputes the same vertices
+// with the same operations, so the chosen points are the reference's bits.
+// Returns true if a manifold was written.
+__device__ bool planeContact(const PhysArgs &P, int32_t w, const SatWork &wk)
+{
+    const ObjDev &O = P.objs;
+    int32_t *flags = P.errorFlags + w;
+    const HullDev ha = O.hulls[wk.aObj];
+    const HullXform xa = hullXform(P, w, P.body[wk.aArch], wk.a.row);
+    const BodyArch &BB = P.body[wk.bArch];
+    const Vector3 b_pos = bcol<Vector3>(BB, Cols::Position, w, wk.b.row);
+    const Quat b_rot = bcol<Quat>(BB, Cols::Rotation, w, wk.b.row);
+    const Vector3 pn = b_rot.rotateVec(Vector3 { 0, 0, 1 });
+    const geometry::Plane plane { pn, dot(pn, b_pos) };
+    float min_dot = FLT_MAX;
+    for (int32_t v = 0; v < ha.numVerts; v++) {
+        const float d = plane.normal.dot(worldVertex(O, ha, xa, v));
+        if (d < min_dot) min_dot = d;
+    }
+    if (min_dot - plane.d > 0.0f) return false;
+    float min_fd = FLT_MAX;
+    int32_t inc_face = -1;
+    for (int32_t f = 0; f < ha.numFaces; f++) {
+        const float d = dot(worldPlane(O, ha, xa, f).normal, plane.normal);
+        if (d < min_fd) { min_fd = d; inc_face = f; }
+    }
+    inc_face = guardIndex(inc_face, ha.numFaces, flags, kGuardPlaneFace);
+    const geometry::HalfEdge *hh = O.hedges + ha.hedgeOffset;
+    const uint32_t start = O.polygons[ha.faceOffset + inc_face];
+    const int32_t cap = P.clipCap;
+    // The face's below-plane points in walk order (the reference's contacts /
+    // depths arrays), capped at cap like the clip buffer.
+    auto walk = [&](auto &&fn) {
+        int32_t n = 0, steps = 0;
+        uint32_t hidx = start;
+        do {
+            hidx = guardIndex(hidx, ha.numHedges, flags, kGuardPlaneWalk);
+            const geometry::HalfEdge he = hh[hidx];
+            hidx = he.next;
+            const Vector3 v = worldVertex(O, ha, xa,
+                                          guardIndex(he.rootVertex, ha.numVerts, flags, kGuardVertex));
+            const float d = distFromPlane(plane, v);
+            if (d < 0.0f && n < cap) {
+                fn(n, v - d * plane.normal, -d);
+                n++;
+            }
+        } while (hidx != start && ++steps <= ha.numHedges);
+        return n;
+    };
+    Vector3 cp[4];
+    float depth[4];
+    for (int i = 0; i < 4; i++) { cp[i] = Vector3::zero(); depth[i] = 0.f; }
+    const int32_t num = walk([&](int32_t i, Vector3 c, float dd) {
+        if (i < 4) {
+            cp[i & 3] = c;
+            depth[i & 3] = dd;
+        }
+    });
+    int32_t m = num;
+    if (num > 4) {
+        m = 4;
+        const Vector3 p0 = cp[0];
+        Vector3 c1 = Vector3::zero(), c2 = Vector3::zero(), c3 = Vector3::zero();
+        float d1 = 0.f, d2 = 0.f, d3 = 0.f;
+        float largest_d2 = 0.0f;
+        int32_t i1 = 0;
+        walk([&](int32_t i, Vector3 c, float dd) {
+            if (i == 0) return;
+            const float dist2 = p0.distance2(c);
+            if (dist2 > largest_d2) { largest_d2 = dist2; c1 = c; d1 = dd; i1 = i; }
+        });
+        const Vector3 diff0 = c1 - p0;
+        int32_t i2 = 0;                                    // largest_area_idx
+        walk([&](int32_t i, Vector3 c, float dd) {
+            if (i == 0) return;
+            if (i == i1) c = p0;                           // contacts[largest_d2_idx] = cp[0]
+            const float area = plane.normal.dot(diff0.cross(c - p0));
+            if (area > 0.0f) { c2 = c; d2 = dd; i2 = i; }
+        });
+        walk([&](int32_t i, Vector3 c, float dd) {
+            if (i == 0) return;
+            if (i == i1 || i == i2) c = p0;                // contacts[largest_area_idx] = cp[0]
+            const float area = plane.normal.dot(diff0.cross(c - p0));
+            if (area < 0.0f) { c3 = c; d3 = dd; }
+        });
+        cp[1] = c1; cp[2] = c2; cp[3] = c3;
+        depth[1] = d1; depth[2] = d2; depth[3] = d3;
+    }
+    if (m == 0) return false;
+    writeFaceManifold(P.candContacts[(size_t)w * P.candCapacity + wk.slot], plane.normal, cp, depth,
+                      m, wk.b, wk.a);
+    return true;
+}
+
+// Body slot (the solver's per-world body index) of a pair member.
+__device__ __forceinline__ int32_t slotOf(const PhysArgs &P, int32_t arch_idx, Loc l)
+{
+    return P.body[arch_idx].slotBase + l.row;
+}
+
+// The survivor's compact solver record: ref / alt body slots.
+__device__ __forceinline__ void recordManifold(const PhysArgs &P, int32_t w, int32_t slot,
+                                               int32_t ref_slot, int32_t alt_slot)
+{
+    P.survInfo[(size_t)w * P.candCapacity + slot] =
+        (uint32_t)(ref_slot & 0xffff) | ((uint32_t)(alt_slot & 0xffff) << 16);
+}
+
+// Narrowphase stage 1, block per world: AABB recheck + type ordering of
+// every candidate, kFilterPer consecutive candidates per thread (their loads
+// in flight together).  One block scan numbers the survivors in candidate
+// order (survivor slot == contact slot, the reference's append order) and,
+// packed in the same scan, the hull-hull and hull-plane survivors; the block
+// then reserves its entries in its bin (world % kNarrowBins) with one atomic
+// per list: hull-hull from the bin's front (for the SAT kernel), hull-plane
+// from its back (for the plane-contact kernel).  The lists' order does not
+// matter: every entry writes only its own slot.
+constexpr int32_t kFilterPer = 3;
+static_assert(kNarrowBlock * kFilterPer < 1024, "10-bit packed scan fields");
+
 __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
     __shared__ int32_t s_scan[kNarrowBlock / 64];
+    __shared__ int32_t s_base[2];
     const int32_t w = blockIdx.x;
     const int32_t cap = P.candCapacity;
     const int32_t num = min(P.numCands[w], cap);
     const CandidateCollision *cands = P.cands + (size_t)w * cap;
-    Contact *slots = P.candContacts + (size_t)w * cap;
-    SatWork *stage = P.satStage + (size_t)w * cap;
+    uint32_t *info = P.survInfo + (size_t)w * cap;
+    const int32_t bin = w % kNarrowBins;
+    SatWork *list = P.satWork + (size_t)bin * P.binCap;
+    SatWork *list_back = list + P.binCap - 1;              // plane entries grow down
     constexpr uint32_t kHull = (uint32_t)CollisionPrimitive::Type::Hull;
     constexpr uint32_t kHullPlane = kHull | (uint32_t)CollisionPrimitive::Type::Plane;
 
-    int32_t S = 0, nhh = 0, npl = 0;
-    for (int32_t chunk = 0; chunk < num; chunk += kNarrowBlock) {
-        const int32_t ci = chunk + threadIdx.x;
-        SatWork wk;
-        const bool keep = ci < num && resolvePair(P, w, cands[ci], wk);
-        const bool hh = keep && wk.test == kHull;
-        const bool pl = keep && wk.test == kHullPlane;
-        // sphere / plane-plane survivors get a slot but no manifold: the
-        // reference asserts on them (narrowphase.cpp:1197-1313)
-        const int32_t packed = (keep ? 1 : 0) | (hh ? 1 << 10 : 0) | (pl ? 1 << 20 : 0);
+    int32_t S = 0;
+    for (int32_t base = 0; base < num; base += kNarrowBlock * kFilterPer) {
+        SatWork wk[kFilterPer];
+        bool keep[kFilterPer];
+        int32_t packed = 0;
+        const int32_t first = base + (int32_t)threadIdx.x * kFilterPer;
+#pragma unroll
+        for (int32_t j = 0; j < kFilterPer; j++) {
+            const int32_t ci = first + j;
+            keep[j] = ci < num && resolvePair(P, w, cands[ci], wk[j]);
+            packed += keep[j] ? 1 : 0;
+            packed += keep[j] && wk[j].test == kHull ? 1 << 10 : 0;
+            packed += keep[j] && wk[j].test == kHullPlane ? 1 << 20 : 0;
+        }
         int32_t total;
         const int32_t off = blockExclusiveScan(packed, s_scan, &total);
-        if (keep) {
-            wk.slot = S + (off & 1023);
-            slots[wk.slot].numPoints = 0;
-            P.survInfo[(size_t)w * cap + wk.slot] = kNoManifold;
-            if (hh) stage[nhh + ((off >> 10) & 1023)] = wk;
-            if (pl) stage[cap - 1 - (npl + (off >> 20))] = wk;
+        if (threadIdx.x == 0) {
+            const int32_t thh = (total >> 10) & 1023, tpl = total >> 20;
+            s_base[0] = thh > 0 ? atomicAdd(binCounter(P, bin, 0), thh) : 0;
+            s_base[1] = tpl > 0 ? atomicAdd(binCounter(P, bin, 1), tpl) : 0;
+        }
+        __syncthreads();
+        int32_t hpos = s_base[0] + ((off >> 10) & 1023);
+        int32_t ppos = s_base[1] + (off >> 20);
+        int32_t slot = S + (off & 1023);
+#pragma unroll
+        for (int32_t j = 0; j < kFilterPer; j++) {
+            if (!keep[j]) continue;
+            wk[j].slot = slot;
+            info[slot] = kNoManifold;
+            if (wk[j].test == kHull) {
+                list[hpos++] = wk[j];
+            } else if (wk[j].test == kHullPlane) {
+                *(list_back - ppos++) = wk[j];
+            }
+            // sphere / plane-plane survivors get a slot but no manifold:
+            // the reference asserts on them (narrowphase.cpp:1197-1313)
+            slot++;
         }
         S += total & 1023;
-        nhh += (total >> 10) & 1023;
-        npl += total >> 20;
     }
-    if (threadIdx.x == 0) {
-        P.survCount[w] = S;
-        P.hhCount[w] = nhh;
-        P.planeCount[w] = npl;
-        // packed (hull-hull | hull-plane << 32) sum of this world's group of
-        // 64: the compact kernel's offsets need only these plus the <= 63
-        // counts before it in its group (no separate scan launch); 64 worlds
-        // share an address, so the atomics barely contend
-        atomicAdd(P.groupCounts + (w >> 6),
-                  (unsigned long long)(uint32_t)nhh | ((unsigned long long)(uint32_t)npl << 32));
-    }
+    if (threadIdx.x == 0) P.survCount[w] = S;
 }
 
-// Stage 2, block per world: the world's offsets in the flat lists (sum of
-// the group sums before its group + the counts before it in its group, one
-// wave), then move its staged pairs there (hull-plane pairs become contact
-// jobs directly).  World order in the flat lists = world index.
-__global__ void __launch_bounds__(kNarrowBlock) narrowCompactKernel(PhysArgs P)
+// Hull-plane contacts, one lane per pair of the bins' back parts.
+__global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
-    __shared__ unsigned long long s_off;
-    const int32_t w = blockIdx.x;
-    const int32_t cap = P.candCapacity;
-    const SatWork *stage = P.satStage + (size_t)w * cap;
-    const int32_t nhh = P.hhCount[w], npl = P.planeCount[w];
-    if (threadIdx.x < 64) {
-        const int32_t g = w >> 6;
-        unsigned long long acc = 0;
-        for (int32_t j = threadIdx.x; j < g; j += 64) acc += P.groupCounts[j];
-        const int32_t wi = (g << 6) + threadIdx.x;
-        if (wi < w) {
-            acc += (unsigned long long)(uint32_t)P.hhCount[wi] |
-                   ((unsigned long long)(uint32_t)P.planeCount[wi] << 32);
+    __shared__ int32_t s_pre[kNarrowBins + 1];
+    loadBinPrefix(P, 1, s_pre);
+    const int32_t total = s_pre[kNarrowBins];
+    for (int32_t i = blockIdx.x * kContactBlock + threadIdx.x; i < total;
+         i += gridDim.x * kContactBlock) {
+        const SatWork wk = P.satWork[binEntry(P, s_pre, i, 1)];
+        const bool ok = (uint32_t)wk.world < (uint32_t)P.numWorlds &&
+                        (uint32_t)wk.slot < (uint32_t)P.candCapacity &&
+                        (uint32_t)wk.aObj < (uint32_t)P.objs.numObjects &&
+                        (uint32_t)wk.aArch < (uint32_t)P.numBodyArchs &&
+                        (uint32_t)wk.bArch < (uint32_t)P.numBodyArchs &&
+                        (uint32_t)wk.a.row < (uint32_t)P.body[wk.aArch].capacity &&
+                        (uint32_t)wk.b.row < (uint32_t)P.body[wk.bArch].capacity;
+        if (!ok) {
+            atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
+            continue;
         }
-#pragma unroll
-        for (int32_t o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-        if (threadIdx.x == 0) {
-            s_off = acc;
-            if (w == P.numWorlds - 1) {                    // list totals
-                *P.satWorkCount = (int32_t)(uint32_t)acc + nhh;
-                *P.jobCount = (int32_t)(acc >> 32) + npl;
-            }
-        }
-    }
-    __syncthreads();
-    SatWork *hh_out = P.satWork + (uint32_t)s_off;
-    ContactJob *pl_out = P.planeJobs + (uint32_t)(s_off >> 32);
-    for (int32_t i = threadIdx.x; i < nhh; i += kNarrowBlock) hh_out[i] = stage[i];
-    for (int32_t i = threadIdx.x; i < npl; i += kNarrowBlock) {
-        ContactJob job;
-        job.pair = stage[cap - 1 - i];
-        job.kind = kJobPlane;
-        job.refIsA = 0;
-        job.feature0 = 0;
-        job.feature1 = 0;
-        job.plane = geometry::Plane { { 0, 0, 0 }, 0 };
-        pl_out[i] = job;
+        if (planeContact(P, wk.world, wk))
+            recordManifold(P, wk.world, wk.slot, slotOf(P, wk.bArch, wk.b), slotOf(P, wk.aArch, wk.a));
     }
 }
 
@@ -631,10 +758,12 @@ __global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKern
     const int32_t group = threadIdx.x / kGroup;
     const int32_t lane = threadIdx.x % kGroup;
     const GroupLDS g = groupLDS(smem, group, P.objs);
-    const int32_t total = *(volatile int32_t *)P.satWorkCount;
+    __shared__ int32_t s_pre[kNarrowBins + 1];
+    loadBinPrefix(P, 0, s_pre);
+    const int32_t total = s_pre[kNarrowBins];
     const int32_t stride = gridDim.x * kGroupsPerBlock;
     for (int32_t idx = blockIdx.x * kGroupsPerBlock + group; idx < total; idx += stride) {
-        const SatWork wk = P.satWork[idx];
+        const SatWork wk = P.satWork[binEntry(P, s_pre, idx, 0)];
         const bool ok = (uint32_t)wk.world < (uint32_t)P.numWorlds &&
                         (uint32_t)wk.slot < (uint32_t)P.candCapacity &&
                         (uint32_t)wk.aObj < (uint32_t)P.objs.numObjects &&
@@ -665,19 +794,6 @@ size_t contactSharedBytes(const PhysArgs &P)
     return contactLDSBytes(P.clipCap);
 }
 
-// Body slot (the solver's per-world body index) of a pair member.
-__device__ __forceinline__ int32_t slotOf(const PhysArgs &P, int32_t arch_idx, Loc l)
-{
-    return P.body[arch_idx].slotBase + l.row;
-}
-
-// The survivor's compact solver record: ref / alt body slots.
-__device__ __forceinline__ void recordManifold(const PhysArgs &P, int32_t w, int32_t slot,
-                                               int32_t ref_slot, int32_t alt_slot)
-{
-    P.survInfo[(size_t)w * P.candCapacity + slot] =
-        (uint32_t)(ref_slot & 0xffff) | ((uint32_t)(alt_slot & 0xffff) << 16);
-}
 
 // createFaceContact / createFacePlaneContact / createEdgeContact
 // (narrowphase.cpp:866-1121) for one job per lane.
@@ -693,11 +809,12 @@ __global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
     float *depths = (float *)(mine + 2 * a16(sizeof(Vector3) * cap));
     const Quat ident { 1, 0, 0, 0 };
 
-    const int32_t n_plane = *(volatile int32_t *)P.jobCount;
-    const int32_t total = n_plane + *(volatile int32_t *)P.satWorkCount;
+    __shared__ int32_t s_pre[kNarrowBins + 1];
+    loadBinPrefix(P, 0, s_pre);
+    const int32_t total = s_pre[kNarrowBins];
     for (int32_t i = blockIdx.x * kContactBlock + threadIdx.x; i < total;
          i += gridDim.x * kContactBlock) {
-        const ContactJob job = i < n_plane ? P.planeJobs[i] : P.hhJobs[i - n_plane];
+        const ContactJob job = P.hhJobs[i];
         if (job.kind == kJobNone) continue;
         const SatWork &wk = job.pair;
         const int32_t w = wk.world;
@@ -705,48 +822,7 @@ __global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
         Contact &out = P.candContacts[(size_t)w * P.candCapacity + wk.slot];
         const HullDev ha = O.hulls[wk.aObj];
 
-        if (job.kind == kJobPlane) {
-            // doSATPlane (:760-788) + createFacePlaneContact (:974-1017);
-            // hull a against the plane of body b
-            const HullXform xa = hullXform(P, w, P.body[wk.aArch], wk.a.row);
-            const BodyArch &BB = P.body[wk.bArch];
-            const Vector3 b_pos = bcol<Vector3>(BB, Cols::Position, w, wk.b.row);
-            const Quat b_rot = bcol<Quat>(BB, Cols::Rotation, w, wk.b.row);
-            const Vector3 pn = b_rot.rotateVec(Vector3 { 0, 0, 1 });
-            const geometry::Plane plane { pn, dot(pn, b_pos) };
-            float min_dot = FLT_MAX;
-            for (int32_t v = 0; v < ha.numVerts; v++) {
-                const float d = plane.normal.dot(worldVertex(O, ha, xa, v));
-                if (d < min_dot) min_dot = d;
-            }
-            if (min_dot - plane.d > 0.0f) continue;
-            float min_fd = FLT_MAX;
-            int32_t inc_face = -1;
-            for (int32_t f = 0; f < ha.numFaces; f++) {
-                const float d = dot(worldPlane(O, ha, xa, f).normal, plane.normal);
-                if (d < min_fd) { min_fd = d; inc_face = f; }
-            }
-            inc_face = guardIndex(inc_face, ha.numFaces, flags, kGuardPlaneFace);
-            const geometry::HalfEdge *hh = O.hedges + ha.hedgeOffset;
-            int32_t n = 0, steps = 0;
-            uint32_t hidx = O.polygons[ha.faceOffset + inc_face], start = hidx;
-            do {
-                hidx = guardIndex(hidx, ha.numHedges, flags, kGuardPlaneWalk);
-                const geometry::HalfEdge he = hh[hidx];
-                hidx = he.next;
-                const Vector3 v = worldVertex(O, ha, xa,
-                                              guardIndex(he.rootVertex, ha.numVerts, flags,
-                                                         kGuardVertex));
-                const float d = distFromPlane(plane, v);
-                if (d < 0.0f && n < cap) {
-                    clip0[n] = v - d * plane.normal;
-                    depths[n] = -d;
-                    n++;
-                }
-            } while (hidx != start && ++steps <= ha.numHedges);
-            storeFaceManifold(out, plane.normal, clip0, depths, n, wk.b, wk.a);
-            if (n > 0) recordManifold(P, w, wk.slot, slotOf(P, wk.bArch, wk.b), slotOf(P, wk.aArch, wk.a));
-        } else if (job.kind == kJobFace) {
+        if (job.kind == kJobFace) {
             const bool a_is_ref = job.refIsA != 0;
             const HullDev hb = O.hulls[wk.bObj];
             const HullDev ref = a_is_ref ? ha : hb;

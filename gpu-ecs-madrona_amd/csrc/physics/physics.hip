@@ -316,14 +316,9 @@ void PhysicsModule::upload(void *stream_ptr)
     P.bodyAABBs = devAlloc<AABB>((size_t)W * std::max(P.maxBodiesPerWorld, 1), stream);
     P.survInfo = devAlloc<uint32_t>((size_t)W * P.candCapacity, stream);
     P.survCount = devAlloc<int32_t>(W, stream);
-    P.satWork = devAlloc<SatWork>((size_t)W * P.candCapacity, stream);
-    P.satWorkCount = devAlloc<int32_t>(2, stream);
-    P.jobCount = P.satWorkCount + 1;
-    P.satStage = devAlloc<SatWork>((size_t)W * P.candCapacity, stream);
-    P.hhCount = devAlloc<int32_t>(W, stream);
-    P.planeCount = devAlloc<int32_t>(W, stream);
-    P.groupCounts = devAlloc<unsigned long long>((size_t)(W + 63) / 64, stream);
-    P.planeJobs = devAlloc<ContactJob>((size_t)W * P.candCapacity, stream);
+    P.binCap = (W + kNarrowBins - 1) / kNarrowBins * P.candCapacity;
+    P.satWork = devAlloc<SatWork>((size_t)kNarrowBins * P.binCap, stream);
+    P.satWorkCount = devAlloc<int32_t>(kNarrowBins * kBinStride, stream);
     P.hhJobs = devAlloc<ContactJob>((size_t)W * P.candCapacity, stream);
     P.candContacts = devAlloc<Contact>((size_t)W * P.candCapacity, stream);
     P.maxContacts = maxContacts;
@@ -367,6 +362,9 @@ void PhysicsModule::upload(void *stream_ptr)
     MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, narrowContactKernel, kContactBlock, contactSharedBytes(P)));
     P.contactGrid = std::max(1, cus * std::max(per_cu, 1));
+    MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, narrowPlaneKernel,
+                                                              kContactBlock, 0));
+    P.planeGrid = std::max(1, cus * std::max(per_cu, 1));
     uploaded = true;
 }
 
@@ -452,9 +450,10 @@ struct SubstepRigidBodiesNode : PhysNodeBase {
 // the per-survivor manifolds into the ordered contact list.
 MW_PHYS_NODE(NarrowphaseNode,
     hipLaunchKernelGGL(narrowFilterKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
-    hipLaunchKernelGGL(narrowCompactKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
     hipLaunchKernelGGL(narrowSATKernel, dim3(lc.persistentGrid(P.satGrid)), dim3(kNarrowBlock),
                        narrowphaseSharedBytes(P), stream, P);
+    hipLaunchKernelGGL(narrowPlaneKernel, dim3(lc.persistentGrid(P.planeGrid)),
+                       dim3(kContactBlock), 0, stream, P);
     hipLaunchKernelGGL(narrowContactKernel, dim3(lc.persistentGrid(P.contactGrid)),
                        dim3(kContactBlock), contactSharedBytes(P), stream, P);)
 

@@ -131,18 +131,19 @@ struct PhysArgs {
                                   // its manifold's ref | alt << 16, kNoManifold without one
                                   // (the solver reads this instead of the Contact records)
     int32_t *survCount;           // [W] survivors per world
-    struct SatWork *satWork;      // [W * candCapacity] SAT work list (one per survivor)
-    int32_t *satWorkCount;        // [1] entries in satWork this substep
-    SatWork *satStage;            // [W][candCapacity] survivors per world (filter output)
-    int32_t *hhCount, *planeCount;    // [W] hull-hull / hull-plane survivors
-    unsigned long long *groupCounts;  // [W/64] packed (hull-hull | hull-plane << 32)
-                                      // survivor sums per group of 64 worlds
-    ContactJob *planeJobs;        // [W * candCapacity] flat hull-plane contact jobs
+    struct SatWork *satWork;      // [kNarrowBins][binCap] SAT / plane work lists: bin
+                                  // w % kNarrowBins holds world w's hull-hull survivors
+                                  // from its front and hull-plane survivors from its back
+    int32_t *satWorkCount;        // [kNarrowBins][kBinStride] per-bin counters: [0] hull-hull,
+                                  // [kBinStride/2] hull-plane entries this substep; the
+                                  // filter appends, the integrate kernel / fused solver
+                                  // tail resets
+    int32_t binCap;               // entries per bin (worlds per bin x candCapacity)
     ContactJob *hhJobs;           // [W * candCapacity] SAT verdict per satWork entry
-    int32_t *jobCount;            // [1] hull-plane jobs this substep
     int32_t contactGrid;          // persistent contact-kernel grid (blocks)
     int32_t clipCap;              // clip polygon capacity (2 x largest face)
     int32_t satGrid;              // persistent SAT grid (blocks)
+    int32_t planeGrid;            // persistent plane-contact grid (blocks)
     Contact *candContacts;        // [W][candCapacity] manifold per survivor slot
     int32_t maxContacts;          // SolverData::maxContacts (reference assert)
     int32_t *contactOrder;        // [W][candCapacity] scratch: ordered contact list

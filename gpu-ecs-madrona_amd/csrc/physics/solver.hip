@@ -159,10 +159,12 @@ __device__ __forceinline__ bool boundedInput(const ContactIn &c)
     return ok;
 }
 
-__device__ int32_t solveContactPositions(const PhysArgs &P, int32_t w, SMut &b1, int32_t s1,
-                                         SMut &b2, int32_t s2, const ContactIn &c,
-                                         float *lambda_out, bool sk1, bool sk2)
+template <int ST>
+__device__ __forceinline__ int32_t solveContactPositionsT(const PhysArgs &P, int32_t w, SMut &b1,
+                                                          int32_t s1, SMut &b2, int32_t s2,
+                                                          const ContactIn &c, float *lambda_out)
 {                                                          // physics.cpp:281-476
+    constexpr bool sk1 = ST == 1, sk2 = ST == 2;
     const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
     const auto ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
     const auto ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
@@ -383,10 +385,13 @@ __device__ __forceinline__ void applyVelocityUpdate(Vector3 &v1, Vector3 &v2, Ve
     o2 -= q2.rotateVec(o2u);
 }
 
-__device__ int32_t solveContactVelocities(const PhysArgs &P, int32_t w, SMut &b1, int32_t s1,
-                                          SMut &b2, int32_t s2, const ContactIn &c, float h,
-                                          float rest_thresh, bool sk1, bool sk2)
+template <int ST>
+__device__ __forceinline__ int32_t solveContactVelocitiesT(const PhysArgs &P, int32_t w, SMut &b1,
+                                                           int32_t s1, SMut &b2, int32_t s2,
+                                                           const ContactIn &c, float h,
+                                                           float rest_thresh)
 {                                                          // physics.cpp:865-993
+    constexpr bool sk1 = ST == 1, sk2 = ST == 2;
     const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
     solver::PreSolvePositional ps1 {}, ps2 {};
     solver::PreSolveVelocity pv1 {}, pv2 {};
@@ -572,7 +577,10 @@ __host__ __device__ inline size_t solverWorldLDSBytes(int32_t nb)
 // kind), so one pass over a level keeps all of the block's lanes on that
 // level's items from all of its worlds.
 constexpr int32_t kSolverItems = kSolverWorlds * kSolverLDSContacts;
-constexpr int32_t kSolverBuckets = kNumKinds * (kSolverLDSContacts + 2);
+#ifndef MW_SOLVER_MAX_LEVELS
+#define MW_SOLVER_MAX_LEVELS kSolverLDSContacts
+#endif
+constexpr int32_t kSolverBuckets = kNumKinds * (MW_SOLVER_MAX_LEVELS + 2);
 
 __host__ __device__ inline size_t solverBlockLDSBytes(int32_t nb)
 {
@@ -933,11 +941,40 @@ static __device__ unsigned long long g_solverBlockT[2 * 16384];   // start, end 
 // skipping solve meets a non-finite lambda it is redone in full, which
 // writes the static body the level schedule treated as untouched: the world
 // is flagged.
-__device__ __forceinline__ void skipSides(int32_t kind, const ContactIn &c, bool &sk1, bool &sk2)
+// The solves by static side (ST: 0 = both bodies, 1 = skip the ref body --
+// the ground plane of a hull-plane manifold, nearly every contact --,
+// 2 = skip the alt body).
+__device__ __forceinline__ int32_t solvePositionsGeneral(const PhysArgs &P, int32_t w, SMut &b1,
+                                                      int32_t s1, SMut &b2, int32_t s2,
+                                                      const ContactIn &c, float *lambda_out)
 {
-    sk1 = kind == kKindStaticRef;
-    sk2 = kind == kKindStaticAlt;
-    if ((sk1 || sk2) && !boundedInput(c)) sk1 = sk2 = false;
+    return solveContactPositionsT<0>(P, w, b1, s1, b2, s2, c, lambda_out);
+}
+__device__ __forceinline__ int32_t solvePositionsStaticAlt(const PhysArgs &P, int32_t w, SMut &b1,
+                                                        int32_t s1, SMut &b2, int32_t s2,
+                                                        const ContactIn &c, float *lambda_out)
+{
+    return solveContactPositionsT<2>(P, w, b1, s1, b2, s2, c, lambda_out);
+}
+__device__ __forceinline__ int32_t solveVelocitiesGeneral(const PhysArgs &P, int32_t w, SMut &b1,
+                                                       int32_t s1, SMut &b2, int32_t s2,
+                                                       const ContactIn &c, float h, float rt)
+{
+    return solveContactVelocitiesT<0>(P, w, b1, s1, b2, s2, c, h, rt);
+}
+__device__ __forceinline__ int32_t solveVelocitiesStaticAlt(const PhysArgs &P, int32_t w, SMut &b1,
+                                                         int32_t s1, SMut &b2, int32_t s2,
+                                                         const ContactIn &c, float h, float rt)
+{
+    return solveContactVelocitiesT<2>(P, w, b1, s1, b2, s2, c, h, rt);
+}
+
+// Which solve an item takes: its kind, unless a contact's inputs are out of
+// the bound the skipping solves rely on.
+__device__ __forceinline__ int32_t solveKind(int32_t kind, const ContactIn &c)
+{
+    if (kind != kKindGeneral && !boundedInput(c)) return kKindGeneral;
+    return kind;
 }
 
 __device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w, SolverLDS &L,
@@ -947,11 +984,16 @@ __device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w,
         Contact &cr = P.candContacts[(size_t)w * P.candCapacity + r.slot];
         const ContactIn c = loadContact(cr);
         SMut &b1 = L.bodies[r.s1], &b2 = L.bodies[r.s2];
-        bool sk1, sk2;
-        skipSides(kind, c, sk1, sk2);
-        while (solveContactPositions(P, w, b1, r.s1, b2, r.s2, c, cr.lambdaN, sk1, sk2) != kSolveDone) {
-            atomicOr(P.errorFlags + w, kErrStaticSchedule);
-            sk1 = sk2 = false;
+        const int32_t k = solveKind(kind, c);
+        int32_t res = kSolveNonFinite;
+        if (k == kKindStaticRef) {
+            res = solveContactPositionsT<1>(P, w, b1, r.s1, b2, r.s2, c, cr.lambdaN);
+        } else if (k == kKindStaticAlt) {
+            res = solvePositionsStaticAlt(P, w, b1, r.s1, b2, r.s2, c, cr.lambdaN);
+        }
+        if (res != kSolveDone) {
+            if (k != kKindGeneral) atomicOr(P.errorFlags + w, kErrStaticSchedule);
+            solvePositionsGeneral(P, w, b1, r.s1, b2, r.s2, c, cr.lambdaN);
         }
     } else {
         const JointConstraint &j = P.joints[(size_t)w * P.jointCapacity + (-1 - r.slot)];
@@ -966,12 +1008,16 @@ __device__ __forceinline__ void solveItemVelocities(const PhysArgs &P, int32_t w
     const ContactIn c = loadContact(P.candContacts[(size_t)w * P.candCapacity + r.slot]);
     const SolverData &sd = P.solver[w];
     SMut &b1 = L.bodies[r.s1], &b2 = L.bodies[r.s2];
-    bool sk1, sk2;
-    skipSides(kind, c, sk1, sk2);
-    while (solveContactVelocities(P, w, b1, r.s1, b2, r.s2, c, sd.h, sd.restitutionThreshold,
-                                  sk1, sk2) != kSolveDone) {
-        atomicOr(P.errorFlags + w, kErrStaticSchedule);
-        sk1 = sk2 = false;
+    const int32_t k = solveKind(kind, c);
+    int32_t res = kSolveNonFinite;
+    if (k == kKindStaticRef) {
+        res = solveContactVelocitiesT<1>(P, w, b1, r.s1, b2, r.s2, c, sd.h, sd.restitutionThreshold);
+    } else if (k == kKindStaticAlt) {
+        res = solveVelocitiesStaticAlt(P, w, b1, r.s1, b2, r.s2, c, sd.h, sd.restitutionThreshold);
+    }
+    if (res != kSolveDone) {
+        if (k != kKindGeneral) atomicOr(P.errorFlags + w, kErrStaticSchedule);
+        solveVelocitiesGeneral(P, w, b1, r.s1, b2, r.s2, c, sd.h, sd.restitutionThreshold);
     }
 }
 
@@ -1069,7 +1115,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     if (!fits) {
         // some world of the block overflows the LDS records: every world
         // of the block solves on its own wave with global records
-        if (integrate_next && blockIdx.x == 0) zeroGroupCounts(P, threadIdx.x, kSolverThreads);
+        if (integrate_next && blockIdx.x == 0) resetNarrowLists(P, threadIdx.x, kSolverThreads);
         if (live) {
             solveWorldGlobal(P, w, L, J, lane);
             writeWorldBodies(P, w, L, lane, integrate_next != 0);
@@ -1156,7 +1202,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     }
 
     MW_SOLVER_MARK(5);
-    if (integrate_next && blockIdx.x == 0) zeroGroupCounts(P, threadIdx.x, kSolverThreads);
+    if (integrate_next && blockIdx.x == 0) resetNarrowLists(P, threadIdx.x, kSolverThreads);
     if (live) writeWorldBodies(P, w, L, lane, integrate_next != 0);
     __syncthreads();
     MW_SOLVER_MARK(6);
