@@ -190,6 +190,315 @@ __global__ void __launch_bounds__(64) bvhRebuildKernel(PhysArgs P)
     }
 }
 
+// ---------------------------------------------------------------------------
+// BVH::rebuild (broadphase.cpp:42-280) with one wave per world.  The serial
+// kernel above walks the explicit stack on one lane; here the same stack walk
+// runs wave-uniformly (entries in LDS, fields read through readfirstlane, so
+// the control flow is scalar) and every midpoint split runs across the wave:
+//  * centroid bounds: lane-strided fminRef / fmaxRef, then a shuffle
+//    reduction.  fminRef ignores NaN on either side, so the result is the
+//    serial scan's up to the sign of a zero, which neither the axis choice
+//    (strict >) nor `c < split_val` can observe;
+//  * the in-place two-pointer partition: it swaps the i-th element >= split
+//    left of k (= #elements < split) with the i-th element < split right of
+//    k counted from the end, so the misplaced positions are ranked by
+//    ballots and swapped pairwise -- the serial loop's exact permutation.
+// Node ids are handed out in the stack walk's order, so nodes, slots and
+// parents are byte-identical.  No node is read back: a node's combined
+// bounds are the in-order merge of its slots, accumulated in its stack entry
+// as its children complete (every child of an inner node is a node, even an
+// empty one, so slot c is always the c-th child to complete).  The leaf
+// emission order of findOverlaps (inner children pushed in slot order, leaf
+// children emitted in slot order) lists the leaf nodes' sorted segments in
+// reverse, each segment forwards: a leaf node over [off, off + n) emits at
+// numLeaves - off - n.
+// ---------------------------------------------------------------------------
+struct RebuildEntry {
+    int32_t nodeID, parentID, offset, numObjs;
+    int32_t parentIdx;          // stack index of the parent's entry
+    int32_t nextSlot;           // inner node: children completed so far
+    AABB acc;                   // inner node: merge of its completed slots
+};
+
+__device__ __forceinline__ void rebuildWaveSync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float uniformF(float v)
+{
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+__device__ __forceinline__ int32_t uniformI(int32_t v)
+{
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// Wave-wide fminRef / fmaxRef: DPP within each row of 16 (swap pairs, swap
+// pairs of pairs, half-row mirror, row mirror), then the four row results
+// combined in row order from readlanes, so every lane ends with one value.
+template <int Ctrl>
+__device__ __forceinline__ float dppF(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), Ctrl, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ float readlaneF(float v, int lane)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+__device__ __forceinline__ float waveMinRef(float v)
+{
+    v = fminRef(v, dppF<0xB1>(v));      // quad_perm [1,0,3,2]
+    v = fminRef(v, dppF<0x4E>(v));      // quad_perm [2,3,0,1]
+    v = fminRef(v, dppF<0x141>(v));     // row_half_mirror
+    v = fminRef(v, dppF<0x140>(v));     // row_mirror
+    return fminRef(fminRef(fminRef(readlaneF(v, 0), readlaneF(v, 16)), readlaneF(v, 32)),
+                   readlaneF(v, 48));
+}
+
+__device__ __forceinline__ float waveMaxRef(float v)
+{
+    v = fmaxRef(v, dppF<0xB1>(v));
+    v = fmaxRef(v, dppF<0x4E>(v));
+    v = fmaxRef(v, dppF<0x141>(v));
+    v = fmaxRef(v, dppF<0x140>(v));
+    return fmaxRef(fmaxRef(fmaxRef(readlaneF(v, 0), readlaneF(v, 16)), readlaneF(v, 32)),
+                   readlaneF(v, 48));
+}
+
+size_t rebuildSharedBytes(const PhysArgs &P)
+{
+    const size_t L = (size_t)P.maxLeaves;
+    return L * (3 * sizeof(float) + sizeof(AABB) + 2 * sizeof(int32_t)) +
+           kRebuildStack * sizeof(RebuildEntry) + 16;
+}
+
+// Up to kSplitRegChunks x 64 elements the segment's leaf ids and centroids
+// stay in registers across the bounds / count / rank passes; longer segments
+// (worlds over 192 leaves) re-read them from LDS per pass.
+constexpr int32_t kSplitRegChunks = 3;
+
+__device__ __forceinline__ int32_t pickAxis(Vector3 d)
+{
+    if (d.x > d.y && d.x > d.z) return 0;
+    if (d.y > d.x && d.y > d.z) return 1;
+    return 2;
+}
+
+__device__ __forceinline__ float comp(Vector3 v, int32_t axis)
+{
+    return axis == 0 ? v.x : (axis == 1 ? v.y : v.z);
+}
+
+__device__ __forceinline__ int32_t waveMidpointSplit(const float *cx, const float *cy, const float *cz,
+                                     int32_t *sorted, int32_t *misL, int32_t *misR,
+                                     int32_t base, int32_t n, int32_t lane)
+{
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    Vector3 cmin { FLT_MAX, FLT_MAX, FLT_MAX };
+    Vector3 cmax { -FLT_MAX, -FLT_MAX, -FLT_MAX };
+    int32_t k = 0, nl = 0, nr = 0;
+    if (n <= 64 * kSplitRegChunks) {
+        Vector3 c[kSplitRegChunks];
+#pragma unroll
+        for (int32_t j = 0; j < kSplitRegChunks; j++) {
+            const int32_t i = j * 64 + lane;
+            c[j] = Vector3 { FLT_MAX, FLT_MAX, FLT_MAX };
+            if (i < n) {
+                const int32_t l = sorted[base + i];
+                c[j] = Vector3 { cx[l], cy[l], cz[l] };
+                cmin = Vector3::min(cmin, c[j]);
+                cmax = Vector3::max(cmax, c[j]);
+            }
+        }
+        cmin = Vector3 { waveMinRef(cmin.x), waveMinRef(cmin.y), waveMinRef(cmin.z) };
+        cmax = Vector3 { waveMaxRef(cmax.x), waveMaxRef(cmax.y), waveMaxRef(cmax.z) };
+        const int32_t axis = pickAxis(cmax - cmin);
+        const float split_val = 0.5f * (comp(cmin, axis) + comp(cmax, axis));
+        bool lt[kSplitRegChunks];
+#pragma unroll
+        for (int32_t j = 0; j < kSplitRegChunks; j++) {
+            lt[j] = j * 64 + lane < n && comp(c[j], axis) < split_val;
+            k += __popcll(__ballot(lt[j]));
+        }
+#pragma unroll
+        for (int32_t j = 0; j < kSplitRegChunks; j++) {
+            const int32_t i = j * 64 + lane;
+            const bool valid = i < n;
+            const bool ml = valid && i < k && !lt[j];
+            const bool mr = valid && i >= k && lt[j];
+            const uint64_t bl = __ballot(ml), br = __ballot(mr);
+            if (ml) misL[nl + __popcll(bl & lt_mask)] = i;
+            if (mr) misR[nr + __popcll(br & lt_mask)] = i;
+            nl += __popcll(bl);
+            nr += __popcll(br);
+        }
+    } else {
+        for (int32_t i = lane; i < n; i += 64) {
+            const int32_t l = sorted[base + i];
+            const Vector3 c { cx[l], cy[l], cz[l] };
+            cmin = Vector3::min(cmin, c);
+            cmax = Vector3::max(cmax, c);
+        }
+        cmin = Vector3 { waveMinRef(cmin.x), waveMinRef(cmin.y), waveMinRef(cmin.z) };
+        cmax = Vector3 { waveMaxRef(cmax.x), waveMaxRef(cmax.y), waveMaxRef(cmax.z) };
+        const int32_t axis = pickAxis(cmax - cmin);
+        const float split_val = 0.5f * (comp(cmin, axis) + comp(cmax, axis));
+        const float *ca = axis == 0 ? cx : (axis == 1 ? cy : cz);
+        for (int32_t j = 0; j < n; j += 64) {
+            const int32_t i = j + lane;
+            const bool lt = i < n && ca[sorted[base + i]] < split_val;
+            k += __popcll(__ballot(lt));
+        }
+        for (int32_t j = 0; j < n; j += 64) {
+            const int32_t i = j + lane;
+            const bool valid = i < n;
+            const bool lt = valid && ca[sorted[base + i]] < split_val;
+            const bool ml = valid && i < k && !lt;
+            const bool mr = valid && i >= k && lt;
+            const uint64_t bl = __ballot(ml), br = __ballot(mr);
+            if (ml) misL[nl + __popcll(bl & lt_mask)] = i;
+            if (mr) misR[nr + __popcll(br & lt_mask)] = i;
+            nl += __popcll(bl);
+            nr += __popcll(br);
+        }
+    }
+    if (nl == 0) return (k > 0 && k < n) ? k : n / 2;      // already partitioned
+    rebuildWaveSync();
+    for (int32_t t = lane; t < nl; t += 64) {     // nl == nr
+        const int32_t p = base + misL[t], q = base + misR[nl - 1 - t];
+        const int32_t a = sorted[p], b = sorted[q];
+        sorted[p] = b;
+        sorted[q] = a;
+    }
+    rebuildWaveSync();
+    return (k > 0 && k < n) ? k : n / 2;
+}
+
+__global__ void __launch_bounds__(64) bvhRebuildWaveKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    const int32_t w = blockIdx.x;
+    const int32_t lane = threadIdx.x;
+    broadphase::BVH &bvh = P.bvh[w];
+    if (!uniformI(bvh.forceRebuild)) return;              // BVH::updateTree
+    const int32_t L = uniformI(bvh.numLeaves);
+    if (lane == 0) {
+        bvh.forceRebuild = 0;
+        bvh.numNodes = numInternalNodes(L);
+    }
+
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int32_t ML = P.maxLeaves;
+    AABB *s_aabb = (AABB *)smem;
+    RebuildEntry *stack = (RebuildEntry *)(s_aabb + ML);
+    float *cx = (float *)(stack + kRebuildStack);
+    float *cy = cx + ML, *cz = cy + ML;
+    int32_t *sorted = (int32_t *)(cz + ML);
+    int32_t *scratch = sorted + ML;              // misplaced positions, ML/2 + 1 each side
+    int32_t *misL = scratch, *misR = scratch + ML / 2 + 1;
+
+    BVHNode *nodes = P.nodes + (size_t)w * P.maxNodes;
+    const AABB *aabbs = P.leafAABBs + (size_t)w * ML;
+    const int32_t *g_sorted = P.sortedLeaves + (size_t)w * ML;
+    uint32_t *parents = P.leafParents + (size_t)w * ML;
+    int32_t *order = P.leafOrder + (size_t)w * ML;
+
+    for (int32_t i = lane; i < L; i += 64) {
+        const AABB a = aabbs[i];
+        s_aabb[i] = a;
+        const Vector3 c = (a.pMin + a.pMax) / 2.f;
+        cx[i] = c.x; cy[i] = c.y; cz[i] = c.z;
+        sorted[i] = g_sorted[i];
+    }
+    if (lane == 0) stack[0] = { -1, -1, 0, L, -1, 0, AABB::invalid() };
+    rebuildWaveSync();
+
+    int32_t sp = 1, cur = 0;
+    while (sp > 0) {
+        const int32_t top = sp - 1;
+        const int32_t e_node = uniformI(stack[top].nodeID);
+        const int32_t e_parent = uniformI(stack[top].parentID);
+        const int32_t e_off = uniformI(stack[top].offset);
+        const int32_t e_n = uniformI(stack[top].numObjs);
+        const int32_t e_pidx = uniformI(stack[top].parentIdx);
+        int32_t node_id;
+        AABB combined = AABB::invalid();
+        if (e_n <= 4) {
+            node_id = cur++;
+            BVHNode &node = nodes[node_id];
+            if (lane == 0) node.parentID = e_parent;
+            if (lane < 4) {
+                if (lane < e_n) {
+                    const int32_t leaf_id = sorted[e_off + lane];
+                    const AABB a = s_aabb[leaf_id];
+                    parents[leaf_id] = ((uint32_t)node_id << 2) | (uint32_t)lane;
+                    node.children[lane] = (int32_t)(0x80000000u | (uint32_t)leaf_id);
+                    node.minX[lane] = a.pMin.x; node.minY[lane] = a.pMin.y; node.minZ[lane] = a.pMin.z;
+                    node.maxX[lane] = a.pMax.x; node.maxY[lane] = a.pMax.y; node.maxZ[lane] = a.pMax.z;
+                    order[L - e_off - e_n + lane] = leaf_id;
+                } else {
+                    node.children[lane] = -1;
+                    node.minX[lane] = FLT_MAX; node.minY[lane] = FLT_MAX; node.minZ[lane] = FLT_MAX;
+                    node.maxX[lane] = -FLT_MAX; node.maxY[lane] = -FLT_MAX; node.maxZ[lane] = -FLT_MAX;
+                }
+            }
+            for (int32_t i = 0; i < e_n; i++) combined = AABB::merge(combined, s_aabb[sorted[e_off + i]]);
+        } else if (e_node == -1) {
+            node_id = cur++;
+            if (lane == 0) nodes[node_id].parentID = e_parent;
+            // second = split(all), first = split(lower half), third =
+            // split(upper half): one inlined split body run three times
+            int32_t split[3];
+#pragma unroll 1
+            for (int32_t q = 0; q < 3; q++) {
+                const int32_t sb = q == 2 ? e_off + split[0] : e_off;
+                const int32_t sn = q == 0 ? e_n : (q == 1 ? split[0] : e_n - split[0]);
+                split[q] = waveMidpointSplit(cx, cy, cz, sorted, misL, misR, sb, sn, lane);
+            }
+            const int32_t second = split[0], first = split[1], third = split[2];
+            const int32_t nh1 = second;
+            const int32_t nh2 = e_n - second;
+            if (sp + 4 > kRebuildStack) {
+                if (lane == 0) atomicOr(P.errorFlags + w, kErrBVHStack);
+                return;
+            }
+            if (lane == 0) {
+                stack[top].nodeID = node_id;
+                stack[sp + 0] = { -1, node_id, e_off + nh1 + third, nh2 - third, top, 0, AABB::invalid() };
+                stack[sp + 1] = { -1, node_id, e_off + nh1, third, top, 0, AABB::invalid() };
+                stack[sp + 2] = { -1, node_id, e_off + first, nh1 - first, top, 0, AABB::invalid() };
+                stack[sp + 3] = { -1, node_id, e_off, first, top, 0, AABB::invalid() };
+            }
+            sp += 4;
+            rebuildWaveSync();
+            continue;
+        } else {
+            node_id = e_node;
+            combined = stack[top].acc;
+        }
+        sp -= 1;
+        if (e_parent == -1) continue;
+        const int32_t c = uniformI(stack[e_pidx].nextSlot);
+        BVHNode &parent = nodes[e_parent];
+        if (lane == 0) {
+            parent.children[c] = node_id;
+            parent.minX[c] = combined.pMin.x; parent.minY[c] = combined.pMin.y;
+            parent.minZ[c] = combined.pMin.z; parent.maxX[c] = combined.pMax.x;
+            parent.maxY[c] = combined.pMax.y; parent.maxZ[c] = combined.pMax.z;
+            stack[e_pidx].acc = AABB::merge(stack[e_pidx].acc, combined);
+            stack[e_pidx].nextSlot = c + 1;
+        }
+        rebuildWaveSync();
+    }
+    if (lane == 0) bvh.usedNodes = cur;
+}
+
 // refitEntry -> BVH::refitLeaf (broadphase.cpp:545-642, 891-895), one block
 // per world with the world's used BVH nodes staged in LDS: every leaf's slot
 // read-modify-write and its expansion walk to the root run on LDS (atomic

@@ -407,8 +407,14 @@ MW_PHYS_NODE(UpdateLeafPositionsNode,
     if (P.numBodyArchs > 0)
         hipLaunchKernelGGL(leafUpdateKernel, rowGrid(P), dim3(256), 0, stream, P);)
 
+// One wave per world while the world's leaves fit the LDS image (129 leaves:
+// ≈11 KB); the lane-per-world kernel otherwise.
 MW_PHYS_NODE(UpdateBVHNode,
-    hipLaunchKernelGGL(bvhRebuildKernel, dim3((P.numWorlds + 63) / 64), dim3(64), 0, stream, P);)
+    if (rebuildSharedBytes(P) <= 64 * 1024)
+        hipLaunchKernelGGL(bvhRebuildWaveKernel, dim3(P.numWorlds), dim3(64),
+                           rebuildSharedBytes(P), stream, P);
+    else
+        hipLaunchKernelGGL(bvhRebuildKernel, dim3((P.numWorlds + 63) / 64), dim3(64), 0, stream, P);)
 
 MW_PHYS_NODE(RefitNode,
     if (P.numBodyArchs > 0)

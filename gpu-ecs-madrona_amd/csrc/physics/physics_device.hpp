@@ -138,6 +138,9 @@ __device__ __forceinline__ Vector3 multDiag(Vector3 d, Vector3 v)
 // Kernel entry points (one launch processes every world).
 __global__ void leafUpdateKernel(PhysArgs P);
 __global__ void bvhRebuildKernel(PhysArgs P);
+__global__ void bvhRebuildWaveKernel(PhysArgs P);
+constexpr int32_t kRebuildStack = 128;            // broadphase.cpp:58 stack[128]
+size_t rebuildSharedBytes(const PhysArgs &P);
 __global__ void refitKernel(PhysArgs P);
 __global__ void findOverlapsKernel(PhysArgs P);
 __global__ void integrateKernel(PhysArgs P);
