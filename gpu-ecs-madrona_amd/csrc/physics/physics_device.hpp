@@ -15,11 +15,6 @@ namespace madrona::phys {
 using namespace math;
 using namespace base;
 
-__host__ __device__ inline int32_t numInternalNodes(int32_t num_leaves)   // broadphase.cpp:33-40
-{
-    int32_t a = (num_leaves - 1 + 2) / 3;
-    return (a > 1 ? a : 1) + num_leaves;
-}
 
 template <typename T>
 __device__ __forceinline__ T &bcol(const BodyArch &B, int col, int32_t w, int32_t r)
@@ -221,8 +216,7 @@ __device__ __forceinline__ void integrateBody(const PhysArgs &P, const BodyArch 
 // bin w % kNarrowBins), each with its own counters on their own cache lines:
 // a device-wide list with one counter serialised every filter block's
 // reservation at that address (measured 86 -> 480 us per filter launch).
-constexpr int32_t kNarrowBins = 64;
-constexpr int32_t kBinStride = 32;        // ints per bin: hull-hull at 0, hull-plane at 16
+// kNarrowBins / kBinStride: physics_impl.hpp
 
 __device__ __forceinline__ int32_t *binCounter(const PhysArgs &P, int32_t bin, int32_t which)
 {

@@ -167,6 +167,16 @@ struct PhysArgs {
 
 inline constexpr uint32_t kNoManifold = 0xFFFF'FFFFu;
 
+MW_INLINE int32_t numInternalNodes(int32_t num_leaves)   // broadphase.cpp:33-40
+{
+    int32_t a = (num_leaves - 1 + 2) / 3;
+    return (a > 1 ? a : 1) + num_leaves;
+}
+
+// Narrowphase work-list bins (narrowphase.hip; world w in bin w % kNarrowBins).
+constexpr int32_t kNarrowBins = 64;
+constexpr int32_t kBinStride = 32;        // ints per bin: hull-hull at 0, hull-plane at 16
+
 // Error flag bits (StateView::errorFlags)
 inline constexpr int32_t kErrIDStoreFull = 1;
 inline constexpr int32_t kErrTableFull = 2;

@@ -1,4 +1,7 @@
-// C ABI (include/madrona_mw.h) over the MI355X executor.
+// C ABI (include/madrona_mw.h) over the MI355X executor.  The same source
+// builds the CPU back end's ABI (libmadrona_cpu.so, MW_CPU_BACKEND): the
+// arena is host memory there, and the RCCL / stream entry points report
+// that they are gfx950 features.
 #include "../../../include/madrona_mw.h"
 
 #include "env_registry.hpp"
@@ -8,8 +11,10 @@
 #include <madrona/launch_config.hpp>
 #include <madrona/physics_assets.hpp>
 
+#if !defined(MW_CPU_BACKEND)
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#endif
 
 #include <dlfcn.h>
 
@@ -20,6 +25,7 @@
 #include <string>
 #include <vector>
 
+#if !defined(MW_CPU_BACKEND)
 // RCCL is resolved at first use (dlopen of librccl.so.1) rather than linked:
 // a process that already holds an RCCL (PyTorch's bundled one) shares it and
 // its HIP runtime instead of mapping a second copy next to it.
@@ -52,6 +58,8 @@ static const RcclApi &rccl()
     }();
     return api;
 }
+
+#endif
 
 namespace madrona {
 namespace phys { PhysArgs *physicsArgs(StateManager &mgr); }
@@ -88,8 +96,10 @@ using namespace madrona;
 
 struct mw_exec {
     Executor *exec;
+#if !defined(MW_CPU_BACKEND)
     ncclComm_t comm = nullptr;    // RCCL communicator for the world-shard hand-off
     hipEvent_t stepDone = nullptr; // mw_stream_wait: recorded behind the enqueued steps
+#endif
 };
 
 static thread_local std::string g_last_error;
@@ -107,11 +117,27 @@ static void setError(const char *what) { g_last_error = what ? what : "unknown e
         return fail;                                       \
     }
 
+#if !defined(MW_CPU_BACKEND)
 #define MW_HIP_OK(expr)                                                  \
     do {                                                                 \
         hipError_t e__ = (expr);                                         \
         if (e__ != hipSuccess) throw std::runtime_error(hipGetErrorString(e__)); \
     } while (0)
+
+// Arena (device) -> caller (host) read-back.
+static void copyOut(void *dst, const void *src, size_t bytes)
+{
+    copyOut(dst, src, bytes);
+}
+#else
+static void copyOut(void *dst, const void *src, size_t bytes) { memcpy(dst, src, bytes); }
+
+[[noreturn]] static void gfx950Only(const char *what)
+{
+    throw std::runtime_error(std::string(what) + " is a gfx950 feature (libmadrona_mw.so); "
+                             "the CPU back end steps synchronously in host memory");
+}
+#endif
 
 extern "C" {
 
@@ -123,11 +149,14 @@ mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
         EnvFactory f = findEnv(env);
         if (!f) throw std::runtime_error(std::string("mw_create: unknown environment '") + env + "'");
         if (cfg->num_worlds <= 0) throw std::runtime_error("mw_create: num_worlds must be > 0");
+#if !defined(MW_CPU_BACKEND)
         int ndev = 0;
         MW_HIP_OK(hipGetDeviceCount(&ndev));
         if (cfg->gpu_id < 0 || cfg->gpu_id >= ndev) {
             throw std::runtime_error("mw_create: no HIP device " + std::to_string(cfg->gpu_id));
         }
+#endif
+        if (cfg->num_workers < 0) throw std::runtime_error("mw_create: num_workers must be >= 0");
         ExecConfig ec;
         ec.numWorlds = cfg->num_worlds;
         ec.gpuID = cfg->gpu_id;
@@ -136,6 +165,7 @@ mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
         ec.useGraph = cfg->use_graph;
         ec.tmpAllocBytesPerWorld = cfg->tmp_alloc_bytes;
         ec.maxDeferredPerWorld = cfg->max_deferred_destroys;
+        ec.numWorkers = cfg->num_workers;
         if (cfg->tmp_alloc_bytes < -1 || cfg->max_deferred_destroys < 0 ||
             cfg->max_deferred_destroys > 65536) {
             throw std::runtime_error("mw_create: tmp_alloc_bytes >= -1 and 0 <= max_deferred_destroys <= 65536");
@@ -221,11 +251,15 @@ void *mw_stream(mw_exec *exec) { return exec ? exec->exec->stream() : nullptr; }
 int mw_stream_wait(mw_exec *exec, void *stream)
 {
     MW_TRY({
+#if defined(MW_CPU_BACKEND)
+        (void)exec; (void)stream;          // steps complete before mw_step returns
+#else
         if (!exec->stepDone) {
             MW_HIP_OK(hipEventCreateWithFlags(&exec->stepDone, hipEventDisableTiming));
         }
         MW_HIP_OK(hipEventRecord(exec->stepDone, (hipStream_t)exec->exec->stream()));
         MW_HIP_OK(hipStreamWaitEvent((hipStream_t)stream, exec->stepDone, 0));
+#endif
         return 0;
     }, -1)
 }
@@ -234,8 +268,10 @@ int mw_destroy(mw_exec *exec)
 {
     MW_TRY({
         if (exec) {
+#if !defined(MW_CPU_BACKEND)
             if (exec->comm) (void)rccl().commDestroy(exec->comm);
             if (exec->stepDone) (void)hipEventDestroy(exec->stepDone);
+#endif
             delete exec->exec;
             delete exec;
         }
@@ -275,6 +311,7 @@ int mw_load_hull(const char *obj_path, int32_t *counts_out, float *aabb_out, flo
 // Training hand-off across world shards: RCCL over xGMI, issued on the
 // executor's stream right behind the step that produced the export.
 // ---------------------------------------------------------------------------
+#if !defined(MW_CPU_BACKEND)
 #define MW_NCCL_OK(expr)                                                     \
     do {                                                                     \
         ncclResult_t r__ = (expr);                                           \
@@ -340,6 +377,40 @@ int mw_device_free(mw_exec *exec, void *ptr)
     }, -1)
 }
 
+#else
+int mw_rccl_get_unique_id(void *)
+{
+    MW_TRY({ gfx950Only("mw_rccl_get_unique_id"); }, -1)
+}
+
+int mw_rccl_init(mw_exec *, const void *, int32_t, int32_t)
+{
+    MW_TRY({ gfx950Only("mw_rccl_init"); }, -1)
+}
+
+int mw_allgather_exported(mw_exec *, int32_t, void *, int64_t)
+{
+    MW_TRY({ gfx950Only("mw_allgather_exported"); }, -1)
+}
+
+// "Device" memory of the CPU back end is host memory.
+void *mw_device_alloc(mw_exec *, int64_t bytes)
+{
+    MW_TRY({
+        void *p = calloc(1, (size_t)std::max<int64_t>(bytes, 256));
+        if (!p) throw std::runtime_error("mw_device_alloc: out of memory");
+        return p;
+    }, nullptr)
+}
+
+int mw_device_free(mw_exec *, void *ptr)
+{
+    free(ptr);
+    return 0;
+}
+
+#endif
+
 int32_t mw_num_worlds(mw_exec *exec) { return exec->exec->numWorlds(); }
 
 int32_t mw_export_row_bytes(mw_exec *exec, int32_t slot)
@@ -396,8 +467,7 @@ int32_t mw_read_column(mw_exec *exec, int32_t archetype, int32_t column, int32_t
         int32_t n = exec->exec->numRows(archetype, world);
         int32_t copy = n < max_rows ? n : max_rows;
         if (copy > 0) {
-            MW_HIP_OK(hipMemcpy(out, base + (size_t)world * cap * bytes, (size_t)copy * bytes,
-                                hipMemcpyDeviceToHost));
+            copyOut(out, base + (size_t)world * cap * bytes, (size_t)copy * bytes);
         }
         return n;
     }, -1)
@@ -410,11 +480,11 @@ int32_t mw_phys_read_candidates(mw_exec *exec, int32_t world, void *out, int32_t
         phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
         if (!P) return -1;
         int32_t n = 0;
-        MW_HIP_OK(hipMemcpy(&n, P->lastNumCands + world, 4, hipMemcpyDeviceToHost));
+        copyOut(&n, P->lastNumCands + world, 4);
         int32_t copy = n < cap ? n : cap;
         if (copy > 0) {
-            MW_HIP_OK(hipMemcpy(out, P->cands + (size_t)world * P->candCapacity,
-                                sizeof(phys::CandidateCollision) * copy, hipMemcpyDeviceToHost));
+            copyOut(out, P->cands + (size_t)world * P->candCapacity,
+                                sizeof(phys::CandidateCollision) * copy);
         }
         return n;
     }, -1)
@@ -427,15 +497,15 @@ int32_t mw_phys_read_contacts(mw_exec *exec, int32_t world, void *out, int32_t c
         phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
         if (!P) return -1;
         int32_t n = 0;
-        MW_HIP_OK(hipMemcpy(&n, P->lastNumContacts + world, 4, hipMemcpyDeviceToHost));
+        copyOut(&n, P->lastNumContacts + world, 4);
         std::vector<int32_t> order(n);
         if (n > 0) {
-            MW_HIP_OK(hipMemcpy(order.data(), P->contactOrder + (size_t)world * P->candCapacity,
-                                4 * n, hipMemcpyDeviceToHost));
+            copyOut(order.data(), P->contactOrder + (size_t)world * P->candCapacity,
+                                4 * n);
         }
         std::vector<phys::Contact> slots(P->candCapacity);
-        MW_HIP_OK(hipMemcpy(slots.data(), P->candContacts + (size_t)world * P->candCapacity,
-                            sizeof(phys::Contact) * P->candCapacity, hipMemcpyDeviceToHost));
+        copyOut(slots.data(), P->candContacts + (size_t)world * P->candCapacity,
+                            sizeof(phys::Contact) * P->candCapacity);
         phys::Contact *o = (phys::Contact *)out;
         for (int32_t i = 0; i < n && i < cap; i++) o[i] = slots[order[i]];
         return n;
@@ -450,15 +520,15 @@ int32_t mw_phys_read_bvh(mw_exec *exec, int32_t world, void *nodes_out, float *l
         phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
         if (!P) return -1;
         phys::broadphase::BVH bvh;
-        MW_HIP_OK(hipMemcpy(&bvh, P->bvh + world, sizeof(bvh), hipMemcpyDeviceToHost));
+        copyOut(&bvh, P->bvh + world, sizeof(bvh));
         int32_t n = bvh.usedNodes < cap_nodes ? bvh.usedNodes : cap_nodes;
         if (nodes_out && n > 0) {
-            MW_HIP_OK(hipMemcpy(nodes_out, P->nodes + (size_t)world * P->maxNodes,
-                                sizeof(phys::BVHNode) * n, hipMemcpyDeviceToHost));
+            copyOut(nodes_out, P->nodes + (size_t)world * P->maxNodes,
+                                sizeof(phys::BVHNode) * n);
         }
         if (leaf_aabbs_out && bvh.numLeaves > 0) {
-            MW_HIP_OK(hipMemcpy(leaf_aabbs_out, P->leafAABBs + (size_t)world * P->maxLeaves,
-                                sizeof(math::AABB) * bvh.numLeaves, hipMemcpyDeviceToHost));
+            copyOut(leaf_aabbs_out, P->leafAABBs + (size_t)world * P->maxLeaves,
+                                sizeof(math::AABB) * bvh.numLeaves);
         }
         return bvh.usedNodes;
     }, -1)
@@ -571,11 +641,10 @@ extern "C" int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *co
         phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
         if (!P) return -1;
         if (cands_out) {
-            MW_HIP_OK(hipMemcpy(cands_out, P->lastNumCands, 4 * P->numWorlds, hipMemcpyDeviceToHost));
+            copyOut(cands_out, P->lastNumCands, 4 * P->numWorlds);
         }
         if (contacts_out) {
-            MW_HIP_OK(hipMemcpy(contacts_out, P->lastNumContacts, 4 * P->numWorlds,
-                                hipMemcpyDeviceToHost));
+            copyOut(contacts_out, P->lastNumContacts, 4 * P->numWorlds);
         }
         return P->numWorlds;
     }, -1)

@@ -6,7 +6,9 @@
 // lays every archetype out as [world][capacity] column slabs (state.hpp).
 #include <madrona/state.hpp>
 
+#if !defined(MW_CPU_BACKEND)
 #include <hip/hip_runtime.h>
+#endif
 
 #include <algorithm>
 #include <cstdio>
@@ -19,6 +21,7 @@
 
 namespace madrona {
 
+#if !defined(MW_CPU_BACKEND)
 #define MW_HIP_CHECK(expr)                                                          \
     do {                                                                            \
         hipError_t err__ = (expr);                                                  \
@@ -28,6 +31,7 @@ namespace madrona {
             throw std::runtime_error(hipGetErrorString(err__));                     \
         }                                                                           \
     } while (0)
+#endif
 
 struct ArchetypeInfo {
     uint64_t key;
@@ -64,8 +68,10 @@ struct StateManager::Impl {
     ~Impl()
     {
         for (char *p : hostAllocs) free(p);
+#if !defined(MW_CPU_BACKEND)
         for (void *p : devAllocs) (void)hipFree(p);
         if (devView) (void)hipFree(devView);
+#endif
     }
 };
 
@@ -266,6 +272,31 @@ void StateManager::finalizeLayout(uint32_t world_data_bytes, uint32_t world_data
     I.finalized = true;
 }
 
+#if defined(MW_CPU_BACKEND)
+// CPU back end: the host mirror IS the arena.  Temporaries get their
+// (zero-filled) slabs now, the "device" view is the host view, and the
+// module extensions build their slabs in host memory.
+void StateManager::uploadToDevice(void *stream_ptr)
+{
+    Impl &I = *impl_;
+    StateView &h = I.host;
+    size_t ci = 0;
+    for (int32_t a = 0; a < h.numArchetypes; a++) {
+        for (int32_t c = 0; c < h.arch[a].numColumns; c++, ci++) {
+            Impl::ColAlloc &ca = I.colAllocs[ci];
+            if (!ca.host) {
+                ca.host = hostAlloc(I, ca.bytes);
+                h.arch[a].cols[c] = ca.host;
+            }
+        }
+    }
+    I.devView = &I.host;
+    I.devHostCopy = I.host;
+    for (auto &ext : I.extensions) ext.second->upload(stream_ptr);
+}
+
+void StateManager::downloadFromDevice(void *) {}
+#else
 void StateManager::uploadToDevice(void *stream_ptr)
 {
     Impl &I = *impl_;
@@ -376,6 +407,7 @@ void StateManager::downloadFromDevice(void *stream_ptr)
                                 hipMemcpyDeviceToHost, stream));
     MW_HIP_CHECK(hipStreamSynchronize(stream));
 }
+#endif
 
 int32_t StateManager::resolveQuery(const uint64_t *keys, int32_t num_keys,
                                    int32_t *out_archetypes, int32_t *out_cols,

@@ -21,6 +21,15 @@
 #define MW_DEVICE_PASS 0
 #endif
 
+// 1 where node bodies execute: the device pass of hipcc and the CPU back
+// end's g++ build (0 only in hipcc's host pass, where a device node's run()
+// is compiled but never called).
+#if defined(__HIP_DEVICE_COMPILE__) || !defined(__HIPCC__)
+#define MW_EXEC_PASS 1
+#else
+#define MW_EXEC_PASS 0
+#endif
+
 namespace madrona {
 using CountT = int64_t;
 

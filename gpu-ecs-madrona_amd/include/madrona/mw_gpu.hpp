@@ -34,6 +34,8 @@ struct ExecConfig {
     int32_t useGraph;               // capture the step into a hipGraph
     int32_t tmpAllocBytesPerWorld = -1;   // -1: kDefaultTmpAllocBytes, 0: no arena
     int32_t maxDeferredPerWorld = 0;      // 0: kDefaultDeferredPerWorld
+    int32_t numWorkers = 0;               // CPU back end: worker threads (0: every core
+                                          // of the process's affinity mask)
 };
 
 // Non-template core (csrc/runtime/executor.cpp).

@@ -80,6 +80,29 @@ struct LaunchCtx {
     }
 };
 
+// The CPU back end (libmadrona_cpu.so, csrc/runtime/cpu_executor.cpp; the
+// reference's TaskGraphExecutor, include/madrona/mw_cpu.hpp:53-81) runs the
+// same graph on host threads.  A world-local node runs for one world at a
+// time (runWorld), so a run of consecutive world-local nodes executes world
+// by world on a pinned worker, like the reference's per-world TaskGraph::run
+// (src/core/taskgraph.cpp:111-122); a global node (runGlobal: node data
+// shared by every world, e.g. addDynamicCountNode) runs once, between them.
+class CpuThreadPool;
+struct CpuRunCtx {
+    StateView *state;            // host arena
+    StateManager *mgr;
+    int32_t numWorlds;
+    char *nodeData;              // host copies of the graph's node data blocks
+    CpuThreadPool *pool;
+};
+using CpuWorldFn = void (*)(void *node, CpuRunCtx &rc, int32_t world);
+using CpuGlobalFn = void (*)(void *node, CpuRunCtx &rc);
+
+// Parallel loop over [0, n) on the CPU back end's pinned workers (the
+// caller's thread joins in); fn(begin, end) gets contiguous chunks.
+void cpuParallelFor(CpuRunCtx &rc, int64_t n, void (*fn)(void *arg, int64_t begin, int64_t end),
+                    void *arg);
+
 // Base of every node's data (reference device NodeBase,
 // src/mw/device/include/madrona/taskgraph.hpp:23-25).  For nodes whose run()
 // executes on the device (addNodeFn / addOneOffNode / addDynamicCountNode)
@@ -94,6 +117,9 @@ struct NodeBase {
 #if defined(__HIPCC__)
     template <typename ContextT>
     __device__ inline ContextT makeContext(WorldID world) const;
+#else
+    template <typename ContextT>
+    inline ContextT makeContext(WorldID world) const;
 #endif
 };
 
@@ -116,6 +142,14 @@ public:
     };
 
     using LaunchFn = void (*)(void *node, LaunchCtx &lc);
+
+    // How a node runs: kernels (LaunchFn, hipcc builds) and / or on host
+    // threads (CPU back end, g++ builds) -- per world or once per step.
+    struct NodeFns {
+        LaunchFn launch = nullptr;
+        CpuWorldFn cpuWorld = nullptr;
+        CpuGlobalFn cpuGlobal = nullptr;
+    };
 
     // Node flags: a framework node whose kernels never call Context::tmpAlloc
     // (static constexpr bool kNoTmpAlloc), and ResetTmpAllocNode itself.  A
@@ -203,8 +237,15 @@ public:
                 uint32_t flags = 0;
                 if constexpr (requires { NodeT::kNoTmpAlloc; }) flags |= kNodeNoTmpAlloc;
                 if constexpr (requires { NodeT::kTmpAllocReset; }) flags |= kNodeTmpAllocReset;
-                return registerNode(std::static_pointer_cast<void>(data),
-                                    [](void *n, LaunchCtx &lc) { NodeT::launch((NodeT *)n, lc); },
+                NodeFns fns;
+                fns.launch = [](void *n, LaunchCtx &lc) { NodeT::launch((NodeT *)n, lc); };
+                if constexpr (requires(NodeT *n, CpuRunCtx &rc, int32_t w) { NodeT::runWorld(n, rc, w); }) {
+                    fns.cpuWorld = [](void *n, CpuRunCtx &rc, int32_t w) { NodeT::runWorld((NodeT *)n, rc, w); };
+                }
+                if constexpr (requires(NodeT *n, CpuRunCtx &rc) { NodeT::runGlobal(n, rc); }) {
+                    fns.cpuGlobal = [](void *n, CpuRunCtx &rc) { NodeT::runGlobal((NodeT *)n, rc); };
+                }
+                return registerNode(std::static_pointer_cast<void>(data), fns,
                                     dependencies, NodeT::nodeName(), flags);
             } else {
                 auto data_id = constructNodeData<NodeT>(std::forward<Args>(args)...);
@@ -238,12 +279,12 @@ public:
             node->numDynamicInvocations = (uint32_t)node->numInvocations();
         }
 
-        NodeID registerNode(std::shared_ptr<void> data, LaunchFn fn,
+        NodeID registerNode(std::shared_ptr<void> data, NodeFns fns,
                             Span<const NodeID> deps, const char *name, uint32_t flags = 0);
 
         struct Staged {
             std::shared_ptr<void> data;
-            LaunchFn fn;
+            NodeFns fn;
             std::vector<uint32_t> deps;
             const char *name;
             uint32_t flags;
@@ -257,7 +298,9 @@ public:
 
     TaskGraph() = default;
     void launch(LaunchCtx &lc) const;
-    void launchNode(int32_t i, LaunchCtx &lc) const { nodes_[i].fn(nodes_[i].data.get(), lc); }
+    void launchNode(int32_t i, LaunchCtx &lc) const { nodes_[i].fn.launch(nodes_[i].data.get(), lc); }
+    const NodeFns &nodeFns(int32_t i) const { return nodes_[i].fn; }
+    void *nodeState(int32_t i) const { return nodes_[i].data.get(); }
     int32_t numNodes() const { return (int32_t)nodes_.size(); }
     const char *nodeName(int32_t i) const { return nodes_[i].name; }
     uint32_t nodeFlags(int32_t i) const { return nodes_[i].flags; }
@@ -271,7 +314,7 @@ public:
 private:
     struct Node {
         std::shared_ptr<void> data;
-        LaunchFn fn;
+        NodeFns fn;
         const char *name;
         uint32_t flags;
     };
@@ -309,15 +352,13 @@ void launchNodeFnKernel(const void *kernel, LaunchCtx &lc, void *node_dev, uint3
 // no-op for worlds whose lanes made / destroyed nothing.
 void launchStructuralCommit(LaunchCtx &lc);
 
-#if defined(__HIPCC__)
 template <typename ContextT>
-__device__ inline ContextT worldContext(StateView *st, int32_t w)
+MW_INLINE ContextT worldContext(StateView *st, int32_t w, StateManager *mgr = nullptr)
 {
     using WorldT = typename WorldOf<ContextT>::type;
     return ContextT((WorldT *)(st->worldData + (size_t)w * st->worldDataStride),
-                    WorkerInit { st, w, nullptr });
+                    WorkerInit { st, w, mgr });
 }
-#endif
 
 }
 
@@ -327,7 +368,15 @@ __device__ inline ContextT NodeBase::makeContext(WorldID world) const
 {
     return detail::worldContext<ContextT>(mwState, world.idx);
 }
+#else
+template <typename ContextT>
+inline ContextT NodeBase::makeContext(WorldID world) const
+{
+    return detail::worldContext<ContextT>(mwState, world.idx);
+}
+#endif
 
+#if defined(__HIPCC__)
 namespace mwGPU {
 // Lane within the invocation of a CustomParallelForNode / multi-thread
 // node (invocations are aligned groups of threads_per_invocation lanes).
@@ -336,6 +385,14 @@ __device__ inline int32_t invocationLane()
 {
     return (int32_t)(threadIdx.x & (threads_per_invocation - 1));
 }
+}
+#else
+namespace mwGPU {
+// CPU back end: an invocation's lanes run one after another on the worker
+// thread, each seeing its own lane index.
+namespace detail { inline thread_local int32_t cpuInvocationLane = 0; }
+template <int32_t threads_per_invocation>
+inline int32_t invocationLane() { return detail::cpuInvocationLane; }
 }
 #endif
 
@@ -439,6 +496,32 @@ public:
 #endif
     }
 
+#if !defined(__HIPCC__)
+    // CPU back end: the reference's ParallelForNode::run (taskgraph.inl:
+    // 63-71) -- the world's matching rows in query order, rows counted when
+    // each archetype's walk starts, structural ops immediate (world-serial).
+    // A cooperative Fn runs once per invocation lane, lanes in order.
+    static void runWorld(CustomParallelForNode *self, CpuRunCtx &rc, int32_t w)
+    {
+        ContextT ctx = detail::worldContext<ContextT>(rc.state, w, rc.mgr);
+        StateView *st = rc.state;
+        for (int32_t a = 0; a < self->query_.numArchetypes; a++) {
+            const int32_t arch = self->query_.archetypes[a];
+            const int32_t n = st->arch[arch].numRows[w];
+            const int32_t *cols = self->query_.cols[a];
+            [&]<size_t... Is>(std::index_sequence<Is...>) {
+                for (int32_t r = 0; r < n; r++) {
+                    for (int32_t t = 0; t < threads_per_invocation; t++) {
+                        mwGPU::detail::cpuInvocationLane = t;
+                        Fn(ctx, st->column<std::remove_const_t<ComponentTs>>(arch, cols[Is], w)[r]...);
+                    }
+                }
+            }(std::index_sequence_for<ComponentTs...> {});
+        }
+        mwGPU::detail::cpuInvocationLane = 0;
+    }
+#endif
+
     static const char *nodeName()
     {
         return threads_per_invocation == 1 && items_per_invocation == 1 ? "ParallelForNode"
@@ -506,19 +589,62 @@ TaskGraph::NodeID TaskGraph::Builder::addNodeFn(TypedDataID<NodeT> data,
     };
     auto desc = std::make_shared<Desc>(Desc { data.id, fixed_num_invocations,
                                               num_threads_per_invocation });
-    return registerNode(std::static_pointer_cast<void>(desc),
-                        [](void *d, LaunchCtx &lc) {
+    NodeFns fns;
+    fns.launch = [](void *d, LaunchCtx &lc) {
 #if defined(__HIPCC__)
-                            const Desc &dd = *(const Desc *)d;
-                            void *node = lc.nodeData + (size_t)dd.dataIdx * maxNodeDataBytes;
-                            detail::launchNodeFnKernel(
-                                (const void *)&detail::nodeFnKernel<NodeT, fn>, lc, node,
-                                dd.fixedCount, dd.threads);
+        const Desc &dd = *(const Desc *)d;
+        void *node = lc.nodeData + (size_t)dd.dataIdx * maxNodeDataBytes;
+        detail::launchNodeFnKernel((const void *)&detail::nodeFnKernel<NodeT, fn>, lc, node,
+                                   dd.fixedCount, dd.threads);
 #else
-                            (void)d; (void)lc;
+        (void)d; (void)lc;
 #endif
-                        },
-                        dependencies, "NodeFn");
+    };
+#if !defined(__HIPCC__)
+    // CPU back end.  A fixed count per world is world-local (invocation
+    // world * count + k, k in order, each by every one of its lanes in
+    // turn); the single count invocation and a dynamic count (invocations
+    // over all worlds, read from the node data) run once per step.
+    if (fixed_num_invocations > 0 && fixed_num_invocations != 0xFFFF'FFFFu) {
+        fns.cpuWorld = [](void *d, CpuRunCtx &rc, int32_t w) {
+            const Desc &dd = *(const Desc *)d;
+            NodeT *node = (NodeT *)(rc.nodeData + (size_t)dd.dataIdx * maxNodeDataBytes);
+            for (uint32_t k = 0; k < dd.fixedCount; k++) {
+                for (uint32_t t = 0; t < dd.threads; t++) {
+                    mwGPU::detail::cpuInvocationLane = (int32_t)t;
+                    std::invoke(fn, node, (int32_t)((int64_t)w * dd.fixedCount + k));
+                }
+            }
+            mwGPU::detail::cpuInvocationLane = 0;
+        };
+    } else {
+        fns.cpuGlobal = [](void *d, CpuRunCtx &rc) {
+            const Desc &dd = *(const Desc *)d;
+            NodeT *node = (NodeT *)(rc.nodeData + (size_t)dd.dataIdx * maxNodeDataBytes);
+            if (dd.fixedCount == 0xFFFF'FFFFu) {
+                for (uint32_t t = 0; t < dd.threads; t++) {
+                    mwGPU::detail::cpuInvocationLane = (int32_t)t;
+                    std::invoke(fn, node, 0);
+                }
+                mwGPU::detail::cpuInvocationLane = 0;
+                return;
+            }
+            struct Arg { NodeT *node; uint32_t threads; } arg { node, dd.threads };
+            cpuParallelFor(rc, (int64_t)node->numDynamicInvocations,
+                           [](void *a, int64_t b, int64_t e) {
+                               Arg &ar = *(Arg *)a;
+                               for (int64_t i = b; i < e; i++) {
+                                   for (uint32_t t = 0; t < ar.threads; t++) {
+                                       mwGPU::detail::cpuInvocationLane = (int32_t)t;
+                                       std::invoke(fn, ar.node, (int32_t)i);
+                                   }
+                               }
+                               mwGPU::detail::cpuInvocationLane = 0;
+                           }, &arg);
+        };
+    }
+#endif
+    return registerNode(std::static_pointer_cast<void>(desc), fns, dependencies, "NodeFn");
 }
 
 // ---------------------------------------------------------------------------
@@ -560,6 +686,13 @@ public:
         (void)lc;
 #endif
     }
+#if !defined(__HIPCC__)
+    static void runWorld(PerWorldNode *, CpuRunCtx &rc, int32_t w)
+    {
+        ContextT ctx = detail::worldContext<ContextT>(rc.state, w, rc.mgr);
+        Fn(ctx);
+    }
+#endif
 
     static const char *nodeName() { return "PerWorldNode"; }
 };
@@ -586,6 +719,10 @@ public:
         return builder.addDefaultNode<ClearTmpNode>(deps, builder.context());
     }
     static void launch(ClearTmpNode *self, LaunchCtx &lc) { launchClearRows(lc, self->archetype_); }
+    static void runWorld(ClearTmpNode *self, CpuRunCtx &rc, int32_t w)
+    {                                              // clearTemporaries: numRows = 0
+        rc.state->arch[self->archetype_].numRows[w] = 0;
+    }
     static const char *nodeName() { return "ClearTmpNode"; }
     static constexpr bool kNoTmpAlloc = true;
 
@@ -605,6 +742,10 @@ public:
         return builder.addDefaultNode<ResetTmpAllocNode>(deps);
     }
     static void launch(ResetTmpAllocNode *, LaunchCtx &lc) { launchResetTmpAlloc(lc); }
+    static void runWorld(ResetTmpAllocNode *, CpuRunCtx &rc, int32_t w)
+    {
+        if (rc.state->tmpOffset) rc.state->tmpOffset[w] = 0;
+    }
     static const char *nodeName() { return "ResetTmpAllocNode"; }
     static constexpr bool kNoTmpAlloc = true;
     static constexpr bool kTmpAllocReset = true;

@@ -54,7 +54,8 @@ if len(_mapped_hip_runtimes()) > 1:
 class MwConfig(ctypes.Structure):
     _fields_ = [("num_worlds", ctypes.c_int32), ("gpu_id", ctypes.c_int32),
                 ("default_capacity", ctypes.c_int32), ("use_graph", ctypes.c_int32),
-                ("tmp_alloc_bytes", ctypes.c_int32), ("max_deferred_destroys", ctypes.c_int32)]
+                ("tmp_alloc_bytes", ctypes.c_int32), ("max_deferred_destroys", ctypes.c_int32),
+                ("num_workers", ctypes.c_int32)]
 
 
 class CollisionsConfig(ctypes.Structure):
@@ -90,77 +91,103 @@ JC_ROW_DTYPE = np.dtype([("gen", np.uint32), ("id", np.int32), ("pos", np.float3
                          ("rot", np.float32, 4), ("aabb", np.float32, 6)])
 
 
-_lib.mw_create.restype = ctypes.c_void_p
-_lib.mw_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(MwConfig), ctypes.c_void_p,
-                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
-_lib.mw_step.argtypes = [ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_step_async.argtypes = [ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_sync.argtypes = [ctypes.c_void_p]
-_lib.mw_get_exported.restype = ctypes.c_void_p
-_lib.mw_get_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
-_lib.mw_stream.restype = ctypes.c_void_p
-_lib.mw_stream.argtypes = [ctypes.c_void_p]
-_lib.mw_stream_wait.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-_lib.mw_destroy.argtypes = [ctypes.c_void_p]
-_lib.mw_last_error.restype = ctypes.c_char_p
-_lib.mw_num_worlds.argtypes = [ctypes.c_void_p]
-_lib.mw_export_row_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_load_env.argtypes = [ctypes.c_char_p]
-_lib.mw_entity_loc.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
-                               ctypes.c_void_p, ctypes.c_void_p]
-_lib.mw_env_name.restype = ctypes.c_char_p
-_lib.mw_env_name.argtypes = [ctypes.c_int32]
-_lib.mw_error_flags.argtypes = [ctypes.c_void_p]
-_lib.mw_num_archetypes.argtypes = [ctypes.c_void_p]
-_lib.mw_read_column.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                                ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_column_info.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
-                                ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
-_lib.mw_phys_read_candidates.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_phys_read_contacts.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
-                                  ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_phys_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-_lib.mw_copy_exported.restype = ctypes.c_int64
-_lib.mw_copy_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
-_lib.mw_copy_exported_async.restype = ctypes.c_int64
-_lib.mw_copy_exported_async.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
-                                        ctypes.c_int64]
-_lib.mw_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
-_lib.mw_gen_fvs_inits.argtypes = [ctypes.c_int32] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
-_lib.mw_phys_time_node.restype = ctypes.c_double
-_lib.mw_phys_time_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
-_lib.mw_rccl_get_unique_id.argtypes = [ctypes.c_void_p]
-_lib.mw_rccl_init.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
-_lib.mw_allgather_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
-                                       ctypes.c_int64]
-_lib.mw_device_alloc.restype = ctypes.c_void_p
-_lib.mw_device_alloc.argtypes = [ctypes.c_void_p, ctypes.c_int64]
-_lib.mw_device_free.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-RCCL_ID_BYTES = 128
-_lib.mw_load_hull.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                             ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
-                             ctypes.c_int32]
-_lib.mw_trace_enable.argtypes = [ctypes.c_void_p, ctypes.c_int64]
-_lib.mw_trace_block_records.restype = ctypes.c_int
-_lib.mw_trace_read.restype = ctypes.c_int64
-_lib.mw_trace_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
-                               ctypes.POINTER(ctypes.c_int64)]
-_lib.mw_trace_func_name.restype = ctypes.c_char_p
-_lib.mw_trace_func_name.argtypes = [ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_set_timed_node.restype = ctypes.c_int32
-_lib.mw_set_timed_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
-_lib.mw_timed_node_ms.restype = ctypes.c_double
-_lib.mw_timed_node_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
-_lib.mw_num_nodes.argtypes = [ctypes.c_void_p]
-_lib.mw_node_name.restype = ctypes.c_char_p
-_lib.mw_node_name.argtypes = [ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_node_blocks_per_cu.argtypes = [ctypes.c_void_p, ctypes.c_int32]
-_lib.mw_set_node_blocks_per_cu.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
-_lib.mw_parse_exec_config_override.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
-_lib.mw_parse_exec_config_file.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
-                                           ctypes.c_int32]
+def _declare(lib):
+    """ctypes signatures of the C ABI (either library)."""
+    lib.mw_create.restype = ctypes.c_void_p
+    lib.mw_create.argtypes = [ctypes.c_char_p, ctypes.POINTER(MwConfig), ctypes.c_void_p,
+                               ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    lib.mw_step.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_step_async.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_sync.argtypes = [ctypes.c_void_p]
+    lib.mw_get_exported.restype = ctypes.c_void_p
+    lib.mw_get_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
+    lib.mw_stream.restype = ctypes.c_void_p
+    lib.mw_stream.argtypes = [ctypes.c_void_p]
+    lib.mw_stream_wait.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.mw_destroy.argtypes = [ctypes.c_void_p]
+    lib.mw_last_error.restype = ctypes.c_char_p
+    lib.mw_num_worlds.argtypes = [ctypes.c_void_p]
+    lib.mw_export_row_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_load_env.argtypes = [ctypes.c_char_p]
+    lib.mw_entity_loc.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
+                                   ctypes.c_void_p, ctypes.c_void_p]
+    lib.mw_env_name.restype = ctypes.c_char_p
+    lib.mw_env_name.argtypes = [ctypes.c_int32]
+    lib.mw_error_flags.argtypes = [ctypes.c_void_p]
+    lib.mw_num_archetypes.argtypes = [ctypes.c_void_p]
+    lib.mw_read_column.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_column_info.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+    lib.mw_phys_read_candidates.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_phys_read_contacts.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_phys_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.mw_copy_exported.restype = ctypes.c_int64
+    lib.mw_copy_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
+    lib.mw_copy_exported_async.restype = ctypes.c_int64
+    lib.mw_copy_exported_async.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                            ctypes.c_int64]
+    lib.mw_gen_collisions_inits.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    lib.mw_gen_fvs_inits.argtypes = [ctypes.c_int32] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
+    lib.mw_phys_time_node.restype = ctypes.c_double
+    lib.mw_phys_time_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
+    lib.mw_rccl_get_unique_id.argtypes = [ctypes.c_void_p]
+    lib.mw_rccl_init.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+    lib.mw_allgather_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_int64]
+    lib.mw_device_alloc.restype = ctypes.c_void_p
+    lib.mw_device_alloc.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    lib.mw_device_free.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    RCCL_ID_BYTES = 128
+    lib.mw_load_hull.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                 ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                 ctypes.c_int32]
+    lib.mw_trace_enable.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    lib.mw_trace_block_records.restype = ctypes.c_int
+    lib.mw_trace_read.restype = ctypes.c_int64
+    lib.mw_trace_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                   ctypes.POINTER(ctypes.c_int64)]
+    lib.mw_trace_func_name.restype = ctypes.c_char_p
+    lib.mw_trace_func_name.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_set_timed_node.restype = ctypes.c_int32
+    lib.mw_set_timed_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.mw_timed_node_ms.restype = ctypes.c_double
+    lib.mw_timed_node_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+    lib.mw_num_nodes.argtypes = [ctypes.c_void_p]
+    lib.mw_node_name.restype = ctypes.c_char_p
+    lib.mw_node_name.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_node_blocks_per_cu.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    lib.mw_set_node_blocks_per_cu.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+    lib.mw_parse_exec_config_override.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    lib.mw_parse_exec_config_file.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_int32]
+    return lib
+
+
+_declare(_lib)
+
+CPU_LIB_PATH = os.environ.get("MADRONA_MW_CPU_LIB") or os.path.join(
+    os.path.dirname(PKG_DIR), "build_cpu", "libmadrona_cpu.so")
+_cpu_lib = None
+# Back end of executors created without an explicit `backend`.
+DEFAULT_BACKEND = os.environ.get("MADRONA_MW_BACKEND", "gpu")
+
+
+def cpu_library():
+    """The CPU back end (libmadrona_cpu.so: the same worlds and C ABI on a
+    pinned host thread pool, the reference's TaskGraphExecutor); loaded on
+    first use."""
+    global _cpu_lib
+    if _cpu_lib is None:
+        if not os.path.exists(CPU_LIB_PATH):
+            raise ImportError(f"madrona_mi355x: CPU library missing at {CPU_LIB_PATH}; "
+                              "build it with `make -C gpu-ecs-madrona_amd cpu`")
+        _cpu_lib = _declare(ctypes.CDLL(CPU_LIB_PATH))
+    return _cpu_lib
+
 
 # The symbols include/madrona_mw.h declares (checked by tests/test_capi_symbols.py).
 C_ABI_SYMBOLS = (
@@ -199,19 +226,28 @@ def parse_exec_config_file(text):
     return [(int(a), int(b)) for a, b in zip(nodes[:n], blocks[:n])]
 
 
-def load_env(so_path):
+def backend_library(backend=None):
+    """The C-ABI library of a back end: "gpu" (libmadrona_mw.so, gfx950) or
+    "cpu" (libmadrona_cpu.so)."""
+    return cpu_library() if (backend or DEFAULT_BACKEND) == "cpu" else _lib
+
+
+def load_env(so_path, backend=None):
     """Load an out-of-tree world (a shared object built against
-    include/madrona that registers itself with MADRONA_BUILD_MWGPU_ENTRY);
-    returns the number of environments it registered."""
-    n = _lib.mw_load_env(os.fsencode(so_path))
+    include/madrona that registers itself with MADRONA_BUILD_MWGPU_ENTRY,
+    linked to the back end's library); returns the number of environments
+    it registered."""
+    lib = backend_library(backend)
+    n = lib.mw_load_env(os.fsencode(so_path))
     if n < 0:
-        raise _err()
+        raise _err(lib)
     return n
 
 
-def env_names():
+def env_names(backend=None):
     """Every registered environment name (built-in and loaded)."""
-    return [_lib.mw_env_name(i).decode() for i in range(_lib.mw_num_envs())]
+    lib = backend_library(backend)
+    return [lib.mw_env_name(i).decode() for i in range(lib.mw_num_envs())]
 
 
 def rccl_unique_id():
@@ -274,8 +310,8 @@ class MadronaError(RuntimeError):
     pass
 
 
-def _err():
-    return MadronaError(_lib.mw_last_error().decode())
+def _err(lib=None):
+    return MadronaError((lib or _lib).mw_last_error().decode())
 
 
 def library():
@@ -316,15 +352,22 @@ class Executor:
 
     def __init__(self, env, num_worlds, user_cfg, inits, init_stride, gpu_id=0,
                  default_capacity=64, use_graph=True, tmp_alloc_bytes=-1,
-                 max_deferred_destroys=0):
+                 max_deferred_destroys=0, backend=None, num_workers=0):
+        # backend "cpu": the same world on the CPU back end (num_workers
+        # pinned host threads, 0 = every core of the affinity mask)
+        backend = backend or DEFAULT_BACKEND
+        if backend not in ("gpu", "cpu"):
+            raise ValueError(f"backend must be 'gpu' or 'cpu', not {backend!r}")
+        self._lib = backend_library(backend)
+        self.backend = backend
         cfg = MwConfig(num_worlds, gpu_id, default_capacity, 1 if use_graph else 0,
-                       tmp_alloc_bytes, max_deferred_destroys)
+                       tmp_alloc_bytes, max_deferred_destroys, num_workers)
         self._keep = (user_cfg, inits)
-        self.h = _lib.mw_create(env.encode(), ctypes.byref(cfg), ctypes.byref(user_cfg),
+        self.h = self._lib.mw_create(env.encode(), ctypes.byref(cfg), ctypes.byref(user_cfg),
                                 ctypes.sizeof(user_cfg), ctypes.cast(inits, ctypes.c_void_p),
                                 init_stride)
         if not self.h:
-            raise _err()
+            raise _err(self._lib)
         self.num_worlds = num_worlds
         self.gpu_id = gpu_id
 
@@ -332,8 +375,8 @@ class Executor:
         """Device-side ordering: `stream` (an int hipStream_t, e.g.
         torch.cuda.current_stream().cuda_stream) waits for every step
         enqueued so far; no host sync (reference CudaSync::wait)."""
-        if _lib.mw_stream_wait(self.h, ctypes.c_void_p(stream)) != 0:
-            raise _err()
+        if self._lib.mw_stream_wait(self.h, ctypes.c_void_p(stream)) != 0:
+            raise _err(self._lib)
 
     def exported_tensor(self, slot, element_type, dims):
         """Zero-copy view of export `slot` as a madrona_mi355x.python.Tensor
@@ -346,132 +389,132 @@ class Executor:
         return Tensor.from_device_ptr(ptr, element_type, dims, self.gpu_id, owner=self)
 
     def step(self, n=1):
-        if _lib.mw_step(self.h, n) != 0:
-            raise _err()
+        if self._lib.mw_step(self.h, n) != 0:
+            raise _err(self._lib)
 
     def step_async(self, n=1):
-        if _lib.mw_step_async(self.h, n) != 0:
-            raise _err()
+        if self._lib.mw_step_async(self.h, n) != 0:
+            raise _err(self._lib)
 
     def sync(self):
-        if _lib.mw_sync(self.h) != 0:
-            raise _err()
+        if self._lib.mw_sync(self.h) != 0:
+            raise _err(self._lib)
 
     @property
     def stream(self):
-        return _lib.mw_stream(self.h)
+        return self._lib.mw_stream(self.h)
 
     def exported(self, slot):
         rows = ctypes.c_int64(0)
-        ptr = _lib.mw_get_exported(self.h, slot, ctypes.byref(rows))
+        ptr = self._lib.mw_get_exported(self.h, slot, ctypes.byref(rows))
         return ptr, rows.value
 
     def exported_array(self, slot, dtype):
         """Host copy of export `slot` (packed [world-major, row] rows)."""
         dtype = np.dtype(dtype)
         _, rows = self.exported(slot)
-        row_bytes = _lib.mw_export_row_bytes(self.h, slot)
+        row_bytes = self._lib.mw_export_row_bytes(self.h, slot)
         if row_bytes <= 0:
-            raise _err()
+            raise _err(self._lib)
         out = np.empty(max(rows, 1) * row_bytes, np.uint8)
         n = self.copy_exported(slot, out.ctypes.data, out.nbytes)
         return out[:n].view(dtype)
 
     def error_flags(self):
-        return _lib.mw_error_flags(self.h)
+        return self._lib.mw_error_flags(self.h)
 
     def entity_loc(self, world, entity_id, gen):
         """(archetype, row) of a live entity, None when it is not alive."""
         a, r = ctypes.c_int32(), ctypes.c_int32()
-        rc = _lib.mw_entity_loc(self.h, world, entity_id, gen, ctypes.byref(a), ctypes.byref(r))
+        rc = self._lib.mw_entity_loc(self.h, world, entity_id, gen, ctypes.byref(a), ctypes.byref(r))
         if rc < 0:
-            raise _err()
+            raise _err(self._lib)
         return None if rc else (a.value, r.value)
 
     def read_column(self, archetype, column, world, dtype, max_rows=4096):
         b = ctypes.c_int32()
         cap = ctypes.c_int32()
-        if _lib.mw_column_info(self.h, archetype, column, ctypes.byref(b), ctypes.byref(cap)) != 0:
+        if self._lib.mw_column_info(self.h, archetype, column, ctypes.byref(b), ctypes.byref(cap)) != 0:
             raise MadronaError(f"no column {archetype}:{column}")
         buf = np.zeros(max(cap.value, 1) * b.value, np.uint8)
-        n = _lib.mw_read_column(self.h, archetype, column, world,
+        n = self._lib.mw_read_column(self.h, archetype, column, world,
                                 buf.ctypes.data_as(ctypes.c_void_p), cap.value)
         if n < 0:
-            raise _err()
+            raise _err(self._lib)
         return buf[: n * b.value].view(dtype)
 
     def copy_exported(self, slot, dst_ptr, max_bytes):
-        n = _lib.mw_copy_exported(self.h, slot, ctypes.c_void_p(dst_ptr), max_bytes)
+        n = self._lib.mw_copy_exported(self.h, slot, ctypes.c_void_p(dst_ptr), max_bytes)
         if n < 0:
-            raise _err()
+            raise _err(self._lib)
         return n
 
     def copy_exported_async(self, slot, dst_ptr, max_bytes):
         """Enqueue the hand-off copy of export `slot` into device memory
         dst_ptr on the executor stream (no host wait)."""
-        n = _lib.mw_copy_exported_async(self.h, slot, ctypes.c_void_p(dst_ptr), max_bytes)
+        n = self._lib.mw_copy_exported_async(self.h, slot, ctypes.c_void_p(dst_ptr), max_bytes)
         if n < 0:
-            raise _err()
+            raise _err(self._lib)
         return n
 
     def rccl_init(self, uid, nranks, rank):
         """Join the world-shard communicator (RCCL over xGMI)."""
         buf = ctypes.create_string_buffer(bytes(uid), RCCL_ID_BYTES)
-        if _lib.mw_rccl_init(self.h, buf, nranks, rank) != 0:
-            raise _err()
+        if self._lib.mw_rccl_init(self.h, buf, nranks, rank) != 0:
+            raise _err(self._lib)
 
     def allgather_exported(self, slot, dst_ptr, bytes_per_rank):
         """Enqueue an all-gather of export `slot` into device memory dst_ptr
         (nranks * bytes_per_rank bytes, rank order) on the executor stream."""
-        if _lib.mw_allgather_exported(self.h, slot, ctypes.c_void_p(dst_ptr), bytes_per_rank) != 0:
-            raise _err()
+        if self._lib.mw_allgather_exported(self.h, slot, ctypes.c_void_p(dst_ptr), bytes_per_rank) != 0:
+            raise _err(self._lib)
 
     def device_alloc(self, nbytes):
-        p = _lib.mw_device_alloc(self.h, nbytes)
+        p = self._lib.mw_device_alloc(self.h, nbytes)
         if not p:
-            raise _err()
+            raise _err(self._lib)
         return p
 
     def device_free(self, ptr):
-        if _lib.mw_device_free(self.h, ctypes.c_void_p(ptr)) != 0:
-            raise _err()
+        if self._lib.mw_device_free(self.h, ctypes.c_void_p(ptr)) != 0:
+            raise _err(self._lib)
 
     def time_node(self, name, steps):
         """Eager timing of `steps` extra steps (advances the simulation)."""
-        return _lib.mw_phys_time_node(self.h, name.encode(), steps)
+        return self._lib.mw_phys_time_node(self.h, name.encode(), steps)
 
     def nodes(self):
         """Node kinds of the sorted step graph, by node index."""
-        return [_lib.mw_node_name(self.h, i).decode() for i in range(_lib.mw_num_nodes(self.h))]
+        return [self._lib.mw_node_name(self.h, i).decode() for i in range(self._lib.mw_num_nodes(self.h))]
 
     def node_blocks_per_cu(self, node=-1):
         """Effective launch configuration (blocks per CU, 0 = full grid) of
         `node`; node -1: the default."""
-        return _lib.mw_node_blocks_per_cu(self.h, node)
+        return self._lib.mw_node_blocks_per_cu(self.h, node)
 
     def set_node_blocks_per_cu(self, node, blocks_per_cu):
         """Per-node launch configuration (node -1: the default; value -1 on a
         node: back to the default).  Re-captures the step graph."""
-        if _lib.mw_set_node_blocks_per_cu(self.h, node, blocks_per_cu) != 0:
-            raise _err()
+        if self._lib.mw_set_node_blocks_per_cu(self.h, node, blocks_per_cu) != 0:
+            raise _err(self._lib)
 
     def set_timed_node(self, name):
         """Bracket every launch of node kind `name` with HIP events inside the
         replayed step (None disables); resets the accumulators."""
-        if _lib.mw_set_timed_node(self.h, name.encode() if name else None) != 0:
-            raise _err()
+        if self._lib.mw_set_timed_node(self.h, name.encode() if name else None) != 0:
+            raise _err(self._lib)
 
     def timed_node(self):
         """(total ms, launches) accumulated since set_timed_node."""
         n = ctypes.c_int64(0)
-        ms = _lib.mw_timed_node_ms(self.h, ctypes.byref(n))
+        ms = self._lib.mw_timed_node_ms(self.h, ctypes.byref(n))
         return ms, n.value
 
     def enable_tracing(self, max_records=1 << 20):
         """Device tracing (reference MADRONA_TRACING, mw_gpu/tracing.hpp): every
         following step logs 40-byte DeviceLog records; 0 disables."""
-        if _lib.mw_trace_enable(self.h, int(max_records)) != 0:
-            raise _err()
+        if self._lib.mw_trace_enable(self.h, int(max_records)) != 0:
+            raise _err(self._lib)
 
     @staticmethod
     def trace_block_records():
@@ -481,18 +524,18 @@ class Executor:
     def trace_records(self):
         """(records as a TRACE_DTYPE array, number dropped to a full buffer)."""
         dropped = ctypes.c_int64(0)
-        n = _lib.mw_trace_read(self.h, None, 0, ctypes.byref(dropped))
+        n = self._lib.mw_trace_read(self.h, None, 0, ctypes.byref(dropped))
         if n < 0:
-            raise _err()
+            raise _err(self._lib)
         out = np.zeros(n // TRACE_DTYPE.itemsize, TRACE_DTYPE)
-        if _lib.mw_trace_read(self.h, out.ctypes.data, n, ctypes.byref(dropped)) < 0:
-            raise _err()
+        if self._lib.mw_trace_read(self.h, out.ctypes.data, n, ctypes.byref(dropped)) < 0:
+            raise _err(self._lib)
         return out, int(dropped.value)
 
     def trace_func_names(self):
         names, i = [], 0
         while True:
-            s = _lib.mw_trace_func_name(self.h, i)
+            s = self._lib.mw_trace_func_name(self.h, i)
             if s is None:
                 return names
             names.append(s.decode())
@@ -508,7 +551,7 @@ class Executor:
 
     def close(self):
         if getattr(self, "h", None):
-            _lib.mw_destroy(self.h)
+            self._lib.mw_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -536,7 +579,7 @@ def default_collisions_config(num_cubes=128, num_substeps=4, max_contacts=4096,
 class CollisionsSim(Executor):
     """The `collisions` rigid-body environment (RigidBodyPhysicsSystem)."""
 
-    def __init__(self, num_worlds, pos, rot, cfg=None, gpu_id=0, use_graph=True):
+    def __init__(self, num_worlds, pos, rot, cfg=None, gpu_id=0, use_graph=True, **kw):
         cfg = cfg or default_collisions_config(num_cubes=pos.shape[1])
         self._pos = np.ascontiguousarray(pos, np.float32)
         self._rot = np.ascontiguousarray(rot, np.float32)
@@ -551,7 +594,7 @@ class CollisionsSim(Executor):
         self.cfg = cfg
         self.num_bodies = cfg.num_cubes + 1
         super().__init__("collisions", num_worlds, cfg, inits, ctypes.sizeof(CollisionsInit),
-                         gpu_id=gpu_id, default_capacity=64, use_graph=use_graph)
+                         gpu_id=gpu_id, default_capacity=64, use_graph=use_graph, **kw)
 
     def bodies(self, w):
         """Per-body state of world w in the oracle's record layout."""
@@ -579,33 +622,33 @@ class CollisionsSim(Executor):
 
     def candidates(self, w, cap=1 << 15):
         out = np.zeros((cap, 4), np.int32)
-        n = _lib.mw_phys_read_candidates(self.h, w, out.ctypes.data_as(ctypes.c_void_p), cap)
+        n = self._lib.mw_phys_read_candidates(self.h, w, out.ctypes.data_as(ctypes.c_void_p), cap)
         if n < 0:
-            raise _err()
+            raise _err(self._lib)
         return out[:n]
 
     def contacts(self, w, cap=1 << 14):
         out = np.zeros(cap, CONTACT_DTYPE)
-        n = _lib.mw_phys_read_contacts(self.h, w, out.ctypes.data_as(ctypes.c_void_p), cap)
+        n = self._lib.mw_phys_read_contacts(self.h, w, out.ctypes.data_as(ctypes.c_void_p), cap)
         if n < 0:
-            raise _err()
+            raise _err(self._lib)
         return out[:n]
 
     def counts(self):
         c = np.zeros(self.num_worlds, np.int32)
         k = np.zeros(self.num_worlds, np.int32)
-        if _lib.mw_phys_counts(self.h, c.ctypes.data_as(ctypes.c_void_p),
+        if self._lib.mw_phys_counts(self.h, c.ctypes.data_as(ctypes.c_void_p),
                                k.ctypes.data_as(ctypes.c_void_p)) < 0:
-            raise _err()
+            raise _err(self._lib)
         return c, k
 
     def bvh(self, w, cap=4096):
         nodes = np.zeros(cap, BVH_NODE_DTYPE)
         aabbs = np.zeros((self.num_bodies, 6), np.float32)
-        n = _lib.mw_phys_read_bvh(self.h, w, nodes.ctypes.data_as(ctypes.c_void_p),
+        n = self._lib.mw_phys_read_bvh(self.h, w, nodes.ctypes.data_as(ctypes.c_void_p),
                                   aabbs.ctypes.data_as(ctypes.c_void_p), cap)
         if n < 0:
-            raise _err()
+            raise _err(self._lib)
         return nodes[:n], aabbs
 
 
@@ -634,7 +677,7 @@ class FvsSim(Executor):
     DRAGON, KNIGHT, TRACKER = 0, 1, 2
 
     def __init__(self, num_worlds, inits, first_world=0, gpu_id=0, use_graph=True,
-                 env="fantasy_vs"):
+                 env="fantasy_vs", **kw):
         # env "fantasy_vs_jobs": the same game written against the job API
         self._inits = {k: np.ascontiguousarray(v) for k, v in inits.items()}
         nd = self._inits["dragon_mana"].shape[1]
@@ -650,7 +693,7 @@ class FvsSim(Executor):
             arr[w].knight_arrows = base["knight_arrows"] + w * nk * 4
             arr[w].world_index = first_world + w
         super().__init__(env, num_worlds, self.cfg, arr, ctypes.sizeof(FvsInit),
-                         gpu_id=gpu_id, default_capacity=64, use_graph=use_graph)
+                         gpu_id=gpu_id, default_capacity=64, use_graph=use_graph, **kw)
 
     def table(self, w, arch):
         """Rows of Dragon / Knight of world w in the oracle's record layout."""
@@ -677,7 +720,7 @@ class JobsCollisionsSim(Executor):
     API; pos [W, N, 3] / rot [W, N, 4] from gen_collisions_inits."""
     CUBE, CANDIDATE, CONTACT = 0, 1, 2
 
-    def __init__(self, num_worlds, pos, rot, max_candidates=1024, gpu_id=0, use_graph=True):
+    def __init__(self, num_worlds, pos, rot, max_candidates=1024, gpu_id=0, use_graph=True, **kw):
         self._pos = np.ascontiguousarray(pos, np.float32)
         self._rot = np.ascontiguousarray(rot, np.float32)
         n = self._pos.shape[1]
@@ -689,7 +732,7 @@ class JobsCollisionsSim(Executor):
             arr[w].pos = self._pos.ctypes.data + w * n * 12
             arr[w].rot = self._rot.ctypes.data + w * n * 16
         super().__init__("collisions_jobs", num_worlds, self.cfg, arr, ctypes.sizeof(CollisionsInit),
-                         gpu_id=gpu_id, default_capacity=64, use_graph=use_graph)
+                         gpu_id=gpu_id, default_capacity=64, use_graph=use_graph, **kw)
 
     def cubes(self, w):
         """CubeObject rows of world w (JC_ROW_DTYPE), table order."""
@@ -711,7 +754,7 @@ class SimpleSim(CollisionsSim):
     archetypes (Sphere: objects + test object, Agent)."""
     SPHERE, AGENT = BODY_ARCHETYPE, BODY_ARCHETYPE + 1
 
-    def __init__(self, num_worlds, pos, rot, cfg=None, gpu_id=0, use_graph=True):
+    def __init__(self, num_worlds, pos, rot, cfg=None, gpu_id=0, use_graph=True, **kw):
         cfg = cfg or default_collisions_config(num_cubes=pos.shape[1])
         self._pos = np.ascontiguousarray(pos, np.float32)
         self._rot = np.ascontiguousarray(rot, np.float32)
@@ -723,7 +766,7 @@ class SimpleSim(CollisionsSim):
         self.num_bodies = cfg.num_cubes + 2
         Executor.__init__(self, "simple_taskgraph", num_worlds, cfg, inits,
                           ctypes.sizeof(CollisionsInit), gpu_id=gpu_id, default_capacity=64,
-                          use_graph=use_graph)
+                          use_graph=use_graph, **kw)
 
     def bodies(self, w):
         """Sphere rows then Agent rows (the reference query order)."""

@@ -19,3 +19,14 @@ MW_HIPFLAGS := -std=c++20 -O3 -fPIC --offload-arch=$(MW_ARCH) -mcode-object-vers
                -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt \
                -I$(MADRONA_MW)/include
 MW_LDFLAGS := -L$(MADRONA_MW)/$(MW_BUILD) -lmadrona_mw -Wl,-rpath,$(abspath $(MADRONA_MW)/$(MW_BUILD))
+
+# The same world for the CPU back end (libmadrona_cpu.so): g++, no HIP.
+#
+#     libmyworld_cpu.so: myworld.hip
+#     	$(MW_CPU_CXX) $(MW_CPU_CXXFLAGS) -shared -o $@ -x c++ $< $(MW_CPU_LDFLAGS)
+MW_CPU_CXX ?= g++
+MW_CPU_BUILD ?= build_cpu
+MW_CPU_CXXFLAGS := -std=c++20 -O2 -fPIC -ffp-contract=off -fno-fast-math -pthread \
+                   -DMW_CPU_BACKEND -I$(MADRONA_MW)/include
+MW_CPU_LDFLAGS := -L$(MADRONA_MW)/$(MW_CPU_BUILD) -lmadrona_cpu \
+                  -Wl,-rpath,$(abspath $(MADRONA_MW)/$(MW_CPU_BUILD))

@@ -22,6 +22,14 @@
  *
  * All pointers are plain host pointers except those documented as device
  * pointers (mw_get_exported, mw_stream).  No torch types cross this boundary.
+ *
+ * Two libraries export this ABI: libmadrona_mw.so (gfx950) and
+ * libmadrona_cpu.so, the CPU back end built from the same world sources
+ * with g++ (the reference's TaskGraphExecutor on a pinned thread pool,
+ * include/madrona/mw_cpu.hpp:53-81, src/mw/cpu_exec.cpp:31-284).  In the
+ * CPU library "device" pointers are host pointers, mw_step is synchronous
+ * and the RCCL / tracing / launch-configuration entry points fail with a
+ * status.
  */
 #ifndef MADRONA_MW_H
 #define MADRONA_MW_H
@@ -46,6 +54,10 @@ typedef struct mw_config {
     int32_t max_deferred_destroys; /* destroyEntityNow calls per world per
                                   row-parallel node (applied in the reference's
                                   order after the node); 0: 256              */
+    int32_t num_workers;       /* CPU back end: worker threads, pinned one per
+                                  core (reference ThreadPoolExecutor::Config::
+                                  numWorkers, mw_cpu.hpp:20-27); 0: every core
+                                  of the affinity mask.  Ignored on gfx950.   */
 } mw_config;
 
 /* "collisions": rigid-body workload of SURVEY.md §8(d) C3/C4 (128 unit cube

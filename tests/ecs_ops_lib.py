@@ -13,6 +13,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ENV_SO = os.path.join(ROOT, "tests", "ext_env", "build", "libecs_ops.so")
+ENV_SO_CPU = os.path.join(ROOT, "tests", "ext_env", "build", "libecs_ops_cpu.so")
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libmadrona_ref_ecs.so")
 ENV_NAME = "EcsOps::World"
 NUM_AGENTS = 40
@@ -46,18 +47,20 @@ class EcsInit(ctypes.Structure):
     _fields_ = [("worldIndex", ctypes.c_int32)]
 
 
-def load_env():
+def load_env(backend=None):
     import madrona_mi355x as mw
-    if ENV_NAME not in mw.env_names():
-        if not os.path.exists(ENV_SO):
-            raise FileNotFoundError(f"{ENV_SO} not built (make -C tests/ext_env)")
-        assert mw.load_env(ENV_SO) == 1
+    backend = backend or mw.DEFAULT_BACKEND
+    so = ENV_SO_CPU if backend == "cpu" else ENV_SO
+    if ENV_NAME not in mw.env_names(backend):
+        if not os.path.exists(so):
+            raise FileNotFoundError(f"{so} not built (make -C tests/ext_env)")
+        assert mw.load_env(so, backend) == 1
     return mw
 
 
 class EcsOpsSim:
     def __init__(self, num_worlds, first_world=0, tmp_alloc_bytes=64 * 1024, **kw):
-        mw = load_env()
+        mw = load_env(kw.get("backend"))
         inits = (EcsInit * num_worlds)(*[EcsInit(first_world + w) for w in range(num_worlds)])
         self.exec = mw.Executor(ENV_NAME, num_worlds, EcsConfig(NUM_AGENTS), inits,
                                 ctypes.sizeof(EcsInit), tmp_alloc_bytes=tmp_alloc_bytes, **kw)

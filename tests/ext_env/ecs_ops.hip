@@ -187,7 +187,7 @@ MW_HD void World::spawnSystem(Engine &ctx, Entity e, Counter &c)
 struct StatsNode : NodeBase {
     MW_HD void run(int32_t world)
     {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if MW_EXEC_PASS
         Engine ctx = makeContext<Engine>(WorldID { world });
         Stats &st = ctx.getSingleton<Stats>();
         st.numPairs = ctx.numRows<PairTemp>();
@@ -210,7 +210,7 @@ struct TickNode : NodeBase {
     MW_HD uint32_t numInvocations() const { return (uint32_t)mwNumWorlds; }
     MW_HD void run(int32_t world)
     {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if MW_EXEC_PASS
         if (mwGPU::invocationLane<2>() != 0) return;
         Engine ctx = makeContext<Engine>(WorldID { world });
         ctx.data().tick += 1;

@@ -40,11 +40,23 @@ def test_library_exports_every_declared_symbol():
 
 def test_exported_symbols_are_unmangled_c():
     import madrona_mi355x as mw
-    out = subprocess.run(["nm", "-D", "--defined-only", mw.LIB_PATH], capture_output=True,
-                         text=True, check=True).stdout
-    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
-    for n in _declared_functions():
-        assert n in exported, n
+    for path in (mw.LIB_PATH, mw.CPU_LIB_PATH):
+        out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True,
+                             text=True, check=True).stdout
+        exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+        for n in _declared_functions():
+            assert n in exported, (path, n)
+
+
+def test_cpu_library_exports_every_declared_symbol_without_hip():
+    # the CPU back end is the same ABI with no HIP / RCCL dependency
+    import madrona_mi355x as mw
+    lib = mw.cpu_library()
+    missing = [n for n in _declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    deps = subprocess.run(["readelf", "-d", mw.CPU_LIB_PATH], capture_output=True, text=True,
+                          check=True).stdout
+    assert "amdhip" not in deps and "rccl" not in deps, deps
 
 
 def test_struct_layout_matches_header(tmp_path):
