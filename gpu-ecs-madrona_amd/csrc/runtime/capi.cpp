@@ -127,7 +127,7 @@ static void setError(const char *what) { g_last_error = what ? what : "unknown e
 // Arena (device) -> caller (host) read-back.
 static void copyOut(void *dst, const void *src, size_t bytes)
 {
-    copyOut(dst, src, bytes);
+    MW_HIP_OK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
 }
 #else
 static void copyOut(void *dst, const void *src, size_t bytes) { memcpy(dst, src, bytes); }

@@ -91,6 +91,9 @@ JC_ROW_DTYPE = np.dtype([("gen", np.uint32), ("id", np.int32), ("pos", np.float3
                          ("rot", np.float32, 4), ("aabb", np.float32, 6)])
 
 
+RCCL_ID_BYTES = 128
+
+
 def _declare(lib):
     """ctypes signatures of the C ABI (either library)."""
     lib.mw_create.restype = ctypes.c_void_p
@@ -141,7 +144,6 @@ def _declare(lib):
     lib.mw_device_alloc.restype = ctypes.c_void_p
     lib.mw_device_alloc.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     lib.mw_device_free.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    RCCL_ID_BYTES = 128
     lib.mw_load_hull.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                  ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                  ctypes.c_int32]
