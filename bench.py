@@ -87,6 +87,9 @@ def parse():
     p.add_argument("--cpu-target-s", type=float, default=10.0)
     p.add_argument("--cpu-max-batches", type=int, default=12)
     p.add_argument("--cpu-port", action="store_true", help="time oracle/ instead of oracle/_ref")
+    p.add_argument("--cpu-executor", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--no-cpu-executor", action="store_true",
+                   help="skip timing the framework's own CPU back end (libmadrona_cpu.so)")
     p.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--cpu-first-world", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--no-roofline", action="store_true")
@@ -105,7 +108,18 @@ def _cpu_child(args):
     pos, rot = ol.gen_collisions_inits(first + W, args.cubes, seed=0)
     pos, rot = pos[first:], rot[first:]
     ocfg = ol.default_phys_config(args.cubes, args.substeps, max_contacts=4096)
-    if ol.ref_available() and not args.cpu_port:
+    if args.cpu_executor:
+        # the framework's CPU back end: same world sources, pinned workers
+        import madrona_mi355x as mw
+        g = mw.default_collisions_config(args.cubes, args.substeps, 4096, 4096)
+        sim = mw.CollisionsSim(W, pos, rot, g, backend="cpu", num_workers=threads)
+        kind = "port"
+        sim.step(args.settle + args.warmup)
+        t0 = time.perf_counter()
+        sim.step(args.cpu_steps)
+        dt = time.perf_counter() - t0
+        assert sim.error_flags() == 0
+    elif ol.ref_available() and not args.cpu_port:
         lib = ol.load_ref()
         lib.ref_phys_step_mt.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
         sim = ol.ReferencePhys(ocfg, pos, rot)
@@ -147,7 +161,7 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(args):
+def cpu_baseline(args, executor=False):
     """Reference CPU executor (oracle/_ref, built from the reference's own
     src/core + src/physics) on a bounded sample of the same workload and the
     same step window as the timed GPU region (steps warmup+1 .. warmup+K of
@@ -167,7 +181,8 @@ def cpu_baseline(args):
                "--cpu-first-world", str(batches * args.cpu_worlds),
                "--cpu-threads", str(threads), "--cubes", str(args.cubes),
                "--substeps", str(args.substeps), "--cpu-steps", str(args.cpu_steps),
-               "--settle", str(args.settle), "--warmup", str(args.warmup)] + (["--cpu-port"] if args.cpu_port else [])
+               "--settle", str(args.settle), "--warmup", str(args.warmup)] + \
+              (["--cpu-port"] if args.cpu_port else []) + (["--cpu-executor"] if executor else [])
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             raise RuntimeError(f"cpu baseline child failed: {r.stderr[-2000:]}")
@@ -338,9 +353,15 @@ def main():
             "mean_contacts_per_world": round(float(contacts.mean()), 1),
         }
 
-    cpu = None
+    cpu = cpu_exec = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
+        if not args.no_cpu_executor:
+            # the framework's own CPU back end (the reference's
+            # TaskGraphExecutor restated, libmadrona_cpu.so) on the same
+            # cores, worlds and step window, reported beside the reference
+            cpu_exec = cpu_baseline(args, executor=True)
+            cpu_exec["sample"] = "libmadrona_cpu.so: " + cpu_exec["sample"]
 
     if rank == 0:
         out = {
@@ -367,6 +388,7 @@ def main():
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "cpu_executor": cpu_exec,
             "error_flags": flags,
             "nodes": node_table,
             "startup": startup,
