@@ -166,16 +166,29 @@ __device__ __forceinline__ void groupArgMax(float &v, int32_t &k)
 // Transform one body's hull into the group's LDS and copy its edge topology.
 // Not inlined: the two transforms, interleaved into the SAT body by the
 // scheduler, set the kernel's register peak (156 -> ~110 VGPRs apart), and
-// the call only takes plain values and pointers.
+// the call only takes scalars and pointers (aggregates would be passed
+// byval through scratch).
 __device__ __noinline__ void stageHullRaw(const Vector3 *obj_verts,
                                           const geometry::Plane *obj_planes,
-                                          const EdgeQuad *obj_quads, const HullDev hd,
-                                          const Vector3 x, const Quat rot,
-                                          const Diag3x3 scale, Vector3 *v,
-                                          geometry::Plane *pl, EdgeQuad *q, int32_t lane)
+                                          const EdgeQuad *obj_quads, int32_t vert_off,
+                                          int32_t num_verts, int32_t face_off, int32_t num_faces,
+                                          int32_t edge_off, int32_t num_edges,
+                                          float xx, float xy, float xz, float qw, float qx,
+                                          float qy, float qz, float s0, float s1, float s2,
+                                          Vector3 *v, geometry::Plane *pl, EdgeQuad *q,
+                                          int32_t lane)
 {
-    const Mat3x3 unscaled_rot = Mat3x3::fromQuat(rot);
+    const Vector3 x { xx, xy, xz };
+    const Diag3x3 scale { s0, s1, s2 };
+    const Mat3x3 unscaled_rot = Mat3x3::fromQuat(Quat { qw, qx, qy, qz });
     const HullXform xf { unscaled_rot * scale, unscaled_rot * scale.inv(), x };
+    HullDev hd {};
+    hd.vertOffset = vert_off;
+    hd.numVerts = num_verts;
+    hd.faceOffset = face_off;
+    hd.numFaces = num_faces;
+    hd.edgeOffset = edge_off;
+    hd.numEdges = num_edges;
     for (int32_t i = lane; i < hd.numVerts; i += kGroup)
         v[i] = xf.vtx * obj_verts[hd.vertOffset + i] + xf.x;
     for (int32_t i = lane; i < hd.numFaces; i += kGroup) {
@@ -193,8 +206,11 @@ __device__ __forceinline__ Vector3 stageHull(const PhysArgs &P, int32_t w, const
 {
     const ObjDev &O = P.objs;
     const Vector3 x = bcol<Vector3>(B, Cols::Position, w, row);
-    stageHullRaw(O.vertices, O.planes, O.edgeQuads, hd, x, bcol<Quat>(B, Cols::Rotation, w, row),
-                 bcol<Diag3x3>(B, Cols::Scale, w, row), v, pl, q, lane);
+    const Quat r = bcol<Quat>(B, Cols::Rotation, w, row);
+    const Diag3x3 sc = bcol<Diag3x3>(B, Cols::Scale, w, row);
+    stageHullRaw(O.vertices, O.planes, O.edgeQuads, hd.vertOffset, hd.numVerts, hd.faceOffset,
+                 hd.numFaces, hd.edgeOffset, hd.numEdges, x.x, x.y, x.z, r.w, r.x, r.y, r.z,
+                 sc.d0, sc.d1, sc.d2, v, pl, q, lane);
     return x;
 }
 
@@ -348,7 +364,10 @@ __device__ void storeFaceManifold(Contact &c, Vector3 n, Vector3 *contacts, cons
     int32_t m;
     if (num <= 4) {
         m = num;
-        for (int32_t i = 0; i < num; i++) { cp[i] = contacts[i]; depth[i] = depths[i]; }
+#pragma unroll
+        for (int32_t i = 0; i < 4; i++) {          // static indices: cp stays in registers
+            if (i < num) { cp[i] = contacts[i]; depth[i] = depths[i]; }
+        }
     } else {
         m = 4;
         cp[0] = contacts[0];

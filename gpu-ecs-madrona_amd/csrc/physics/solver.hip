@@ -150,11 +150,14 @@ __device__ __forceinline__ bool boundedInput(const ContactIn &c)
     constexpr float kBound = 1e18f;
     bool ok = fabsf(c.n.x) <= kBound && fabsf(c.n.y) <= kBound &&
               fabsf(c.n.z) <= kBound;   // false for NaN
+    // fully unrolled with static indices (a `break` here kept the loop, and
+    // its dynamic c.pts[i] sent the whole ContactIn through scratch)
+#pragma unroll
     for (int i = 0; i < 4; i++) {
-        if (i >= c.np) break;
         const Vector4 p = c.pts[i];
-        ok = ok && fabsf(p.x) <= kBound && fabsf(p.y) <= kBound && fabsf(p.z) <= kBound &&
-             fabsf(p.w) <= kBound;
+        const bool in = fabsf(p.x) <= kBound && fabsf(p.y) <= kBound && fabsf(p.z) <= kBound &&
+                        fabsf(p.w) <= kBound;
+        ok = ok && (i >= c.np || in);
     }
     return ok;
 }
