@@ -454,9 +454,9 @@ __device__ __forceinline__ geometry::Segment shortestSegmentBetween(const geomet
 __device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
                                             const CandidateCollision &cand, SatWork &out)
 {
-    // Every load is issued unconditionally (rows clamped into range) so the
-    // AABB, ObjectID and type reads overlap instead of forming a chain of
-    // branches; the verdict is combined at the end.
+    // Both members' records (AABB, object, type: BodyBox, written by this
+    // substep's integration) are loaded unconditionally (rows clamped into
+    // range), one 32-byte load each; the verdict is combined at the end.
     const int32_t ia = bodyArchIndex(P, cand.a.archetype);
     const int32_t ib = bodyArchIndex(P, cand.b.archetype);
     const BodyArch &BA = P.body[ia];
@@ -464,12 +464,12 @@ __device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
     const bool rows_ok = (uint32_t)cand.a.row < (uint32_t)BA.capacity &&
                          (uint32_t)cand.b.row < (uint32_t)BB.capacity;
     const int32_t ra = rows_ok ? cand.a.row : 0, rb = rows_ok ? cand.b.row : 0;
-    const AABB *aabbs = P.bodyAABBs + (size_t)w * P.maxBodiesPerWorld;
-    const AABB a = aabbs[BA.slotBase + ra];
-    const AABB b = aabbs[BB.slotBase + rb];
-    const int32_t oa = bcol<ObjectID>(BA, Cols::ObjectID, w, ra).idx;
-    const int32_t ob = bcol<ObjectID>(BB, Cols::ObjectID, w, rb).idx;
-    const uint32_t ta = P.objs.types[oa], tb = P.objs.types[ob];
+    const BodyBox *boxes = P.bodyBoxes + (size_t)w * P.maxBodiesPerWorld;
+    const BodyBox A = boxes[BA.slotBase + ra];
+    const BodyBox Bx = boxes[BB.slotBase + rb];
+    const AABB a = A.box, b = Bx.box;
+    const int32_t oa = A.obj, ob = Bx.obj;
+    const uint32_t ta = A.type, tb = Bx.type;
     if (!rows_ok) {
         atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardWork << 8));
         return false;

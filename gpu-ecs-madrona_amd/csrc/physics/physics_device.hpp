@@ -208,8 +208,8 @@ __device__ __forceinline__ void integrateBody(const PhysArgs &P, const BodyArch 
         ps_vel.omega = omega;
     }
     const Diag3x3 scale = bcol<Diag3x3>(B, Cols::Scale, w, r);
-    P.bodyAABBs[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r] =
-        P.objs.aabbs[obj].applyTRS(x, q, scale);
+    P.bodyBoxes[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r] =
+        BodyBox { P.objs.aabbs[obj].applyTRS(x, q, scale), obj, P.objs.types[obj] };
 }
 
 // The narrowphase work lists are split into kNarrowBins bins (world w in

@@ -226,7 +226,7 @@ void PhysicsModule::buildArgs(void *stream)
     O.edgeQuads = upload(edgeQuads, stream);
     O.polygons = upload(polygons, stream);
 
-    P.bodyAABBs = alloc<AABB>((size_t)W * std::max(P.maxBodiesPerWorld, 1), stream);
+    P.bodyBoxes = alloc<BodyBox>((size_t)W * std::max(P.maxBodiesPerWorld, 1), stream);
     P.survInfo = alloc<uint32_t>((size_t)W * P.candCapacity, stream);
     P.survCount = alloc<int32_t>(W, stream);
     P.binCap = (W + kNarrowBins - 1) / kNarrowBins * P.candCapacity;

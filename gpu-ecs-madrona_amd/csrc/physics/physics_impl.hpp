@@ -69,6 +69,17 @@ struct BodyArch {
     char *cols[13];               // Entity + Cols::Position..LeafID
 };
 
+// What the narrowphase filter needs of a body, in one 32-byte record per body
+// slot: its world AABB of the substep and its object / primitive type (so a
+// candidate resolves with one load per member instead of a chain through
+// the ObjectID column and the object table).
+struct BodyBox {
+    math::AABB box;
+    int32_t obj;
+    uint32_t type;                // CollisionPrimitive::Type
+};
+static_assert(sizeof(BodyBox) == 32);
+
 // One narrowphase pair that passed the AABB recheck, fully resolved by the
 // filter kernel so the SAT kernel starts from a single load.
 struct SatWork {
@@ -126,7 +137,8 @@ struct PhysArgs {
     int32_t *leafOrder;           // [W][maxLeaves] leaves in BVH traversal (emission) order
 
 
-    math::AABB *bodyAABBs;        // [W][maxBodiesPerWorld] world AABB per body slot (substep)
+    struct BodyBox *bodyBoxes;    // [W][maxBodiesPerWorld] per body slot, written by the
+                                  // substep's integration: world AABB + object / type
     uint32_t *survInfo;           // [W][candCapacity] per survivor slot: the body slots of
                                   // its manifold's ref | alt << 16, kNoManifold without one
                                   // (the solver reads this instead of the Contact records)
