@@ -14,7 +14,12 @@ namespace madrona::phys {
 __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
-    if (blockIdx.x == 0 && blockIdx.y == 0) resetNarrowLists(P, threadIdx.x, blockDim.x);
+    // first substep: both list sets start empty (this substep's filter fills
+    // satWork, the solver's fused filter nextSatWork)
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+        resetNarrowLists(P.satWorkCount, threadIdx.x, blockDim.x);
+        resetNarrowLists(P.nextSatWorkCount, threadIdx.x, blockDim.x);
+    }
     const BodyArch &B = P.body[blockIdx.y];
     RowIdx ri = rowIndex(P, B);
     if (!ri.valid) return;
@@ -454,40 +459,7 @@ __device__ __forceinline__ geometry::Segment shortestSegmentBetween(const geomet
 __device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
                                             const CandidateCollision &cand, SatWork &out)
 {
-    // Both members' records (AABB, object, type: BodyBox, written by this
-    // substep's integration) are loaded unconditionally (rows clamped into
-    // range), one 32-byte load each; the verdict is combined at the end.
-    const int32_t ia = bodyArchIndex(P, cand.a.archetype);
-    const int32_t ib = bodyArchIndex(P, cand.b.archetype);
-    const BodyArch &BA = P.body[ia];
-    const BodyArch &BB = P.body[ib];
-    const bool rows_ok = (uint32_t)cand.a.row < (uint32_t)BA.capacity &&
-                         (uint32_t)cand.b.row < (uint32_t)BB.capacity;
-    const int32_t ra = rows_ok ? cand.a.row : 0, rb = rows_ok ? cand.b.row : 0;
-    const BodyBox *boxes = P.bodyBoxes + (size_t)w * P.maxBodiesPerWorld;
-    const BodyBox A = boxes[BA.slotBase + ra];
-    const BodyBox Bx = boxes[BB.slotBase + rb];
-    const AABB a = A.box, b = Bx.box;
-    const int32_t oa = A.obj, ob = Bx.obj;
-    const uint32_t ta = A.type, tb = Bx.type;
-    if (!rows_ok) {
-        atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardWork << 8));
-        return false;
-    }
-    if (!a.overlaps(b)) return false;
-    out.world = w;
-    out.test = ta | tb;
-    out.pad = 0;
-    if (ta > tb) {
-        out.a = cand.b; out.b = cand.a;
-        out.aArch = ib; out.bArch = ia;
-        out.aObj = ob; out.bObj = oa;
-    } else {
-        out.a = cand.a; out.b = cand.b;
-        out.aArch = ia; out.bArch = ib;
-        out.aObj = oa; out.bObj = ob;
-    }
-    return true;
+    return resolvePairFrom(P, w, cand, P.bodyBoxes + (size_t)w * P.maxBodiesPerWorld, out);
 }
 
 // buildFaceContactManifold (narrowphase.cpp:790-864) written straight into
@@ -777,6 +749,10 @@ __global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKern
     const int32_t group = threadIdx.x / kGroup;
     const int32_t lane = threadIdx.x % kGroup;
     const GroupLDS g = groupLDS(smem, group, P.objs);
+    // the set the solver of this substep will fill (read last by the
+    // previous substep's kernels); null when integrateKernel reset it
+    if (blockIdx.x == 0 && P.nextSatWorkCount)
+        resetNarrowLists(P.nextSatWorkCount, threadIdx.x, blockDim.x);
     __shared__ int32_t s_pre[kNarrowBins + 1];
     loadBinPrefix(P, 0, s_pre);
     const int32_t total = s_pre[kNarrowBins];

@@ -151,6 +151,21 @@ MW_PHYS_NODE(FindOverlappingNode,
     hipLaunchKernelGGL(findOverlapsKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
                        findOverlapsSharedBytes(P), stream, P);)
 
+// The narrowphase work lists come in two sets (PhysArgs::satWorkSet):
+// substep i's narrowphase reads set i % 2, and its filter for substep i + 1
+// (fused into substep i's solver) appends to set (i + 1) % 2.  The launch
+// copies of PhysArgs point satWork / satWorkCount at the set a kernel reads
+// and nextSatWork / nextSatWorkCount at the set it fills or resets.
+static PhysArgs substepArgs(const PhysArgs &P, int32_t i, bool reset_next)
+{
+    PhysArgs Q = P;
+    Q.satWork = P.satWorkSet[i & 1];
+    Q.satWorkCount = P.satWorkCountSet[i & 1];
+    Q.nextSatWork = P.satWorkSet[(i + 1) & 1];
+    Q.nextSatWorkCount = reset_next || i > 0 ? P.satWorkCountSet[(i + 1) & 1] : nullptr;
+    return Q;
+}
+
 // substepRigidBodies.  Substeps after the first are integrated by the
 // previous substep's solver kernel as it writes its bodies back (fused: the
 // bodies are already in its LDS); their nodes keep the graph shape.
@@ -169,44 +184,65 @@ struct SubstepRigidBodiesNode : PhysNodeBase {
     {
         const PhysArgs &P = self->mod->args;
         if (self->fused || P.numBodyArchs == 0) return;
-        hipLaunchKernelGGL(integrateKernel, rowGrid(P), dim3(256), 0, (hipStream_t)lc.stream, P);
+        // resets both list sets
+        hipLaunchKernelGGL(integrateKernel, rowGrid(P), dim3(256), 0, (hipStream_t)lc.stream,
+                           substepArgs(P, 0, true));
     }
 };
 
-// Narrowphase = AABB recheck + survivor numbering (block per world), a
-// per-world compaction into flat lists, a persistent SAT kernel (16-lane
-// group per hull-hull pair) and a persistent contact kernel (lane per
+// Narrowphase = AABB recheck + survivor numbering (the first substep's
+// filter kernel, block per world; later substeps' filters run in the
+// previous solver's tail), a persistent SAT kernel (16-lane group per
+// hull-hull pair), a plane kernel and a persistent contact kernel (lane per
 // manifold); see narrowphase.hip.  The node's launch configuration (blocks
-// per CU) sizes the two persistent grids; by default they are exactly the
-// resident blocks.  The solver turns
-// the per-survivor manifolds into the ordered contact list.
-MW_PHYS_NODE(NarrowphaseNode,
-    hipLaunchKernelGGL(narrowFilterKernel, dim3(P.numWorlds), dim3(kNarrowBlock), 0, stream, P);
-    hipLaunchKernelGGL(narrowSATKernel, dim3(lc.persistentGrid(P.satGrid)), dim3(kNarrowBlock),
-                       narrowphaseSharedBytes(P), stream, P);
-    hipLaunchKernelGGL(narrowPlaneKernel, dim3(lc.persistentGrid(P.planeGrid)),
-                       dim3(kContactBlock), 0, stream, P);
-    hipLaunchKernelGGL(narrowContactKernel, dim3(lc.persistentGrid(P.contactGrid)),
-                       dim3(kContactBlock), contactSharedBytes(P), stream, P);)
-
-// solvePositions + setVelocities + solveVelocities (one per-world kernel);
-// integrate_next: also substepRigidBodies of the next substep.
-struct SolverNode : PhysNodeBase {
-    int32_t integrateNext;
-    SolverNode(Context &ctx, bool integrate_next)
-        : PhysNodeBase(ctx), integrateNext(integrate_next ? 1 : 0) {}
+// per CU) sizes the persistent grids; by default they are exactly the
+// resident blocks.  The solver turns the per-survivor manifolds into the
+// ordered contact list.
+struct NarrowphaseNode : PhysNodeBase {
+    int32_t substep;
+    NarrowphaseNode(Context &ctx, int32_t i) : PhysNodeBase(ctx), substep(i) {}
     static TaskGraph::NodeID addToGraph(Context &ctx, TaskGraph::Builder &b,
                                         Span<const TaskGraph::NodeID> deps)
     {
-        return b.addDefaultNode<SolverNode>(deps, ctx, false);
+        return b.addDefaultNode<NarrowphaseNode>(deps, ctx, 0);
+    }
+    static const char *nodeName() { return "NarrowphaseNode"; }
+    static constexpr bool kNoTmpAlloc = true;
+    static void launch(NarrowphaseNode *self, LaunchCtx &lc)
+    {
+        const PhysArgs Q = substepArgs(self->mod->args, self->substep, false);
+        hipStream_t stream = (hipStream_t)lc.stream;
+        if (self->substep == 0)
+            hipLaunchKernelGGL(narrowFilterKernel, dim3(Q.numWorlds), dim3(kNarrowBlock), 0, stream, Q);
+        hipLaunchKernelGGL(narrowSATKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
+                           narrowphaseSharedBytes(Q), stream, Q);
+        hipLaunchKernelGGL(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),
+                           dim3(kContactBlock), 0, stream, Q);
+        hipLaunchKernelGGL(narrowContactKernel, dim3(lc.persistentGrid(Q.contactGrid)),
+                           dim3(kContactBlock), contactSharedBytes(Q), stream, Q);
+    }
+};
+
+// solvePositions + setVelocities + solveVelocities (one per-world kernel);
+// integrate_next: also substepRigidBodies and the narrowphase filter of the
+// next substep.
+struct SolverNode : PhysNodeBase {
+    int32_t substep;
+    int32_t integrateNext;
+    SolverNode(Context &ctx, int32_t i, bool integrate_next)
+        : PhysNodeBase(ctx), substep(i), integrateNext(integrate_next ? 1 : 0) {}
+    static TaskGraph::NodeID addToGraph(Context &ctx, TaskGraph::Builder &b,
+                                        Span<const TaskGraph::NodeID> deps)
+    {
+        return b.addDefaultNode<SolverNode>(deps, ctx, 0, false);
     }
     static const char *nodeName() { return "SolverNode"; }
     static constexpr bool kNoTmpAlloc = true;
     static void launch(SolverNode *self, LaunchCtx &lc)
     {
-        const PhysArgs &P = self->mod->args;
-        hipLaunchKernelGGL(solverKernel, dim3((P.numWorlds + kSolverWorlds - 1) / kSolverWorlds),
-                           dim3(kSolverThreads), solverSharedBytes(P), (hipStream_t)lc.stream, P,
+        const PhysArgs Q = substepArgs(self->mod->args, self->substep, true);
+        hipLaunchKernelGGL(solverKernel, dim3((Q.numWorlds + kSolverWorlds - 1) / kSolverWorlds),
+                           dim3(kSolverThreads), solverSharedBytes(Q), (hipStream_t)lc.stream, Q,
                            self->integrateNext);
     }
 };
@@ -235,12 +271,13 @@ TaskGraph::NodeID RigidBodyPhysicsSystem::setupSubstepTasks(TaskGraph::Builder &
         auto collect = builder.addToGraph<CollectConstraintsNode>({ cur });
         auto integrate = builder.addDefaultNode<SubstepRigidBodiesNode>({ cur }, builder.context(),
                                                                         i > 0);
-        auto narrow = builder.addToGraph<NarrowphaseNode>({ integrate });
+        auto narrow = builder.addDefaultNode<NarrowphaseNode>({ integrate }, builder.context(),
+                                                              (int32_t)i);
         auto reset1 = builder.addToGraph<ResetTmpAllocNode>({ narrow });
         // solvePositions + setVelocities + solveVelocities: one per-world
         // kernel (the three reference nodes are consecutive per world).
         auto solve = builder.addDefaultNode<SolverNode>({ reset1, collect }, builder.context(),
-                                                        i + 1 < num_substeps);
+                                                        (int32_t)i, i + 1 < num_substeps);
         cur = builder.addToGraph<ResetTmpAllocNode>({ solve });
     }
     auto clear = builder.addToGraph<ClearTmpNode<CandidateTemporary>>({ cur });

@@ -150,7 +150,7 @@ __global__ void solverKernel(PhysArgs P, int32_t integrate_next);
 // columns; the solver's fused tail passes the values it is about to write
 // back -- the same inputs, so the same bits), plus the world AABB the
 // narrowphase recheck uses (narrowphase.cpp:1590-1594), indexed by body slot.
-__device__ __forceinline__ void integrateBody(const PhysArgs &P, const BodyArch &B, int32_t w,
+__device__ __forceinline__ BodyBox integrateBody(const PhysArgs &P, const BodyArch &B, int32_t w,
                                               int32_t r, Vector3 x, Quat q, Vector3 v_in,
                                               Vector3 omega_in)
 {
@@ -208,8 +208,9 @@ __device__ __forceinline__ void integrateBody(const PhysArgs &P, const BodyArch 
         ps_vel.omega = omega;
     }
     const Diag3x3 scale = bcol<Diag3x3>(B, Cols::Scale, w, r);
-    P.bodyBoxes[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r] =
-        BodyBox { P.objs.aabbs[obj].applyTRS(x, q, scale), obj, P.objs.types[obj] };
+    const BodyBox bb { P.objs.aabbs[obj].applyTRS(x, q, scale), obj, P.objs.types[obj] };
+    P.bodyBoxes[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r] = bb;
+    return bb;
 }
 
 // The narrowphase work lists are split into kNarrowBins bins (world w in
@@ -223,12 +224,13 @@ __device__ __forceinline__ int32_t *binCounter(const PhysArgs &P, int32_t bin, i
     return P.satWorkCount + bin * kBinStride + which * (kBinStride / 2);
 }
 
-// Reset the work lists the next narrowphase filter appends to (their
-// readers, the previous substep's SAT and contact kernels, have finished).
-__device__ __forceinline__ void resetNarrowLists(const PhysArgs &P, int32_t tid, int32_t nthreads)
+// Reset the counters of a list set (`counts`: satWorkCount or
+// nextSatWorkCount) before a filter appends to it; its readers, an earlier
+// substep's SAT / plane / contact kernels, have finished.
+__device__ __forceinline__ void resetNarrowLists(int32_t *counts, int32_t tid, int32_t nthreads)
 {
     for (int32_t i = tid; i < 2 * kNarrowBins; i += nthreads)
-        *binCounter(P, i >> 1, i & 1) = 0;
+        counts[(i >> 1) * kBinStride + (i & 1) * (kBinStride / 2)] = 0;
 }
 
 // Exclusive prefix of the bins' counts of list `which` into s_pre[0..64]
@@ -261,6 +263,108 @@ __device__ __forceinline__ size_t binEntry(const PhysArgs &P, const int32_t *s_p
     const size_t k = (size_t)(i - s_pre[lo]);
     const size_t base = (size_t)lo * P.binCap;
     return which == 0 ? base + k : base + P.binCap - 1 - k;
+}
+
+// Narrowphase pair resolution and the per-wave world filter (shared by
+// narrowphase.hip and the solver kernel's fused tail).
+template <typename BoxPtr>
+__device__ __forceinline__ bool resolvePairFrom(const PhysArgs &P, int32_t w,
+                                                const CandidateCollision &cand, BoxPtr boxes,
+                                                SatWork &out)
+{
+    // Both members' records (AABB, object, type: BodyBox, written by this
+    // substep's integration) are loaded unconditionally (rows clamped into
+    // range), one 32-byte load each; the verdict is combined at the end.
+    // The archetype table is read with a uniform loop index (a lane-varying
+    // index into the kernel-argument table makes the compiler copy it to
+    // scratch in kernels that also pass PhysArgs by reference).
+    int32_t ia = 0, ib = 0, cap_a = 0, cap_b = 0, base_a = 0, base_b = 0;
+    for (int32_t i = P.numBodyArchs - 1; i >= 0; i--) {
+        const uint32_t arch = (uint32_t)P.body[i].archetype;
+        const int32_t cap = P.body[i].capacity, base = P.body[i].slotBase;
+        if (arch == cand.a.archetype || (i == 0 && ia == 0)) { ia = i; cap_a = cap; base_a = base; }
+        if (arch == cand.b.archetype || (i == 0 && ib == 0)) { ib = i; cap_b = cap; base_b = base; }
+    }
+    const bool rows_ok = (uint32_t)cand.a.row < (uint32_t)cap_a &&
+                         (uint32_t)cand.b.row < (uint32_t)cap_b;
+    const int32_t ra = rows_ok ? cand.a.row : 0, rb = rows_ok ? cand.b.row : 0;
+    const BodyBox A = boxes[base_a + ra];
+    const BodyBox Bx = boxes[base_b + rb];
+    const AABB a = A.box, b = Bx.box;
+    const int32_t oa = A.obj, ob = Bx.obj;
+    const uint32_t ta = A.type, tb = Bx.type;
+    if (!rows_ok) {
+        atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardWork << 8));
+        return false;
+    }
+    if (!a.overlaps(b)) return false;
+    out.world = w;
+    out.test = ta | tb;
+    out.pad = 0;
+    if (ta > tb) {
+        out.a = cand.b; out.b = cand.a;
+        out.aArch = ib; out.bArch = ia;
+        out.aObj = ob; out.bObj = oa;
+    } else {
+        out.a = cand.a; out.b = cand.b;
+        out.aArch = ia; out.bArch = ib;
+        out.aObj = oa; out.bObj = ob;
+    }
+    return true;
+}
+
+// The filter for one world on one wave (the solver kernel's tail, after it
+// integrated the world's next substep into its LDS box image): the same
+// survivors, slots and list entries as narrowFilterKernel, into the
+// nextSatWork set.  Two passes over the candidates (count, then write) so the
+// world reserves its bin entries with one atomic per list.
+__device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, const BodyBox *boxes,
+                                                  int32_t lane)
+{
+    const int32_t cap = P.candCapacity;
+    const int32_t num = min(P.numCands[w], cap);
+    const CandidateCollision *cands = P.cands + (size_t)w * cap;
+    uint32_t *info = P.survInfo + (size_t)w * cap;
+    const int32_t bin = w % kNarrowBins;
+    SatWork *list = P.nextSatWork + (size_t)bin * P.binCap;
+    SatWork *list_back = list + P.binCap - 1;              // plane entries grow down
+    int32_t *counts = P.nextSatWorkCount + bin * kBinStride;
+    constexpr uint32_t kHull = (uint32_t)CollisionPrimitive::Type::Hull;
+    constexpr uint32_t kHullPlane = kHull | (uint32_t)CollisionPrimitive::Type::Plane;
+    const uint64_t lt = (1ull << lane) - 1;
+    int32_t n_hh = 0, n_hp = 0;
+    for (int32_t base = 0; base < num; base += 64) {
+        const int32_t i = base + lane;
+        SatWork wk;
+        const bool keep = i < num && resolvePairFrom(P, w, cands[i], boxes, wk);
+        n_hh += __popcll(__ballot(keep && wk.test == kHull));
+        n_hp += __popcll(__ballot(keep && wk.test == kHullPlane));
+    }
+    int32_t b_hh = 0, b_hp = 0;
+    if (lane == 0) {
+        b_hh = n_hh > 0 ? atomicAdd(counts, n_hh) : 0;
+        b_hp = n_hp > 0 ? atomicAdd(counts + kBinStride / 2, n_hp) : 0;
+    }
+    b_hh = __shfl(b_hh, 0);
+    b_hp = __shfl(b_hp, 0);
+    int32_t S = 0;
+    for (int32_t base = 0; base < num; base += 64) {
+        const int32_t i = base + lane;
+        SatWork wk;
+        const bool keep = i < num && resolvePairFrom(P, w, cands[i], boxes, wk);
+        const bool hh = keep && wk.test == kHull, hp = keep && wk.test == kHullPlane;
+        const uint64_t mk = __ballot(keep), mh = __ballot(hh), mp = __ballot(hp);
+        if (keep) {
+            wk.slot = S + __popcll(mk & lt);
+            info[wk.slot] = kNoManifold;
+            if (hh) list[b_hh + __popcll(mh & lt)] = wk;
+            if (hp) *(list_back - (b_hp + __popcll(mp & lt))) = wk;
+        }
+        S += __popcll(mk);
+        b_hh += __popcll(mh);
+        b_hp += __popcll(mp);
+    }
+    if (lane == 0) P.survCount[w] = S;
 }
 
 size_t findOverlapsSharedBytes(const PhysArgs &P);

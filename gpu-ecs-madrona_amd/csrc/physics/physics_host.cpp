@@ -230,8 +230,14 @@ void PhysicsModule::buildArgs(void *stream)
     P.survInfo = alloc<uint32_t>((size_t)W * P.candCapacity, stream);
     P.survCount = alloc<int32_t>(W, stream);
     P.binCap = (W + kNarrowBins - 1) / kNarrowBins * P.candCapacity;
-    P.satWork = alloc<SatWork>((size_t)kNarrowBins * P.binCap, stream);
-    P.satWorkCount = alloc<int32_t>(kNarrowBins * kBinStride, stream);
+    for (int32_t set = 0; set < 2; set++) {
+        P.satWorkSet[set] = alloc<SatWork>((size_t)kNarrowBins * P.binCap, stream);
+        P.satWorkCountSet[set] = alloc<int32_t>(kNarrowBins * kBinStride, stream);
+    }
+    P.satWork = P.satWorkSet[0];
+    P.satWorkCount = P.satWorkCountSet[0];
+    P.nextSatWork = P.satWorkSet[1];
+    P.nextSatWorkCount = P.satWorkCountSet[1];
     P.hhJobs = alloc<ContactJob>((size_t)W * P.candCapacity, stream);
     P.candContacts = alloc<Contact>((size_t)W * P.candCapacity, stream);
     P.maxContacts = maxContacts;

@@ -151,6 +151,14 @@ struct PhysArgs {
                                   // filter appends, the integrate kernel / fused solver
                                   // tail resets
     int32_t binCap;               // entries per bin (worlds per bin x candCapacity)
+    // Two list sets: substep s reads set s % 2 while its solver kernel's
+    // tail (integrating substep s + 1) filters into set (s + 1) % 2.  The
+    // node launches point satWork / satWorkCount at the set a kernel reads
+    // and nextSatWork / nextSatWorkCount at the set it fills or resets.
+    struct SatWork *satWorkSet[2];
+    int32_t *satWorkCountSet[2];
+    struct SatWork *nextSatWork;
+    int32_t *nextSatWorkCount;
     ContactJob *hhJobs;           // [W * candCapacity] SAT verdict per satWork entry
     int32_t contactGrid;          // persistent contact-kernel grid (blocks)
     int32_t clipCap;              // clip polygon capacity (2 x largest face)

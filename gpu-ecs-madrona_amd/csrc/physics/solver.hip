@@ -909,10 +909,18 @@ __device__ __forceinline__ void setWorldVelocities(const PhysArgs &P, int32_t w,
 }
 
 // Write the solved bodies back; integrate_next: then run the next
-// substep's substepRigidBodies on them (integrateBody writes the pose).
+// substep's substepRigidBodies on them (integrateBody writes the pose) and
+// the next substep's narrowphase filter for the world (filterWorldOnWave,
+// into the nextSatWork list set) from the bodies' new boxes, which are kept
+// in the world's LDS image: box slot s (32 B) overwrites the SMut bytes of
+// slots <= s only, and slots are processed in increasing order with every
+// lane's SMut reads of a round issued before its box writes, so no SMut
+// entry is overwritten before it is read.
 __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, SolverLDS &L,
                                                  int32_t lane, bool integrate_next)
 {
+    static_assert(sizeof(BodyBox) <= sizeof(SMut), "box image aliases the body image");
+    BodyBox *boxes = (BodyBox *)L.bodies;
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
@@ -924,7 +932,9 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
             stV3(&vel.linear, v);
             stV3(&vel.angular, om);
             if (integrate_next) {
-                integrateBody(P, B, w, r, x, q, v, om);
+                const BodyBox bb = integrateBody(P, B, w, r, x, q, v, om);
+                waveSync();                               // the round's SMut reads first
+                boxes[B.slotBase + r] = bb;
             } else {
                 stV3(&bcol<Vector3>(B, Cols::Position, w, r), x);
                 stQ(&bcol<Quat>(B, Cols::Rotation, w, r), q);
@@ -932,6 +942,10 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
         }
     }
     if (lane == 0) P.solver[w].numContacts = 0;           // physics.cpp:1007
+    if (integrate_next) {
+        waveSync();
+        filterWorldOnWave(P, w, boxes, lane);
+    }
 }
 
 #if defined(MW_SOLVER_PROFILE)
@@ -1118,7 +1132,6 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     if (!fits) {
         // some world of the block overflows the LDS records: every world
         // of the block solves on its own wave with global records
-        if (integrate_next && blockIdx.x == 0) resetNarrowLists(P, threadIdx.x, kSolverThreads);
         if (live) {
             solveWorldGlobal(P, w, L, J, lane);
             writeWorldBodies(P, w, L, lane, integrate_next != 0);
@@ -1205,7 +1218,6 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     }
 
     MW_SOLVER_MARK(5);
-    if (integrate_next && blockIdx.x == 0) resetNarrowLists(P, threadIdx.x, kSolverThreads);
     if (live) writeWorldBodies(P, w, L, lane, integrate_next != 0);
     __syncthreads();
     MW_SOLVER_MARK(6);
