@@ -241,6 +241,7 @@ struct SolverNode : PhysNodeBase {
     static void launch(SolverNode *self, LaunchCtx &lc)
     {
         const PhysArgs Q = substepArgs(self->mod->args, self->substep, true);
+        hipLaunchKernelGGL(solverOrderKernel, dim3(1), dim3(kOrderThreads), 0, (hipStream_t)lc.stream, Q);
         hipLaunchKernelGGL(solverKernel, dim3((Q.numWorlds + kSolverWorlds - 1) / kSolverWorlds),
                            dim3(kSolverThreads), solverSharedBytes(Q), (hipStream_t)lc.stream, Q,
                            self->integrateNext);

@@ -143,6 +143,8 @@ struct PhysArgs {
                                   // its manifold's ref | alt << 16, kNoManifold without one
                                   // (the solver reads this instead of the Contact records)
     int32_t *survCount;           // [W] survivors per world
+    int32_t *solverOrder;         // [W] worlds by descending survivor count: the solver
+                                  // grid's world order (heaviest blocks dispatched first)
     struct SatWork *satWork;      // [kNarrowBins][binCap] SAT / plane work lists: bin
                                   // w % kNarrowBins holds world w's hull-hull survivors
                                   // from its front and hull-plane survivors from its back

@@ -1086,6 +1086,48 @@ __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, S
 #define MW_SOLVER_MARK(i) ((void)0)
 #endif
 
+// Solver world order.  Block durations follow the worlds' contact counts
+// (p50 / p99 ~ 1 : 3), so with the grid in world-index order the heavy
+// blocks that happen to be dispatched last set the launch's tail.  One
+// block counting-sorts the worlds by descending survivor count (this
+// substep's filter wrote survCount) into solverOrder; the solver grid takes
+// its worlds in that order (longest first), and a block's two worlds have
+// similar work.  Which block or partner solves a world does not change its
+// bits: a world's items only touch its own bodies.
+constexpr int32_t kOrderBuckets = kOrderThreads;
+
+__device__ __forceinline__ int32_t orderBucket(const PhysArgs &P, int32_t w)
+{
+    const int32_t n = P.survCount[w];
+    return kOrderBuckets - 1 - min(max(n, 0), kOrderBuckets - 1);
+}
+
+__global__ void __launch_bounds__(kOrderThreads) solverOrderKernel(PhysArgs P)
+{
+    __shared__ int32_t s_off[kOrderBuckets];
+    __shared__ int32_t s_wave[kOrderThreads / 64];
+    const int32_t t = threadIdx.x, W = P.numWorlds;
+    s_off[t] = 0;
+    __syncthreads();
+    for (int32_t w = t; w < W; w += kOrderThreads) atomicAdd(&s_off[orderBucket(P, w)], 1);
+    __syncthreads();
+    const int32_t v = s_off[t];
+    int32_t x = v;
+#pragma unroll
+    for (int32_t o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if ((t & 63) >= o) x += y;
+    }
+    if ((t & 63) == 63) s_wave[t >> 6] = x;
+    __syncthreads();
+    int32_t before = 0;
+    for (int32_t i = 0; i < (t >> 6); i++) before += s_wave[i];
+    s_off[t] = before + x - v;
+    __syncthreads();
+    for (int32_t w = t; w < W; w += kOrderThreads)
+        P.solverOrder[atomicAdd(&s_off[orderBucket(P, w)], 1)] = w;
+}
+
 // Occupancy: latency bound (dependent LDS / column reads per contact), so
 // residency matters more than packed math; built without SLP vectorisation
 // (Makefile) it fits 3 waves per SIMD without spills.
@@ -1107,8 +1149,11 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     const int32_t nb = P.maxBodiesPerWorld;
     const int32_t wi = threadIdx.x / kSolverBlock;
     const int32_t lane = threadIdx.x % kSolverBlock;
-    const int32_t w = blockIdx.x * kSolverWorlds + wi;
-    const bool live = w < P.numWorlds;
+    __shared__ int32_t s_worlds[kSolverWorlds];
+    const int32_t wslot = blockIdx.x * kSolverWorlds + wi;
+    const bool live = wslot < P.numWorlds;
+    const int32_t w = live ? P.solverOrder[wslot] : 0;
+    if (lane == 0) s_worlds[wi] = w;
     SolverLDS L = solverWorldLDS(smem, nb, wi);
     SolverBlockLDS BL = solverBlockLDS(smem, nb);
 
@@ -1192,7 +1237,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
         for (int32_t t = beg + threadIdx.x; t < end; t += kSolverThreads) {
             const uint32_t it = BL.items[t];
             const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xfffu);
-            const int32_t ww = blockIdx.x * kSolverWorlds + iw;
+            const int32_t ww = s_worlds[iw];
             SolverLDS LW = solverWorldLDS(smem, nb, iw);
             solveItemPositions(P, ww, LW, LW.recs[k], (int32_t)((it >> 12) & 0xfu));
         }
@@ -1210,7 +1255,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
         for (int32_t t = beg + threadIdx.x; t < end; t += kSolverThreads) {
             const uint32_t it = BL.items[t];
             const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xfffu);
-            const int32_t ww = blockIdx.x * kSolverWorlds + iw;
+            const int32_t ww = s_worlds[iw];
             SolverLDS LW = solverWorldLDS(smem, nb, iw);
             solveItemVelocities(P, ww, LW, LW.recs[k], (int32_t)((it >> 12) & 0xfu));
         }
