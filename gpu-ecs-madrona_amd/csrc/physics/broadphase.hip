@@ -645,6 +645,7 @@ struct alignas(16) OrderedLeaf {
     int32_t id;                   // entity id (the e.id < other.id rule)
     int32_t isStatic;
     Loc loc;
+    uint32_t slot;                // body slot | arch index << 16 | bad-row flag << 24
 };
 static_assert(sizeof(OrderedLeaf) == 48);
 
@@ -708,7 +709,8 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
         const int sub = (int)(lp & 3);
         const Entity e = P.leafEntities[(size_t)w * P.maxLeaves + leaf];
         const Loc loc = entityLoc(P, w, e);
-        const BodyArch &OB = P.body[bodyArchIndex(P, loc.archetype)];
+        const int32_t oa = bodyArchIndex(P, loc.archetype);
+        const BodyArch &OB = P.body[oa];
         const int32_t row = guardIndex(loc.row, OB.capacity, flags, kGuardLeaf);
         OrderedLeaf ol;
         ol.minX = n.minX[sub]; ol.minY = n.minY[sub]; ol.minZ = n.minZ[sub];
@@ -717,6 +719,8 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
         ol.isStatic =
             bcol<ResponseType>(OB, Cols::ResponseType, w, row) == ResponseType::Static ? 1 : 0;
         ol.loc = loc;
+        ol.slot = (uint32_t)(OB.slotBase + row) | (uint32_t)oa << 16 |
+                  ((uint32_t)loc.row < (uint32_t)OB.capacity ? 0u : 1u << 24);
         leaves[k] = ol;
         rank_of[leaf] = k;
     }
@@ -757,20 +761,28 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
             int32_t total;
             const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
             CandidateCollision *out = P.cands + (size_t)w * P.candCapacity;
+            uint64_t *out_slots = P.candSlots + (size_t)w * P.candCapacity;
             if (cnt > 0) {
                 const Loc a_loc = me.loc;
+                const uint64_t a_slot = me.slot;
                 if (cnt <= kOverlapBuf) {
                     for (int32_t i = 0; i < cnt; i++) {
                         const int32_t slot = base + off + i;
-                        if (slot < P.candCapacity) out[slot] = CandidateCollision { a_loc, leaves[buf[i]].loc };
+                        const OrderedLeaf &o = leaves[buf[i]];
+                        if (slot < P.candCapacity) {
+                            out[slot] = CandidateCollision { a_loc, o.loc };
+                            out_slots[slot] = a_slot | (uint64_t)o.slot << 32;
+                        }
                     }
                 } else {
                     int32_t i = 0;
                     for (int32_t k = 0; k < nleaves; k++) {
                         if (leafHit(leaves, k, q, e_id, a_static)) {
                             const int32_t slot = base + off + i++;
-                            if (slot < P.candCapacity)
+                            if (slot < P.candCapacity) {
                                 out[slot] = CandidateCollision { a_loc, leaves[k].loc };
+                                out_slots[slot] = a_slot | (uint64_t)leaves[k].slot << 32;
+                            }
                         }
                     }
                 }

@@ -453,15 +453,6 @@ __device__ __forceinline__ geometry::Segment shortestSegmentBetween(const geomet
     return { s1.p1 + s * v1, s2.p1 + t * v2 };
 }
 
-// World-space AABB recheck (narrowphase.cpp:1589-1603) against the per-body
-// AABBs the integrate kernel cached (same applyTRS, same inputs), then the
-// type ordering of runNarrowphase (:1574-1580) for pairs that survive.
-__device__ __forceinline__ bool resolvePair(const PhysArgs &P, int32_t w,
-                                            const CandidateCollision &cand, SatWork &out)
-{
-    return resolvePairFrom(P, w, cand, P.bodyBoxes + (size_t)w * P.maxBodiesPerWorld, out);
-}
-
 // buildFaceContactManifold (narrowphase.cpp:790-864) written straight into
 // the contact slot from up to four chosen points (storeFaceManifold's tail).
 __device__ __forceinline__ void writeFaceManifold(Contact &c, Vector3 n, const Vector3 *cp,
@@ -615,6 +606,8 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
     const int32_t cap = P.candCapacity;
     const int32_t num = min(P.numCands[w], cap);
     const CandidateCollision *cands = P.cands + (size_t)w * cap;
+    const uint64_t *slots = P.candSlots + (size_t)w * cap;
+    const BodyBox *boxes = P.bodyBoxes + (size_t)w * P.maxBodiesPerWorld;
     uint32_t *info = P.survInfo + (size_t)w * cap;
     const int32_t bin = w % kNarrowBins;
     SatWork *list = P.satWork + (size_t)bin * P.binCap;
@@ -631,7 +624,10 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
 #pragma unroll
         for (int32_t j = 0; j < kFilterPer; j++) {
             const int32_t ci = first + j;
-            keep[j] = ci < num && resolvePair(P, w, cands[ci], wk[j]);
+            BodyBox A, B;
+            const uint64_t cs = ci < num ? slots[ci] : 0;
+            keep[j] = ci < num && candOverlaps(P, w, cs, boxes, A, B);
+            if (keep[j]) wk[j] = candWork(cands[ci], cs, A, B, w);
             packed += keep[j] ? 1 : 0;
             packed += keep[j] && wk[j].test == kHull ? 1 << 10 : 0;
             packed += keep[j] && wk[j].test == kHullPlane ? 1 << 20 : 0;

@@ -194,7 +194,8 @@ struct SubstepRigidBodiesNode : PhysNodeBase {
 // filter kernel, block per world; later substeps' filters run in the
 // previous solver's tail), a persistent SAT kernel (16-lane group per
 // hull-hull pair), a plane kernel and a persistent contact kernel (lane per
-// manifold); see narrowphase.hip.  The node's launch configuration (blocks
+// manifold); see narrowphase.hip.  It also sorts the worlds for the solver
+// grid (solverOrderKernel, solver.hip).  The node's launch configuration (blocks
 // per CU) sizes the persistent grids; by default they are exactly the
 // resident blocks.  The solver turns the per-survivor manifolds into the
 // ordered contact list.
@@ -214,6 +215,8 @@ struct NarrowphaseNode : PhysNodeBase {
         hipStream_t stream = (hipStream_t)lc.stream;
         if (self->substep == 0)
             hipLaunchKernelGGL(narrowFilterKernel, dim3(Q.numWorlds), dim3(kNarrowBlock), 0, stream, Q);
+        // the solver's world order from this substep's survivor counts
+        hipLaunchKernelGGL(solverOrderKernel, dim3(1), dim3(kOrderThreads), 0, stream, Q);
         hipLaunchKernelGGL(narrowSATKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
                            narrowphaseSharedBytes(Q), stream, Q);
         hipLaunchKernelGGL(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),
@@ -241,7 +244,6 @@ struct SolverNode : PhysNodeBase {
     static void launch(SolverNode *self, LaunchCtx &lc)
     {
         const PhysArgs Q = substepArgs(self->mod->args, self->substep, true);
-        hipLaunchKernelGGL(solverOrderKernel, dim3(1), dim3(kOrderThreads), 0, (hipStream_t)lc.stream, Q);
         hipLaunchKernelGGL(solverKernel, dim3((Q.numWorlds + kSolverWorlds - 1) / kSolverWorlds),
                            dim3(kSolverThreads), solverSharedBytes(Q), (hipStream_t)lc.stream, Q,
                            self->integrateNext);

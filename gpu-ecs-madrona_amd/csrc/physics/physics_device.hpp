@@ -269,63 +269,60 @@ __device__ __forceinline__ size_t binEntry(const PhysArgs &P, const int32_t *s_p
 
 // Narrowphase pair resolution and the per-wave world filter (shared by
 // narrowphase.hip and the solver kernel's fused tail).
+//
+// The AABB recheck (narrowphase.cpp:1589-1603) of a candidate from its packed body slots (candSlots,
+// written by findOverlaps beside the candidate): both members' records
+// (AABB, object, type: BodyBox, written by this substep's integration), one
+// 32-byte load each.  A candidate whose row failed findOverlaps' guard is
+// dropped and flags the world.
 template <typename BoxPtr>
-__device__ __forceinline__ bool resolvePairFrom(const PhysArgs &P, int32_t w,
-                                                const CandidateCollision &cand, BoxPtr boxes,
-                                                SatWork &out)
+__device__ __forceinline__ bool candOverlaps(const PhysArgs &P, int32_t w, uint64_t cs, BoxPtr boxes,
+                                             BodyBox &A, BodyBox &B)
 {
-    // Both members' records (AABB, object, type: BodyBox, written by this
-    // substep's integration) are loaded unconditionally (rows clamped into
-    // range), one 32-byte load each; the verdict is combined at the end.
-    // The archetype table is read with a uniform loop index (a lane-varying
-    // index into the kernel-argument table makes the compiler copy it to
-    // scratch in kernels that also pass PhysArgs by reference).
-    int32_t ia = 0, ib = 0, cap_a = 0, cap_b = 0, base_a = 0, base_b = 0;
-    for (int32_t i = P.numBodyArchs - 1; i >= 0; i--) {
-        const uint32_t arch = (uint32_t)P.body[i].archetype;
-        const int32_t cap = P.body[i].capacity, base = P.body[i].slotBase;
-        if (arch == cand.a.archetype || (i == 0 && ia == 0)) { ia = i; cap_a = cap; base_a = base; }
-        if (arch == cand.b.archetype || (i == 0 && ib == 0)) { ib = i; cap_b = cap; base_b = base; }
-    }
-    const bool rows_ok = (uint32_t)cand.a.row < (uint32_t)cap_a &&
-                         (uint32_t)cand.b.row < (uint32_t)cap_b;
-    const int32_t ra = rows_ok ? cand.a.row : 0, rb = rows_ok ? cand.b.row : 0;
-    const BodyBox A = boxes[base_a + ra];
-    const BodyBox Bx = boxes[base_b + rb];
-    const AABB a = A.box, b = Bx.box;
-    const int32_t oa = A.obj, ob = Bx.obj;
-    const uint32_t ta = A.type, tb = Bx.type;
-    if (!rows_ok) {
+    A = boxes[(uint32_t)cs & 0xffffu];
+    B = boxes[(uint32_t)(cs >> 32) & 0xffffu];
+    if ((cs & (1ull << 24 | 1ull << 56)) != 0) {
         atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardWork << 8));
         return false;
     }
-    if (!a.overlaps(b)) return false;
+    return A.box.overlaps(B.box);
+}
+
+// A surviving candidate's work entry, in runNarrowphase's type order
+// (narrowphase.cpp:1574-1580).
+__device__ __forceinline__ SatWork candWork(const CandidateCollision &cand, uint64_t cs,
+                                            const BodyBox &A, const BodyBox &B, int32_t w)
+{
+    const int32_t ia = (int32_t)((cs >> 16) & 0xffu), ib = (int32_t)((cs >> 48) & 0xffu);
+    SatWork out;
     out.world = w;
-    out.test = ta | tb;
+    out.test = A.type | B.type;
     out.pad = 0;
-    if (ta > tb) {
+    if (A.type > B.type) {
         out.a = cand.b; out.b = cand.a;
         out.aArch = ib; out.bArch = ia;
-        out.aObj = ob; out.bObj = oa;
+        out.aObj = B.obj; out.bObj = A.obj;
     } else {
         out.a = cand.a; out.b = cand.b;
         out.aArch = ia; out.bArch = ib;
-        out.aObj = oa; out.bObj = ob;
+        out.aObj = A.obj; out.bObj = B.obj;
     }
-    return true;
+    return out;
 }
 
 // The filter for one world on one wave (the solver kernel's tail, after it
 // integrated the world's next substep into its LDS box image): the same
 // survivors, slots and list entries as narrowFilterKernel, into the
-// nextSatWork set.  Two passes over the candidates (count, then write) so the
-// world reserves its bin entries with one atomic per list.
+// nextSatWork set.  Two passes over the candidates' packed slots (count,
+// then write) so the world reserves its bin entries with one atomic per
+// list; the second pass loads a candidate's Locs only if it survives.
 __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, const BodyBox *boxes,
                                                   int32_t lane)
 {
     const int32_t cap = P.candCapacity;
     const int32_t num = min(P.numCands[w], cap);
     const CandidateCollision *cands = P.cands + (size_t)w * cap;
+    const uint64_t *slots = P.candSlots + (size_t)w * cap;
     uint32_t *info = P.survInfo + (size_t)w * cap;
     const int32_t bin = w % kNarrowBins;
     SatWork *list = P.nextSatWork + (size_t)bin * P.binCap;
@@ -337,10 +334,11 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
     int32_t n_hh = 0, n_hp = 0;
     for (int32_t base = 0; base < num; base += 64) {
         const int32_t i = base + lane;
-        SatWork wk;
-        const bool keep = i < num && resolvePairFrom(P, w, cands[i], boxes, wk);
-        n_hh += __popcll(__ballot(keep && wk.test == kHull));
-        n_hp += __popcll(__ballot(keep && wk.test == kHullPlane));
+        BodyBox A, B;
+        const bool keep = i < num && candOverlaps(P, w, slots[i], boxes, A, B);
+        const uint32_t t = A.type | B.type;
+        n_hh += __popcll(__ballot(keep && t == kHull));
+        n_hp += __popcll(__ballot(keep && t == kHullPlane));
     }
     int32_t b_hh = 0, b_hp = 0;
     if (lane == 0) {
@@ -352,11 +350,14 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
     int32_t S = 0;
     for (int32_t base = 0; base < num; base += 64) {
         const int32_t i = base + lane;
-        SatWork wk;
-        const bool keep = i < num && resolvePairFrom(P, w, cands[i], boxes, wk);
-        const bool hh = keep && wk.test == kHull, hp = keep && wk.test == kHullPlane;
+        BodyBox A, B;
+        const uint64_t cs = i < num ? slots[i] : 0;
+        const bool keep = i < num && candOverlaps(P, w, cs, boxes, A, B);
+        const uint32_t t = A.type | B.type;
+        const bool hh = keep && t == kHull, hp = keep && t == kHullPlane;
         const uint64_t mk = __ballot(keep), mh = __ballot(hh), mp = __ballot(hp);
         if (keep) {
+            SatWork wk = candWork(cands[i], cs, A, B, w);
             wk.slot = S + __popcll(mk & lt);
             info[wk.slot] = kNoManifold;
             if (hh) list[b_hh + __popcll(mh & lt)] = wk;

@@ -228,6 +228,7 @@ void PhysicsModule::buildArgs(void *stream)
 
     P.bodyBoxes = alloc<BodyBox>((size_t)W * std::max(P.maxBodiesPerWorld, 1), stream);
     P.survInfo = alloc<uint32_t>((size_t)W * P.candCapacity, stream);
+    P.candSlots = alloc<uint64_t>((size_t)W * P.candCapacity, stream);
     P.survCount = alloc<int32_t>(W, stream);
     P.solverOrder = alloc<int32_t>(W, stream);
     P.binCap = (W + kNarrowBins - 1) / kNarrowBins * P.candCapacity;

@@ -142,6 +142,9 @@ struct PhysArgs {
     uint32_t *survInfo;           // [W][candCapacity] per survivor slot: the body slots of
                                   // its manifold's ref | alt << 16, kNoManifold without one
                                   // (the solver reads this instead of the Contact records)
+    uint64_t *candSlots;          // [W][candCapacity] per candidate (findOverlaps): body slot
+                                  // of a | arch index of a << 16 | bad-row flag << 24 |
+                                  // body slot of b << 32 | arch index of b << 48
     int32_t *survCount;           // [W] survivors per world
     int32_t *solverOrder;         // [W] worlds by descending survivor count: the solver
                                   // grid's world order (heaviest blocks dispatched first)
