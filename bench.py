@@ -93,6 +93,9 @@ def parse():
     p.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--cpu-first-world", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--no-roofline", action="store_true")
+    p.add_argument("--timed-every", type=int, default=10,
+                   help="time the dominant kernel's launches in every N-th timed step (the "
+                        "graph is split at that node only in those steps)")
     p.add_argument("--no-handoff", action="store_true")
     return p.parse_args()
 
@@ -304,7 +307,7 @@ def main():
                                     "ms_per_step": round(ms * launches[name], 4)}
         dom = max((n for n in node_table if n in BYTES),
                   key=lambda n: node_table[n]["ms_per_step"])
-        sim.set_timed_node(dom)
+        sim.set_timed_node(dom, every=args.timed_every)
 
     for _ in range(args.warmup):
         step()
@@ -346,7 +349,11 @@ def main():
             "traffic": pmc_traffic(dom),
             "bytes_per_launch": int(nbytes), "ms_per_launch": round(ms, 4),
             "timed_launches": int(ev_n1 - ev_n0),
-            "timing": "HIP events on the executor stream around every launch of the kernel during the timed steps (step graph split at that node)",
+            "timing": ("HIP events on the executor stream around every launch of the kernel in "
+                       + ("every timed step" if args.timed_every <= 1 else
+                          f"every {args.timed_every}th timed step (the first of each run of "
+                          f"{args.timed_every}; the step graph is split at that node in those "
+                          "steps only, the others replay the unsplit graph)")),
             "step_algorithmic_bytes": int(step_bytes),
             "step_achieved_gbs": round(step_bytes / (elapsed / args.steps) / 1e9, 2),
             "mean_candidates_per_world": round(float(cands.mean()), 1),

@@ -589,8 +589,14 @@ int32_t mw_parse_exec_config_file(const char *json, int32_t *nodes, int32_t *blo
 
 int32_t mw_set_timed_node(mw_exec *exec, const char *node_name)
 {
+    return mw_set_timed_node_every(exec, node_name, 1);
+}
+
+int32_t mw_set_timed_node_every(mw_exec *exec, const char *node_name, int32_t every)
+{
     MW_TRY({
-        exec->exec->setTimedNode(node_name);
+        if (every < 1) throw std::invalid_argument("mw_set_timed_node_every: every must be >= 1");
+        exec->exec->setTimedNode(node_name, every);
         return 0;
     }, -1)
 }

@@ -435,8 +435,9 @@ double Executor::timeNode(const char *name, int32_t num_steps)
     return l > 0 ? (double)ns * 1e-6 / (double)l : -1.0;
 }
 
-void Executor::setTimedNode(const char *name)
+void Executor::setTimedNode(const char *name, int32_t every)
 {
+    (void)every;   // host timing costs no graph split: every step is timed
     impl_->timedName = name ? name : "";
     impl_->timedNs = 0;
     impl_->timedLaunches = 0;

@@ -492,6 +492,11 @@ struct Executor::Impl {
         int32_t timedNode = -1;   // node launched (timed) after this segment
     };
     std::vector<Segment> segs;
+    // Sampled live timing (timedEvery > 1): the unsplit step graph, replayed
+    // on the steps that are not timed.
+    std::vector<Segment> plainSegs;
+    int32_t timedEvery = 1;
+    int64_t stepIndex = 0;
     std::vector<ExportBuf> exports;
     int64_t *hostRowsTotal = nullptr;
 
@@ -556,9 +561,11 @@ Executor::~Executor()
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
-    for (auto &sg : impl_->segs) {
-        if (sg.exec) (void)hipGraphExecDestroy(sg.exec);
-        if (sg.graph) (void)hipGraphDestroy(sg.graph);
+    for (auto *v : { &impl_->segs, &impl_->plainSegs }) {
+        for (auto &sg : *v) {
+            if (sg.exec) (void)hipGraphExecDestroy(sg.exec);
+            if (sg.graph) (void)hipGraphDestroy(sg.graph);
+        }
     }
     if (impl_->trace) {
         (void)hipStreamSynchronize(impl_->stream);
@@ -770,13 +777,32 @@ static void launchStep(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
     traceStepEnd(I);
 }
 
-static void captureGraph(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
+static void destroySegments(std::vector<Executor::Impl::Segment> &segs)
 {
-    for (auto &sg : I.segs) {
+    for (auto &sg : segs) {
         if (sg.exec) MW_HIP_CHECK(hipGraphExecDestroy(sg.exec));
         if (sg.graph) MW_HIP_CHECK(hipGraphDestroy(sg.graph));
     }
-    I.segs.clear();
+    segs.clear();
+}
+
+static void captureSegments(Executor::Impl &I, LaunchCtx &lc, const StateView &dv, bool split);
+
+static void captureGraph(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
+{
+    destroySegments(I.segs);
+    destroySegments(I.plainSegs);
+    captureSegments(I, lc, dv, true);
+    if (I.timedPerStep > 0 && I.timedEvery > 1) {
+        std::swap(I.segs, I.plainSegs);
+        captureSegments(I, lc, dv, false);
+        std::swap(I.segs, I.plainSegs);
+    }
+}
+
+// The step graph into I.segs; split: at every launch of the timed kind.
+static void captureSegments(Executor::Impl &I, LaunchCtx &lc, const StateView &dv, bool split)
+{
     const int32_t n = I.graph.numNodes();
     // Live node timing splits the step graph at each launch of the timed
     // kind, which runs on the stream between segments bracketed by events:
@@ -787,7 +813,7 @@ static void captureGraph(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
     int32_t start = 0;
     for (int32_t i = 0; i <= n; i++) {
         const bool last = i == n;
-        if (!last && !isTimed(I, i)) continue;
+        if (!last && !(split && isTimed(I, i))) continue;
         Executor::Impl::Segment sg;
         sg.timedNode = last ? -1 : i;
         if (i > start || last || (start == 0 && I.trace)) {
@@ -920,9 +946,13 @@ void Executor::runAsync()
     Impl &I = *impl_;
     const StateView &dv = I.mgr->deviceViewHost();
     LaunchCtx lc = makeLaunchCtx(I, this);
+    // sampled timing: the first step of every run of timedEvery is the
+    // split, timed one
+    const bool sampled = I.plainSegs.empty() || I.stepIndex % I.timedEvery == 0;
+    I.stepIndex++;
     if (!I.segs.empty()) {
         int32_t ev = 0;
-        for (auto &sg : I.segs) {
+        for (auto &sg : sampled ? I.segs : I.plainSegs) {
             if (sg.exec) MW_HIP_CHECK(hipGraphLaunch(sg.exec, I.stream));
             if (sg.timedNode >= 0) {
                 MW_HIP_CHECK(hipEventRecord(timedPair(I, ev).first, I.stream));
@@ -934,7 +964,7 @@ void Executor::runAsync()
     } else {
         launchStep(I, lc, dv);
     }
-    if (I.timedPerStep > 0) I.pendingSteps++;
+    if (I.timedPerStep > 0 && sampled) I.pendingSteps++;
 }
 
 void Executor::sync()
@@ -958,10 +988,12 @@ void Executor::run()
     sync();
 }
 
-void Executor::setTimedNode(const char *name)
+void Executor::setTimedNode(const char *name, int32_t every)
 {
     sync();
     impl_->timedName = name ? name : "";
+    impl_->timedEvery = std::max(1, every);
+    impl_->stepIndex = 0;
     impl_->timedMs = 0.0;
     impl_->timedLaunches = 0;
     impl_->timedPerStep = 0;

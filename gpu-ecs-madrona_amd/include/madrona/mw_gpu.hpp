@@ -86,7 +86,9 @@ public:
     double timeNode(const char *name, int32_t num_steps);
     // Live timing of one node kind inside the replayed step (HIP events on
     // the executor stream); setTimedNode re-captures the graph and resets.
-    void setTimedNode(const char *name);
+    // every > 1: only every every-th step (the first of each run of
+    // `every`) is split and timed, the others replay the unsplit graph.
+    void setTimedNode(const char *name, int32_t every = 1);
     double timedNodeMs(int64_t *launches);
 
     // Device tracing (reference mw_gpu/tracing.hpp): records of every step

@@ -156,6 +156,8 @@ def _declare(lib):
     lib.mw_trace_func_name.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     lib.mw_set_timed_node.restype = ctypes.c_int32
     lib.mw_set_timed_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    lib.mw_set_timed_node_every.restype = ctypes.c_int32
+    lib.mw_set_timed_node_every.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
     lib.mw_timed_node_ms.restype = ctypes.c_double
     lib.mw_timed_node_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
     lib.mw_num_nodes.argtypes = [ctypes.c_void_p]
@@ -197,7 +199,7 @@ C_ABI_SYMBOLS = (
     "mw_destroy", "mw_last_error", "mw_num_worlds", "mw_error_flags", "mw_num_archetypes",
     "mw_read_column", "mw_column_info", "mw_phys_read_candidates", "mw_phys_read_contacts",
     "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_copy_exported",
-    "mw_gen_collisions_inits", "mw_set_timed_node", "mw_timed_node_ms",
+    "mw_gen_collisions_inits", "mw_set_timed_node", "mw_set_timed_node_every", "mw_timed_node_ms",
     "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
     "mw_device_free", "mw_gen_fvs_inits", "mw_stream_wait", "mw_load_hull",
     "mw_trace_enable", "mw_trace_read", "mw_trace_func_name", "mw_trace_block_records",
@@ -500,10 +502,12 @@ class Executor:
         if self._lib.mw_set_node_blocks_per_cu(self.h, node, blocks_per_cu) != 0:
             raise _err(self._lib)
 
-    def set_timed_node(self, name):
+    def set_timed_node(self, name, every=1):
         """Bracket every launch of node kind `name` with HIP events inside the
-        replayed step (None disables); resets the accumulators."""
-        if self._lib.mw_set_timed_node(self.h, name.encode() if name else None) != 0:
+        replayed step (None disables); resets the accumulators.  every > 1:
+        only the first step of every run of `every` steps is timed."""
+        if self._lib.mw_set_timed_node_every(self.h, name.encode() if name else None,
+                                             int(every)) != 0:
             raise _err(self._lib)
 
     def timed_node(self):

@@ -210,6 +210,10 @@ double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps
  * returns the accumulated ms and the number of timed launches since the
  * last mw_set_timed_node (NULL/"" disables and restores the single graph). */
 int32_t mw_set_timed_node(mw_exec *exec, const char *node_name);
+/* the same, timing only every `every`-th step (the first of each run of
+ * `every` steps is split and timed; the others replay the unsplit graph, so
+ * the timing costs 1/every of the split's overhead). every >= 1.          */
+int32_t mw_set_timed_node_every(mw_exec *exec, const char *node_name, int32_t every);
 double mw_timed_node_ms(mw_exec *exec, int64_t *launches);
 
 /* ---- job-API environments -----------------------------
