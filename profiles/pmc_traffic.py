@@ -10,8 +10,10 @@
   WRITE_SIZE cannot share a pass on gfx950), with the MI355X_MICROARCH.md
   gfx950 correction FETCH_SIZE x 2; counters are in KB.
 
-A node's launch may be several kernels (NarrowphaseNode = filter + SAT);
-their per-launch values are summed.
+A node's launch may be several kernels (NarrowphaseNode = filter + order +
+SAT + plane + contact); their per-launch values are summed, each weighted by
+its launches per step over the node's (the first substep's integrate and
+filter kernels run in one of the four substep launches).
 """
 import argparse
 import collections
@@ -20,18 +22,20 @@ import glob
 import json
 import os
 
+# kernel -> (node, launches per step)
 NODE_OF = {
-    "leafUpdateKernel": "UpdateLeafPositionsNode",
-    "bvhRebuildKernel": "UpdateBVHNode",
-    "refitKernel": "RefitNode",
-    "findOverlapsKernel": "FindOverlappingNode",
-    "integrateKernel": "SubstepRigidBodiesNode",
-    "narrowFilterKernel": "NarrowphaseNode",
-    "narrowScanKernel": "NarrowphaseNode",
-    "narrowCompactKernel": "NarrowphaseNode",
-    "narrowSATKernel": "NarrowphaseNode",
-    "narrowContactKernel": "NarrowphaseNode",
-    "solverKernel": "SolverNode",
+    "leafUpdateKernel": ("UpdateLeafPositionsNode", 2),
+    "bvhRebuildKernel": ("UpdateBVHNode", 1),
+    "bvhRebuildWaveKernel": ("UpdateBVHNode", 1),
+    "refitKernel": ("RefitNode", 2),
+    "findOverlapsKernel": ("FindOverlappingNode", 1),
+    "integrateKernel": ("SubstepRigidBodiesNode", 1),     # substep 0 only (later: solver tail)
+    "narrowFilterKernel": ("NarrowphaseNode", 1),         # substep 0 only (later: solver tail)
+    "solverOrderKernel": ("NarrowphaseNode", 4),
+    "narrowSATKernel": ("NarrowphaseNode", 4),
+    "narrowPlaneKernel": ("NarrowphaseNode", 4),
+    "narrowContactKernel": ("NarrowphaseNode", 4),
+    "solverKernel": ("SolverNode", 4),
 }
 PER_STEP = {"UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
             "FindOverlappingNode": 1, "SubstepRigidBodiesNode": 4, "NarrowphaseNode": 4,
@@ -60,7 +64,7 @@ def last_per_kernel(rows, steps, key_fn, val_fn):
             by[k].append(val_fn(r))
     out = {}
     for k, vals in by.items():
-        n = PER_STEP[NODE_OF[k]] * steps
+        n = NODE_OF[k][1] * steps
         tail = vals[-n:] if n and len(vals) >= n else vals
         out[k] = sum(tail) / len(tail)
     return out
@@ -88,16 +92,20 @@ def main():
     fetch = counter(a.fetch, "FETCH_SIZE") if a.fetch else {}
     write = counter(a.write, "WRITE_SIZE") if a.write else {}
 
+    # a node launch's share of each kernel: kernel launches per step / node
+    # launches per step (the first substep's integrate / filter kernels run
+    # in one of the four substep node launches)
     nodes = {}
-    for k, node in NODE_OF.items():
+    for k, (node, kper) in NODE_OF.items():
         if k not in ms:
             continue
+        f = kper / PER_STEP[node]
         e = nodes.setdefault(node, {"kernels": [], "ms_per_launch": 0.0,
                                     "fetch_bytes": 0.0, "write_bytes": 0.0})
         e["kernels"].append(k)
-        e["ms_per_launch"] += ms[k]
-        e["fetch_bytes"] += 2.0 * fetch.get(k, 0.0)
-        e["write_bytes"] += write.get(k, 0.0)
+        e["ms_per_launch"] += f * ms[k]
+        e["fetch_bytes"] += f * 2.0 * fetch.get(k, 0.0)
+        e["write_bytes"] += f * write.get(k, 0.0)
     for e in nodes.values():
         e["ms_per_launch"] = round(e["ms_per_launch"], 4)
         e["bytes_per_launch"] = (int(e["fetch_bytes"] + e["write_bytes"])
