@@ -189,6 +189,24 @@ def test_live_node_timing_does_not_perturb_state():
     assert a.timed_node() == (0.0, 0)
 
 
+def test_sampled_node_timing_counts_and_does_not_perturb_state():
+    # set_timed_node(every=3): only the first of every 3 steps is split and
+    # timed, the rest replay the unsplit graph (bench.py's --timed-every).
+    mw = _mw()
+    gcfg, _ = _cfg_pair()
+    pos, rot = gen_collisions_inits(16, 128, seed=3)
+    a = mw.CollisionsSim(16, pos, rot, gcfg)
+    b = mw.CollisionsSim(16, pos, rot, gcfg)
+    a.set_timed_node("SolverNode", every=3)
+    a.step(10)             # steps 0, 3, 6, 9 are timed
+    b.step(10)
+    ms, n = a.timed_node()
+    assert n == 4 * gcfg.num_substeps and ms > 0
+    for w in range(16):
+        assert a.bodies(w).tobytes() == b.bodies(w).tobytes()
+        assert a.contacts(w).tobytes() == b.contacts(w).tobytes()
+
+
 def test_episode_return_export_matches_oracle():
     # ParallelForNode over the EpisodeReturn singleton (Context::forEach over
     # a two-component query) + the packed export buffer (getExported slot 2).
