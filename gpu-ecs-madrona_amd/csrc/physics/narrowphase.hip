@@ -480,9 +480,9 @@ __device__ __forceinline__ void writeFaceManifold(Contact &c, Vector3 n, const V
 // earlier choices replaced by p0).  Every walk recomputes the same vertices
 // with the same operations, so the chosen points are the reference's bits.
 // Returns true if a manifold was written.
-__device__ bool planeContact(const PhysArgs &P, int32_t w, const SatWork &wk)
+__device__ __forceinline__ bool planeContact(const PhysArgs &P, const ObjDev &O, int32_t w,
+                                             const SatWork &wk)
 {
-    const ObjDev &O = P.objs;
     int32_t *flags = P.errorFlags + w;
     const HullDev ha = O.hulls[wk.aObj];
     const HullXform xa = hullXform(P, w, P.body[wk.aArch], wk.a.row);
@@ -529,10 +529,14 @@ __device__ bool planeContact(const PhysArgs &P, int32_t w, const SatWork &wk)
     Vector3 cp[4];
     float depth[4];
     for (int i = 0; i < 4; i++) { cp[i] = Vector3::zero(); depth[i] = 0.f; }
+    // static indices only (a dynamic cp[i] store sends both arrays to scratch)
     const int32_t num = walk([&](int32_t i, Vector3 c, float dd) {
-        if (i < 4) {
-            cp[i & 3] = c;
-            depth[i & 3] = dd;
+#pragma unroll
+        for (int32_t j = 0; j < 4; j++) {
+            if (i == j) {
+                cp[j] = c;
+                depth[j] = dd;
+            }
         }
     });
     int32_t m = num;
@@ -662,10 +666,52 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
     if (threadIdx.x == 0) P.survCount[w] = S;
 }
 
+// The plane kernel's LDS copy of the hull tables it walks (hulls, vertices,
+// face planes, half-edges, face polygons): each pair's vertex / face scans
+// and incident-face walk are chains of dependent reads over a few hundred
+// bytes shared by every pair.
+
+__host__ __device__ inline size_t planeGeoBytesFor(const ObjDev &O)
+{
+    return a16(sizeof(HullDev) * O.numObjects) + a16(sizeof(Vector3) * O.numVertsTotal) +
+           a16(sizeof(geometry::Plane) * O.numPlanesTotal) +
+           a16(sizeof(geometry::HalfEdge) * O.numHedgesTotal) +
+           a16(sizeof(uint32_t) * O.numPolygonsTotal);
+}
+
+size_t planeSharedBytes(const PhysArgs &P)
+{
+    const size_t b = planeGeoBytesFor(P.objs);
+    return b <= 16 * 1024 ? b : 0;
+}
+
+__device__ __forceinline__ void *stageTable(char *&dst, const void *src, size_t bytes)
+{
+    uint32_t *d = (uint32_t *)dst;
+    const uint32_t *s = (const uint32_t *)src;
+    for (size_t i = threadIdx.x; i < bytes / 4; i += blockDim.x) d[i] = s[i];
+    void *out = dst;
+    dst += a16(bytes);
+    return out;
+}
+
 // Hull-plane contacts, one lane per pair of the bins' back parts.
 __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    ObjDev O = P.objs;
+    if (P.planeGeoBytes > 0) {
+        static_assert(sizeof(HullDev) % 4 == 0 && sizeof(geometry::HalfEdge) % 4 == 0, "dword copies");
+        char *dst = smem;
+        O.hulls = (HullDev *)stageTable(dst, P.objs.hulls, sizeof(HullDev) * O.numObjects);
+        O.vertices = (Vector3 *)stageTable(dst, P.objs.vertices, sizeof(Vector3) * O.numVertsTotal);
+        O.planes = (geometry::Plane *)stageTable(dst, P.objs.planes,
+                                                 sizeof(geometry::Plane) * O.numPlanesTotal);
+        O.hedges = (geometry::HalfEdge *)stageTable(dst, P.objs.hedges,
+                                                    sizeof(geometry::HalfEdge) * O.numHedgesTotal);
+        O.polygons = (uint32_t *)stageTable(dst, P.objs.polygons, sizeof(uint32_t) * O.numPolygonsTotal);
+    }
     __shared__ int32_t s_pre[kNarrowBins + 1];
     loadBinPrefix(P, 1, s_pre);
     const int32_t total = s_pre[kNarrowBins];
@@ -683,7 +729,7 @@ __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
             atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
             continue;
         }
-        if (planeContact(P, wk.world, wk))
+        if (planeContact(P, O, wk.world, wk))
             recordManifold(P, wk.world, wk.slot, slotOf(P, wk.bArch, wk.b), slotOf(P, wk.aArch, wk.a));
     }
 }

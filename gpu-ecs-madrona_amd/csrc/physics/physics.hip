@@ -87,8 +87,9 @@ void PhysicsModule::upload(void *stream_ptr)
     MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, narrowContactKernel, kContactBlock, contactSharedBytes(P)));
     P.contactGrid = std::max(1, cus * std::max(per_cu, 1));
+    P.planeGeoBytes = (int32_t)planeSharedBytes(P);
     MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, narrowPlaneKernel,
-                                                              kContactBlock, 0));
+                                                              kContactBlock, P.planeGeoBytes));
     P.planeGrid = std::max(1, cus * std::max(per_cu, 1));
     uploaded = true;
 }
@@ -220,7 +221,7 @@ struct NarrowphaseNode : PhysNodeBase {
         hipLaunchKernelGGL(narrowSATKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
                            narrowphaseSharedBytes(Q), stream, Q);
         hipLaunchKernelGGL(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),
-                           dim3(kContactBlock), 0, stream, Q);
+                           dim3(kContactBlock), Q.planeGeoBytes, stream, Q);
         hipLaunchKernelGGL(narrowContactKernel, dim3(lc.persistentGrid(Q.contactGrid)),
                            dim3(kContactBlock), contactSharedBytes(Q), stream, Q);
     }

@@ -375,6 +375,7 @@ size_t refitSharedBytes(const PhysArgs &P);
 size_t solverSharedBytes(const PhysArgs &P);
 size_t narrowphaseSharedBytes(const PhysArgs &P);
 size_t contactSharedBytes(const PhysArgs &P);
+size_t planeSharedBytes(const PhysArgs &P);
 
 constexpr int32_t kOverlapBlock = 192;
 constexpr int32_t kNarrowBlock = 256;

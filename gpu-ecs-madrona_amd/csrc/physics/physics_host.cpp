@@ -225,6 +225,10 @@ void PhysicsModule::buildArgs(void *stream)
     O.edges = upload(edges, stream);
     O.edgeQuads = upload(edgeQuads, stream);
     O.polygons = upload(polygons, stream);
+    O.numVertsTotal = (int32_t)vertices.size();
+    O.numPlanesTotal = (int32_t)planes.size();
+    O.numHedgesTotal = (int32_t)hedges.size();
+    O.numPolygonsTotal = (int32_t)polygons.size();
 
     P.bodyBoxes = alloc<BodyBox>((size_t)W * std::max(P.maxBodiesPerWorld, 1), stream);
     P.survInfo = alloc<uint32_t>((size_t)W * P.candCapacity, stream);

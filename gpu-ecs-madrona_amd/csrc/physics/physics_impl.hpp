@@ -57,6 +57,8 @@ struct ObjDev {
     uint32_t *edges;              // half-edge index per edge
     uint32_t *polygons;           // half-edge index per face
     EdgeQuad *edgeQuads;          // per edge (same offsets as edges)
+    // table sizes (entries), for the kernels that stage the geometry in LDS
+    int32_t numVertsTotal, numPlanesTotal, numHedgesTotal, numPolygonsTotal;
 };
 
 inline constexpr int32_t kMaxBodyArchetypes = 4;
@@ -166,6 +168,8 @@ struct PhysArgs {
     int32_t *nextSatWorkCount;
     ContactJob *hhJobs;           // [W * candCapacity] SAT verdict per satWork entry
     int32_t contactGrid;          // persistent contact-kernel grid (blocks)
+    int32_t planeGeoBytes;        // plane kernel's LDS copy of the hull tables (0: read
+                                  // them from HBM; tables too large)
     int32_t clipCap;              // clip polygon capacity (2 x largest face)
     int32_t satGrid;              // persistent SAT grid (blocks)
     int32_t planeGrid;            // persistent plane-contact grid (blocks)
