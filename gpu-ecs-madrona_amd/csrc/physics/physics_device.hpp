@@ -377,7 +377,10 @@ size_t narrowphaseSharedBytes(const PhysArgs &P);
 size_t contactSharedBytes(const PhysArgs &P);
 size_t planeSharedBytes(const PhysArgs &P);
 
-constexpr int32_t kOverlapBlock = 192;
+#ifndef MW_OVERLAP_BLOCK
+#define MW_OVERLAP_BLOCK 192
+#endif
+constexpr int32_t kOverlapBlock = MW_OVERLAP_BLOCK;
 constexpr int32_t kNarrowBlock = 256;
 constexpr int32_t kContactBlock = 128;
 constexpr int32_t kSolverBlock = 64;      // lanes per world (one wave)
