@@ -121,9 +121,14 @@ __host__ __device__ inline size_t groupLDSBytes(const ObjDev &O)
            2 * a16(sizeof(EdgeQuad) * O.maxEdges);
 }
 
+// The group staging area; block 0 first uses it for the solver's world
+// sort (kOrderBuckets ints, sortWorldsForSolver below), so it is never
+// smaller than that.
+constexpr size_t kOrderSortBytes = 1024 * sizeof(int32_t);
+
 size_t narrowphaseSharedBytes(const PhysArgs &P)
 {
-    return kGroupsPerBlock * groupLDSBytes(P.objs);
+    return std::max(kGroupsPerBlock * groupLDSBytes(P.objs), kOrderSortBytes);
 }
 
 __device__ __forceinline__ GroupLDS groupLDS(char *smem, int32_t group, const ObjDev &O)
@@ -777,6 +782,48 @@ __device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS
     return true;
 }
 
+// Solver world order.  Block durations follow the worlds' contact counts
+// (p50 / p99 ~ 1 : 3), so with the grid in world-index order the heavy
+// blocks that happen to be dispatched last set the launch's tail.  Block 0
+// of the SAT kernel (before its pairs; the persistent grid's other blocks
+// take them meanwhile) counting-sorts the worlds by descending survivor
+// count (this substep's filter wrote survCount) into solverOrder; the solver
+// grid takes its worlds in that order (longest first), and a block's two
+// worlds have similar work.  Which block or partner solves a world does not
+// change its bits: a world's items only touch its own bodies.
+constexpr int32_t kOrderBuckets = 1024;
+static_assert(kOrderBuckets % kNarrowBlock == 0, "buckets per thread");
+
+__device__ __forceinline__ int32_t orderBucket(const PhysArgs &P, int32_t w)
+{
+    const int32_t n = P.survCount[w];
+    return kOrderBuckets - 1 - min(max(n, 0), kOrderBuckets - 1);
+}
+
+// s_off: kOrderBuckets ints of LDS, s_scan: blockDim.x / 64 ints.
+__device__ __forceinline__ void sortWorldsForSolver(const PhysArgs &P, int32_t *s_off, int32_t *s_scan)
+{
+    const int32_t t = threadIdx.x, nt = blockDim.x, W = P.numWorlds;
+    const int32_t per = kOrderBuckets / nt;
+    for (int32_t b = t; b < kOrderBuckets; b += nt) s_off[b] = 0;
+    __syncthreads();
+    for (int32_t w = t; w < W; w += nt) atomicAdd(&s_off[orderBucket(P, w)], 1);
+    __syncthreads();
+    int32_t sum = 0;
+    for (int32_t j = 0; j < per; j++) sum += s_off[t * per + j];
+    int32_t total;
+    int32_t run = blockExclusiveScan(sum, s_scan, &total);
+    for (int32_t j = 0; j < per; j++) {
+        const int32_t c = s_off[t * per + j];
+        s_off[t * per + j] = run;
+        run += c;
+    }
+    __syncthreads();
+    for (int32_t w = t; w < W; w += nt)
+        P.solverOrder[atomicAdd(&s_off[orderBucket(P, w)], 1)] = w;
+    __syncthreads();
+}
+
 // Stage 4, persistent: each group takes hull-hull pairs off the flat list
 // and leaves its verdict in the job at the same index (kind kJobNone when
 // separated).  The grid is what is resident at once; every group reaches
@@ -795,6 +842,13 @@ __global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKern
     // previous substep's kernels); null when integrateKernel reset it
     if (blockIdx.x == 0 && P.nextSatWorkCount)
         resetNarrowLists(P.nextSatWorkCount, threadIdx.x, blockDim.x);
+    if (blockIdx.x == 0) {
+        // the group staging area is free until the first pair (and at
+        // least kOrderSortBytes: narrowphaseSharedBytes)
+        static_assert(kOrderBuckets * sizeof(int32_t) == kOrderSortBytes, "sort scratch");
+        __shared__ int32_t s_sort_scan[kNarrowBlock / 64];
+        sortWorldsForSolver(P, (int32_t *)smem, s_sort_scan);
+    }
     __shared__ int32_t s_pre[kNarrowBins + 1];
     loadBinPrefix(P, 0, s_pre);
     const int32_t total = s_pre[kNarrowBins];

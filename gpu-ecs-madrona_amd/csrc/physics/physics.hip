@@ -194,9 +194,9 @@ struct SubstepRigidBodiesNode : PhysNodeBase {
 // Narrowphase = AABB recheck + survivor numbering (the first substep's
 // filter kernel, block per world; later substeps' filters run in the
 // previous solver's tail), a persistent SAT kernel (16-lane group per
-// hull-hull pair), a plane kernel and a persistent contact kernel (lane per
-// manifold); see narrowphase.hip.  It also sorts the worlds for the solver
-// grid (solverOrderKernel, solver.hip).  The node's launch configuration (blocks
+// hull-hull pair; its block 0 also sorts the worlds for the solver grid), a
+// plane kernel and a persistent contact kernel (lane per manifold); see
+// narrowphase.hip.  The node's launch configuration (blocks
 // per CU) sizes the persistent grids; by default they are exactly the
 // resident blocks.  The solver turns the per-survivor manifolds into the
 // ordered contact list.
@@ -216,8 +216,6 @@ struct NarrowphaseNode : PhysNodeBase {
         hipStream_t stream = (hipStream_t)lc.stream;
         if (self->substep == 0)
             hipLaunchKernelGGL(narrowFilterKernel, dim3(Q.numWorlds), dim3(kNarrowBlock), 0, stream, Q);
-        // the solver's world order from this substep's survivor counts
-        hipLaunchKernelGGL(solverOrderKernel, dim3(1), dim3(kOrderThreads), 0, stream, Q);
         hipLaunchKernelGGL(narrowSATKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
                            narrowphaseSharedBytes(Q), stream, Q);
         hipLaunchKernelGGL(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),

@@ -144,8 +144,6 @@ __global__ void narrowSATKernel(PhysArgs P);
 __global__ void narrowPlaneKernel(PhysArgs P);
 __global__ void narrowContactKernel(PhysArgs P);
 __global__ void solverKernel(PhysArgs P, int32_t integrate_next);
-__global__ void solverOrderKernel(PhysArgs P);
-constexpr int32_t kOrderThreads = 1024;           // solverOrderKernel: one block
 
 // substepRigidBodies (physics.cpp:79-164) for one body row, from its
 // current pose and velocity (the integrate kernel reads them from the

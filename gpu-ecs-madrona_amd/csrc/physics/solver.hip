@@ -1086,48 +1086,6 @@ __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, S
 #define MW_SOLVER_MARK(i) ((void)0)
 #endif
 
-// Solver world order.  Block durations follow the worlds' contact counts
-// (p50 / p99 ~ 1 : 3), so with the grid in world-index order the heavy
-// blocks that happen to be dispatched last set the launch's tail.  One
-// block counting-sorts the worlds by descending survivor count (this
-// substep's filter wrote survCount) into solverOrder; the solver grid takes
-// its worlds in that order (longest first), and a block's two worlds have
-// similar work.  Which block or partner solves a world does not change its
-// bits: a world's items only touch its own bodies.
-constexpr int32_t kOrderBuckets = kOrderThreads;
-
-__device__ __forceinline__ int32_t orderBucket(const PhysArgs &P, int32_t w)
-{
-    const int32_t n = P.survCount[w];
-    return kOrderBuckets - 1 - min(max(n, 0), kOrderBuckets - 1);
-}
-
-__global__ void __launch_bounds__(kOrderThreads) solverOrderKernel(PhysArgs P)
-{
-    __shared__ int32_t s_off[kOrderBuckets];
-    __shared__ int32_t s_wave[kOrderThreads / 64];
-    const int32_t t = threadIdx.x, W = P.numWorlds;
-    s_off[t] = 0;
-    __syncthreads();
-    for (int32_t w = t; w < W; w += kOrderThreads) atomicAdd(&s_off[orderBucket(P, w)], 1);
-    __syncthreads();
-    const int32_t v = s_off[t];
-    int32_t x = v;
-#pragma unroll
-    for (int32_t o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if ((t & 63) >= o) x += y;
-    }
-    if ((t & 63) == 63) s_wave[t >> 6] = x;
-    __syncthreads();
-    int32_t before = 0;
-    for (int32_t i = 0; i < (t >> 6); i++) before += s_wave[i];
-    s_off[t] = before + x - v;
-    __syncthreads();
-    for (int32_t w = t; w < W; w += kOrderThreads)
-        P.solverOrder[atomicAdd(&s_off[orderBucket(P, w)], 1)] = w;
-}
-
 // Occupancy: latency bound (dependent LDS / column reads per contact), so
 // residency matters more than packed math; built without SLP vectorisation
 // (Makefile) it fits 3 waves per SIMD without spills.
