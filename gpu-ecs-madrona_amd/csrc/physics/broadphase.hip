@@ -686,9 +686,35 @@ size_t findOverlapsSharedBytes(const PhysArgs &P)
     return overlapLDSBytes(P.maxLeaves);
 }
 
+// Phase profile (experiments only, -DMW_SOLVER_PROFILE, the solver's
+// profiling build): per-phase sums of block time in device-clock ticks,
+// read (and reset) by mw_debug_overlap_phases.
+#if defined(MW_SOLVER_PROFILE)
+static __device__ unsigned long long g_overlapPhase[8];
+#define MW_OVERLAP_MARK(i)                                                       \
+    do {                                                                         \
+        if (threadIdx.x == 0) {                                                  \
+            const long long t__ = wall_clock64();                                \
+            atomicAdd(&g_overlapPhase[(i)], (unsigned long long)(t__ - prof_t)); \
+            prof_t = t__;                                                        \
+        }                                                                        \
+    } while (0)
+extern "C" int mw_debug_overlap_phases(unsigned long long *out)
+{
+    unsigned long long z[8] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_overlapPhase), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_overlapPhase), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#else
+#define MW_OVERLAP_MARK(i) ((void)0)
+#endif
+
 __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
+#if defined(MW_SOLVER_PROFILE)
+    long long prof_t = wall_clock64();
+#endif
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int32_t scan_scratch[kOverlapBlock / 64];
     const int32_t w = blockIdx.x;
@@ -725,6 +751,7 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
         rank_of[leaf] = k;
     }
     __syncthreads();
+    MW_OVERLAP_MARK(0);                                   // staging
 
     uint16_t *buf = bufs + threadIdx.x * kOverlapBuf;
     int32_t base = 0;
@@ -758,8 +785,10 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
                     cnt++;
                 }
             }
+            MW_OVERLAP_MARK(1);                           // sweep (thread 0's wave)
             int32_t total;
             const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
+            MW_OVERLAP_MARK(2);                           // scan (waits for every wave)
             CandidateCollision *out = P.cands + (size_t)w * P.candCapacity;
             uint64_t *out_slots = P.candSlots + (size_t)w * P.candCapacity;
             if (cnt > 0) {
@@ -788,6 +817,7 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
                 }
             }
             base += total;
+            MW_OVERLAP_MARK(3);                           // candidate writes (thread 0's)
         }
     }
     if (threadIdx.x == 0) {
@@ -798,6 +828,9 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
         P.numCands[w] = base;
         P.lastNumCands[w] = base;
     }
+#if defined(MW_SOLVER_PROFILE)
+    if (threadIdx.x == 0) atomicAdd(&g_overlapPhase[7], 1ull);
+#endif
 }
 
 }
