@@ -6,7 +6,7 @@ set -euo pipefail
 T=${1:-sq}
 OUT=$PWD/gpurun_out/$T
 B="$PWD/bench.py --no-cpu-baseline --steps 3 --warmup 1"
-RX="solverKernel|solverOrderKernel|narrowSATKernel|narrowContactKernel|narrowPlaneKernel|findOverlapsKernel|refitKernel|narrowFilterKernel|integrateKernel|bvhRebuildWaveKernel|leafUpdateKernel"
+RX="solverKernel|narrowSATKernel|narrowContactKernel|narrowPlaneKernel|findOverlapsKernel|refitKernel|narrowFilterKernel|integrateKernel|bvhRebuildWaveKernel|leafUpdateKernel"
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
