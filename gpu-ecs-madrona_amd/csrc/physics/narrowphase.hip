@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
 //      every candidate; a block scan numbers the survivors in candidate order
 //      (survivor slot == contact slot); hull-hull survivors go to the SAT
 //      work list, hull-plane survivors straight to the contact job list.
-//   2. narrowSATKernel, persistent, one 16-lane group per hull-hull pair:
+//   2. narrowSATKernel, persistent, one kGroup-lane group (8) per hull-hull pair:
 //      both hulls are transformed into LDS and the SAT queries are spread
 //      over the group with (value, index) reductions that reproduce the
 //      reference's serial strict-'>' scans (first occurrence wins, NaN never
@@ -44,7 +44,10 @@ __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
 //   3. narrowContactKernel, persistent, one lane per contact job: clipping
 //      and manifold reduction (all lanes busy, clip polygons in LDS).
 // ===========================================================================
-constexpr int32_t kGroup = 16;
+#ifndef MW_SAT_GROUP
+#define MW_SAT_GROUP 8
+#endif
+constexpr int32_t kGroup = MW_SAT_GROUP;               // lanes per hull-hull pair
 constexpr int32_t kGroupsPerBlock = kNarrowBlock / kGroup;
 
 __host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
@@ -99,7 +102,7 @@ __device__ __forceinline__ Vector3 planeIntersection(const geometry::Plane &p, c
 }
 
 // ---------------------------------------------------------------------------
-// SAT kernel helpers (group of 16 lanes, hulls staged in LDS)
+// SAT kernel helpers (group of kGroup lanes, hulls staged in LDS)
 // ---------------------------------------------------------------------------
 struct HullRef {
     const Vector3 *verts;          // world space (LDS copy)

@@ -193,7 +193,7 @@ struct SubstepRigidBodiesNode : PhysNodeBase {
 
 // Narrowphase = AABB recheck + survivor numbering (the first substep's
 // filter kernel, block per world; later substeps' filters run in the
-// previous solver's tail), a persistent SAT kernel (16-lane group per
+// previous solver's tail), a persistent SAT kernel (8-lane group per
 // hull-hull pair; its block 0 also sorts the worlds for the solver grid), a
 // plane kernel and a persistent contact kernel (lane per manifold); see
 // narrowphase.hip.  The node's launch configuration (blocks
