@@ -380,7 +380,10 @@ size_t planeSharedBytes(const PhysArgs &P);
 #endif
 constexpr int32_t kOverlapBlock = MW_OVERLAP_BLOCK;
 constexpr int32_t kNarrowBlock = 256;
-constexpr int32_t kContactBlock = 128;
+#ifndef MW_CONTACT_BLOCK
+#define MW_CONTACT_BLOCK 128
+#endif
+constexpr int32_t kContactBlock = MW_CONTACT_BLOCK;   // plane / contact kernels
 constexpr int32_t kSolverBlock = 64;      // lanes per world (one wave)
 #ifndef MW_SOLVER_WORLDS
 #define MW_SOLVER_WORLDS 2
