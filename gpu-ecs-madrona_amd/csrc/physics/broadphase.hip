@@ -543,16 +543,18 @@ size_t refitSharedBytes(const PhysArgs &P)
     return sizeof(BVHNode) * (size_t)P.maxNodes;
 }
 
-__global__ void __launch_bounds__(kRefitBlock) refitKernel(PhysArgs P)
+// kGlobal: the world's nodes exceed a workgroup's LDS; the same walk runs on
+// the node slab in place (refitGlobalKernel).
+template <bool kGlobal>
+__device__ __forceinline__ void refitWorld(const PhysArgs &P)
 {
-    MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    BVHNode *lnodes = (BVHNode *)smem;
     const int32_t w = blockIdx.x;
     const int32_t used = min(P.bvh[w].usedNodes, P.maxNodes);
     if (used <= 0) return;
     BVHNode *gnodes = P.nodes + (size_t)w * P.maxNodes;
-    {
+    BVHNode *lnodes = kGlobal ? gnodes : (BVHNode *)smem;
+    if (!kGlobal) {
         const uint32_t *src = (const uint32_t *)gnodes;
         uint32_t *dst = (uint32_t *)lnodes;
         const int32_t words = used * (int32_t)(sizeof(BVHNode) / 4);
@@ -615,13 +617,25 @@ __global__ void __launch_bounds__(kRefitBlock) refitKernel(PhysArgs P)
         }
     }
     __syncthreads();
-    {   // bounds only: children / parents are unchanged by a refit
+    if (!kGlobal) {   // bounds only: children / parents are unchanged by a refit
         const int32_t per = 24;                          // minX..maxZ dwords per node
         for (int32_t i = threadIdx.x; i < used * per; i += kRefitBlock) {
             const int32_t n = i / per, k = i - n * per;
             ((uint32_t *)&gnodes[n])[k] = ((const uint32_t *)&lnodes[n])[k];
         }
     }
+}
+
+__global__ void __launch_bounds__(kRefitBlock) refitKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    refitWorld<false>(P);
+}
+
+__global__ void __launch_bounds__(kRefitBlock) refitGlobalKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    refitWorld<true>(P);
 }
 
 // findOverlappingEntry + BVH::findOverlaps (broadphase.cpp:897-932,
@@ -686,6 +700,11 @@ size_t findOverlapsSharedBytes(const PhysArgs &P)
     return overlapLDSBytes(P.maxLeaves);
 }
 
+size_t findOverlapsImageBytes(const PhysArgs &P)
+{
+    return overlapLDSBytes(P.maxLeaves);
+}
+
 // Phase profile (experiments only, -DMW_SOLVER_PROFILE, the solver's
 // profiling build): per-phase sums of block time in device-clock ticks,
 // read (and reset) by mw_debug_overlap_phases.
@@ -709,17 +728,20 @@ extern "C" int mw_debug_overlap_phases(unsigned long long *out)
 #define MW_OVERLAP_MARK(i) ((void)0)
 #endif
 
-__global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
+// kGlobal: the world's leaf image exceeds a workgroup's LDS; it is staged in
+// the world's slab of P.overlapImage instead (findOverlapsGlobalKernel).
+template <bool kGlobal>
+__device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
 {
-    MW_TRACE_BLOCK(0);
 #if defined(MW_SOLVER_PROFILE)
     long long prof_t = wall_clock64();
 #endif
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int32_t scan_scratch[kOverlapBlock / 64];
     const int32_t w = blockIdx.x;
-    OrderedLeaf *leaves = (OrderedLeaf *)smem;
-    int32_t *rank_of = (int32_t *)(smem + a16b(sizeof(OrderedLeaf) * P.maxLeaves));
+    char *img = kGlobal ? P.overlapImage + (size_t)w * overlapLDSBytes(P.maxLeaves) : smem;
+    OrderedLeaf *leaves = (OrderedLeaf *)img;
+    int32_t *rank_of = (int32_t *)(img + a16b(sizeof(OrderedLeaf) * P.maxLeaves));
     uint16_t *bufs = (uint16_t *)((char *)rank_of + a16b(4 * P.maxLeaves));
 
     // Stage leaf slots (from the refit tree) + identity in emission order.
@@ -831,6 +853,18 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
 #if defined(MW_SOLVER_PROFILE)
     if (threadIdx.x == 0) atomicAdd(&g_overlapPhase[7], 1ull);
 #endif
+}
+
+__global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    findOverlapsWorld<false>(P);
+}
+
+__global__ void __launch_bounds__(kOverlapBlock) findOverlapsGlobalKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    findOverlapsWorld<true>(P);
 }
 
 }

@@ -834,13 +834,17 @@ __device__ __forceinline__ void sortWorldsForSolver(const PhysArgs &P, int32_t *
 #ifndef MW_SAT_MIN_BLOCKS
 #define MW_SAT_MIN_BLOCKS 4
 #endif
-__global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKernel(PhysArgs P)
+// kGlobal: the groups' hull staging exceeds a workgroup's LDS and lives in
+// the block's slab of P.satImage (narrowSATGlobalKernel); the world sort
+// still uses kOrderSortBytes of LDS.
+template <bool kGlobal>
+__device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
 {
-    MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int32_t group = threadIdx.x / kGroup;
     const int32_t lane = threadIdx.x % kGroup;
-    const GroupLDS g = groupLDS(smem, group, P.objs);
+    char *stage = kGlobal ? P.satImage + (size_t)blockIdx.x * kGroupsPerBlock * groupLDSBytes(P.objs) : smem;
+    const GroupLDS g = groupLDS(stage, group, P.objs);
     // the set the solver of this substep will fill (read last by the
     // previous substep's kernels); null when integrateKernel reset it
     if (blockIdx.x == 0 && P.nextSatWorkCount)
@@ -878,6 +882,28 @@ __global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKern
     }
 }
 
+__global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    narrowSATBlock<false>(P);
+}
+
+__global__ void __launch_bounds__(kNarrowBlock) narrowSATGlobalKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    narrowSATBlock<true>(P);
+}
+
+size_t narrowphaseImageBytes(const PhysArgs &P)
+{
+    return kGroupsPerBlock * groupLDSBytes(P.objs);
+}
+
+size_t narrowphaseGlobalSharedBytes(const PhysArgs &)
+{
+    return kOrderSortBytes;
+}
+
 __host__ __device__ inline size_t contactLDSBytes(int32_t clip_cap)
 {
     return (size_t)kContactBlock * (2 * a16(sizeof(Vector3) * clip_cap) + a16(4 * clip_cap));
@@ -888,16 +914,24 @@ size_t contactSharedBytes(const PhysArgs &P)
     return contactLDSBytes(P.clipCap);
 }
 
+size_t contactImageBytes(const PhysArgs &P)
+{
+    return contactLDSBytes(P.clipCap);
+}
+
 
 // createFaceContact / createFacePlaneContact / createEdgeContact
 // (narrowphase.cpp:866-1121) for one job per lane.
-__global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
+// kGlobal: the lanes' clip buffers exceed a workgroup's LDS and live in the
+// block's slab of P.clipImage (narrowContactGlobalKernel).
+template <bool kGlobal>
+__device__ __forceinline__ void narrowContactBlock(const PhysArgs &P)
 {
-    MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const ObjDev &O = P.objs;
     const int32_t cap = P.clipCap;
-    char *mine = smem + (size_t)threadIdx.x * (2 * a16(sizeof(Vector3) * cap) + a16(4 * cap));
+    char *base = kGlobal ? P.clipImage + (size_t)blockIdx.x * contactLDSBytes(cap) : smem;
+    char *mine = base + (size_t)threadIdx.x * (2 * a16(sizeof(Vector3) * cap) + a16(4 * cap));
     Vector3 *clip0 = (Vector3 *)mine;
     Vector3 *clip1 = (Vector3 *)(mine + a16(sizeof(Vector3) * cap));
     float *depths = (float *)(mine + 2 * a16(sizeof(Vector3) * cap));
@@ -1007,6 +1041,18 @@ __global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
             recordManifold(P, w, wk.slot, slotOf(P, wk.aArch, wk.a), slotOf(P, wk.bArch, wk.b));
         }
     }
+}
+
+__global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    narrowContactBlock<false>(P);
+}
+
+__global__ void __launch_bounds__(kContactBlock) narrowContactGlobalKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    narrowContactBlock<true>(P);
 }
 
 }

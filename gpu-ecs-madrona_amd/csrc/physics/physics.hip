@@ -21,22 +21,16 @@
 
 #include <hip/hip_runtime.h>
 
+#include "../runtime/hip_launch.hpp"
+
 #include <cstdio>
+#include <cstdlib>
 
 namespace madrona::phys {
 
 using namespace math;
 using namespace base;
 
-#define MW_HIP_CHECK(expr)                                                          \
-    do {                                                                            \
-        hipError_t err__ = (expr);                                                  \
-        if (err__ != hipSuccess) {                                                  \
-            fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(err__),    \
-                    __FILE__, __LINE__);                                            \
-            throw std::runtime_error(hipGetErrorString(err__));                     \
-        }                                                                           \
-    } while (0)
 
 PhysicsModule::~PhysicsModule()
 {
@@ -57,18 +51,54 @@ void PhysicsModule::rawCopy(void *dst, const void *src, size_t bytes, void *stre
     MW_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
 }
 
+// Launch sizing and the LDS-image decision of every LDS-staging kernel.  A
+// kernel whose image (a world's leaves, BVH nodes or bodies; a block's hull
+// staging or clip polygons) does not fit a workgroup's LDS runs its
+// global-image variant (the same code on a global slab: same bits); a shape
+// that cannot launch either way throws here, at mw_create, naming the kernel
+// and the bytes (hip_launch.hpp).  MADRONA_MW_FORCE_GLOBAL_IMAGES=1 selects
+// the global variants everywhere (the parity tests of the fallback).
 void PhysicsModule::upload(void *stream_ptr)
 {
     if (!initialized) return;          // physics types registered but never used
     buildArgs(stream_ptr);
     PhysArgs &P = args;
-    // Persistent SAT grid: exactly the blocks that can be resident at once.
-    int dev = 0, cus = 0, per_cu = 0;
+    int dev = 0, cus = 0;
     MW_HIP_CHECK(hipGetDevice(&dev));
     MW_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, narrowSATKernel, kNarrowBlock, narrowphaseSharedBytes(P)));
-    P.satGrid = std::max(1, cus * std::max(per_cu, 1));
+    const char *force_env = std::getenv("MADRONA_MW_FORCE_GLOBAL_IMAGES");
+    const bool force = force_env && force_env[0] && force_env[0] != '0';
+    auto fitsLDS = [&](const void *fn, int32_t threads, size_t lds) {
+        return !force && hipx::residentBlocksNoThrow(fn, threads, lds) > 0;
+    };
+    const int32_t W = P.numWorlds;
+    const int32_t solver_blocks = (W + kSolverWorlds - 1) / kSolverWorlds;
+
+    // broadphase: the BVH rebuild picks its variant per launch (<= 64 KB)
+    P.refitGlobal = fitsLDS((const void *)&refitKernel, kRefitBlock, refitSharedBytes(P)) ? 0 : 1;
+    if (P.refitGlobal) hipx::residentBlocks((const void *)&refitGlobalKernel, "refitGlobalKernel", kRefitBlock, 0);
+    P.overlapImage = nullptr;
+    if (!fitsLDS((const void *)&findOverlapsKernel, kOverlapBlock, findOverlapsSharedBytes(P))) {
+        hipx::residentBlocks((const void *)&findOverlapsGlobalKernel, "findOverlapsGlobalKernel",
+                             kOverlapBlock, 0);
+        P.overlapImage = alloc<char>((size_t)W * findOverlapsImageBytes(P), stream_ptr);
+    }
+
+    // SAT: persistent grid of exactly the blocks that can be resident
+    P.satImage = nullptr;
+    P.satImageBlocks = 0;
+    if (fitsLDS((const void *)&narrowSATKernel, kNarrowBlock, narrowphaseSharedBytes(P))) {
+        P.satGrid = cus * hipx::residentBlocks((const void *)&narrowSATKernel, "narrowSATKernel",
+                                               kNarrowBlock, narrowphaseSharedBytes(P));
+    } else {
+        const int32_t per_cu = hipx::residentBlocks((const void *)&narrowSATGlobalKernel,
+                                                    "narrowSATGlobalKernel", kNarrowBlock,
+                                                    narrowphaseGlobalSharedBytes(P));
+        P.satGrid = cus * std::min(per_cu, 2);
+        P.satImageBlocks = P.satGrid;
+        P.satImage = alloc<char>((size_t)P.satGrid * narrowphaseImageBytes(P), stream_ptr);
+    }
+
     int32_t max_face_verts = 1;
     for (const HullDev &h : hulls) {
         for (int32_t f = 0; f < h.numFaces; f++) {
@@ -84,13 +114,32 @@ void PhysicsModule::upload(void *stream_ptr)
     // clipping an incident face against a reference face's side planes
     // yields at most |incident| + |reference| vertices
     P.clipCap = 2 * max_face_verts;
-    MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, narrowContactKernel, kContactBlock, contactSharedBytes(P)));
-    P.contactGrid = std::max(1, cus * std::max(per_cu, 1));
+    P.clipImage = nullptr;
+    P.clipImageBlocks = 0;
+    if (fitsLDS((const void *)&narrowContactKernel, kContactBlock, contactSharedBytes(P))) {
+        P.contactGrid = cus * hipx::residentBlocks((const void *)&narrowContactKernel,
+                                                   "narrowContactKernel", kContactBlock,
+                                                   contactSharedBytes(P));
+    } else {
+        const int32_t per_cu = hipx::residentBlocks((const void *)&narrowContactGlobalKernel,
+                                                    "narrowContactGlobalKernel", kContactBlock, 0);
+        P.contactGrid = cus * std::min(per_cu, 2);
+        P.clipImageBlocks = P.contactGrid;
+        P.clipImage = alloc<char>((size_t)P.contactGrid * contactImageBytes(P), stream_ptr);
+    }
+    // plane kernel: hull tables in LDS up to 16 KB, else read from HBM
     P.planeGeoBytes = (int32_t)planeSharedBytes(P);
-    MW_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, narrowPlaneKernel,
-                                                              kContactBlock, P.planeGeoBytes));
-    P.planeGrid = std::max(1, cus * std::max(per_cu, 1));
+    P.planeGrid = cus * hipx::residentBlocks((const void *)&narrowPlaneKernel, "narrowPlaneKernel",
+                                             kContactBlock, P.planeGeoBytes);
+
+    P.solverImage = nullptr;
+    if (!fitsLDS((const void *)&solverKernel, kSolverThreads, solverSharedBytes(P))) {
+        hipx::residentBlocks((const void *)&solverGlobalKernel, "solverGlobalKernel", kSolverThreads,
+                             solverGlobalSharedBytes(P));
+        P.solverImage = alloc<char>((size_t)solver_blocks * solverImageBytes(P), stream_ptr);
+    }
+    // the remaining kernels stage nothing of variable size
+    hipx::residentBlocks((const void *)&narrowFilterKernel, "narrowFilterKernel", kNarrowBlock, 0);
     uploaded = true;
 }
 
@@ -132,25 +181,30 @@ struct PhysNodeBase : NodeBase {
 
 MW_PHYS_NODE(UpdateLeafPositionsNode,
     if (P.numBodyArchs > 0)
-        hipLaunchKernelGGL(leafUpdateKernel, rowGrid(P), dim3(256), 0, stream, P);)
+        MW_LAUNCH(leafUpdateKernel, rowGrid(P), dim3(256), 0, stream, P);)
 
 // One wave per world while the world's leaves fit the LDS image (129 leaves:
 // ≈11 KB); the lane-per-world kernel otherwise.
 MW_PHYS_NODE(UpdateBVHNode,
     if (rebuildSharedBytes(P) <= 64 * 1024)
-        hipLaunchKernelGGL(bvhRebuildWaveKernel, dim3(P.numWorlds), dim3(64),
+        MW_LAUNCH(bvhRebuildWaveKernel, dim3(P.numWorlds), dim3(64),
                            rebuildSharedBytes(P), stream, P);
     else
-        hipLaunchKernelGGL(bvhRebuildKernel, dim3((P.numWorlds + 63) / 64), dim3(64), 0, stream, P);)
+        MW_LAUNCH(bvhRebuildKernel, dim3((P.numWorlds + 63) / 64), dim3(64), 0, stream, P);)
 
 MW_PHYS_NODE(RefitNode,
-    if (P.numBodyArchs > 0)
-        hipLaunchKernelGGL(refitKernel, dim3(P.numWorlds), dim3(kRefitBlock),
-                           refitSharedBytes(P), stream, P);)
+    if (P.numBodyArchs == 0) return;
+    if (P.refitGlobal)
+        MW_LAUNCH(refitGlobalKernel, dim3(P.numWorlds), dim3(kRefitBlock), 0, stream, P);
+    else
+        MW_LAUNCH(refitKernel, dim3(P.numWorlds), dim3(kRefitBlock), refitSharedBytes(P), stream, P);)
 
 MW_PHYS_NODE(FindOverlappingNode,
-    hipLaunchKernelGGL(findOverlapsKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
-                       findOverlapsSharedBytes(P), stream, P);)
+    if (P.overlapImage)
+        MW_LAUNCH(findOverlapsGlobalKernel, dim3(P.numWorlds), dim3(kOverlapBlock), 0, stream, P);
+    else
+        MW_LAUNCH(findOverlapsKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
+                  findOverlapsSharedBytes(P), stream, P);)
 
 // The narrowphase work lists come in two sets (PhysArgs::satWorkSet):
 // substep i's narrowphase reads set i % 2, and its filter for substep i + 1
@@ -186,7 +240,7 @@ struct SubstepRigidBodiesNode : PhysNodeBase {
         const PhysArgs &P = self->mod->args;
         if (self->fused || P.numBodyArchs == 0) return;
         // resets both list sets
-        hipLaunchKernelGGL(integrateKernel, rowGrid(P), dim3(256), 0, (hipStream_t)lc.stream,
+        MW_LAUNCH(integrateKernel, rowGrid(P), dim3(256), 0, (hipStream_t)lc.stream,
                            substepArgs(P, 0, true));
     }
 };
@@ -215,13 +269,24 @@ struct NarrowphaseNode : PhysNodeBase {
         const PhysArgs Q = substepArgs(self->mod->args, self->substep, false);
         hipStream_t stream = (hipStream_t)lc.stream;
         if (self->substep == 0)
-            hipLaunchKernelGGL(narrowFilterKernel, dim3(Q.numWorlds), dim3(kNarrowBlock), 0, stream, Q);
-        hipLaunchKernelGGL(narrowSATKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
-                           narrowphaseSharedBytes(Q), stream, Q);
-        hipLaunchKernelGGL(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),
+            MW_LAUNCH(narrowFilterKernel, dim3(Q.numWorlds), dim3(kNarrowBlock), 0, stream, Q);
+        if (Q.satImage) {       // the grid never exceeds the slabs of the image
+            const uint32_t g = std::min<uint32_t>(lc.persistentGrid(Q.satGrid), Q.satImageBlocks);
+            MW_LAUNCH(narrowSATGlobalKernel, dim3(g), dim3(kNarrowBlock),
+                      narrowphaseGlobalSharedBytes(Q), stream, Q);
+        } else {
+            MW_LAUNCH(narrowSATKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
+                      narrowphaseSharedBytes(Q), stream, Q);
+        }
+        MW_LAUNCH(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),
                            dim3(kContactBlock), Q.planeGeoBytes, stream, Q);
-        hipLaunchKernelGGL(narrowContactKernel, dim3(lc.persistentGrid(Q.contactGrid)),
-                           dim3(kContactBlock), contactSharedBytes(Q), stream, Q);
+        if (Q.clipImage) {
+            const uint32_t g = std::min<uint32_t>(lc.persistentGrid(Q.contactGrid), Q.clipImageBlocks);
+            MW_LAUNCH(narrowContactGlobalKernel, dim3(g), dim3(kContactBlock), 0, stream, Q);
+        } else {
+            MW_LAUNCH(narrowContactKernel, dim3(lc.persistentGrid(Q.contactGrid)),
+                      dim3(kContactBlock), contactSharedBytes(Q), stream, Q);
+        }
     }
 };
 
@@ -243,9 +308,13 @@ struct SolverNode : PhysNodeBase {
     static void launch(SolverNode *self, LaunchCtx &lc)
     {
         const PhysArgs Q = substepArgs(self->mod->args, self->substep, true);
-        hipLaunchKernelGGL(solverKernel, dim3((Q.numWorlds + kSolverWorlds - 1) / kSolverWorlds),
-                           dim3(kSolverThreads), solverSharedBytes(Q), (hipStream_t)lc.stream, Q,
-                           self->integrateNext);
+        const dim3 grid((Q.numWorlds + kSolverWorlds - 1) / kSolverWorlds);
+        if (Q.solverImage)
+            MW_LAUNCH(solverGlobalKernel, grid, dim3(kSolverThreads), solverGlobalSharedBytes(Q),
+                      (hipStream_t)lc.stream, Q, self->integrateNext);
+        else
+            MW_LAUNCH(solverKernel, grid, dim3(kSolverThreads), solverSharedBytes(Q),
+                      (hipStream_t)lc.stream, Q, self->integrateNext);
     }
 };
 

@@ -144,6 +144,14 @@ __global__ void narrowSATKernel(PhysArgs P);
 __global__ void narrowPlaneKernel(PhysArgs P);
 __global__ void narrowContactKernel(PhysArgs P);
 __global__ void solverKernel(PhysArgs P, int32_t integrate_next);
+// The same kernels with their per-world / per-group / per-lane LDS image in
+// a global slab (PhysArgs::*Image), for worlds and hulls whose image does not
+// fit a workgroup's LDS: same code, same order of operations, same bits.
+__global__ void refitGlobalKernel(PhysArgs P);
+__global__ void findOverlapsGlobalKernel(PhysArgs P);
+__global__ void narrowSATGlobalKernel(PhysArgs P);
+__global__ void narrowContactGlobalKernel(PhysArgs P);
+__global__ void solverGlobalKernel(PhysArgs P, int32_t integrate_next);
 
 // substepRigidBodies (physics.cpp:79-164) for one body row, from its
 // current pose and velocity (the integrate kernel reads them from the
@@ -374,6 +382,14 @@ size_t solverSharedBytes(const PhysArgs &P);
 size_t narrowphaseSharedBytes(const PhysArgs &P);
 size_t contactSharedBytes(const PhysArgs &P);
 size_t planeSharedBytes(const PhysArgs &P);
+// Global-image variants: dynamic LDS they still use, and image bytes per
+// world (findOverlaps, solver), per SAT block and per contact block.
+size_t findOverlapsImageBytes(const PhysArgs &P);
+size_t solverGlobalSharedBytes(const PhysArgs &P);
+size_t solverImageBytes(const PhysArgs &P);
+size_t narrowphaseGlobalSharedBytes(const PhysArgs &P);
+size_t narrowphaseImageBytes(const PhysArgs &P);
+size_t contactImageBytes(const PhysArgs &P);
 
 #ifndef MW_OVERLAP_BLOCK
 #define MW_OVERLAP_BLOCK 192

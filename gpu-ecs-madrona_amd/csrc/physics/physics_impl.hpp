@@ -191,6 +191,16 @@ struct PhysArgs {
     JointConstraint *joints;      // [W][jointCapacity]
     int32_t *lastNumCands;        // [W] debug: candidates of the last step
 
+    // LDS images that do not fit a workgroup live in global slabs instead
+    // (null: the kernel stages them in LDS); physics.hip upload() decides.
+    char *overlapImage;           // [W][findOverlapsImageBytes] leaf image per world
+    int32_t refitGlobal;          // refit walks the node slab in place
+    char *satImage;               // [satImageBlocks][narrowphaseImageBytes] hull staging
+    int32_t satImageBlocks;
+    char *clipImage;              // [clipImageBlocks][contactImageBytes] clip polygons
+    int32_t clipImageBlocks;
+    char *solverImage;            // [solver blocks][solverImageBytes] body image per block
+
     ObjDev objs;
 };
 

@@ -618,10 +618,11 @@ __device__ __forceinline__ SolverLDS solverWorldLDS(char *smem, int32_t nb, int3
     return L;
 }
 
-__device__ __forceinline__ SolverBlockLDS solverBlockLDS(char *smem, int32_t nb)
+// p: the block schedule's LDS (after the world images, or all of the
+// dynamic LDS when the images are global)
+__device__ __forceinline__ SolverBlockLDS solverBlockLDS(char *p)
 {
     SolverBlockLDS B;
-    char *p = smem + kSolverWorlds * solverWorldLDSBytes(nb);
     B.items = (uint32_t *)p;
     p += sizeof(uint32_t) * kSolverItems;
     B.bucketOff = (int32_t *)p;
@@ -1098,13 +1099,17 @@ __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, S
 // block's (level, kind)-sorted (world, item) list, so a level's items from
 // all of the block's worlds share the lanes and a wave's lanes mostly share
 // a code path.
-__global__ void __launch_bounds__(kSolverThreads)
-__attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(PhysArgs P,
-                                                                            int32_t integrate_next)
+// kGlobal: the worlds' body images exceed a workgroup's LDS and live in the
+// block's slab of P.solverImage (solverGlobalKernel); the block schedule
+// (items, buckets) stays in LDS.
+template <bool kGlobal>
+__device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate_next)
 {
-    MW_TRACE_BLOCK(0);
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int32_t nb = P.maxBodiesPerWorld;
+    // world images at `smem`, the block schedule after kSolverWorlds of them
+    char *smem = kGlobal ? P.solverImage + (size_t)blockIdx.x * kSolverWorlds * solverWorldLDSBytes(nb)
+                         : smem_raw;
     const int32_t wi = threadIdx.x / kSolverBlock;
     const int32_t lane = threadIdx.x % kSolverBlock;
     __shared__ int32_t s_worlds[kSolverWorlds];
@@ -1113,7 +1118,7 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
     const int32_t w = live ? P.solverOrder[wslot] : 0;
     if (lane == 0) s_worlds[wi] = w;
     SolverLDS L = solverWorldLDS(smem, nb, wi);
-    SolverBlockLDS BL = solverBlockLDS(smem, nb);
+    SolverBlockLDS BL = solverBlockLDS(kGlobal ? smem_raw : smem + kSolverWorlds * solverWorldLDSBytes(nb));
 
 #if defined(MW_SOLVER_PROFILE)
     long long prof_t = wall_clock64();
@@ -1231,6 +1236,20 @@ __attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(Phy
 #endif
 }
 
+__global__ void __launch_bounds__(kSolverThreads)
+__attribute__((amdgpu_waves_per_eu(MW_SOLVER_WAVES_PER_EU, 8))) solverKernel(PhysArgs P,
+                                                                            int32_t integrate_next)
+{
+    MW_TRACE_BLOCK(0);
+    solverBlock<false>(P, integrate_next);
+}
+
+__global__ void __launch_bounds__(kSolverThreads) solverGlobalKernel(PhysArgs P, int32_t integrate_next)
+{
+    MW_TRACE_BLOCK(0);
+    solverBlock<true>(P, integrate_next);
+}
+
 #if defined(MW_SOLVER_PROFILE)
 extern "C" int mw_debug_solver_block_times(unsigned long long *out, int n)
 {
@@ -1248,6 +1267,16 @@ extern "C" int mw_debug_solver_phases(unsigned long long *out)
 size_t solverSharedBytes(const PhysArgs &P)
 {
     return solverBlockLDSBytes(P.maxBodiesPerWorld);
+}
+
+size_t solverGlobalSharedBytes(const PhysArgs &P)
+{
+    return solverBlockLDSBytes(P.maxBodiesPerWorld) - kSolverWorlds * solverWorldLDSBytes(P.maxBodiesPerWorld);
+}
+
+size_t solverImageBytes(const PhysArgs &P)
+{
+    return kSolverWorlds * solverWorldLDSBytes(P.maxBodiesPerWorld);
 }
 
 }

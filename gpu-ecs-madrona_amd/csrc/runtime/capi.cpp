@@ -70,11 +70,19 @@ static std::map<std::string, EnvFactory> &envTable()
     return t;
 }
 
+// Names an object tried to register that were already taken (mw_load_env
+// reports them).
+static std::vector<std::string> &envClashes()
+{
+    static std::vector<std::string> v;
+    return v;
+}
+
 EnvRegistration::EnvRegistration(const char *name, EnvFactory factory)
 {
     // A name registered twice (two loaded objects defining one world) keeps
-    // the first factory; the C ABI reports the clash at load time.
-    envTable().emplace(name, factory);
+    // the first factory; mw_load_env reports the clash.
+    if (!envTable().emplace(name, factory).second) envClashes().push_back(name);
 }
 
 static std::vector<std::string> envNames()
@@ -163,7 +171,11 @@ mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
         ec.defaultCapacity = cfg->default_capacity > 0 ? cfg->default_capacity : 64;
         ec.numExportedBuffers = 0;
         ec.useGraph = cfg->use_graph;
-        ec.tmpAllocBytesPerWorld = cfg->tmp_alloc_bytes;
+        // C ABI: 0 = default, -1 = none (a zero-initialised mw_config gets
+        // the default arena); ExecConfig: -1 = default, 0 = none
+        ec.tmpAllocBytesPerWorld = cfg->tmp_alloc_bytes == 0    ? -1
+                                   : cfg->tmp_alloc_bytes == -1 ? 0
+                                                                : cfg->tmp_alloc_bytes;
         ec.maxDeferredPerWorld = cfg->max_deferred_destroys;
         ec.numWorkers = cfg->num_workers;
         if (cfg->tmp_alloc_bytes < -1 || cfg->max_deferred_destroys < 0 ||
@@ -180,11 +192,19 @@ int32_t mw_load_env(const char *so_path)
     MW_TRY({
         if (!so_path) throw std::runtime_error("mw_load_env: null path");
         const size_t before = envTable().size();
+        envClashes().clear();
         // RTLD_NOW: unresolved symbols fail here, not at the first step.
         // The object's DT_NEEDED libmadrona_mw.so resolves to this loaded
         // library by its soname, so the world registers into this table.
         void *h = dlopen(so_path, RTLD_NOW | RTLD_LOCAL);
         if (!h) throw std::runtime_error(std::string("mw_load_env: ") + dlerror());
+        if (!envClashes().empty()) {
+            std::string names;
+            for (const std::string &n : envClashes()) names += (names.empty() ? "'" : ", '") + n + "'";
+            envClashes().clear();
+            throw std::runtime_error(std::string("mw_load_env: ") + so_path + " registers " + names +
+                                     ", already registered by another object (the first one stays)");
+        }
         return (int32_t)(envTable().size() - before);
     }, -1)
 }
@@ -653,5 +673,22 @@ extern "C" int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *co
             copyOut(contacts_out, P->lastNumContacts, 4 * P->numWorlds);
         }
         return P->numWorlds;
+    }, -1)
+}
+
+extern "C" int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t n)
+{
+    MW_TRY({
+        phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
+        if (!P || !out) return -1;
+        int32_t v[6];
+        v[0] = P->refitGlobal != 0;
+        v[1] = P->overlapImage != nullptr;
+        v[2] = P->satImage != nullptr;
+        v[3] = P->clipImage != nullptr;
+        v[4] = P->solverImage != nullptr;
+        v[5] = P->planeGeoBytes > 0;
+        for (int32_t i = 0; i < n && i < 6; i++) out[i] = v[i];
+        return 6;
     }, -1)
 }

@@ -8,6 +8,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "hip_launch.hpp"
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -20,15 +22,6 @@
 
 namespace madrona {
 
-#define MW_HIP_CHECK(expr)                                                          \
-    do {                                                                            \
-        hipError_t err__ = (expr);                                                  \
-        if (err__ != hipSuccess) {                                                  \
-            fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(err__),    \
-                    __FILE__, __LINE__);                                            \
-            throw std::runtime_error(hipGetErrorString(err__));                     \
-        }                                                                           \
-    } while (0)
 
 // TaskGraph::Builder / build / launch: csrc/runtime/taskgraph.cpp (shared
 // with the CPU back end).
@@ -44,6 +37,7 @@ void launchWorldKernel(const void *kernel, LaunchCtx &lc)
     void *args[] = { &st };
     const uint32_t blocks = lc.capGrid((uint32_t)((lc.numWorlds + 63) / 64));
     if (blocks == 0) return;
+    hipx::residentBlocks(kernel, "perWorldKernel", 64, 0);
     MW_HIP_CHECK(hipLaunchKernel(kernel, dim3(blocks), dim3(64), args, 0,
                                  (hipStream_t)lc.stream));
 }
@@ -62,6 +56,7 @@ void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype, int32
     StateView *st = lc.devState;
     int32_t arch = archetype, qa = query_arch;
     void *kargs[] = { &st, &arch, &qa, const_cast<void *>(cols) };
+    hipx::residentBlocks(kernel, "parallelForKernel", 256, 0);
     MW_HIP_CHECK(hipLaunchKernel(kernel, grid, block, kargs, 0, (hipStream_t)lc.stream));
 }
 
@@ -81,6 +76,7 @@ void launchNodeFnKernel(const void *kernel, LaunchCtx &lc, void *node_dev, uint3
     }
     if (blocks == 0) return;
     void *kargs[] = { &node_dev, &fixed_count, &threads };
+    hipx::residentBlocks(kernel, "nodeFnKernel", 256, 0);
     MW_HIP_CHECK(hipLaunchKernel(kernel, dim3(blocks), dim3(256), kargs, 0,
                                  (hipStream_t)lc.stream));
 }
@@ -111,6 +107,13 @@ struct CommitArgs {
     int32_t sortA;                 // pow2 >= capMax
     int32_t sortO;                 // pow2 >= deferCap
 };
+
+// LDS of one commit block: slot / where per row, the append keys and the
+// destroy keys (each padded to a power of two for the bitonic sort).
+static size_t commitSharedBytes(const CommitArgs &A)
+{
+    return (size_t)A.capMax * 8 + (size_t)(A.sortA + A.sortO) * 8;
+}
 
 static constexpr uint64_t kAppliedOp = 0xFFFF'FFFE'FFFF'FFFFull;
 
@@ -334,8 +337,8 @@ void launchStructuralCommit(LaunchCtx &lc)
     const CommitArgs *A = lc.exec ? (const CommitArgs *)lc.exec->commitArgs() : nullptr;
     if (!A || A->capMax <= 0) return;
     const uint32_t blocks = (uint32_t)std::min<int64_t>((lc.numWorlds + 255) / 256, 512);
-    const size_t lds = (size_t)A->capMax * 8 + (size_t)(A->sortA + A->sortO) * 8;
-    hipLaunchKernelGGL(structuralCommitKernel, dim3(blocks), dim3(256), lds,
+    const size_t lds = commitSharedBytes(*A);
+    MW_LAUNCH(structuralCommitKernel, dim3(blocks), dim3(256), lds,
                        (hipStream_t)lc.stream, *A);
 }
 
@@ -351,7 +354,7 @@ __global__ void clearRowsKernel(int32_t *num_rows, int32_t num_worlds)
 void launchClearRows(LaunchCtx &lc, int32_t archetype)
 {
     int32_t *rows = lc.view->arch[archetype].numRows;
-    hipLaunchKernelGGL(clearRowsKernel, dim3((lc.numWorlds + 255) / 256), dim3(256), 0,
+    MW_LAUNCH(clearRowsKernel, dim3((lc.numWorlds + 255) / 256), dim3(256), 0,
                        (hipStream_t)lc.stream, rows, lc.numWorlds);
 }
 
@@ -368,7 +371,7 @@ __global__ void resetTmpAllocKernel(uint32_t *offsets, int32_t num_worlds)
 void launchResetTmpAlloc(LaunchCtx &lc)
 {
     if (!lc.view->tmpOffset) return;
-    hipLaunchKernelGGL(resetTmpAllocKernel, dim3((lc.numWorlds + 255) / 256), dim3(256), 0,
+    MW_LAUNCH(resetTmpAllocKernel, dim3((lc.numWorlds + 255) / 256), dim3(256), 0,
                        (hipStream_t)lc.stream, lc.view->tmpOffset, lc.numWorlds);
 }
 
@@ -635,6 +638,17 @@ void Executor::uploadState()
         A.scratchPerBlock = ((uint64_t)A.capMax * col_max + 255) / 256 * 256;
         const int64_t blocks = std::min<int64_t>(dv.numWorlds, 512);
         if (A.capMax > 0) {
+            // refuse a configuration whose commit cannot launch (it would
+            // silently drop every structural op of a row-parallel node)
+            const size_t lds = commitSharedBytes(A);
+            if (hipx::residentBlocksNoThrow((const void *)&structuralCommitKernel, 256, lds) <= 0) {
+                throw std::runtime_error(
+                    "ordered commit needs " + std::to_string(lds) + " B of LDS per block (" +
+                    std::to_string(A.capMax) + " table rows, " + std::to_string(dv.deferCap) +
+                    " deferred destroys per world) but a workgroup holds " +
+                    std::to_string(hipx::maxLDSPerBlock()) +
+                    " B: lower max_deferred_destroys or the table capacities");
+            }
             MW_HIP_CHECK(hipMalloc(&A.scratch, std::max<size_t>(A.scratchPerBlock * blocks, 256)));
         }
     }
@@ -682,12 +696,12 @@ static void launchExports(Executor::Impl &I, const StateView &dv)
         }
         const ArchetypeView &av = dv.arch[b.archetype];
         if (b.scanOwner) {
-            hipLaunchKernelGGL(exportScanKernel, dim3(1), dim3(1024), 0, I.stream,
+            MW_LAUNCH(exportScanKernel, dim3(1), dim3(1024), 0, I.stream,
                                av.numRows, dv.numWorlds, b.offsets);
         }
         const uint32_t words = b.bytes / 4;
         const unsigned bx = (unsigned)std::max<int64_t>(1, ((int64_t)av.capacity * words + 255) / 256);
-        hipLaunchKernelGGL(exportCopyKernel, dim3(bx, dv.numWorlds), dim3(256), 0, I.stream,
+        MW_LAUNCH(exportCopyKernel, dim3(bx, dv.numWorlds), dim3(256), 0, I.stream,
                            (const uint32_t *)av.cols[b.column], av.capacity, words, av.numRows,
                            b.offsets, (uint32_t *)b.buf);
         if (I.trace) {
@@ -705,7 +719,7 @@ static bool isTimed(const Executor::Impl &I, int32_t node)
 static void traceMarker(Executor::Impl &I, mwGPU::DeviceEvent ev, uint32_t func, uint32_t inv,
                         uint32_t node)
 {
-    hipLaunchKernelGGL(mwGPU::traceMarkerKernel, dim3(1), dim3(1), 0, I.stream, I.trace,
+    MW_LAUNCH(mwGPU::traceMarkerKernel, dim3(1), dim3(1), 0, I.stream, I.trace,
                        (uint32_t)ev, func, inv, node);
 }
 
@@ -818,13 +832,23 @@ static void captureSegments(Executor::Impl &I, LaunchCtx &lc, const StateView &d
         sg.timedNode = last ? -1 : i;
         if (i > start || last || (start == 0 && I.trace)) {
             MW_HIP_CHECK(hipStreamBeginCapture(I.stream, hipStreamCaptureModeThreadLocal));
-            if (start == 0) traceStepBegin(I);
-            for (int32_t k = start; k < i; k++) launchNode(I, k, lc);
-            if (last) {
-                launchExports(I, dv);
-                traceStepEnd(I);
+            try {
+                if (start == 0) traceStepBegin(I);
+                for (int32_t k = start; k < i; k++) launchNode(I, k, lc);
+                if (last) {
+                    launchExports(I, dv);
+                    traceStepEnd(I);
+                }
+            } catch (...) {
+                // a launch refused its shape: leave the stream usable
+                hipGraph_t partial = nullptr;
+                (void)hipStreamEndCapture(I.stream, &partial);
+                if (partial) (void)hipGraphDestroy(partial);
+                (void)hipGetLastError();
+                throw;
             }
             MW_HIP_CHECK(hipStreamEndCapture(I.stream, &sg.graph));
+            if (!sg.graph) throw std::runtime_error("step graph capture returned no graph");
             MW_HIP_CHECK(hipGraphInstantiate(&sg.exec, sg.graph, nullptr, nullptr, 0));
         }
         I.segs.push_back(sg);

@@ -1,0 +1,54 @@
+// Kernel launch checks of the gfx950 back end.
+//
+// The reference aborts on every CUDA error (include/madrona/cuda_utils.hpp:
+// 46-54, ERR_CUDA / REQ_CUDA).  Here every failure becomes a
+// std::runtime_error that names the kernel; the C ABI turns it into a status
+// code plus mw_last_error().  Two kinds of failure are caught:
+//   * a launch shape the device cannot run: more LDS (static + dynamic) than
+//     a workgroup may hold, more lanes than the kernel's launch bounds, or
+//     zero resident blocks per CU.  A graph captured with such a launch
+//     replays without running the kernel and without an error, so the shape
+//     is checked on the host before every launch (cached per shape);
+//   * an error the runtime reports for the launch (hipGetLastError right
+//     after it).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace madrona::hipx {
+
+[[noreturn]] void hipFail(hipError_t err, const char *expr, const char *file, int line);
+
+// LDS one workgroup may hold on the current device (163840 B on gfx950).
+size_t maxLDSPerBlock();
+
+// Blocks of `threads` lanes with `dyn_lds` bytes of dynamic LDS that one CU
+// holds at once (>= 1), or throws naming `name` and the byte counts.
+int32_t residentBlocks(const void *fn, const char *name, int32_t threads, size_t dyn_lds);
+
+// The same test without throwing: 0 when the shape cannot launch.
+int32_t residentBlocksNoThrow(const void *fn, int32_t threads, size_t dyn_lds);
+
+// hipGetLastError after a launch; throws naming the kernel.
+void checkLaunched(const char *name);
+
+}
+
+#define MW_HIP_CHECK(expr)                                                          \
+    do {                                                                            \
+        const hipError_t err__ = (expr);                                            \
+        if (err__ != hipSuccess) ::madrona::hipx::hipFail(err__, #expr, __FILE__, __LINE__); \
+    } while (0)
+
+// hipLaunchKernelGGL with the shape check before and the error check after.
+#define MW_LAUNCH(kernel, grid, block, lds, stream, ...)                               \
+    do {                                                                               \
+        const dim3 blk__ = (block);                                                     \
+        ::madrona::hipx::residentBlocks((const void *)&(kernel), #kernel,              \
+                                        (int32_t)(blk__.x * blk__.y * blk__.z), (lds)); \
+        hipLaunchKernelGGL(kernel, grid, blk__, lds, stream, __VA_ARGS__);             \
+        ::madrona::hipx::checkLaunched(#kernel);                                       \
+    } while (0)

@@ -212,6 +212,7 @@ protected:
     MW_INLINE void clear(int32_t archetype, bool is_temporary);
     MW_INLINE uint64_t nextAppendKey() { return ((uint64_t)rowKey_ << 32) | ((uint64_t)(seq_++ & 0xFFFFu) << 16); }
     MW_INLINE Entity lockedAcquire(int32_t arch, int32_t row);
+    MW_INLINE void raiseFlag(int32_t bit);
     template <typename Fn> MW_INLINE void runJob(Fn &fn);
     MW_INLINE void drainDeferredJobs();
     MW_INLINE bool jobRunning(uint64_t key) const
@@ -349,12 +350,22 @@ MW_INLINE Loc Context::makeTemporary()
     return Loc { (uint32_t)arch, row };
 }
 
+// A world's error bit; row-parallel lanes of one world set bits concurrently.
+MW_INLINE void Context::raiseFlag(int32_t bit)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    atomicOr(state_->errorFlags + world_, bit);
+#else
+    state_->errorFlags[world_] |= bit;
+#endif
+}
+
 MW_INLINE void Context::clear(int32_t arch, bool is_temporary)
 {                                              // src/core/state.cpp:565-581
     if (rowParallel()) {
         // a clear inside a row walk has no per-row order to keep: use a
         // ClearTmpNode or a world-serial node
-        state_->errorFlags[world_] |= kErrFlagRowParallelOp;
+        raiseFlag(kErrFlagRowParallelOp);
         return;
     }
     if (!is_temporary) {
@@ -374,7 +385,7 @@ MW_INLINE void *Context::tmpAlloc(uint64_t num_bytes)
     const uint64_t bytes = (num_bytes + 255) & ~uint64_t(255);
     if (bytes == 0) return nullptr;
     if (bytes > state_->tmpBytesPerWorld || !state_->tmpArena) {
-        state_->errorFlags[world_] |= kErrFlagTmpAllocFull;
+        raiseFlag(kErrFlagTmpAllocFull);
         return nullptr;
     }
     uint32_t off;
@@ -388,11 +399,7 @@ MW_INLINE void *Context::tmpAlloc(uint64_t num_bytes)
         if ((uint64_t)off + bytes <= state_->tmpBytesPerWorld) state_->tmpOffset[world_] = off + (uint32_t)bytes;
     }
     if ((uint64_t)off + bytes > state_->tmpBytesPerWorld) {
-#if defined(__HIP_DEVICE_COMPILE__)
-        atomicOr(state_->errorFlags + world_, kErrFlagTmpAllocFull);
-#else
-        state_->errorFlags[world_] |= kErrFlagTmpAllocFull;
-#endif
+        raiseFlag(kErrFlagTmpAllocFull);
         return nullptr;
     }
     return state_->tmpArena + (size_t)world_ * state_->tmpBytesPerWorld + off;
@@ -511,7 +518,7 @@ MW_INLINE JobID Context::submit(Fn &&fn, bool is_child, DepTs &&...)
                 return JobID { 0, jobDepth_ + 1 };
             }
         }
-        state_->errorFlags[world_] |= kErrFlagJobDropped;
+        raiseFlag(kErrFlagJobDropped);
         return JobID::none();
     }
     runJob(fn);

@@ -127,6 +127,7 @@ def _declare(lib):
     lib.mw_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_int32]
     lib.mw_phys_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.mw_phys_kernel_variants.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
     lib.mw_copy_exported.restype = ctypes.c_int64
     lib.mw_copy_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
     lib.mw_copy_exported_async.restype = ctypes.c_int64
@@ -206,7 +207,7 @@ C_ABI_SYMBOLS = (
     "mw_num_nodes", "mw_node_name", "mw_node_blocks_per_cu", "mw_set_node_blocks_per_cu",
     "mw_parse_exec_config_override", "mw_parse_exec_config_file",
     "mw_export_row_bytes", "mw_load_env", "mw_num_envs", "mw_env_name",
-    "mw_entity_loc", "mw_copy_exported_async",
+    "mw_entity_loc", "mw_copy_exported_async", "mw_phys_kernel_variants",
 )
 
 
@@ -355,7 +356,7 @@ class Executor:
     """A batch of worlds of one environment on one GPU."""
 
     def __init__(self, env, num_worlds, user_cfg, inits, init_stride, gpu_id=0,
-                 default_capacity=64, use_graph=True, tmp_alloc_bytes=-1,
+                 default_capacity=64, use_graph=True, tmp_alloc_bytes=0,
                  max_deferred_destroys=0, backend=None, num_workers=0):
         # backend "cpu": the same world on the CPU back end (num_workers
         # pinned host threads, 0 = every core of the affinity mask)
@@ -647,6 +648,15 @@ class CollisionsSim(Executor):
                                k.ctypes.data_as(ctypes.c_void_p)) < 0:
             raise _err(self._lib)
         return c, k
+
+    def kernel_variants(self):
+        """{kernel: True when it runs its global-image variant} (mw_create
+        decides per LDS image; plane_lds: the plane kernel's LDS hull tables)."""
+        out = np.zeros(6, np.int32)
+        if self._lib.mw_phys_kernel_variants(self.h, out.ctypes.data_as(ctypes.c_void_p), 6) < 0:
+            raise _err(self._lib)
+        keys = ("refit", "find_overlaps", "sat", "contact", "solver", "plane_lds")
+        return {k: bool(v) for k, v in zip(keys, out)}
 
     def bvh(self, w, cap=4096):
         nodes = np.zeros(cap, BVH_NODE_DTYPE)

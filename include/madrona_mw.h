@@ -50,7 +50,9 @@ typedef struct mw_config {
     int32_t default_capacity;  /* rows per world for archetypes w/o a size   */
     int32_t use_graph;         /* 1: replay the step as one hipGraph         */
     int32_t tmp_alloc_bytes;   /* Context::tmpAlloc arena per world (reference
-                                  StateManager::tmpAlloc); -1: 16 KiB, 0: none */
+                                  StateManager::tmpAlloc) in bytes; 0: the
+                                  default 16 KiB, -1: no arena (tmpAlloc
+                                  returns null and flags the world)         */
     int32_t max_deferred_destroys; /* destroyEntityNow calls per world per
                                   row-parallel node (applied in the reference's
                                   order after the node); 0: 256              */
@@ -198,6 +200,14 @@ int32_t mw_phys_read_bvh(mw_exec *exec, int32_t world, void *nodes_out,
 
 /* per-world candidate / contact counts of the last step / substep. */
 int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *contacts_out);
+
+/* Which variant of each LDS-staging physics kernel the executor runs (mw_create
+ * picks it: a world / hull image that does not fit a workgroup's LDS moves to
+ * a global slab, same results).  out[0..5] = 1 for: refit on the global node
+ * slab, findOverlaps / SAT / contact / solver with a global image, and (last)
+ * the plane kernel's LDS hull tables.  Returns 6, or -1 without physics.
+ * MADRONA_MW_FORCE_GLOBAL_IMAGES=1 at mw_create forces the global variants. */
+int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t n);
 
 /* physics kernel timing hook for the bench: records HIP events around each
  * launch of the named node kind on the executor stream ("SolverNode", ...).

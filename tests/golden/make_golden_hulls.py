@@ -30,13 +30,15 @@ sys.path.insert(0, os.path.dirname(HERE))
 import oracle_lib as ol  # noqa: E402
 
 DATA = os.path.join(ROOT, "gpu-ecs-madrona_amd", "data")
-NAMES = ("cube", "wedge", "hex_prism", "octahedron", "disc16")
+NAMES = ("cube", "wedge", "hex_prism", "octahedron", "disc16", "disc64")
 CASES = {
     "mixed": dict(hulls=("cube", "wedge", "hex_prism"), W=3, N=24, SEED=5,
                   SNAPS=(1, 50, 150, 300), ORC=(300,)),
     "octa": dict(hulls=("octahedron",), W=3, N=64, SEED=7, SNAPS=(1, 60, 200), ORC=(200,)),
     "disc": dict(hulls=("disc16", "octahedron"), W=3, N=32, SEED=7, SNAPS=(1, 20),
                  ORC=(120,)),
+    # 64-vertex caps: the GPU contact / SAT kernels' global-image variants
+    "disc64": dict(hulls=("disc64", "cube"), W=3, N=32, SEED=3, SNAPS=(1, 20), ORC=(100,)),
 }
 
 

@@ -27,10 +27,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 DATA = os.path.join(ROOT, "gpu-ecs-madrona_amd", "data")
 GOLDEN = os.path.join(HERE, "golden", "hulls_ref.npz")
-NAMES = ("cube", "wedge", "hex_prism", "octahedron", "disc16")
+NAMES = ("cube", "wedge", "hex_prism", "octahedron", "disc16", "disc64")
 CASES = {"mixed": ("cube", "wedge", "hex_prism"), "octa": ("octahedron",),
-         "disc": ("disc16", "octahedron")}
-CASE_N = {"mixed": 24, "octa": 64, "disc": 32}
+         "disc": ("disc16", "octahedron"), "disc64": ("disc64", "cube")}
+CASE_N = {"mixed": 24, "octa": 64, "disc": 32, "disc64": 32}
 
 
 def _eq(a, b):
@@ -171,6 +171,7 @@ def test_oracle_hull_matches_live_reference(name):
 @pytest.mark.parametrize("hulls,n,seed,steps", [
     (("cube", "wedge", "hex_prism", "octahedron"), 48, 11, 150),
     (("disc16", "hex_prism"), 24, 2, 100),
+    (("disc64", "cube"), 24, 4, 60),
     (("octahedron", "wedge"), 128, 1, 30),
 ])
 def test_hull_worlds_oracle_matches_live_reference_until_undefined(hulls, n, seed, steps):
