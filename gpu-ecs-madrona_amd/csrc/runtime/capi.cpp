@@ -178,6 +178,7 @@ mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
                                                                 : cfg->tmp_alloc_bytes;
         ec.maxDeferredPerWorld = cfg->max_deferred_destroys;
         ec.numWorkers = cfg->num_workers;
+        ec.serialNodes = cfg->serial_nodes != 0;
         if (cfg->tmp_alloc_bytes < -1 || cfg->max_deferred_destroys < 0 ||
             cfg->max_deferred_destroys > 65536) {
             throw std::runtime_error("mw_create: tmp_alloc_bytes >= -1 and 0 <= max_deferred_destroys <= 65536");

@@ -60,6 +60,18 @@ void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype, int32
     MW_HIP_CHECK(hipLaunchKernel(kernel, grid, block, kargs, 0, (hipStream_t)lc.stream));
 }
 
+// World-serial row nodes: numWorlds invocations of `threads` lanes.
+void launchSerialKernel(const void *kernel, LaunchCtx &lc, int32_t threads, const void *query)
+{
+    const int64_t lanes = (int64_t)lc.numWorlds * threads;
+    const uint32_t blocks = lc.capGrid((uint32_t)std::min<int64_t>((lanes + 255) / 256, 0x7fffffff));
+    if (blocks == 0) return;
+    StateView *st = lc.devState;
+    void *kargs[] = { &st, const_cast<void *>(query) };
+    hipx::residentBlocks(kernel, "serialForKernel", 256, 0);
+    MW_HIP_CHECK(hipLaunchKernel(kernel, dim3(blocks), dim3(256), kargs, 0, (hipStream_t)lc.stream));
+}
+
 // addNodeFn nodes: a fixed count per world sizes the grid; a dynamic count
 // is only known on the device, so its grid is persistent (grid-stride).
 void launchNodeFnKernel(const void *kernel, LaunchCtx &lc, void *node_dev, uint32_t fixed_count,
@@ -542,6 +554,7 @@ static LaunchCtx makeLaunchCtx(Executor::Impl &I, Executor *exec)
     const StateView &dv = I.mgr->deviceViewHost();
     LaunchCtx lc { I.stream, I.mgr->deviceView(), &dv, I.cfg.numWorlds, exec };
     lc.nodeData = I.nodeDataDev;
+    lc.serialNodes = I.cfg.serialNodes;
     return lc;
 }
 

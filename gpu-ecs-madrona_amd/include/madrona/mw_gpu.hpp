@@ -36,6 +36,9 @@ struct ExecConfig {
     int32_t maxDeferredPerWorld = 0;      // 0: kDefaultDeferredPerWorld
     int32_t numWorkers = 0;               // CPU back end: worker threads (0: every core
                                           // of the process's affinity mask)
+    int32_t serialNodes = 0;              // 1: every ParallelForNode / CustomParallelForNode
+                                          // runs world-serially (WorldSerialForNode); the
+                                          // CPU back end always does
 };
 
 // Non-template core (csrc/runtime/executor.cpp).

@@ -60,6 +60,10 @@ struct LaunchCtx {
     // Device copies of the graph's node data blocks (TaskGraph::NodeData,
     // constructNodeData), uploaded once when the graph is set.
     char *nodeData = nullptr;
+    // Executor-wide world-serial mode (ExecConfig::serialNodes): every
+    // ParallelForNode / CustomParallelForNode walks each world's rows in
+    // order on one invocation, as the reference's ParallelForNode::run does.
+    int32_t serialNodes = 0;
 
     // Grid for a grid-stride kernel that needs `blocks` blocks to cover its
     // work in one pass: capped at numCUs x blocksPerCU when configured.
@@ -348,6 +352,10 @@ void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype, int32
 void launchWorldKernel(const void *kernel, LaunchCtx &lc);
 void launchNodeFnKernel(const void *kernel, LaunchCtx &lc, void *node_dev, uint32_t fixed_count,
                         uint32_t threads_per_invocation);
+// World-serial row walk: one invocation (threads_per_invocation lanes) per
+// world; `query` points at the node's Query (a kernel argument by value).
+void launchSerialKernel(const void *kernel, LaunchCtx &lc, int32_t threads_per_invocation,
+                        const void *query);
 // The ordered structural commit of a row-parallel node (see Context): a
 // no-op for worlds whose lanes made / destroyed nothing.
 void launchStructuralCommit(LaunchCtx &lc);
@@ -455,30 +463,82 @@ parallelForKernel(const StateView *__restrict__ st_in, int32_t arch, int32_t que
 
 }
 
+namespace detail {
+
+#if defined(__HIPCC__)
+// World-serial walk (reference ParallelForNode::run, taskgraph.inl:63-71;
+// the reference's megakernel also runs a world's rows on one thread,
+// src/mw/device/megakernel_impl.inl:44-55): invocation = world, its
+// threads_per_invocation lanes walk the query's archetypes in order and
+// every row in order, rows counted when each archetype's walk starts.  The
+// context is world-serial, so structural ops act immediately and entity IDs
+// are exactly the reference's; a row sees every write of the rows before it.
+template <typename ContextT, auto Fn, int32_t threads, typename... ComponentTs>
+__global__ void __launch_bounds__(256)
+serialForKernel(const StateView *__restrict__ st_in, Query<ComponentTs...> q)
+{
+    MW_TRACE_BLOCK(0);
+    StateView *st = const_cast<StateView *>(st_in);
+    const int64_t total = (int64_t)st->numWorlds * threads;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t w = (int32_t)(t / threads);
+        ContextT ctx = worldContext<ContextT>(st, w);
+        for (int32_t a = 0; a < q.numArchetypes; a++) {
+            const int32_t arch = q.archetypes[a];
+            ColArgs<sizeof...(ComponentTs)> cols;
+            for (int32_t c = 0; c < (int32_t)sizeof...(ComponentTs); c++) cols.c[c] = q.cols[a][c];
+            const int32_t n = st->arch[arch].numRows[w];
+#pragma unroll 1
+            for (int32_t r = 0; r < n; r++) {
+                invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, r,
+                                                        std::index_sequence_for<ComponentTs...> {});
+                if constexpr (threads > 1) {
+                    // the group's writes before its next row
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
+            }
+        }
+    }
+}
+#endif
+
+// ParallelForNode / CustomParallelForNode (kSerial = false: row-parallel
+// unless the executor runs every node world-serially) and WorldSerialForNode
+// (kSerial = true: always world-serial).
 template <typename ContextT, auto Fn, int32_t threads_per_invocation, int32_t items_per_invocation,
-          typename... ComponentTs>
-class CustomParallelForNode : public NodeBase {
+          bool kSerial, typename... ComponentTs>
+class RowForNode : public NodeBase {
     static_assert(threads_per_invocation >= 1 && threads_per_invocation <= 64 &&
                   (threads_per_invocation & (threads_per_invocation - 1)) == 0,
                   "threads_per_invocation: a power of two <= 64 (one wave)");
     static_assert(items_per_invocation >= 1);
 public:
-    explicit CustomParallelForNode(Context &ctx) : query_(ctx.query<ComponentTs...>()) {}
+    explicit RowForNode(Context &ctx) : query_(ctx.query<ComponentTs...>()) {}
 
     static TaskGraph::NodeID addToGraph(Context &ctx, TaskGraph::Builder &builder,
                                         Span<const TaskGraph::NodeID> deps)
     {
-        return builder.addDefaultNode<CustomParallelForNode>(deps, ctx);
+        return builder.addDefaultNode<RowForNode>(deps, ctx);
     }
     static TaskGraph::NodeID addToGraph(TaskGraph::Builder &builder,
                                         Span<const TaskGraph::NodeID> deps)
     {
-        return builder.addDefaultNode<CustomParallelForNode>(deps, builder.context());
+        return builder.addDefaultNode<RowForNode>(deps, builder.context());
     }
 
-    static void launch(CustomParallelForNode *self, LaunchCtx &lc)
+    static void launch(RowForNode *self, LaunchCtx &lc)
     {
 #if defined(__HIPCC__)
+        if (kSerial || lc.serialNodes) {
+            detail::launchSerialKernel(
+                (const void *)&detail::serialForKernel<ContextT, Fn, threads_per_invocation,
+                                                       ComponentTs...>,
+                lc, threads_per_invocation, &self->query_);
+            return;
+        }
         for (int32_t a = 0; a < self->query_.numArchetypes; a++) {
             detail::ColArgs<sizeof...(ComponentTs)> cols;
             for (int32_t c = 0; c < (int32_t)sizeof...(ComponentTs); c++) {
@@ -501,7 +561,7 @@ public:
     // 63-71) -- the world's matching rows in query order, rows counted when
     // each archetype's walk starts, structural ops immediate (world-serial).
     // A cooperative Fn runs once per invocation lane, lanes in order.
-    static void runWorld(CustomParallelForNode *self, CpuRunCtx &rc, int32_t w)
+    static void runWorld(RowForNode *self, CpuRunCtx &rc, int32_t w)
     {
         ContextT ctx = detail::worldContext<ContextT>(rc.state, w, rc.mgr);
         StateView *st = rc.state;
@@ -524,6 +584,7 @@ public:
 
     static const char *nodeName()
     {
+        if (kSerial) return "WorldSerialForNode";
         return threads_per_invocation == 1 && items_per_invocation == 1 ? "ParallelForNode"
                                                                         : "CustomParallelForNode";
     }
@@ -531,10 +592,25 @@ public:
     Query<ComponentTs...> query_;
 };
 
+}
+
+template <typename ContextT, auto Fn, int32_t threads_per_invocation, int32_t items_per_invocation,
+          typename... ComponentTs>
+using CustomParallelForNode = detail::RowForNode<ContextT, Fn, threads_per_invocation,
+                                                 items_per_invocation, false, ComponentTs...>;
+
 // Reference device taskgraph.hpp:184-186 (the CPU class of the same name
-// walks rows serially; the commit keeps its order).
+// walks rows serially; the commit keeps its structural order).
 template <typename ContextT, auto Fn, typename... ComponentTs>
 using ParallelForNode = CustomParallelForNode<ContextT, Fn, 1, 1, ComponentTs...>;
+
+// A ParallelForNode that always runs world-serially: for bodies whose result
+// depends on the reference's row order beyond structural ops -- a row that
+// reads or writes another row's components (ctx.get<T>(other)) which this
+// node also writes, state carried from row to row through world data, or
+// entity IDs that must equal the reference's.
+template <typename ContextT, auto Fn, typename... ComponentTs>
+using WorldSerialForNode = detail::RowForNode<ContextT, Fn, 1, 1, true, ComponentTs...>;
 
 // ---------------------------------------------------------------------------
 // Device nodes of addNodeFn (run(int32_t invocation_idx) on the device).

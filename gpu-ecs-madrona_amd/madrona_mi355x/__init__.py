@@ -55,7 +55,7 @@ class MwConfig(ctypes.Structure):
     _fields_ = [("num_worlds", ctypes.c_int32), ("gpu_id", ctypes.c_int32),
                 ("default_capacity", ctypes.c_int32), ("use_graph", ctypes.c_int32),
                 ("tmp_alloc_bytes", ctypes.c_int32), ("max_deferred_destroys", ctypes.c_int32),
-                ("num_workers", ctypes.c_int32)]
+                ("num_workers", ctypes.c_int32), ("serial_nodes", ctypes.c_int32)]
 
 
 class CollisionsConfig(ctypes.Structure):
@@ -357,16 +357,19 @@ class Executor:
 
     def __init__(self, env, num_worlds, user_cfg, inits, init_stride, gpu_id=0,
                  default_capacity=64, use_graph=True, tmp_alloc_bytes=0,
-                 max_deferred_destroys=0, backend=None, num_workers=0):
+                 max_deferred_destroys=0, backend=None, num_workers=0, serial_nodes=False):
         # backend "cpu": the same world on the CPU back end (num_workers
-        # pinned host threads, 0 = every core of the affinity mask)
+        # pinned host threads, 0 = every core of the affinity mask).
+        # serial_nodes: every ParallelForNode walks each world's rows in
+        # order (the reference's semantics for any node body)
         backend = backend or DEFAULT_BACKEND
         if backend not in ("gpu", "cpu"):
             raise ValueError(f"backend must be 'gpu' or 'cpu', not {backend!r}")
         self._lib = backend_library(backend)
         self.backend = backend
         cfg = MwConfig(num_worlds, gpu_id, default_capacity, 1 if use_graph else 0,
-                       tmp_alloc_bytes, max_deferred_destroys, num_workers)
+                       tmp_alloc_bytes, max_deferred_destroys, num_workers,
+                       1 if serial_nodes else 0)
         self._keep = (user_cfg, inits)
         self.h = self._lib.mw_create(env.encode(), ctypes.byref(cfg), ctypes.byref(user_cfg),
                                 ctypes.sizeof(user_cfg), ctypes.cast(inits, ctypes.c_void_p),

@@ -60,6 +60,13 @@ typedef struct mw_config {
                                   core (reference ThreadPoolExecutor::Config::
                                   numWorkers, mw_cpu.hpp:20-27); 0: every core
                                   of the affinity mask.  Ignored on gfx950.   */
+    int32_t serial_nodes;      /* 1: run every ParallelForNode /
+                                  CustomParallelForNode world-serially (one
+                                  invocation per world walks its rows in order,
+                                  as the reference's ParallelForNode::run,
+                                  taskgraph.inl:63-71); 0: row-parallel lanes
+                                  with the ordered structural commit.  The CPU
+                                  back end is always world-serial.          */
 } mw_config;
 
 /* "collisions": rigid-body workload of SURVEY.md §8(d) C3/C4 (128 unit cube

@@ -154,10 +154,15 @@ class RefEcsOps:
 SPAWN_CONTENT = ("p_gen", "p_id", "born", "hits", "serial")
 
 
-def compare_world(sim, ref, w, where=""):
+def compare_world(sim, ref, w, where="", exact_ids=False):
     """Bit-exact agents, pairs, stats and spawn contents / row order; spawn
     entity IDs (made by parallel lanes) checked for consistency: unique,
-    alive, mapped to their own row (SURVEY.md §8c relabelling rule)."""
+    alive, mapped to their own row (SURVEY.md §8c relabelling rule).
+    exact_ids: the spawn rows' entity IDs equal the reference's too (a
+    world-serial run: mw_config.serial_nodes or the CPU back end)."""
+    if exact_ids:
+        a, b = sim.spawns(w), ref.spawns(w)
+        assert a.tobytes() == b.tobytes(), f"{where} world {w}: spawn rows / IDs differ"
     a, b = sim.agents(w), ref.agents(w)
     assert a.tobytes() == b.tobytes(), f"{where} world {w}: agents differ"
     a, b = sim.pairs(w), ref.pairs(w)
