@@ -98,6 +98,26 @@ EnvFactory findEnv(const char *name)
     return it == envTable().end() ? nullptr : it->second;
 }
 
+int32_t loadEnvObject(const char *so_path)
+{
+    if (!so_path) throw std::runtime_error("mw_load_env: null path");
+    const size_t before = envTable().size();
+    envClashes().clear();
+    // RTLD_NOW: unresolved symbols fail here, not at the first step.
+    // The object's DT_NEEDED libmadrona_mw.so resolves to this loaded
+    // library by its soname, so the world registers into this table.
+    void *h = dlopen(so_path, RTLD_NOW | RTLD_LOCAL);
+    if (!h) throw std::runtime_error(std::string("mw_load_env: ") + dlerror());
+    if (!envClashes().empty()) {
+        std::string names;
+        for (const std::string &n : envClashes()) names += (names.empty() ? "'" : ", '") + n + "'";
+        envClashes().clear();
+        throw std::runtime_error(std::string("mw_load_env: ") + so_path + " registers " + names +
+                                 ", already registered by another object (the first one stays)");
+    }
+    return (int32_t)(envTable().size() - before);
+}
+
 }
 
 using namespace madrona;
@@ -179,6 +199,8 @@ mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
         ec.maxDeferredPerWorld = cfg->max_deferred_destroys;
         ec.numWorkers = cfg->num_workers;
         ec.serialNodes = cfg->serial_nodes != 0;
+        if (cfg->tmp_pool_bytes < -1) throw std::runtime_error("mw_create: tmp_pool_bytes >= -1");
+        ec.tmpPoolBytes = cfg->tmp_pool_bytes == 0 ? -1 : cfg->tmp_pool_bytes == -1 ? 0 : cfg->tmp_pool_bytes;
         if (cfg->tmp_alloc_bytes < -1 || cfg->max_deferred_destroys < 0 ||
             cfg->max_deferred_destroys > 65536) {
             throw std::runtime_error("mw_create: tmp_alloc_bytes >= -1 and 0 <= max_deferred_destroys <= 65536");
@@ -190,24 +212,7 @@ mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
 
 int32_t mw_load_env(const char *so_path)
 {
-    MW_TRY({
-        if (!so_path) throw std::runtime_error("mw_load_env: null path");
-        const size_t before = envTable().size();
-        envClashes().clear();
-        // RTLD_NOW: unresolved symbols fail here, not at the first step.
-        // The object's DT_NEEDED libmadrona_mw.so resolves to this loaded
-        // library by its soname, so the world registers into this table.
-        void *h = dlopen(so_path, RTLD_NOW | RTLD_LOCAL);
-        if (!h) throw std::runtime_error(std::string("mw_load_env: ") + dlerror());
-        if (!envClashes().empty()) {
-            std::string names;
-            for (const std::string &n : envClashes()) names += (names.empty() ? "'" : ", '") + n + "'";
-            envClashes().clear();
-            throw std::runtime_error(std::string("mw_load_env: ") + so_path + " registers " + names +
-                                     ", already registered by another object (the first one stays)");
-        }
-        return (int32_t)(envTable().size() - before);
-    }, -1)
+    MW_TRY({ return loadEnvObject(so_path); }, -1)
 }
 
 int32_t mw_num_envs(void) { return (int32_t)envTable().size(); }

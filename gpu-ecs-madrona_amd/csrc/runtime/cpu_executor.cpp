@@ -194,7 +194,11 @@ Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
     impl_->mgr.reset(new StateManager(StateManager::Config {
         cfg.numWorlds, cfg.defaultCapacity,
         cfg.tmpAllocBytesPerWorld >= 0 ? cfg.tmpAllocBytesPerWorld : kDefaultTmpAllocBytes,
-        cfg.maxDeferredPerWorld > 0 ? cfg.maxDeferredPerWorld : kDefaultDeferredPerWorld }));
+        cfg.maxDeferredPerWorld > 0 ? cfg.maxDeferredPerWorld : kDefaultDeferredPerWorld,
+        cfg.tmpPoolBytes >= 0 ? cfg.tmpPoolBytes
+                              : defaultTmpPoolBytes(cfg.numWorlds, cfg.tmpAllocBytesPerWorld >= 0
+                                                                       ? cfg.tmpAllocBytesPerWorld
+                                                                       : kDefaultTmpAllocBytes) }));
     impl_->pool.reset(new CpuThreadPool(cfg.numWorkers));
 }
 

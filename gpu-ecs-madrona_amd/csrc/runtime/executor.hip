@@ -373,18 +373,20 @@ void launchClearRows(LaunchCtx &lc, int32_t archetype)
 // A kernel rather than a memset node: measured on the MI355X box, a
 // hipMemsetAsync captured into the step graph left every other world's
 // offset unreset once host hipMemcpy calls ran between graph replays.
-__global__ void resetTmpAllocKernel(uint32_t *offsets, int32_t num_worlds)
+__global__ void resetTmpAllocKernel(uint32_t *offsets, int32_t num_worlds,
+                                    unsigned long long *pool_offset)
 {
     MW_TRACE_BLOCK(0);
     const int32_t w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w < num_worlds) offsets[w] = 0;
+    if (offsets && w < num_worlds) offsets[w] = 0;
+    if (pool_offset && w == 0) *pool_offset = 0;      // every world resets here
 }
 
 void launchResetTmpAlloc(LaunchCtx &lc)
 {
-    if (!lc.view->tmpOffset) return;
+    if (!lc.view->tmpOffset && !lc.view->tmpPoolOffset) return;
     MW_LAUNCH(resetTmpAllocKernel, dim3((lc.numWorlds + 255) / 256), dim3(256), 0,
-                       (hipStream_t)lc.stream, lc.view->tmpOffset, lc.numWorlds);
+              (hipStream_t)lc.stream, lc.view->tmpOffset, lc.numWorlds, lc.view->tmpPoolOffset);
 }
 
 // Packed export: world w's rows land at offset prefix(numRows)[w]
@@ -568,7 +570,11 @@ Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
     impl_->mgr.reset(new StateManager(StateManager::Config {
         cfg.numWorlds, cfg.defaultCapacity,
         cfg.tmpAllocBytesPerWorld >= 0 ? cfg.tmpAllocBytesPerWorld : kDefaultTmpAllocBytes,
-        cfg.maxDeferredPerWorld > 0 ? cfg.maxDeferredPerWorld : kDefaultDeferredPerWorld }));
+        cfg.maxDeferredPerWorld > 0 ? cfg.maxDeferredPerWorld : kDefaultDeferredPerWorld,
+        cfg.tmpPoolBytes >= 0 ? cfg.tmpPoolBytes
+                              : defaultTmpPoolBytes(cfg.numWorlds, cfg.tmpAllocBytesPerWorld >= 0
+                                                                       ? cfg.tmpAllocBytesPerWorld
+                                                                       : kDefaultTmpAllocBytes) }));
 }
 
 Executor::~Executor()

@@ -65,8 +65,19 @@ struct StateManager::Impl {
     struct ColAlloc { char *host; char *dev; size_t bytes; bool temporary; };
     std::vector<ColAlloc> colAllocs;
 
+    // chained tmpAlloc blocks of the host view, per world
+    struct HostTmpOverflow {
+        std::vector<std::vector<void *>> blocks;
+    };
+    std::unique_ptr<HostTmpOverflow> hostOverflow;
+
     ~Impl()
     {
+        if (hostOverflow) {
+            for (auto &v : hostOverflow->blocks) {
+                for (void *p : v) free(p);
+            }
+        }
         for (char *p : hostAllocs) free(p);
 #if !defined(MW_CPU_BACKEND)
         for (void *p : devAllocs) (void)hipFree(p);
@@ -83,6 +94,23 @@ static char *hostAlloc(StateManager::Impl &impl, size_t bytes)
     memset(p, 0, bytes);
     impl.hostAllocs.push_back(p);
     return p;
+}
+
+void *hostTmpOverflowAlloc(StateView &v, int32_t world, uint64_t bytes)
+{
+    auto *o = (StateManager::Impl::HostTmpOverflow *)v.hostTmpOverflow;
+    if (!o || world < 0 || world >= (int32_t)o->blocks.size()) return nullptr;
+    void *p = aligned_alloc(256, (bytes + 255) & ~uint64_t(255));
+    if (p) o->blocks[world].push_back(p);
+    return p;
+}
+
+void hostTmpOverflowReset(StateView &v, int32_t world)
+{
+    auto *o = (StateManager::Impl::HostTmpOverflow *)v.hostTmpOverflow;
+    if (!o || world < 0 || world >= (int32_t)o->blocks.size()) return;
+    for (void *p : o->blocks[world]) free(p);
+    o->blocks[world].clear();
 }
 
 ECSRegistry::ECSRegistry(StateManager *state_mgr, void **export_ptrs)
@@ -254,6 +282,11 @@ void StateManager::finalizeLayout(uint32_t world_data_bytes, uint32_t world_data
         v.tmpArena = hostAlloc(I, (size_t)v.tmpBytesPerWorld * W);
         v.tmpOffset = (uint32_t *)hostAlloc(I, sizeof(uint32_t) * W);
     }
+    if (I.cfg.tmpPoolBytes > 0) {
+        I.hostOverflow.reset(new Impl::HostTmpOverflow);
+        I.hostOverflow->blocks.resize(W);
+        v.hostTmpOverflow = I.hostOverflow.get();
+    }
     v.deferCap = std::max(1, I.cfg.deferCap);
 
     // Singleton entities, per world in registration order, from the init
@@ -367,6 +400,16 @@ void StateManager::uploadToDevice(void *stream_ptr)
         copy(d.tmpArena, I.host.tmpArena, (size_t)d.tmpBytesPerWorld * W);
         d.tmpOffset = (uint32_t *)devAlloc(sizeof(uint32_t) * W);
         copy(d.tmpOffset, I.host.tmpOffset, sizeof(uint32_t) * W);
+    }
+    d.hostTmpOverflow = nullptr;
+    d.tmpPool = nullptr;
+    d.tmpPoolOffset = nullptr;
+    d.tmpPoolBytes = 0;
+    if (I.cfg.tmpPoolBytes > 0) {
+        d.tmpPoolBytes = (uint64_t)I.cfg.tmpPoolBytes / 256 * 256;
+        d.tmpPool = devAlloc(d.tmpPoolBytes);
+        d.tmpPoolOffset = (unsigned long long *)devAlloc(sizeof(unsigned long long));
+        MW_HIP_CHECK(hipMemsetAsync(d.tmpPoolOffset, 0, sizeof(unsigned long long), stream));
     }
 
     MW_HIP_CHECK(hipMalloc(&I.devView, sizeof(StateView)));

@@ -378,36 +378,49 @@ MW_INLINE void Context::clear(int32_t arch, bool is_temporary)
 
 // Per-world bump allocator (reference TmpAllocator::alloc,
 // src/core/state.cpp:95-114: 256-byte granules); row-parallel lanes bump
-// the world's offset atomically.  Exhaustion returns null and raises
-// kErrFlagTmpAllocFull (the reference chains another block).
+// the world's offset atomically.  Past the world's arena an allocation is
+// chained (the reference allocates another block): from the device pool
+// shared by all worlds, or a host heap block; only when that is exhausted
+// (or off) does tmpAlloc return null and raise kErrFlagTmpAllocFull.
 MW_INLINE void *Context::tmpAlloc(uint64_t num_bytes)
 {
     const uint64_t bytes = (num_bytes + 255) & ~uint64_t(255);
     if (bytes == 0) return nullptr;
-    if (bytes > state_->tmpBytesPerWorld || !state_->tmpArena) {
-        raiseFlag(kErrFlagTmpAllocFull);
-        return nullptr;
-    }
-    uint32_t off;
+    if (state_->tmpArena && bytes <= state_->tmpBytesPerWorld) {
+        uint32_t off;
 #if defined(__HIP_DEVICE_COMPILE__)
-    if (rowParallel()) {
-        off = atomicAdd(state_->tmpOffset + world_, (uint32_t)bytes);
-    } else
+        if (rowParallel()) {
+            off = atomicAdd(state_->tmpOffset + world_, (uint32_t)bytes);
+        } else
 #endif
-    {
-        off = state_->tmpOffset[world_];
-        if ((uint64_t)off + bytes <= state_->tmpBytesPerWorld) state_->tmpOffset[world_] = off + (uint32_t)bytes;
+        {
+            off = state_->tmpOffset[world_];
+            if ((uint64_t)off + bytes <= state_->tmpBytesPerWorld) state_->tmpOffset[world_] = off + (uint32_t)bytes;
+        }
+        if ((uint64_t)off + bytes <= state_->tmpBytesPerWorld) {
+            return state_->tmpArena + (size_t)world_ * state_->tmpBytesPerWorld + off;
+        }
     }
-    if ((uint64_t)off + bytes > state_->tmpBytesPerWorld) {
-        raiseFlag(kErrFlagTmpAllocFull);
-        return nullptr;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (state_->tmpPool) {
+        const unsigned long long off = atomicAdd(state_->tmpPoolOffset, (unsigned long long)bytes);
+        if (off + bytes <= state_->tmpPoolBytes) return state_->tmpPool + off;
     }
-    return state_->tmpArena + (size_t)world_ * state_->tmpBytesPerWorld + off;
+#else
+    if (void *p = hostTmpOverflowAlloc(*state_, world_, bytes)) return p;
+#endif
+    raiseFlag(kErrFlagTmpAllocFull);
+    return nullptr;
 }
 
+// The world's arena (device: its pool blocks are reclaimed at the next
+// ResetTmpAllocNode, which resets every world at once).
 MW_INLINE void Context::resetTmpAlloc()
 {                                              // src/core/state.cpp:116-127
     if (state_->tmpOffset) state_->tmpOffset[world_] = 0;
+#if !defined(__HIP_DEVICE_COMPILE__)
+    hostTmpOverflowReset(*state_, world_);
+#endif
 }
 
 template <typename ComponentT>

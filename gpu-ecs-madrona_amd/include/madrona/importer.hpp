@@ -24,6 +24,13 @@ struct SourceMesh {
     uint32_t numFaces;
 };
 
+// One object of meshes (reference imp::SourceObject), the argument of
+// MWCudaExecutor::loadObjects / TaskGraphExecutor::loadObjects.
+struct SourceObject {
+    const SourceMesh *meshes;
+    int64_t numMeshes;
+};
+
 struct ImportedObject {
     std::vector<std::vector<math::Vector3>> positionArrays;
     std::vector<std::vector<math::Vector3>> normalArrays;

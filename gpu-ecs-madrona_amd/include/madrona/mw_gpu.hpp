@@ -14,6 +14,7 @@
 #pragma once
 
 #include <madrona/taskgraph.hpp>
+#include <madrona/importer.hpp>
 
 #include <functional>
 #include <memory>
@@ -26,6 +27,14 @@ inline constexpr int32_t kDefaultTmpAllocBytes = 16 * 1024;    // Context::tmpAl
 inline constexpr int32_t kDefaultDeferredPerWorld = 256;        // deferred destroys per node per world
 inline constexpr int32_t kCommitMaxRows = 4096;                 // ordered-commit table limit
 
+// Default chained tmpAlloc pool (device): twice the worlds' arenas, at least
+// 16 MiB, at most 1 GiB.
+inline int64_t defaultTmpPoolBytes(int32_t num_worlds, int32_t arena_bytes_per_world)
+{
+    const int64_t b = 2 * (int64_t)num_worlds * (arena_bytes_per_world > 0 ? arena_bytes_per_world : 0);
+    return b < (16ll << 20) ? (16ll << 20) : (b > (1ll << 30) ? (1ll << 30) : b);
+}
+
 struct ExecConfig {
     int32_t numWorlds;
     int32_t gpuID;
@@ -36,9 +45,42 @@ struct ExecConfig {
     int32_t maxDeferredPerWorld = 0;      // 0: kDefaultDeferredPerWorld
     int32_t numWorkers = 0;               // CPU back end: worker threads (0: every core
                                           // of the process's affinity mask)
+    int64_t tmpPoolBytes = -1;            // chained tmpAlloc pool past the per-world arenas:
+                                          // -1: kDefaultTmpPoolBytes rule, 0: none
     int32_t serialNodes = 0;              // 1: every ParallelForNode / CustomParallelForNode
                                           // runs world-serially (WorldSerialForNode); the
                                           // CPU back end always does
+};
+
+namespace render {
+// Reference mw_render.hpp camera modes (the batch renderer itself is out of
+// scope); kept so StateConfig / ThreadPoolExecutor::Config
+// aggregate-initialise exactly as the reference's drivers write them.
+enum class CameraMode : uint32_t {
+    Perspective,
+    Lidar,
+    None,
+};
+}
+
+// Reference ThreadPoolExecutor::Config (include/madrona/mw_cpu.hpp:11-21),
+// the first argument of the CPU TaskGraphExecutor.  Only numWorlds,
+// numExportedBuffers and numWorkers drive the executor; the render fields
+// are accepted and ignored (no renderer).
+class ThreadPoolExecutor {
+public:
+    struct Config {
+        uint32_t numWorlds;
+        uint32_t maxViewsPerWorld;
+        uint32_t maxInstancesPerWorld;
+        uint32_t renderWidth;
+        uint32_t renderHeight;
+        uint32_t maxObjects;
+        uint32_t numExportedBuffers;
+        render::CameraMode cameraMode;
+        int32_t renderGPUID;
+        uint32_t numWorkers = 0;
+    };
 };
 
 // Non-template core (csrc/runtime/executor.cpp).
@@ -124,6 +166,13 @@ private:
 template <typename ContextT, typename WorldT, typename ConfigT, typename InitT>
 class TaskGraphExecutor : public Executor {
 public:
+    // Reference constructor (include/madrona/mw_cpu.hpp:54-63): numWorlds
+    // worlds, numWorkers threads on the CPU back end (0: every core).
+    TaskGraphExecutor(const ThreadPoolExecutor::Config &cfg, const ConfigT &user_cfg,
+                      const InitT *user_inits)
+        : TaskGraphExecutor(fromThreadPoolConfig(cfg), user_cfg, user_inits)
+    {}
+
     TaskGraphExecutor(const ExecConfig &cfg, const ConfigT &user_cfg, const InitT *user_inits)
         : Executor(cfg)
     {
@@ -147,6 +196,113 @@ public:
         WorldT::setupTasks(builder, user_cfg);
         setGraph(builder.build());
     }
+
+    // Reference TaskGraphExecutor::loadObjects feeds the batch renderer,
+    // which is out of scope: refused with an error.
+    int64_t loadObjects(Span<const imp::SourceObject> objs)
+    {
+        if (objs.size() == 0) return 0;
+        throw std::runtime_error("loadObjects: render objects need the batch renderer, which this "
+                                 "framework does not build (physics hulls: PhysicsLoader)");
+    }
+    uint8_t *rgbObservations() const { return nullptr; }
+    float *depthObservations() const { return nullptr; }
+
+private:
+    static ExecConfig fromThreadPoolConfig(const ThreadPoolExecutor::Config &c)
+    {
+        ExecConfig e {};
+        e.numWorlds = (int32_t)c.numWorlds;
+        e.gpuID = 0;
+        e.defaultCapacity = 64;
+        e.numExportedBuffers = (int32_t)c.numExportedBuffers;
+        e.useGraph = 1;
+        e.numWorkers = (int32_t)c.numWorkers;
+        return e;
+    }
 };
+
+// ---------------------------------------------------------------------------
+// Reference MWCudaExecutor (include/madrona/mw_gpu.hpp:20-76,
+// src/mw/cuda_exec.cpp:1692-1815) on gfx950.  The reference NVRTC-compiles
+// CompileConfig::userSources and finds the entry `entryName`; here worlds are
+// compiled ahead of time, so entryName names a registered world (built in, or
+// registered by an object built with world.mk) and every userSources entry
+// that is a shared object (".so") is loaded first, as mw_load_env does.
+// Other source entries and the compile flags / modes are accepted and unused.
+// StateConfig: worldInitPtr holds numWorlds InitT records numWorldInitBytes
+// apart, userConfigPtr the world's ConfigT (numUserConfigBytes must equal its
+// size); the world data size / alignment come from the compiled WorldT.
+// ---------------------------------------------------------------------------
+struct StateConfig {
+    void *worldInitPtr;
+    uint32_t numWorldInitBytes;
+    void *userConfigPtr;
+    uint32_t numUserConfigBytes;
+    uint32_t numWorldDataBytes;
+    uint32_t worldDataAlignment;
+    uint32_t numWorlds;
+    uint32_t maxViewsPerWorld;
+    uint32_t numExportedBuffers;
+    uint32_t gpuID;
+    render::CameraMode cameraMode;
+    uint32_t renderWidth;
+    uint32_t renderHeight;
+};
+
+struct CompileConfig {
+    enum class OptMode : uint32_t {
+        Optimize,
+        LTO,
+        Debug,
+    };
+
+    enum class Executor {
+        JobSystem,
+        TaskGraph,
+    };
+
+    const char *entryName;
+    Span<const char *const> userSources;
+    Span<const char *const> userCompileFlags;
+    OptMode optMode = OptMode::LTO;
+    Executor execMode = Executor::TaskGraph;
+};
+
+class MWHipExecutor {
+public:
+    MWHipExecutor(const StateConfig &state_cfg, const CompileConfig &compile_cfg);
+    MWHipExecutor(MWHipExecutor &&o);
+    ~MWHipExecutor();
+
+    // Render objects go to the batch renderer in the reference (out of scope
+    // here): an empty span returns 0, anything else throws.
+    int64_t loadObjects(Span<const imp::SourceObject> objs);
+
+    // One step of every world; returns when the step has finished (the
+    // reference synchronises its stream, cuda_exec.cpp:1777-1782).
+    void run();
+
+    uint8_t *rgbObservations() const;     // no renderer: nullptr
+    float *depthObservations() const;     // no renderer: nullptr
+
+    // Device pointer of exported buffer `slot` (rows of all worlds,
+    // world-major), valid after run().
+    void *getExported(int64_t slot) const;
+
+    // The framework executor behind it (C ABI, timing, tracing, ...).
+    Executor &executor() const;
+
+private:
+    std::unique_ptr<Executor> exec_;
+};
+
+// The reference's class name, so a driver written against it compiles with
+// only its includes changed.
+using MWCudaExecutor = MWHipExecutor;
+
+// Loads a shared object that registers worlds (mw_load_env); returns the
+// number it registered, throws naming the object on failure or a name clash.
+int32_t loadEnvObject(const char *so_path);
 
 }

@@ -292,6 +292,15 @@ struct StateView {
     uint32_t tmpBytesPerWorld;
     char *tmpArena;             // [numWorlds][tmpBytesPerWorld]
     uint32_t *tmpOffset;        // [numWorlds]
+    // Past a world's arena the reference chains another block
+    // (TmpAllocator::alloc, src/core/state.cpp:95-114).  Device: a bump pool
+    // shared by every world, reset with the arenas by ResetTmpAllocNode; host
+    // (CPU back end, world construction): per-world heap blocks
+    // (hostTmpOverflow*).  Null / 0: no chaining, exhaustion is flagged.
+    char *tmpPool;                       // [tmpPoolBytes] device only
+    uint64_t tmpPoolBytes;
+    unsigned long long *tmpPoolOffset;   // device only
+    void *hostTmpOverflow;               // host only
     uint64_t archKeys[kMaxArchetypes];
     ArchetypeView arch[kMaxArchetypes];
 
@@ -391,6 +400,12 @@ struct StateView {
     }
 };
 
+// Chained tmpAlloc blocks of the host view (state.cpp): a block of `bytes`
+// for `world` (null when chaining is off), and the release of the world's
+// blocks at its tmpAlloc reset.
+void *hostTmpOverflowAlloc(StateView &v, int32_t world, uint64_t bytes);
+void hostTmpOverflowReset(StateView &v, int32_t world);
+
 // ---------------------------------------------------------------------------
 // Host-side registry (StateManager); implementation in csrc/runtime/state.cpp
 // ---------------------------------------------------------------------------
@@ -453,6 +468,8 @@ public:
         int32_t defaultCapacity;     // rows per world for registerArchetype
         int32_t tmpAllocBytesPerWorld = 0;   // Context::tmpAlloc arena per world
         int32_t deferCap = 256;              // deferred destroys per world per node
+        int64_t tmpPoolBytes = 0;            // chained tmpAlloc pool (device bytes;
+                                             // host: > 0 enables the heap blocks)
     };
 
     explicit StateManager(const Config &cfg);

@@ -821,6 +821,7 @@ public:
     static void runWorld(ResetTmpAllocNode *, CpuRunCtx &rc, int32_t w)
     {
         if (rc.state->tmpOffset) rc.state->tmpOffset[w] = 0;
+        hostTmpOverflowReset(*rc.state, w);
     }
     static const char *nodeName() { return "ResetTmpAllocNode"; }
     static constexpr bool kNoTmpAlloc = true;

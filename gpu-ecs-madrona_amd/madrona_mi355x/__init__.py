@@ -55,7 +55,8 @@ class MwConfig(ctypes.Structure):
     _fields_ = [("num_worlds", ctypes.c_int32), ("gpu_id", ctypes.c_int32),
                 ("default_capacity", ctypes.c_int32), ("use_graph", ctypes.c_int32),
                 ("tmp_alloc_bytes", ctypes.c_int32), ("max_deferred_destroys", ctypes.c_int32),
-                ("num_workers", ctypes.c_int32), ("serial_nodes", ctypes.c_int32)]
+                ("num_workers", ctypes.c_int32), ("serial_nodes", ctypes.c_int32),
+                ("tmp_pool_bytes", ctypes.c_int64)]
 
 
 class CollisionsConfig(ctypes.Structure):
@@ -357,7 +358,8 @@ class Executor:
 
     def __init__(self, env, num_worlds, user_cfg, inits, init_stride, gpu_id=0,
                  default_capacity=64, use_graph=True, tmp_alloc_bytes=0,
-                 max_deferred_destroys=0, backend=None, num_workers=0, serial_nodes=False):
+                 max_deferred_destroys=0, backend=None, num_workers=0, serial_nodes=False,
+                 tmp_pool_bytes=0):
         # backend "cpu": the same world on the CPU back end (num_workers
         # pinned host threads, 0 = every core of the affinity mask).
         # serial_nodes: every ParallelForNode walks each world's rows in
@@ -369,7 +371,7 @@ class Executor:
         self.backend = backend
         cfg = MwConfig(num_worlds, gpu_id, default_capacity, 1 if use_graph else 0,
                        tmp_alloc_bytes, max_deferred_destroys, num_workers,
-                       1 if serial_nodes else 0)
+                       1 if serial_nodes else 0, tmp_pool_bytes)
         self._keep = (user_cfg, inits)
         self.h = self._lib.mw_create(env.encode(), ctypes.byref(cfg), ctypes.byref(user_cfg),
                                 ctypes.sizeof(user_cfg), ctypes.cast(inits, ctypes.c_void_p),

@@ -67,6 +67,12 @@ typedef struct mw_config {
                                   taskgraph.inl:63-71); 0: row-parallel lanes
                                   with the ordered structural commit.  The CPU
                                   back end is always world-serial.          */
+    int64_t tmp_pool_bytes;    /* tmpAlloc past a world's arena is chained, as
+                                  the reference chains blocks (state.cpp:
+                                  95-114): a device pool shared by all worlds
+                                  (host: heap blocks), reset with the arenas.
+                                  0: default (2 x the arenas, 16 MiB - 1 GiB),
+                                  -1: none (exhaustion flags the world)     */
 } mw_config;
 
 /* "collisions": rigid-body workload of SURVEY.md §8(d) C3/C4 (128 unit cube

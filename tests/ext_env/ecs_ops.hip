@@ -14,6 +14,7 @@
 #include <madrona/mw_gpu_entry.hpp>
 #include <madrona/taskgraph.hpp>
 
+#include "ecs_ops_init.hpp"
 #include "ecs_ops_rules.hpp"
 
 using namespace madrona;
@@ -47,25 +48,11 @@ struct SpawnInfo {
     int32_t serial;
     int32_t pad;
 };
-struct Stats {
-    int32_t tick;
-    int32_t numPairs;
-    int32_t numSpawns;
-    int32_t sumHits;
-    float sumD2;
-    int32_t dynTicks;
-};
 
 struct Agent : Archetype<Pos, Vel, Counter> {};
 struct PairTemp : Archetype<PairInfo> {};
 struct Spawn : Archetype<SpawnInfo> {};
 
-struct Config {
-    int32_t numAgents;
-};
-struct Init {
-    int32_t worldIndex;
-};
 
 class Engine;
 

@@ -49,6 +49,7 @@ CASES = [
     ("test_jobs_gpu", "test_collisions_jobs_matches_oracle_every_tick", {}),
     ("test_ecs_ops_gpu", "test_ecs_ops_every_step_matches_reference", {}),
     ("test_ecs_ops_gpu", "test_ecs_ops_tmp_alloc_exhaustion_is_flagged_not_silent", {}),
+    ("test_ecs_ops_gpu", "test_ecs_ops_tmp_alloc_chains_past_the_arena", {}),
     ("test_ecs_ops_gpu", "test_ecs_ops_reference_workload_churns", {}),
 ]
 

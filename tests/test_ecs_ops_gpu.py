@@ -85,12 +85,31 @@ def test_ecs_ops_full_size_sampled_worlds():
 
 @pytest.mark.gpu
 def test_ecs_ops_tmp_alloc_exhaustion_is_flagged_not_silent():
-    # 1 KiB per world cannot hold the lanes' scratch: tmpAlloc returns null
-    # (pairsMade = -1 where it did) and kErrFlagTmpAllocFull is raised
-    sim = el.EcsOpsSim(4, tmp_alloc_bytes=1024)
+    # 1 KiB per world and chaining off cannot hold the lanes' scratch:
+    # tmpAlloc returns null (pairsMade = -1 where it did) and
+    # kErrFlagTmpAllocFull is raised
+    sim = el.EcsOpsSim(4, tmp_alloc_bytes=1024, tmp_pool_bytes=-1)
     sim.step(2)
     assert sim.error_flags() & (1 << 17)
     assert (sim.agents(0)["pairsMade"] == -1).any()
+    sim.close()
+
+
+@pytest.mark.gpu
+@needs_ref
+def test_ecs_ops_tmp_alloc_chains_past_the_arena():
+    # 1 KiB per world, default chaining: allocations past the arena come
+    # from the chained pool (host: heap blocks), as the reference chains
+    # blocks (src/core/state.cpp:95-114) -- bit-exact, no flag
+    W, STEPS = 4, 20
+    sim = el.EcsOpsSim(W, tmp_alloc_bytes=1024)
+    ref = el.RefEcsOps(W)
+    for s in range(STEPS):
+        sim.step()
+        ref.step()
+        assert sim.error_flags() == 0, hex(sim.error_flags())
+        for w in range(W):
+            el.compare_world(sim, ref, w, f"step {s}")
     sim.close()
 
 
