@@ -97,7 +97,10 @@ def parse():
                    help="time the dominant kernel's launches in every N-th timed step (the "
                         "graph is split at that node only in those steps)")
     p.add_argument("--no-handoff", action="store_true")
-    return p.parse_args()
+    args = p.parse_args()
+    # at least one timed launch of the dominant kernel however short the run
+    args.timed_every = max(1, min(args.timed_every, args.steps))
+    return args
 
 
 def _cpu_child(args):
@@ -335,7 +338,9 @@ def main():
     roofline = None
     if dom:
         ev_ms1, ev_n1 = sim.timed_node()
-        ms = (ev_ms1 - ev_ms0) / max(1, ev_n1 - ev_n0)
+        if ev_n1 - ev_n0 <= 0:
+            raise RuntimeError(f"bench: no timed launch of {dom} in {args.steps} steps")
+        ms = (ev_ms1 - ev_ms0) / (ev_n1 - ev_n0)
         cands, contacts = sim.counts()
         units = {"body": W * (args.cubes + 1), "cand": float(cands.sum()),
                  "contact": float(contacts.sum())}

@@ -97,7 +97,7 @@ void HalfEdgeMesh::construct(FastPolygonList &polygons, uint32_t vertexCount,
     auto dup = [](const auto &vec) {
         using T = typename std::decay_t<decltype(vec)>::value_type;
         T *p = (T *)malloc(sizeof(T) * std::max<size_t>(vec.size(), 1));
-        memcpy(p, vec.data(), sizeof(T) * vec.size());
+        if (!vec.empty()) memcpy(p, vec.data(), sizeof(T) * vec.size());
         return p;
     };
     mPolygons = dup(polys);

@@ -1623,7 +1623,7 @@ int32_t orc_phys_read_contacts(void *handle, int32_t world, void *out, int32_t c
     auto *sim = (Sim *)handle;
     World &w = sim->worlds[world];
     int32_t n = (int32_t)w.lastContacts.size();
-    memcpy(out, w.lastContacts.data(), sizeof(Contact) * std::min(n, cap));
+    if (n > 0 && cap > 0) memcpy(out, w.lastContacts.data(), sizeof(Contact) * std::min(n, cap));
     return n;
 }
 

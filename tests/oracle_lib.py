@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORC_PATH = os.path.join(ROOT, "oracle", "_build", "liborc.so")
+ORC_PATH = os.environ.get("MADRONA_ORC_LIB") or os.path.join(ROOT, "oracle", "_build", "liborc.so")
 REF_PATH = os.path.join(ROOT, "oracle", "_ref", "libmadrona_ref.so")
 
 
