@@ -321,7 +321,12 @@ __device__ __forceinline__ SatWork candWork(const CandidateCollision &cand, uint
 // survivors, slots and list entries as narrowFilterKernel, into the
 // nextSatWork set.  Two passes over the candidates' packed slots (count,
 // then write) so the world reserves its bin entries with one atomic per
-// list; the second pass loads a candidate's Locs only if it survives.
+// list; the second pass loads a candidate's Locs only if it survives.  Each
+// pass walks the candidates in batches of kFilterBatch 64-candidate chunks
+// whose global loads are all issued before any is used: the wave otherwise
+// waits one memory round trip per chunk (~670 candidates: 22 round trips).
+constexpr int32_t kFilterBatch = 8;
+
 __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, const BodyBox *boxes,
                                                   int32_t lane)
 {
@@ -336,15 +341,26 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
     int32_t *counts = P.nextSatWorkCount + bin * kBinStride;
     constexpr uint32_t kHull = (uint32_t)CollisionPrimitive::Type::Hull;
     constexpr uint32_t kHullPlane = kHull | (uint32_t)CollisionPrimitive::Type::Plane;
+    constexpr int32_t kBatch = 64 * kFilterBatch;
     const uint64_t lt = (1ull << lane) - 1;
     int32_t n_hh = 0, n_hp = 0;
-    for (int32_t base = 0; base < num; base += 64) {
-        const int32_t i = base + lane;
-        BodyBox A, B;
-        const bool keep = i < num && candOverlaps(P, w, slots[i], boxes, A, B);
-        const uint32_t t = A.type | B.type;
-        n_hh += __popcll(__ballot(keep && t == kHull));
-        n_hp += __popcll(__ballot(keep && t == kHullPlane));
+    for (int32_t b0 = 0; b0 < num; b0 += kBatch) {
+        uint64_t s[kFilterBatch];
+#pragma unroll
+        for (int32_t j = 0; j < kFilterBatch; j++) {
+            const int32_t i = b0 + 64 * j + lane;
+            s[j] = i < num ? slots[i] : 0;
+        }
+#pragma unroll
+        for (int32_t j = 0; j < kFilterBatch; j++) {
+            const int32_t i = b0 + 64 * j + lane;
+            if (b0 + 64 * j >= num) continue;                // wave-uniform
+            BodyBox A, B;
+            const bool keep = i < num && candOverlaps(P, w, s[j], boxes, A, B);
+            const uint32_t t = A.type | B.type;
+            n_hh += __popcll(__ballot(keep && t == kHull));
+            n_hp += __popcll(__ballot(keep && t == kHullPlane));
+        }
     }
     int32_t b_hh = 0, b_hp = 0;
     if (lane == 0) {
@@ -354,24 +370,48 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
     b_hh = __shfl(b_hh, 0);
     b_hp = __shfl(b_hp, 0);
     int32_t S = 0;
-    for (int32_t base = 0; base < num; base += 64) {
-        const int32_t i = base + lane;
-        BodyBox A, B;
-        const uint64_t cs = i < num ? slots[i] : 0;
-        const bool keep = i < num && candOverlaps(P, w, cs, boxes, A, B);
-        const uint32_t t = A.type | B.type;
-        const bool hh = keep && t == kHull, hp = keep && t == kHullPlane;
-        const uint64_t mk = __ballot(keep), mh = __ballot(hh), mp = __ballot(hp);
-        if (keep) {
-            SatWork wk = candWork(cands[i], cs, A, B, w);
-            wk.slot = S + __popcll(mk & lt);
-            info[wk.slot] = kNoManifold;
-            if (hh) list[b_hh + __popcll(mh & lt)] = wk;
-            if (hp) *(list_back - (b_hp + __popcll(mp & lt))) = wk;
+    for (int32_t b0 = 0; b0 < num; b0 += kBatch) {
+        uint64_t s[kFilterBatch];
+#pragma unroll
+        for (int32_t j = 0; j < kFilterBatch; j++) {
+            const int32_t i = b0 + 64 * j + lane;
+            s[j] = i < num ? slots[i] : 0;
         }
-        S += __popcll(mk);
-        b_hh += __popcll(mh);
-        b_hp += __popcll(mp);
+        // survivors of the batch first, then their candidates' Locs in one
+        // round of loads
+        uint32_t keep_bits = 0;
+#pragma unroll
+        for (int32_t j = 0; j < kFilterBatch; j++) {
+            const int32_t i = b0 + 64 * j + lane;
+            if (b0 + 64 * j >= num) continue;
+            BodyBox A, B;
+            if (i < num && candOverlaps(P, w, s[j], boxes, A, B)) keep_bits |= 1u << j;
+        }
+        CandidateCollision c[kFilterBatch];
+#pragma unroll
+        for (int32_t j = 0; j < kFilterBatch; j++) {
+            if (keep_bits & (1u << j)) c[j] = cands[b0 + 64 * j + lane];
+        }
+#pragma unroll
+        for (int32_t j = 0; j < kFilterBatch; j++) {
+            if (b0 + 64 * j >= num) continue;
+            const bool keep = (keep_bits >> j) & 1u;
+            const BodyBox A = boxes[(uint32_t)s[j] & 0xffffu];
+            const BodyBox B = boxes[(uint32_t)(s[j] >> 32) & 0xffffu];
+            const uint32_t t = A.type | B.type;
+            const bool hh = keep && t == kHull, hp = keep && t == kHullPlane;
+            const uint64_t mk = __ballot(keep), mh = __ballot(hh), mp = __ballot(hp);
+            if (keep) {
+                SatWork wk = candWork(c[j], s[j], A, B, w);
+                wk.slot = S + __popcll(mk & lt);
+                info[wk.slot] = kNoManifold;
+                if (hh) list[b_hh + __popcll(mh & lt)] = wk;
+                if (hp) *(list_back - (b_hp + __popcll(mp & lt))) = wk;
+            }
+            S += __popcll(mk);
+            b_hh += __popcll(mh);
+            b_hp += __popcll(mp);
+        }
     }
     if (lane == 0) P.survCount[w] = S;
 }
