@@ -158,19 +158,53 @@ __global__ void solverGlobalKernel(PhysArgs P, int32_t integrate_next);
 // columns; the solver's fused tail passes the values it is about to write
 // back -- the same inputs, so the same bits), plus the world AABB the
 // narrowphase recheck uses (narrowphase.cpp:1590-1594), indexed by body slot.
-__device__ __forceinline__ BodyBox integrateBody(const PhysArgs &P, const BodyArch &B, int32_t w,
-                                              int32_t r, Vector3 x, Quat q, Vector3 v_in,
-                                              Vector3 omega_in)
+// Split in two so a caller walking several rows per lane can issue every
+// row's loads before the first row's arithmetic (integrateLoad, then
+// integrateApply): the column and object-table reads are one memory round
+// trip per batch instead of per row.
+struct IntegrateIn {
+    int32_t obj;
+    ResponseType rt;
+    Vector3 extForce, extTorque;
+    Diag3x3 scale;
+};
+
+struct IntegrateObj {
+    float invMass;
+    Vector3 invInertia;
+    AABB aabb;
+    uint32_t type;
+};
+
+__device__ __forceinline__ IntegrateIn integrateLoad(const BodyArch &B, int32_t w, int32_t r)
+{
+    IntegrateIn in;
+    in.obj = bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
+    in.rt = bcol<ResponseType>(B, Cols::ResponseType, w, r);
+    in.extForce = bcol<Vector3>(B, Cols::ExternalForce, w, r);
+    in.extTorque = bcol<Vector3>(B, Cols::ExternalTorque, w, r);
+    in.scale = bcol<Diag3x3>(B, Cols::Scale, w, r);
+    return in;
+}
+
+__device__ __forceinline__ IntegrateObj integrateObj(const PhysArgs &P, int32_t obj)
+{
+    const RigidBodyMetadata md = P.objs.metadata[obj];
+    return IntegrateObj { md.invMass, md.invInertiaTensor, P.objs.aabbs[obj], P.objs.types[obj] };
+}
+
+__device__ __forceinline__ BodyBox integrateApply(const PhysArgs &P, const BodyArch &B, int32_t w,
+                                               int32_t r, const IntegrateIn &in,
+                                               const IntegrateObj &od, Vector3 x, Quat q,
+                                               Vector3 v_in, Vector3 omega_in)
 {
     Vector3 &pos = bcol<Vector3>(B, Cols::Position, w, r);
     Quat &rot = bcol<Quat>(B, Cols::Rotation, w, r);
-    const int32_t obj = bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
-    const ResponseType rt = bcol<ResponseType>(B, Cols::ResponseType, w, r);
     auto &prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
     auto &ps_pos = bcol<solver::PreSolvePositional>(B, Cols::PreSolvePositional, w, r);
     auto &ps_vel = bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
 
-    if (rt == ResponseType::Static) {
+    if (in.rt == ResponseType::Static) {
         prev.prevPosition = x;
         prev.prevRotation = q;
         ps_pos.x = x;
@@ -185,13 +219,12 @@ __device__ __forceinline__ BodyBox integrateBody(const PhysArgs &P, const BodyAr
         prev.prevPosition = x;
         prev.prevRotation = q;
         const SolverData &solver = P.solver[w];
-        const RigidBodyMetadata md = P.objs.metadata[obj];
-        const float inv_m = md.invMass;
-        const Vector3 inv_I = md.invInertiaTensor;
+        const float inv_m = od.invMass;
+        const Vector3 inv_I = od.invInertia;
         const float h = solver.h;
-        const Vector3 ext_force = bcol<Vector3>(B, Cols::ExternalForce, w, r);
-        const Vector3 ext_torque = bcol<Vector3>(B, Cols::ExternalTorque, w, r);
-        if (rt == ResponseType::Dynamic) v += h * solver.g;
+        const Vector3 ext_force = in.extForce;
+        const Vector3 ext_torque = in.extTorque;
+        if (in.rt == ResponseType::Dynamic) v += h * solver.g;
         v += h * inv_m * ext_force;
         x += h * v;
         Vector3 I {
@@ -215,10 +248,17 @@ __device__ __forceinline__ BodyBox integrateBody(const PhysArgs &P, const BodyAr
         ps_vel.v = v;
         ps_vel.omega = omega;
     }
-    const Diag3x3 scale = bcol<Diag3x3>(B, Cols::Scale, w, r);
-    const BodyBox bb { P.objs.aabbs[obj].applyTRS(x, q, scale), obj, P.objs.types[obj] };
+    const BodyBox bb { od.aabb.applyTRS(x, q, in.scale), in.obj, od.type };
     P.bodyBoxes[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r] = bb;
     return bb;
+}
+
+__device__ __forceinline__ BodyBox integrateBody(const PhysArgs &P, const BodyArch &B, int32_t w,
+                                              int32_t r, Vector3 x, Quat q, Vector3 v_in,
+                                              Vector3 omega_in)
+{
+    const IntegrateIn in = integrateLoad(B, w, r);
+    return integrateApply(P, B, w, r, in, integrateObj(P, in.obj), x, q, v_in, omega_in);
 }
 
 // The narrowphase work lists are split into kNarrowBins bins (world w in

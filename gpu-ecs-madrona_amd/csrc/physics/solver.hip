@@ -664,6 +664,12 @@ __device__ __forceinline__ void stQ(void *p, Quat q)
     f[0] = q.w; f[1] = q.x; f[2] = q.y; f[3] = q.z;
 }
 
+// Rows of a world a lane handles per batch in the per-body loops: every
+// column load of a batch is issued before the first row's stores, so a
+// world of up to 64 * kRowBatch bodies pays one memory round trip per loop
+// instead of one per 64 rows (collisions: 129 bodies, 3 rounds -> 1).
+constexpr int32_t kRowBatch = 3;
+
 // Load one world's bodies into its LDS image (wave `lane` 0..63) and reset
 // its ordering state.
 __device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, SolverLDS &L,
@@ -672,33 +678,43 @@ __device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, So
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
-        for (int32_t r = lane; r < rows; r += kSolverBlock) {
-            SMut s;
-            s.x = ldV3(&bcol<Vector3>(B, Cols::Position, w, r));
-            s.q = ldQ(&bcol<Quat>(B, Cols::Rotation, w, r));
-            const Velocity &vel = bcol<Velocity>(B, Cols::Velocity, w, r);
-            s.v = ldV3(&vel.linear);
-            s.omega = ldV3(&vel.angular);
-            const uint32_t obj = (uint32_t)bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
-            const uint32_t rt = (uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r) & 0xffu;
-            s.meta = rt | ((uint32_t)ba << 8) | (obj << 16);
-            bool inv = false;
-            if (rt == (uint32_t)ResponseType::Static) {
-                const auto &pv = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
-                const auto &psv = bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
-                inv = staticInvariant(s, ldV3(&pv.prevPosition), ldQ(&pv.prevRotation),
-                                      ldV3(&psv.v), ldV3(&psv.omega));
+        for (int32_t r0 = 0; r0 < rows; r0 += kSolverBlock * kRowBatch) {
+            SMut s[kRowBatch];
+#pragma unroll
+            for (int32_t j = 0; j < kRowBatch; j++) {
+                const int32_t r = r0 + j * kSolverBlock + lane;
+                if (r >= rows) continue;
+                s[j].x = ldV3(&bcol<Vector3>(B, Cols::Position, w, r));
+                s[j].q = ldQ(&bcol<Quat>(B, Cols::Rotation, w, r));
+                const Velocity &vel = bcol<Velocity>(B, Cols::Velocity, w, r);
+                s[j].v = ldV3(&vel.linear);
+                s[j].omega = ldV3(&vel.angular);
+                const uint32_t obj = (uint32_t)bcol<ObjectID>(B, Cols::ObjectID, w, r).idx;
+                const uint32_t rt = (uint32_t)bcol<ResponseType>(B, Cols::ResponseType, w, r) & 0xffu;
+                s[j].meta = rt | ((uint32_t)ba << 8) | (obj << 16);
             }
-            const int32_t slot = B.slotBase + r;
-            SMut *d = L.bodies + slot;
-            stV3(&d->x, s.x);
-            stQ(&d->q, s.q);
-            stV3(&d->v, s.v);
-            stV3(&d->omega, s.omega);
-            d->meta = s.meta;
-            L.flag[slot] = inv ? (int16_t)-1 : (int16_t)0;
-            L.lastItem[slot] = -1;
-            L.touch[slot] = 0;
+#pragma unroll
+            for (int32_t j = 0; j < kRowBatch; j++) {
+                const int32_t r = r0 + j * kSolverBlock + lane;
+                if (r >= rows) continue;
+                bool inv = false;
+                if ((s[j].meta & 0xffu) == (uint32_t)ResponseType::Static) {
+                    const auto &pv = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
+                    const auto &psv = bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
+                    inv = staticInvariant(s[j], ldV3(&pv.prevPosition), ldQ(&pv.prevRotation),
+                                          ldV3(&psv.v), ldV3(&psv.omega));
+                }
+                const int32_t slot = B.slotBase + r;
+                SMut *d = L.bodies + slot;
+                stV3(&d->x, s[j].x);
+                stQ(&d->q, s[j].q);
+                stV3(&d->v, s[j].v);
+                stV3(&d->omega, s[j].omega);
+                d->meta = s[j].meta;
+                L.flag[slot] = inv ? (int16_t)-1 : (int16_t)0;
+                L.lastItem[slot] = -1;
+                L.touch[slot] = 0;
+            }
         }
     }
 }
@@ -889,34 +905,47 @@ __device__ __forceinline__ void setWorldVelocities(const PhysArgs &P, int32_t w,
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
-        for (int32_t r = lane; r < rows; r += kSolverBlock) {
-            SMut *s = L.bodies + B.slotBase + r;
-            const auto &prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
-            const Vector3 px = ldV3(&prev.prevPosition);
-            const Quat qp = ldQ(&prev.prevRotation);
-            const Vector3 x = ldV3(&s->x);
-            const Quat q = ldQ(&s->q);
-            Quat dq;
-            if (q.w != qp.w || q.x != qp.x || q.y != qp.y || q.z != qp.z) {
-                dq = q * qp.inv();
-            } else {
-                dq = Quat { 1, 0, 0, 0 };
+        for (int32_t r0 = 0; r0 < rows; r0 += kSolverBlock * kRowBatch) {
+            Vector3 px[kRowBatch];
+            Quat qp[kRowBatch];
+#pragma unroll
+            for (int32_t j = 0; j < kRowBatch; j++) {
+                const int32_t r = r0 + j * kSolverBlock + lane;
+                if (r >= rows) continue;
+                const auto &prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
+                px[j] = ldV3(&prev.prevPosition);
+                qp[j] = ldQ(&prev.prevRotation);
             }
-            Vector3 new_omega = 2.f / h * Vector3 { dq.x, dq.y, dq.z };
-            stV3(&s->v, (x - px) / h);
-            stV3(&s->omega, dq.w > 0.f ? new_omega : -new_omega);
+#pragma unroll
+            for (int32_t j = 0; j < kRowBatch; j++) {
+                const int32_t r = r0 + j * kSolverBlock + lane;
+                if (r >= rows) continue;
+                SMut *s = L.bodies + B.slotBase + r;
+                const Vector3 x = ldV3(&s->x);
+                const Quat q = ldQ(&s->q);
+                Quat dq;
+                if (q.w != qp[j].w || q.x != qp[j].x || q.y != qp[j].y || q.z != qp[j].z) {
+                    dq = q * qp[j].inv();
+                } else {
+                    dq = Quat { 1, 0, 0, 0 };
+                }
+                Vector3 new_omega = 2.f / h * Vector3 { dq.x, dq.y, dq.z };
+                stV3(&s->v, (x - px[j]) / h);
+                stV3(&s->omega, dq.w > 0.f ? new_omega : -new_omega);
+            }
         }
     }
 }
 
 // Write the solved bodies back; integrate_next: then run the next
-// substep's substepRigidBodies on them (integrateBody writes the pose) and
+// substep's substepRigidBodies on them (integrateApply writes the pose) and
 // the next substep's narrowphase filter for the world (filterWorldOnWave,
 // into the nextSatWork list set) from the bodies' new boxes, which are kept
 // in the world's LDS image: box slot s (32 B) overwrites the SMut bytes of
 // slots <= s only, and slots are processed in increasing order with every
 // lane's SMut reads of a round issued before its box writes, so no SMut
-// entry is overwritten before it is read.
+// entry is overwritten before it is read.  A batch's integration inputs
+// (columns, then object tables) are loaded before its first row.
 __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, SolverLDS &L,
                                                  int32_t lane, bool integrate_next)
 {
@@ -925,20 +954,43 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
-        for (int32_t r = lane; r < rows; r += kSolverBlock) {
-            const SMut *s = L.bodies + B.slotBase + r;
-            const Vector3 x = ldV3(&s->x), v = ldV3(&s->v), om = ldV3(&s->omega);
-            const Quat q = ldQ(&s->q);
-            Velocity &vel = bcol<Velocity>(B, Cols::Velocity, w, r);
-            stV3(&vel.linear, v);
-            stV3(&vel.angular, om);
+        for (int32_t r0 = 0; r0 < rows; r0 += kSolverBlock * kRowBatch) {
+            IntegrateIn in[kRowBatch];
+            IntegrateObj od[kRowBatch];
             if (integrate_next) {
-                const BodyBox bb = integrateBody(P, B, w, r, x, q, v, om);
-                waveSync();                               // the round's SMut reads first
-                boxes[B.slotBase + r] = bb;
-            } else {
-                stV3(&bcol<Vector3>(B, Cols::Position, w, r), x);
-                stQ(&bcol<Quat>(B, Cols::Rotation, w, r), q);
+#pragma unroll
+                for (int32_t j = 0; j < kRowBatch; j++) {
+                    const int32_t r = r0 + j * kSolverBlock + lane;
+                    if (r < rows) in[j] = integrateLoad(B, w, r);
+                }
+#pragma unroll
+                for (int32_t j = 0; j < kRowBatch; j++) {
+                    const int32_t r = r0 + j * kSolverBlock + lane;
+                    if (r < rows) od[j] = integrateObj(P, in[j].obj);
+                }
+            }
+#pragma unroll
+            for (int32_t j = 0; j < kRowBatch; j++) {
+                const int32_t r = r0 + j * kSolverBlock + lane;
+                const bool live = r < rows;
+                if (live) {
+                    const SMut *s = L.bodies + B.slotBase + r;
+                    const Vector3 x = ldV3(&s->x), v = ldV3(&s->v), om = ldV3(&s->omega);
+                    const Quat q = ldQ(&s->q);
+                    Velocity &vel = bcol<Velocity>(B, Cols::Velocity, w, r);
+                    stV3(&vel.linear, v);
+                    stV3(&vel.angular, om);
+                    if (integrate_next) {
+                        const BodyBox bb = integrateApply(P, B, w, r, in[j], od[j], x, q, v, om);
+                        waveSync();                       // the round's SMut reads first
+                        boxes[B.slotBase + r] = bb;
+                    } else {
+                        stV3(&bcol<Vector3>(B, Cols::Position, w, r), x);
+                        stQ(&bcol<Quat>(B, Cols::Rotation, w, r), q);
+                    }
+                } else if (integrate_next) {
+                    waveSync();                           // matches the live lanes' barrier
+                }
             }
         }
     }
