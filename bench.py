@@ -46,7 +46,7 @@ BYTES = {
     "NarrowphaseNode": {"cand": 16 + 2 * 44, "contact": 112},
     "SolverNode": {"body": 56 + 24, "contact": (112 + 2 * 92 + 2 * 28 + 16) + (112 + 2 * 100 + 2 * 24)},
 }
-NODE_KINDS = list(BYTES.keys()) + ["ParallelForNode"]
+NODE_KINDS = list(BYTES.keys()) + ["CustomParallelForNode"]
 
 
 def pmc_traffic(kernel_node):
@@ -277,7 +277,7 @@ def main():
     launches = {"SubstepRigidBodiesNode": args.substeps, "NarrowphaseNode": args.substeps,
                 "SolverNode": args.substeps, "FindOverlappingNode": 1,
                 "UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
-                "ParallelForNode": 1}
+                "CustomParallelForNode": 1}
     node_table = {}
     dom = None
     breakdown_steps = 0 if args.no_roofline else 2 * len(NODE_KINDS)

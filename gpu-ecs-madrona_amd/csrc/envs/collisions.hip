@@ -62,7 +62,9 @@ struct PhysWorld : public WorldBase {
         auto sub = RigidBodyPhysicsSystem::setupSubstepTasks(builder, { bp },
                                                              cfg.c.num_substeps);
         auto cleanup = RigidBodyPhysicsSystem::setupCleanupTasks(builder, { sub });
-        builder.addToGraph<ParallelForNode<Engine, accumulateReturn, EpisodeReturn>>({ cleanup });
+        // one wave per world (the world's one EpisodeReturn row)
+        builder.addToGraph<CustomParallelForNode<Engine, accumulateReturn, 64, 1, EpisodeReturn>>(
+            { cleanup });
     }
 
     PhysWorld(Engine &ctx, const Config &cfg, const mw_collisions_init &init);
@@ -77,20 +79,56 @@ public:
     using CustomContext::CustomContext;
 };
 
-// Generic ParallelForNode over the EpisodeReturn singleton: one lane per
-// world walks that world's bodies in row order (deterministic sum).
+// The mean height of the world's dynamic bodies, summed in row order (a
+// deterministic serial sum).  On the device the world's wave loads its rows
+// cooperatively (coalesced, 64 per round) and every lane replays the serial
+// sum over them through shuffles -- the same additions in the same order as
+// the host's walk, without one lane's chain of strided loads.
 MW_HD void PhysWorld::accumulateReturn(Engine &ctx, EpisodeReturn &ret)
 {
     float sum = 0.f;
     int32_t n = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const int32_t lane = mwGPU::invocationLane<64>();
+    const Query<Position, ResponseType> &q = ctx.data().bodyQuery;
+    StateView &st = ctx.state();
+    const int32_t w = ctx.worldID().idx;
+    for (int32_t a = 0; a < q.numArchetypes; a++) {
+        const int32_t arch = q.archetypes[a];
+        const int32_t rows = st.arch[arch].numRows[w];
+        const Position *pos = st.column<Position>(arch, q.cols[a][0], w);
+        const ResponseType *rts = st.column<ResponseType>(arch, q.cols[a][1], w);
+        for (int32_t r0 = 0; r0 < rows; r0 += 64) {
+            const int32_t r = r0 + lane;
+            const float z = r < rows ? pos[r].z : 0.f;
+            const int32_t dyn = r < rows && rts[r] == ResponseType::Dynamic ? 1 : 0;
+            const int32_t cnt = min(64, rows - r0);
+            const uint64_t dmask = __ballot(dyn != 0);
+            // lane k's value to a scalar register (v_readlane, independent of
+            // the running sum, so the reads run ahead of the add chain)
+#pragma unroll
+            for (int32_t k = 0; k < 64; k++) {
+                if (k >= cnt) break;
+                const float zk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), k));
+                const bool dk = (dmask >> k) & 1ull;
+                sum = dk ? sum + zk : sum;
+            }
+            n += __popcll(dmask);
+        }
+    }
+    if (lane != 0) return;
+#else
+#if !defined(__HIPCC__)
+    // CPU back end: the invocation's lanes run one after another; one sums
+    if (mwGPU::invocationLane<64>() != 0) return;
+#endif
     ctx.forEach(ctx.data().bodyQuery, [&](const Position &p, const ResponseType &rt) {
-        // branch-free select (same sums): every row's loads issue without
-        // waiting on the previous row's ResponseType
         const bool dyn = rt == ResponseType::Dynamic;
         const float z = p.z;
         sum = dyn ? sum + z : sum;
         n += dyn ? 1 : 0;
     });
+#endif
     ret.value += n > 0 ? sum / (float)n : 0.f;
 }
 

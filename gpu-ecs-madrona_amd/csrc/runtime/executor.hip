@@ -423,6 +423,18 @@ exportScanKernel(const int32_t *num_rows, int32_t num_worlds, int64_t *offsets)
     if (tid == 1023) offsets[num_worlds] = base + x;
 }
 
+// A singleton's slab is already packed (capacity 1, one row per world): the
+// export is a flat copy.
+__global__ void __launch_bounds__(256)
+exportFlatCopyKernel(const uint32_t *__restrict__ src, int64_t n, uint32_t *__restrict__ dst)
+{
+    MW_TRACE_BLOCK(0);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        dst[i] = src[i];
+    }
+}
+
 // Rows are whole 4-byte words for every exported component, so the gather
 // moves dwords (one world per blockIdx.y).
 __global__ void __launch_bounds__(256)
@@ -492,6 +504,7 @@ struct ExportBuf {
     char *buf;
     int64_t *offsets;           // shared by the exports of one archetype
     bool scanOwner;             // this export launches the archetype's scan
+    bool singleton;             // one row per world: offsets fixed (w), flat copy
 };
 
 struct Executor::Impl {
@@ -690,9 +703,17 @@ void Executor::uploadState()
         for (const ExportBuf &o : impl_->exports) {
             if (o.archetype == b.archetype) { b.offsets = o.offsets; b.scanOwner = false; }
         }
+        b.singleton = (dv.arch[b.archetype].flags & kArchSingleton) != 0;
         if (!b.offsets) {
             MW_HIP_CHECK(hipMalloc(&b.offsets, sizeof(int64_t) * (dv.numWorlds + 1)));
-            b.scanOwner = true;
+            // a singleton's packed rows never move: world w at row w, no scan
+            b.scanOwner = !b.singleton;
+            if (b.singleton) {
+                std::vector<int64_t> off(dv.numWorlds + 1);
+                for (int32_t w = 0; w <= dv.numWorlds; w++) off[w] = w;
+                MW_HIP_CHECK(hipMemcpy(b.offsets, off.data(), sizeof(int64_t) * off.size(),
+                                       hipMemcpyHostToDevice));
+            }
         }
         impl_->exports.push_back(b);
     }
@@ -714,15 +735,21 @@ static void launchExports(Executor::Impl &I, const StateView &dv)
                         trace_node);
         }
         const ArchetypeView &av = dv.arch[b.archetype];
-        if (b.scanOwner) {
-            MW_LAUNCH(exportScanKernel, dim3(1), dim3(1024), 0, I.stream,
-                               av.numRows, dv.numWorlds, b.offsets);
-        }
         const uint32_t words = b.bytes / 4;
-        const unsigned bx = (unsigned)std::max<int64_t>(1, ((int64_t)av.capacity * words + 255) / 256);
-        MW_LAUNCH(exportCopyKernel, dim3(bx, dv.numWorlds), dim3(256), 0, I.stream,
-                           (const uint32_t *)av.cols[b.column], av.capacity, words, av.numRows,
-                           b.offsets, (uint32_t *)b.buf);
+        if (b.singleton) {
+            const int64_t n = (int64_t)dv.numWorlds * words;
+            MW_LAUNCH(exportFlatCopyKernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)),
+                      dim3(256), 0, I.stream, (const uint32_t *)av.cols[b.column], n, (uint32_t *)b.buf);
+        } else {
+            if (b.scanOwner) {
+                MW_LAUNCH(exportScanKernel, dim3(1), dim3(1024), 0, I.stream, av.numRows, dv.numWorlds,
+                          b.offsets);
+            }
+            const unsigned bx = (unsigned)std::max<int64_t>(1, ((int64_t)av.capacity * words + 255) / 256);
+            MW_LAUNCH(exportCopyKernel, dim3(bx, dv.numWorlds), dim3(256), 0, I.stream,
+                      (const uint32_t *)av.cols[b.column], av.capacity, words, av.numRows, b.offsets,
+                      (uint32_t *)b.buf);
+        }
         if (I.trace) {
             traceMarker(I, mwGPU::DeviceEvent::nodeFinish, trace_func, (uint32_t)dv.numWorlds,
                         trace_node);

@@ -247,6 +247,9 @@ void StateManager::finalizeLayout(uint32_t world_data_bytes, uint32_t world_data
         av.numColumns = (int32_t)ai.cols.size();
         av.capacity = ai.capacity;
         av.flags = (ai.temporary ? kArchTemporary : 0u) | (ai.moduleRows ? kArchModuleRows : 0u);
+        if (std::find(I.singletons.begin(), I.singletons.end(), ai.key) != I.singletons.end()) {
+            av.flags |= kArchSingleton;
+        }
         av.numRows = (int32_t *)hostAlloc(I, sizeof(int32_t) * W);
         for (int32_t c = 0; c < av.numColumns; c++) {
             size_t bytes = (size_t)W * ai.capacity * ai.cols[c].numBytes;

@@ -258,6 +258,7 @@ struct DeferredDestroy {
 // ---------------------------------------------------------------------------
 inline constexpr uint32_t kArchTemporary = 1;     // rows have no entity IDs
 inline constexpr uint32_t kArchModuleRows = 2;    // rows written by a module's own kernels
+inline constexpr uint32_t kArchSingleton = 4;     // exactly one row per world, always
 
 struct ArchetypeView {
     int32_t numColumns;

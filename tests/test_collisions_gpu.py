@@ -208,8 +208,9 @@ def test_sampled_node_timing_counts_and_does_not_perturb_state():
 
 
 def test_episode_return_export_matches_oracle():
-    # ParallelForNode over the EpisodeReturn singleton (Context::forEach over
-    # a two-component query) + the packed export buffer (getExported slot 2).
+    # CustomParallelForNode (one wave per world) over the EpisodeReturn
+    # singleton + the packed export buffer (getExported slot 2, a singleton:
+    # flat copy, fixed offsets).
     mw = _mw()
     gcfg, ocfg = _cfg_pair()
     W, steps = 5, 12

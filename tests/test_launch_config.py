@@ -56,7 +56,7 @@ def test_collisions_launch_config_does_not_change_results():
     base = _collisions(mw, W, 5)
     cfg = _collisions(mw, W, 5)
     names = cfg.nodes()
-    assert "NarrowphaseNode" in names and "ParallelForNode" in names
+    assert "NarrowphaseNode" in names and "CustomParallelForNode" in names
     cfg.set_node_blocks_per_cu(-1, 1)               # every node: 1 block / CU
     narrow = names.index("NarrowphaseNode")
     cfg.set_node_blocks_per_cu(narrow, 64)          # persistent grids past residency
@@ -84,7 +84,7 @@ if kind == "collisions":
     s = mw.CollisionsSim(40, pos, rot, g)
     names = s.nodes()
     print("CFG", s.node_blocks_per_cu(-1), s.node_blocks_per_cu(names.index("NarrowphaseNode")),
-          s.node_blocks_per_cu(names.index("ParallelForNode")))
+          s.node_blocks_per_cu(names.index("CustomParallelForNode")))
     s.step(15)
     assert s.error_flags() == 0
     np.save(out, np.stack([s.bodies(w) for w in range(40)]))

@@ -19,7 +19,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
 
-TUNABLE = ("ParallelForNode", "PerWorldNode", "NarrowphaseNode")
+TUNABLE = ("ParallelForNode", "CustomParallelForNode", "PerWorldNode", "NarrowphaseNode")
 
 
 def make_sim(mw, env, worlds):
