@@ -3,7 +3,12 @@
 (BASELINE.json configs[2]: 8192 worlds x 128 cube hulls + ground plane, S=4,
 dt=1/60) on MI355X.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--workload simple]
+
+--workload simple measures BASELINE.json configs[1] instead
+(examples/simple_taskgraph, 8192 worlds x 100 objects + test object + agent,
+clamp + physics, S=4) with the same roofline / CPU-baseline legs; its
+hand-off is the exported agent positions (getExported slot 0).
 
 A "step" = one taskgraph step of every world (broadphase, 4 XPBD substeps of
 integrate / narrowphase / solve, cleanup, episode-return node) replayed as one
@@ -46,7 +51,7 @@ BYTES = {
     "NarrowphaseNode": {"cand": 16 + 2 * 44, "contact": 112},
     "SolverNode": {"body": 56 + 24, "contact": (112 + 2 * 92 + 2 * 28 + 16) + (112 + 2 * 100 + 2 * 24)},
 }
-NODE_KINDS = list(BYTES.keys()) + ["CustomParallelForNode"]
+NODE_KINDS = list(BYTES.keys()) + ["CustomParallelForNode", "ParallelForNode"]
 
 
 def pmc_traffic(kernel_node):
@@ -75,7 +80,9 @@ def parse():
     p.add_argument("--settle", type=int, default=120,
                    help="untimed pre-roll steps so the timed window is the settled, "
                         "contact-heavy regime (cubes fall from z<=10 for ~85 steps)")
-    p.add_argument("--cubes", type=int, default=128)
+    p.add_argument("--workload", choices=("collisions", "simple"), default="collisions")
+    p.add_argument("--cubes", type=int, default=0,
+                   help="bodies per world besides the fixed ones (0: 128 collisions, 100 simple)")
     p.add_argument("--substeps", type=int, default=4)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-worlds", type=int, default=0,
@@ -98,6 +105,8 @@ def parse():
                         "graph is split at that node only in those steps)")
     p.add_argument("--no-handoff", action="store_true")
     args = p.parse_args()
+    if args.cubes <= 0:
+        args.cubes = 128 if args.workload == "collisions" else 100
     # at least one timed launch of the dominant kernel however short the run
     args.timed_every = max(1, min(args.timed_every, args.steps))
     return args
@@ -114,11 +123,13 @@ def _cpu_child(args):
     pos, rot = ol.gen_collisions_inits(first + W, args.cubes, seed=0)
     pos, rot = pos[first:], rot[first:]
     ocfg = ol.default_phys_config(args.cubes, args.substeps, max_contacts=4096)
+    simple = args.workload == "simple"
     if args.cpu_executor:
         # the framework's CPU back end: same world sources, pinned workers
         import madrona_mi355x as mw
         g = mw.default_collisions_config(args.cubes, args.substeps, 4096, 4096)
-        sim = mw.CollisionsSim(W, pos, rot, g, backend="cpu", num_workers=threads)
+        Sim = mw.SimpleSim if simple else mw.CollisionsSim
+        sim = Sim(W, pos, rot, g, backend="cpu", num_workers=threads)
         kind = "port"
         sim.step(args.settle + args.warmup)
         t0 = time.perf_counter()
@@ -126,16 +137,16 @@ def _cpu_child(args):
         dt = time.perf_counter() - t0
         assert sim.error_flags() == 0
     elif ol.ref_available() and not args.cpu_port:
-        lib = ol.load_ref()
+        sim = ol.ReferenceSimple(ocfg, pos, rot) if simple else ol.ReferencePhys(ocfg, pos, rot)
+        lib = sim.lib
         lib.ref_phys_step_mt.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
-        sim = ol.ReferencePhys(ocfg, pos, rot)
         kind = "reference"
         lib.ref_phys_step_mt(sim.h, args.settle + args.warmup, threads)
         t0 = time.perf_counter()
         lib.ref_phys_step_mt(sim.h, args.cpu_steps, threads)
         dt = time.perf_counter() - t0
     else:
-        sim = ol.OraclePhys(ocfg, pos, rot)
+        sim = ol.OracleSimple(ocfg, pos, rot) if simple else ol.OraclePhys(ocfg, pos, rot)
         kind = "port"
         sim.step(args.settle + args.warmup, threads)
         t0 = time.perf_counter()
@@ -186,6 +197,7 @@ def cpu_baseline(args, executor=False):
                "--cpu-worlds", str(args.cpu_worlds),
                "--cpu-first-world", str(batches * args.cpu_worlds),
                "--cpu-threads", str(threads), "--cubes", str(args.cubes),
+               "--workload", args.workload,
                "--substeps", str(args.substeps), "--cpu-steps", str(args.cpu_steps),
                "--settle", str(args.settle), "--warmup", str(args.warmup)] + \
               (["--cpu-port"] if args.cpu_port else []) + (["--cpu-executor"] if executor else [])
@@ -205,7 +217,7 @@ def cpu_baseline(args, executor=False):
         "cpu_model": cpu_model(),
         "host_cpus_visible": os.cpu_count(),
         "kind": kind,
-        "sample": f"collisions {batches} batches x {args.cpu_worlds} worlds (worlds 0-"
+        "sample": f"{args.workload} {batches} batches x {args.cpu_worlds} worlds (worlds 0-"
                   f"{batches * args.cpu_worlds - 1}) x {args.cubes} cubes, S={args.substeps}; "
                   f"timed steps {args.settle + args.warmup + 1}-"
                   f"{args.settle + args.warmup + args.cpu_steps} ("
@@ -244,13 +256,18 @@ def main():
                                        max_candidates=4096)
     first_world, W = world_shard(rank, args.worlds)
     pos, rot = mw.gen_collisions_inits(W, args.cubes, seed=0, first_world=first_world)
-    sim = mw.CollisionsSim(W, pos, rot, cfg, gpu_id=local_rank)
+    simple = args.workload == "simple"
+    Sim = mw.SimpleSim if simple else mw.CollisionsSim
+    sim = Sim(W, pos, rot, cfg, gpu_id=local_rank)
     del pos, rot
+    # the training hand-off: collisions -- the per-world episode return
+    # (export slot 2, 1 float); simple -- the agent's position (slot 0, 3)
+    ho_slot, ho_floats = (0, 3) if simple else (2, 1)
 
     if dist is not None:
         bootstrap_rccl(sim, rank, world_size)
     # per-world returns of every rank, in world order: a torch tensor
-    returns = torch.empty(W * world_size, dtype=torch.float32, device=f"cuda:{local_rank}")
+    returns = torch.empty(W * world_size * ho_floats, dtype=torch.float32, device=f"cuda:{local_rank}")
     handoff = returns.data_ptr()
 
     # Every step is enqueued without a host round trip: the step graph, then
@@ -261,9 +278,9 @@ def main():
         if args.no_handoff:
             return
         if dist is not None:
-            sim.allgather_exported(2, handoff, 4 * W)
+            sim.allgather_exported(ho_slot, handoff, 4 * ho_floats * W)
         else:
-            sim.copy_exported_async(2, handoff, 4 * W)
+            sim.copy_exported_async(ho_slot, handoff, 4 * ho_floats * W)
 
     def barrier():
         if dist is not None:
@@ -277,7 +294,7 @@ def main():
     launches = {"SubstepRigidBodiesNode": args.substeps, "NarrowphaseNode": args.substeps,
                 "SolverNode": args.substeps, "FindOverlappingNode": 1,
                 "UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
-                "CustomParallelForNode": 1}
+                "CustomParallelForNode": 1, "ParallelForNode": 1}
     node_table = {}
     dom = None
     breakdown_steps = 0 if args.no_roofline else 2 * len(NODE_KINDS)
@@ -342,7 +359,7 @@ def main():
             raise RuntimeError(f"bench: no timed launch of {dom} in {args.steps} steps")
         ms = (ev_ms1 - ev_ms0) / (ev_n1 - ev_n0)
         cands, contacts = sim.counts()
-        units = {"body": W * (args.cubes + 1), "cand": float(cands.sum()),
+        units = {"body": W * (args.cubes + (2 if simple else 1)), "cand": float(cands.sum()),
                  "contact": float(contacts.sum())}
         nbytes = sum(BYTES[dom].get(u, 0) * units[u] for u in units)
         achieved = nbytes / (ms * 1e-3) / 1e9
@@ -390,8 +407,11 @@ def main():
             "dtype": "f32",
             "data": "synthetic (reference example init: mt19937 seed 0 positions/rotations)",
             "config": {
-                "workload": f"examples/collisions physics: {W} worlds/GPU x {args.cubes} cube hulls "
-                            f"+ ground plane, S={args.substeps}, dt=1/60",
+                "workload": (f"examples/simple_taskgraph: {W} worlds/GPU x {args.cubes} objects + "
+                             f"test object + agent, clamp + physics, S={args.substeps}, dt=1/60"
+                             if simple else
+                             f"examples/collisions physics: {W} worlds/GPU x {args.cubes} cube hulls "
+                             f"+ ground plane, S={args.substeps}, dt=1/60"),
                 "worlds_per_gpu": W, "total_worlds": total_worlds,
                 "timed_steps": f"{args.settle + args.warmup + 1}-{args.settle + args.warmup + args.steps}",
                 "parallelism": f"world-sharded x{world_size}" +

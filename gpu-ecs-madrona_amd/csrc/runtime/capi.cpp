@@ -229,7 +229,7 @@ const char *mw_env_name(int32_t i)
 int mw_step(mw_exec *exec, int32_t num_steps)
 {
     MW_TRY({
-        for (int32_t i = 0; i < num_steps; i++) exec->exec->runAsync();
+        exec->exec->runSteps(num_steps);
         exec->exec->sync();
         return 0;
     }, -1)
@@ -238,7 +238,7 @@ int mw_step(mw_exec *exec, int32_t num_steps)
 int mw_step_async(mw_exec *exec, int32_t num_steps)
 {
     MW_TRY({
-        for (int32_t i = 0; i < num_steps; i++) exec->exec->runAsync();
+        exec->exec->runSteps(num_steps);
         return 0;
     }, -1)
 }

@@ -353,6 +353,33 @@ void Executor::runAsync()
     packExports(I);
 }
 
+// Several steps world-major (every node world-local): each world runs n
+// steps on one worker, then the exports are packed once -- the same states
+// as n single steps, since worlds never read each other.
+void Executor::runSteps(int32_t n)
+{
+    Impl &I = *impl_;
+    if (n <= 0) return;
+    const bool world_local = I.segs.size() == 1 && !I.segs[0].global;
+    if (n == 1 || !world_local || !I.timedName.empty()) {
+        for (int32_t i = 0; i < n; i++) runAsync();
+        return;
+    }
+    CpuRunCtx rc { &I.mgr->hostView(), I.mgr.get(), I.cfg.numWorlds,
+                   I.nodeData.empty() ? nullptr : (char *)I.nodeData.data(), I.pool.get() };
+    struct MultiArg {
+        StepArg step;
+        int32_t steps;
+    } arg { StepArg { &I, &rc, &I.segs[0].nodes, nullptr }, n };
+    I.pool->parallelFor(I.cfg.numWorlds, 1, [](void *a, int64_t begin, int64_t end) {
+        MultiArg &m = *(MultiArg *)a;
+        for (int64_t w = begin; w < end; w++) {
+            for (int32_t s = 0; s < m.steps; s++) runWorlds(&m.step, w, w + 1);
+        }
+    }, &arg);
+    packExports(I);
+}
+
 void Executor::sync() {}
 
 void Executor::run() { runAsync(); }

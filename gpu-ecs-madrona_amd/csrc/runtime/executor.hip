@@ -1037,6 +1037,11 @@ void Executor::runAsync()
     if (I.timedPerStep > 0 && sampled) I.pendingSteps++;
 }
 
+void Executor::runSteps(int32_t n)
+{
+    for (int32_t i = 0; i < n; i++) runAsync();
+}
+
 void Executor::sync()
 {
     Impl &I = *impl_;

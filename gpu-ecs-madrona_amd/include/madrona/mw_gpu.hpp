@@ -101,6 +101,11 @@ public:
 
     void run();                               // step + sync
     void runAsync();                          // step, no sync
+    // n steps, no sync.  gfx950: n graph replays.  CPU back end: when every
+    // node is world-local, each worker steps its worlds n times in a row
+    // (world-major: a world's state stays in the worker's caches), else n
+    // single steps.
+    void runSteps(int32_t n);
     void sync();
     void *stream() const;
 

@@ -96,6 +96,24 @@ def test_worker_count_never_changes_a_bit(cpu, workers):
         assert a.contacts(w).tobytes() == b.contacts(w).tobytes()
 
 
+def test_multi_step_world_major_equals_single_steps(cpu):
+    # mw_step(n) on the CPU back end runs each world's n steps back to back on
+    # one worker (every collisions node is world-local); states and the
+    # exported buffers must equal n separate steps.
+    pos, rot = ol.gen_collisions_inits(5, 64, seed=11)
+    g = cpu.default_collisions_config(64, 4, 2048, 2048)
+    a = cpu.CollisionsSim(5, pos, rot, g, num_workers=3)
+    b = cpu.CollisionsSim(5, pos, rot, g, num_workers=3)
+    a.step(25)
+    for _ in range(25):
+        b.step(1)
+    for w in range(5):
+        assert a.bodies(w).tobytes() == b.bodies(w).tobytes()
+        assert a.contacts(w).tobytes() == b.contacts(w).tobytes()
+    for slot in range(3):
+        assert a.exported_array(slot, np.uint8).tobytes() == b.exported_array(slot, np.uint8).tobytes()
+
+
 @pytest.mark.skipif(not ol.ref_available(), reason="oracle/_ref not built (no /root/reference)")
 def test_collisions_bit_exact_vs_live_reference(cpu):
     # The CPU back end against the reference itself (not the restatement),

@@ -1,8 +1,10 @@
 """Multi-GPU path on CPU: world sharding + the episode-return all-gather
  with world_size 2 over gloo.  Each rank generates only its
-shard's inits (product generator, first_world offset), steps it (oracle as
-the stand-in for the per-GPU stepper), and the gathered returns must equal a
-single-process run over all worlds, in world order."""
+shard's inits (product generator, first_world offset), steps its shard on the
+framework's own executor (the CPU back end, libmadrona_cpu.so: the same world
+sources, graph and export buffers as a GPU rank), reads the packed export
+(getExported slot 2) and all-gathers it; the gathered returns must equal the
+oracle's single-process run over all worlds, in world order."""
 import os
 import socket
 
@@ -53,9 +55,15 @@ def _rank_main(rank, world_size, port, result_q):
         from madrona_mi355x.sharding import gather_world_returns, world_shard
         first, n = world_shard(rank, WORLDS_PER_RANK)
         pos, rot = mw.gen_collisions_inits(n, CUBES, seed=0, first_world=first)
+        cfg = mw.default_collisions_config(CUBES, 4, 1024, 1024)
+        sim = mw.CollisionsSim(n, pos, rot, cfg, backend="cpu", num_workers=1)
         gathered = []
-        for r in _returns(pos, rot, STEPS):
+        for _ in range(STEPS):
+            sim.step(1)
+            r = sim.exported_array(2, np.float32).copy()
             gathered.append(gather_world_returns(torch.from_numpy(r)).numpy().copy())
+        assert sim.error_flags() == 0
+        sim.close()
         if rank == 0:
             result_q.put(np.stack(gathered))
     finally:
