@@ -613,7 +613,7 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
     __shared__ int32_t s_scan[kNarrowBlock / 64];
-    __shared__ int32_t s_base[2];
+    __shared__ int32_t s_base[3];
     const int32_t w = blockIdx.x;
     const int32_t cap = P.candCapacity;
     const int32_t num = min(P.numCands[w], cap);
@@ -650,8 +650,15 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
             const int32_t thh = (total >> 10) & 1023, tpl = total >> 20;
             s_base[0] = thh > 0 ? atomicAdd(binCounter(P, bin, 0), thh) : 0;
             s_base[1] = tpl > 0 ? atomicAdd(binCounter(P, bin, 1), tpl) : 0;
+            // an overrun of the bin is refused and flagged (filterWorldOnWave)
+            s_base[2] = s_base[0] + thh > P.binCap || s_base[1] + tpl > P.binCap;
+            if (s_base[2]) atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardList << 8));
         }
         __syncthreads();
+        if (s_base[2]) {
+            S = 0;
+            break;
+        }
         int32_t hpos = s_base[0] + ((off >> 10) & 1023);
         int32_t ppos = s_base[1] + (off >> 20);
         int32_t slot = S + (off & 1023);

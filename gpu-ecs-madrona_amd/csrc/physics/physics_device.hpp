@@ -35,7 +35,7 @@ __device__ __forceinline__ int bodyArchIndex(const PhysArgs &P, uint32_t archety
 enum GuardSite : int32_t {
     kGuardRefFace = 1, kGuardIncFace, kGuardIncWalk, kGuardRefWalk, kGuardVertex,
     kGuardPlaneFace, kGuardPlaneWalk, kGuardSolverBody, kGuardSolverSlot, kGuardEntity,
-    kGuardLeaf, kGuardNode, kGuardWork,
+    kGuardLeaf, kGuardNode, kGuardWork, kGuardList,
 };
 
 __device__ __forceinline__ int32_t guardIndex(int32_t i, int32_t n, int32_t *flags,
@@ -287,7 +287,9 @@ __device__ __forceinline__ void loadBinPrefix(const PhysArgs &P, int32_t which, 
 {
     static_assert(kNarrowBins == 64, "one wave scans the bins");
     if (threadIdx.x < 64) {
-        const int32_t v = *(volatile int32_t *)binCounter(P, threadIdx.x, which);
+        // a count past the bin (a filter's reservation that overran it was
+        // refused and flagged) is read as the full bin: entries stay in bounds
+        const int32_t v = min(*(volatile int32_t *)binCounter(P, threadIdx.x, which), P.binCap);
         int32_t x = v;
 #pragma unroll
         for (int32_t o = 1; o < 64; o <<= 1) {
@@ -409,6 +411,17 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
     }
     b_hh = __shfl(b_hh, 0);
     b_hp = __shfl(b_hp, 0);
+    // Each list stays inside its bin whatever its counter says (the
+    // reservations fit by construction -- binCap = worlds per bin x
+    // candCapacity -- while the counters were reset before this filter):
+    // an overrun is refused and flagged, never written.
+    if (b_hh + n_hh > P.binCap || b_hp + n_hp > P.binCap) {
+        if (lane == 0) {
+            atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardList << 8));
+            P.survCount[w] = 0;
+        }
+        return;
+    }
     int32_t S = 0;
     for (int32_t b0 = 0; b0 < num; b0 += kBatch) {
         uint64_t s[kFilterBatch];
