@@ -139,3 +139,23 @@ def test_collisions_bit_exact_vs_live_reference(cpu):
             compared += 1
     assert compared >= W * 30, compared
     assert np.sum(sim.counts()[1]) > 0
+
+
+@pytest.mark.skipif(not ol.ref_available(), reason="oracle/_ref not built (no /root/reference)")
+def test_fvs_bit_exact_vs_live_reference(cpu):
+    # fantasy_vs on the CPU back end against the reference's own ECS
+    # (oracle/ref_fvs.cpp), not the restatement: every column of both tables,
+    # ids, generations and the swap-remove row order, through the deaths.
+    W = 3
+    inits = ol.gen_fvs_inits(W, 50, 200, seed=5)
+    sim = cpu.FvsSim(W, inits, backend="cpu", num_workers=2)
+    ref = ol.ReferenceFvs(inits)
+    for t in range(1, 13):
+        sim.step(100)
+        ref.step(100)
+        for w in range(W):
+            for arch in (0, 1):
+                a, b = sim.table(w, arch), ref.table(w, arch)
+                assert a.tobytes() == b.tobytes(), f"tick {100 * t} world {w} arch {arch}"
+    assert sum(len(ref.table(w, 0)) for w in range(W)) < 50 * W      # dragons died
+
