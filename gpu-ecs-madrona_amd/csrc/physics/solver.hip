@@ -77,10 +77,9 @@ struct PairConst {
     float mu;             // avg mu_s (positions) / avg mu_d (velocities)
 };
 
-__device__ __forceinline__ PairConst pairConst(const PhysArgs &P, const SMut &b1, const SMut &b2,
-                                               Vector3 n, bool velocities)
+__device__ __forceinline__ PairConst pairConstOf(const RigidBodyMetadata &m1, const RigidBodyMetadata &m2,
+                                                 const SMut &b1, const SMut &b2, Vector3 n, bool velocities)
 {
-    const RigidBodyMetadata m1 = P.objs.metadata[b1.meta >> 16], m2 = P.objs.metadata[b2.meta >> 16];
     PairConst k;
     k.im1 = m1.invMass;
     k.im2 = m2.invMass;
@@ -91,6 +90,64 @@ __device__ __forceinline__ PairConst pairConst(const PhysArgs &P, const SMut &b1
     k.n = n;
     k.mu = velocities ? 0.5f * (m1.muD + m2.muD) : 0.5f * (m1.muS + m2.muS);
     return k;
+}
+
+// A contact item's global inputs besides the manifold: both bodies' substep
+// columns and object metadata.  Their addresses depend only on the LDS body
+// records, so the item issues them in the same round of loads as the
+// manifold (loaded inside the solves, after the branch on the manifold's
+// bound check, they cost a second memory round trip per item).
+struct PosIn {
+    solver::PreSolvePositional ps1, ps2;
+    solver::SubstepPrevState pv1, pv2;
+    RigidBodyMetadata m1, m2;
+};
+
+struct VelIn {
+    solver::PreSolvePositional ps1, ps2;
+    solver::PreSolveVelocity pv1, pv2;
+    RigidBodyMetadata m1, m2;
+};
+
+// skip1 / skip2: the side's per-substep columns are not read (an invariant
+// static body the solve skips); the general solve of such an item reloads
+// them (loadPosIn with both false).
+__device__ __forceinline__ PosIn loadPosIn(const PhysArgs &P, int32_t w, const SMut &b1, int32_t s1,
+                                           const SMut &b2, int32_t s2, bool skip1, bool skip2)
+{
+    const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
+    PosIn in;
+    in.ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
+    in.ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
+    in.pv1 = {};
+    in.pv2 = {};
+    if (!skip1) in.pv1 = bcol<solver::SubstepPrevState>(P.body[o1.arch], Cols::SubstepPrevState, w, o1.row);
+    if (!skip2) in.pv2 = bcol<solver::SubstepPrevState>(P.body[o2.arch], Cols::SubstepPrevState, w, o2.row);
+    in.m1 = P.objs.metadata[o1.obj];
+    in.m2 = P.objs.metadata[o2.obj];
+    return in;
+}
+
+__device__ __forceinline__ VelIn loadVelIn(const PhysArgs &P, int32_t w, const SMut &b1, int32_t s1,
+                                           const SMut &b2, int32_t s2, bool skip1, bool skip2)
+{
+    const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
+    VelIn in;
+    in.ps1 = {};
+    in.ps2 = {};
+    in.pv1 = {};
+    in.pv2 = {};
+    if (!skip1) {
+        in.ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
+        in.pv1 = bcol<solver::PreSolveVelocity>(P.body[o1.arch], Cols::PreSolveVelocity, w, o1.row);
+    }
+    if (!skip2) {
+        in.ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
+        in.pv2 = bcol<solver::PreSolveVelocity>(P.body[o2.arch], Cols::PreSolveVelocity, w, o2.row);
+    }
+    in.m1 = P.objs.metadata[o1.obj];
+    in.m2 = P.objs.metadata[o2.obj];
+    return in;
 }
 
 // ---------------------------------------------------------------------------
@@ -163,18 +220,13 @@ __device__ __forceinline__ bool boundedInput(const ContactIn &c)
 }
 
 template <int ST>
-__device__ __forceinline__ int32_t solveContactPositionsT(const PhysArgs &P, int32_t w, SMut &b1,
-                                                          int32_t s1, SMut &b2, int32_t s2,
-                                                          const ContactIn &c, float *lambda_out)
+__device__ __forceinline__ int32_t solveContactPositionsT(SMut &b1, SMut &b2, const ContactIn &c,
+                                                          const PosIn &in, float *lambda_out)
 {                                                          // physics.cpp:281-476
     constexpr bool sk1 = ST == 1, sk2 = ST == 2;
-    const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
-    const auto ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
-    const auto ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
-    solver::SubstepPrevState pv1 {}, pv2 {};
-    if (!sk1) pv1 = bcol<solver::SubstepPrevState>(P.body[o1.arch], Cols::SubstepPrevState, w, o1.row);
-    if (!sk2) pv2 = bcol<solver::SubstepPrevState>(P.body[o2.arch], Cols::SubstepPrevState, w, o2.row);
-    const PairConst k = pairConst(P, b1, b2, c.n, false);
+    const solver::PreSolvePositional &ps1 = in.ps1, &ps2 = in.ps2;
+    const solver::SubstepPrevState &pv1 = in.pv1, &pv2 = in.pv2;
+    const PairConst k = pairConstOf(in.m1, in.m2, b1, b2, c.n, false);
     const bool sk = sk1 || sk2;
     const Vector3 n = k.n;
     Vector3 x1 = b1.x, x2 = b2.x;
@@ -389,24 +441,13 @@ __device__ __forceinline__ void applyVelocityUpdate(Vector3 &v1, Vector3 &v2, Ve
 }
 
 template <int ST>
-__device__ __forceinline__ int32_t solveContactVelocitiesT(const PhysArgs &P, int32_t w, SMut &b1,
-                                                           int32_t s1, SMut &b2, int32_t s2,
-                                                           const ContactIn &c, float h,
-                                                           float rest_thresh)
+__device__ __forceinline__ int32_t solveContactVelocitiesT(SMut &b1, SMut &b2, const ContactIn &c,
+                                                           const VelIn &in, float h, float rest_thresh)
 {                                                          // physics.cpp:865-993
     constexpr bool sk1 = ST == 1, sk2 = ST == 2;
-    const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
-    solver::PreSolvePositional ps1 {}, ps2 {};
-    solver::PreSolveVelocity pv1 {}, pv2 {};
-    if (!sk1) {
-        ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
-        pv1 = bcol<solver::PreSolveVelocity>(P.body[o1.arch], Cols::PreSolveVelocity, w, o1.row);
-    }
-    if (!sk2) {
-        ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
-        pv2 = bcol<solver::PreSolveVelocity>(P.body[o2.arch], Cols::PreSolveVelocity, w, o2.row);
-    }
-    const PairConst k = pairConst(P, b1, b2, c.n, true);
+    const solver::PreSolvePositional &ps1 = in.ps1, &ps2 = in.ps2;
+    const solver::PreSolveVelocity &pv1 = in.pv1, &pv2 = in.pv2;
+    const PairConst k = pairConstOf(in.m1, in.m2, b1, b2, c.n, true);
     const bool sk = sk1 || sk2;
     const Quat q1 = b1.q, q2 = b2.q;
     Vector3 v1 = b1.v, o1v = b1.omega, v2 = b2.v, o2v = b2.omega;
@@ -1014,29 +1055,25 @@ static __device__ unsigned long long g_solverBlockT[2 * 16384];   // start, end 
 // The solves by static side (ST: 0 = both bodies, 1 = skip the ref body --
 // the ground plane of a hull-plane manifold, nearly every contact --,
 // 2 = skip the alt body).
-__device__ __forceinline__ int32_t solvePositionsGeneral(const PhysArgs &P, int32_t w, SMut &b1,
-                                                      int32_t s1, SMut &b2, int32_t s2,
-                                                      const ContactIn &c, float *lambda_out)
+__device__ __forceinline__ int32_t solvePositionsGeneral(SMut &b1, SMut &b2, const ContactIn &c,
+                                                         const PosIn &in, float *lambda_out)
 {
-    return solveContactPositionsT<0>(P, w, b1, s1, b2, s2, c, lambda_out);
+    return solveContactPositionsT<0>(b1, b2, c, in, lambda_out);
 }
-__device__ __forceinline__ int32_t solvePositionsStaticAlt(const PhysArgs &P, int32_t w, SMut &b1,
-                                                        int32_t s1, SMut &b2, int32_t s2,
-                                                        const ContactIn &c, float *lambda_out)
+__device__ __forceinline__ int32_t solvePositionsStaticAlt(SMut &b1, SMut &b2, const ContactIn &c,
+                                                           const PosIn &in, float *lambda_out)
 {
-    return solveContactPositionsT<2>(P, w, b1, s1, b2, s2, c, lambda_out);
+    return solveContactPositionsT<2>(b1, b2, c, in, lambda_out);
 }
-__device__ __forceinline__ int32_t solveVelocitiesGeneral(const PhysArgs &P, int32_t w, SMut &b1,
-                                                       int32_t s1, SMut &b2, int32_t s2,
-                                                       const ContactIn &c, float h, float rt)
+__device__ __forceinline__ int32_t solveVelocitiesGeneral(SMut &b1, SMut &b2, const ContactIn &c,
+                                                          const VelIn &in, float h, float rt)
 {
-    return solveContactVelocitiesT<0>(P, w, b1, s1, b2, s2, c, h, rt);
+    return solveContactVelocitiesT<0>(b1, b2, c, in, h, rt);
 }
-__device__ __forceinline__ int32_t solveVelocitiesStaticAlt(const PhysArgs &P, int32_t w, SMut &b1,
-                                                         int32_t s1, SMut &b2, int32_t s2,
-                                                         const ContactIn &c, float h, float rt)
+__device__ __forceinline__ int32_t solveVelocitiesStaticAlt(SMut &b1, SMut &b2, const ContactIn &c,
+                                                            const VelIn &in, float h, float rt)
 {
-    return solveContactVelocitiesT<2>(P, w, b1, s1, b2, s2, c, h, rt);
+    return solveContactVelocitiesT<2>(b1, b2, c, in, h, rt);
 }
 
 // Which solve an item takes: its kind, unless a contact's inputs are out of
@@ -1052,18 +1089,21 @@ __device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w,
 {
     if (r.slot >= 0) {
         Contact &cr = P.candContacts[(size_t)w * P.candCapacity + r.slot];
-        const ContactIn c = loadContact(cr);
         SMut &b1 = L.bodies[r.s1], &b2 = L.bodies[r.s2];
+        // one round of loads: the manifold and the bodies' columns
+        const ContactIn c = loadContact(cr);
+        PosIn in = loadPosIn(P, w, b1, r.s1, b2, r.s2, kind == kKindStaticRef, kind == kKindStaticAlt);
         const int32_t k = solveKind(kind, c);
         int32_t res = kSolveNonFinite;
         if (k == kKindStaticRef) {
-            res = solveContactPositionsT<1>(P, w, b1, r.s1, b2, r.s2, c, cr.lambdaN);
+            res = solveContactPositionsT<1>(b1, b2, c, in, cr.lambdaN);
         } else if (k == kKindStaticAlt) {
-            res = solvePositionsStaticAlt(P, w, b1, r.s1, b2, r.s2, c, cr.lambdaN);
+            res = solvePositionsStaticAlt(b1, b2, c, in, cr.lambdaN);
         }
         if (res != kSolveDone) {
             if (k != kKindGeneral) atomicOr(P.errorFlags + w, kErrStaticSchedule);
-            solvePositionsGeneral(P, w, b1, r.s1, b2, r.s2, c, cr.lambdaN);
+            if (kind != kKindGeneral) in = loadPosIn(P, w, b1, r.s1, b2, r.s2, false, false);
+            solvePositionsGeneral(b1, b2, c, in, cr.lambdaN);
         }
     } else {
         const JointConstraint &j = P.joints[(size_t)w * P.jointCapacity + (-1 - r.slot)];
@@ -1075,19 +1115,21 @@ __device__ __forceinline__ void solveItemVelocities(const PhysArgs &P, int32_t w
                                                     const CRec r, int32_t kind)
 {
     if (r.slot < 0) return;                                // joints: positions only
-    const ContactIn c = loadContact(P.candContacts[(size_t)w * P.candCapacity + r.slot]);
-    const SolverData &sd = P.solver[w];
     SMut &b1 = L.bodies[r.s1], &b2 = L.bodies[r.s2];
+    const ContactIn c = loadContact(P.candContacts[(size_t)w * P.candCapacity + r.slot]);
+    VelIn in = loadVelIn(P, w, b1, r.s1, b2, r.s2, kind == kKindStaticRef, kind == kKindStaticAlt);
+    const SolverData &sd = P.solver[w];
     const int32_t k = solveKind(kind, c);
     int32_t res = kSolveNonFinite;
     if (k == kKindStaticRef) {
-        res = solveContactVelocitiesT<1>(P, w, b1, r.s1, b2, r.s2, c, sd.h, sd.restitutionThreshold);
+        res = solveContactVelocitiesT<1>(b1, b2, c, in, sd.h, sd.restitutionThreshold);
     } else if (k == kKindStaticAlt) {
-        res = solveVelocitiesStaticAlt(P, w, b1, r.s1, b2, r.s2, c, sd.h, sd.restitutionThreshold);
+        res = solveVelocitiesStaticAlt(b1, b2, c, in, sd.h, sd.restitutionThreshold);
     }
     if (res != kSolveDone) {
         if (k != kKindGeneral) atomicOr(P.errorFlags + w, kErrStaticSchedule);
-        solveVelocitiesGeneral(P, w, b1, r.s1, b2, r.s2, c, sd.h, sd.restitutionThreshold);
+        if (kind != kKindGeneral) in = loadVelIn(P, w, b1, r.s1, b2, r.s2, false, false);
+        solveVelocitiesGeneral(b1, b2, c, in, sd.h, sd.restitutionThreshold);
     }
 }
 

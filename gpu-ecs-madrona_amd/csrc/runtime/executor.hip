@@ -183,6 +183,10 @@ __global__ void __launch_bounds__(256) structuralCommitKernel(CommitArgs A)
         if (cw < st.numWorlds && (st.appendDirty[cw] != 0 || st.deferCount[cw] != 0)) {
             work[atomicAdd(&num_work, 1)] = cw;
         }
+        if (cw < st.numWorlds && st.makeTurn) {        // the next node's wave counts
+#pragma unroll
+            for (int32_t s = 0; s < kMakeTurnSlots; s++) st.makeTurn[(size_t)s * st.numWorlds + cw] = 0;
+        }
     }
     __syncthreads();
     const int32_t nwork = num_work;

@@ -398,6 +398,8 @@ void StateManager::uploadToDevice(void *stream_ptr)
     d.deferCount = (int32_t *)devAlloc(sizeof(int32_t) * W);
     MW_HIP_CHECK(hipMemsetAsync(d.deferCount, 0, sizeof(int32_t) * W, stream));
     d.deferLog = (DeferredDestroy *)devAlloc(sizeof(DeferredDestroy) * (size_t)W * d.deferCap);
+    d.makeTurn = (int32_t *)devAlloc(sizeof(int32_t) * kMakeTurnSlots * W);
+    MW_HIP_CHECK(hipMemsetAsync(d.makeTurn, 0, sizeof(int32_t) * kMakeTurnSlots * W, stream));
     if (d.tmpBytesPerWorld > 0) {
         d.tmpArena = devAlloc((size_t)d.tmpBytesPerWorld * W);
         copy(d.tmpArena, I.host.tmpArena, (size_t)d.tmpBytesPerWorld * W);

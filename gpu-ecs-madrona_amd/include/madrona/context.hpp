@@ -17,9 +17,9 @@
 //     rows and deferred destroys by key and replays them in that order --
 //     rows land where the reference's serial walk puts them, swap-removes
 //     happen in its order, moved entities are remapped.  Entity IDs made by
-//     row-parallel lanes come from the world's ID store under a per-world
-//     lock, so they match the reference up to a relabelling (SURVEY.md §8c
-//     rule for in-step churn); clearArchetype is world-serial only.
+//     row-parallel lanes come from the world's ID store in row order
+//     (lockedAcquire): deterministic, and the reference's IDs when each row
+//     makes at most one entity; clearArchetype is world-serial only.
 #pragma once
 
 #include <madrona/state.hpp>
@@ -47,6 +47,7 @@ private:
 };
 
 inline constexpr int32_t kMaxQueryArchetypes = 8;
+static_assert(kMaxQueryArchetypes == kMakeTurnSlots);
 inline constexpr int32_t kMaxQueryComponents = 12;
 
 // A resolved query: matching archetypes and the column of each component.
@@ -148,6 +149,9 @@ public:
     // Row-parallel mode (set by the row-parallel node kernels): the lane's
     // position in the reference's serial walk, (query archetype << 24) | row.
     MW_INLINE void setRowParallel(uint32_t row_key) { rowKey_ = row_key; seq_ = 0; }
+    // The lane's wave index among the waves covering this world's rows and
+    // the world's finished-wave counter (StateView::makeTurn).
+    MW_INLINE void setMakeTurn(int32_t *turn, int32_t chunk) { turn_ = turn; turnChunk_ = chunk; }
     MW_INLINE bool rowParallel() const { return rowKey_ != kSerialRowKey; }
 
     template <typename ArchetypeT, typename... Args>
@@ -229,6 +233,8 @@ protected:
     StateManager *mgr_;
     uint32_t rowKey_ = kSerialRowKey;
     uint32_t seq_ = 0;
+    int32_t *turn_ = nullptr;
+    int32_t turnChunk_ = 0;
     int32_t jobDepth_ = 0;      // nesting of the job being run (0: none)
     // Job API bookkeeping (only touched by job-API worlds).
     uint64_t jobKeys_[kMaxJobDepth];
@@ -252,10 +258,14 @@ public:
 
 // ---------------------------------------------------------------------------
 // Row-parallel makeEntityNow: the world's ID store is serial
-// (id_map_impl.inl:69-182), so lanes take it one at a time -- the lanes of a
-// wave in lane order (no two lanes of one wave contend for the lock), waves
-// through a per-world spin lock with agent-scope fences (a world's rows may
-// run on several XCDs).
+// (id_map_impl.inl:69-182), so lanes take it one at a time, in row order:
+// the lanes of a wave in lane order, and a wave only once every lower wave
+// covering the world's rows has finished (StateView::makeTurn; the row
+// kernel counts finished waves per world).  The IDs are therefore the same
+// run to run, and the reference's when every row makes at most one entity
+// (its serial walk hands them out in row order).  Lower waves are dispatched
+// before higher ones and never wait on them, so the wait always ends.
+// Without a turn counter (other callers) waves go through a per-world lock.
 MW_INLINE Entity Context::lockedAcquire(int32_t arch, int32_t row)
 {
     IDMapView ids = state_->ids(world_);
@@ -266,12 +276,19 @@ MW_INLINE Entity Context::lockedAcquire(int32_t arch, int32_t row)
     while (pending) {
         const uint32_t leader = (uint32_t)__builtin_ctzll(pending);
         if (lane == leader) {
-            while (atomicCAS(&ids.st->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
-            __threadfence();
-            e = ids.acquire(ids.st->worldCache);
-            if (e.id >= 0) ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
-            __threadfence();
-            atomicExch(&ids.st->lock, 0);
+            if (turn_) {
+                while (__hip_atomic_load(turn_, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != turnChunk_)
+                    __builtin_amdgcn_s_sleep(2);
+                e = ids.acquire(ids.st->worldCache);
+                if (e.id >= 0) ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
+            } else {
+                while (atomicCAS(&ids.st->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
+                __threadfence();
+                e = ids.acquire(ids.st->worldCache);
+                if (e.id >= 0) ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
+                __threadfence();
+                atomicExch(&ids.st->lock, 0);
+            }
         }
         pending &= pending - 1;
     }

@@ -272,6 +272,8 @@ struct ArchetypeView {
     uint64_t colKeys[kMaxColumns];
 };
 
+inline constexpr int32_t kMakeTurnSlots = 8;     // = kMaxQueryArchetypes (context.hpp)
+
 struct StateView {
     int32_t numWorlds;
     int32_t numArchetypes;
@@ -287,6 +289,11 @@ struct StateView {
     int32_t *deferCount;        // [numWorlds] deferred destroys of the running node
     DeferredDestroy *deferLog;  // [numWorlds][deferCap]
     int32_t deferCap;
+    // Waves of the running row-parallel node that have finished their rows,
+    // per (query archetype, world): a wave's makeEntityNow calls wait until
+    // every lower wave of the world is done, so IDs are taken in row order
+    // (Context::lockedAcquire); reset by the ordered commit.
+    int32_t *makeTurn;          // [kMakeTurnSlots][numWorlds]
     // Per-world bump allocator (Context::tmpAlloc, reference
     // StateManager::tmpAlloc, src/core/state.cpp:584-602): 256-byte
     // granules, reset by ResetTmpAllocNode.

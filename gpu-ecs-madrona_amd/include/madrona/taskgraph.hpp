@@ -443,19 +443,33 @@ parallelForKernel(const StateView *__restrict__ st_in, int32_t arch, int32_t que
     const int64_t total = (int64_t)st->numWorlds * inv_per_world * threads;
     // grid-stride: one pass with the default grid, several when the node's
     // launch configuration caps the grid (LaunchCtx::capGrid)
+    // finished waves per world (row-ordered makeEntityNow, Context::lockedAcquire)
+    int32_t *turn = st->makeTurn && query_arch < kMakeTurnSlots
+                        ? st->makeTurn + (size_t)query_arch * st->numWorlds : nullptr;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t inv = t / threads;
         const int32_t w = (int32_t)(inv / inv_per_world);
         const int32_t first = (int32_t)(inv - (int64_t)w * inv_per_world) * items;
         const int32_t n = st->arch[arch].numRows[w];
-        if (first >= n) continue;
-        ContextT ctx = worldContext<ContextT>(st, w);
+        if (first < n) {
+            ContextT ctx = worldContext<ContextT>(st, w);
+            // this wave's index among the waves covering world w
+            const int64_t t_w0 = (int64_t)w * inv_per_world * threads;
+            if (turn) ctx.setMakeTurn(turn + w, (int32_t)((t >> 6) - (t_w0 >> 6)));
 #pragma unroll 1
-        for (int32_t k = 0; k < items && first + k < n; k++) {
-            ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k));
-            invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, first + k,
-                                                    std::index_sequence_for<ComponentTs...> {});
+            for (int32_t k = 0; k < items && first + k < n; k++) {
+                ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k));
+                invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, first + k,
+                                                        std::index_sequence_for<ComponentTs...> {});
+            }
+        }
+        if (turn) {
+            // the wave is done with its rows of each world it covers: the
+            // active lanes are a prefix of the wave (t ascends with the lane)
+            const int32_t pw = __shfl_up(w, 1, 64);
+            if (__lane_id() == 0 || pw != w)
+                __hip_atomic_fetch_add(turn + w, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

@@ -84,9 +84,10 @@ def test_row_parallel_mode_diverges_as_documented():
 
 
 def test_ecs_ops_serial_nodes_entity_ids_exact_and_repeatable():
-    """Row-parallel makeEntityNow takes IDs in lock-arrival order (equal to
-    the reference's only up to relabelling); world-serially they are the
-    reference's IDs exactly, and two runs are byte-identical."""
+    """Row-parallel, ecs_ops' IDs differ from the reference's: a row makes
+    several entities, and its destroys release IDs at the commit, not
+    mid-walk; world-serially they are the reference's IDs exactly, and two
+    runs are byte-identical."""
     W, steps = 6, 40
     a = el.EcsOpsSim(W, serial_nodes=True)
     b = el.EcsOpsSim(W, serial_nodes=True)
@@ -99,3 +100,22 @@ def test_ecs_ops_serial_nodes_entity_ids_exact_and_repeatable():
         for w in range(W):
             el.compare_world(a, ref, w, f"step {s}", exact_ids=True)
             assert a.spawns(w).tobytes() == b.spawns(w).tobytes()
+
+
+def test_ecs_ops_row_parallel_entity_ids_repeatable():
+    """Row-parallel makeEntityNow takes IDs in row order (a wave's lanes in
+    order, a world's waves one after another: StateView::makeTurn), so two
+    runs of the same worlds are byte-identical, ID columns included.  40
+    agent rows per world put most worlds across two waves, so the waves of a
+    world race for the ID store unless they are ordered."""
+    W, steps = 2048, 30
+    a = el.EcsOpsSim(W)
+    b = el.EcsOpsSim(W)
+    sample = range(0, W, 37)
+    for s in range(steps):
+        a.step()
+        b.step()
+        assert a.error_flags() == 0
+        for w in sample:
+            assert a.spawns(w).tobytes() == b.spawns(w).tobytes(), f"step {s} world {w}"
+            assert a.agents(w).tobytes() == b.agents(w).tobytes(), f"step {s} world {w}"
