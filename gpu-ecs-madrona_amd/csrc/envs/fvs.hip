@@ -4,7 +4,9 @@
 // and row compaction.  Restated from the reference's job-API example
 // (examples/fantasy_vs/fvs.cpp:111-240, fvs.hpp) onto the TaskGraph API:
 //   actionSelect  ParallelForNode<Entity, Position, Action>   (fvs.cpp:111-151)
-//   caster        ParallelForNode<Entity, Action, Mana>       (fvs.cpp:153-190)
+//   caster        CustomParallelForNode<.., 16, 1, Entity, Action, Mana>
+//                 (fvs.cpp:153-190): the blast's scan of every Position /
+//                 Health row is split over the invocation's 16 lanes
 //   archer        ParallelForNode<Entity, Action, Quiver>     (fvs.cpp:192-214)
 //   cleanup       ParallelForNode<Entity, Health> marks the dead, a
 //                 PerWorldNode makes their trackers, a ParallelForNode over
@@ -63,6 +65,11 @@ struct Config {
 
 class Engine;
 
+// Lanes per casting dragon: a blast tests every Position / Health row of the
+// world (250 at the benchmark size) against its radius; one lane per dragon
+// made that a serial chain of ~250 dependent cache reads.
+constexpr int32_t kCastLanes = 16;
+
 struct Game : public WorldBase {
     static void registerTypes(ECSRegistry &reg, const Config &cfg)
     {
@@ -83,7 +90,7 @@ struct Game : public WorldBase {
         auto act = builder.addToGraph<
             ParallelForNode<Engine, actionSelectSystem, Entity, Position, Action>>({});
         auto cast = builder.addToGraph<
-            ParallelForNode<Engine, casterSystem, Entity, Action, Mana>>({ act });
+            CustomParallelForNode<Engine, casterSystem, kCastLanes, 1, Entity, Action, Mana>>({ act });
         auto shoot = builder.addToGraph<
             ParallelForNode<Engine, archerSystem, Entity, Action, Quiver>>({ act });
         auto mark = builder.addToGraph<
@@ -160,23 +167,50 @@ MW_HD void Game::actionSelectSystem(Engine &ctx, Entity &e, Position &pos, Actio
     }
 }
 
+MW_HD static inline int32_t castLane()
+{
+#if defined(__HIP_DEVICE_COMPILE__) || !defined(__HIPCC__)
+    return mwGPU::invocationLane<kCastLanes>();
+#else
+    return 0;                              // hipcc's host pass: never run
+#endif
+}
+
+// The reference's serial body, cooperatively: every lane of the invocation
+// decides from the row's values (regenerated mana, remaining time), the last
+// lane writes them back (on the device the lanes read in lockstep before the
+// store; on the CPU back end the lanes run in order, so lanes 0..14 read
+// before lane 15 writes), and the lanes share the blast's row scan.  Blast
+// damage is an integer atomic subtraction, so the split leaves every hp as
+// the serial scan does.
 MW_HD void Game::casterSystem(Engine &ctx, Entity &e, Action &action, Mana &mana)
 {                                                          // fvs.cpp:153-190
     const Game &g = ctx.data();
-    mana.mp += kManaRegenRate * kDeltaT;
-    if (action.remainingTime > 0) return;
-    if (mana.mp < kCastCost) return;
-    mana.mp -= kCastCost;
+    const int32_t lane = castLane();
+    const float mp = mana.mp + kManaRegenRate * kDeltaT;
+    const bool cast = !(action.remainingTime > 0) && !(mp < kCastCost);
+    if (lane == kCastLanes - 1) {
+        mana.mp = cast ? mp - kCastCost : mp;
+        if (cast) action.remainingTime = kCastTime;
+    }
+    if (!cast) return;
     const Draw d { g.worldSeed, (uint32_t)e.id, g.tickCount };
     const Vector3 target {
         d.uniform(kDrawTargetX, g.worldBounds.pMin.x, g.worldBounds.pMax.x),
         d.uniform(kDrawTargetY, g.worldBounds.pMin.y, g.worldBounds.pMax.y),
         d.uniform(kDrawTargetZ, g.worldBounds.pMin.z, g.worldBounds.pMax.z),
     };
-    ctx.forEach(g.healthQuery, [&](const Position &p, Health &h) {
-        if (target.distance(p) <= kBlastRadius) damage(h, kBlastDamage);
-    });
-    action.remainingTime = kCastTime;
+    StateView &st = ctx.state();
+    const int32_t w = ctx.worldID().idx;
+    for (int32_t a = 0; a < g.healthQuery.numArchetypes; a++) {
+        const int32_t arch = g.healthQuery.archetypes[a];
+        const Position *pos = st.column<Position>(arch, g.healthQuery.cols[a][0], w);
+        Health *hp = st.column<Health>(arch, g.healthQuery.cols[a][1], w);
+        const int32_t n = st.arch[arch].numRows[w];
+        for (int32_t r = lane; r < n; r += kCastLanes) {
+            if (target.distance(rowRef(pos, r)) <= kBlastRadius) damage(rowRef(hp, r), kBlastDamage);
+        }
+    }
 }
 
 MW_HD void Game::archerSystem(Engine &ctx, Entity &e, Action &action, Quiver &quiver)

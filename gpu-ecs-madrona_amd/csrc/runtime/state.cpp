@@ -398,8 +398,14 @@ void StateManager::uploadToDevice(void *stream_ptr)
     d.deferCount = (int32_t *)devAlloc(sizeof(int32_t) * W);
     MW_HIP_CHECK(hipMemsetAsync(d.deferCount, 0, sizeof(int32_t) * W, stream));
     d.deferLog = (DeferredDestroy *)devAlloc(sizeof(DeferredDestroy) * (size_t)W * d.deferCap);
-    d.makeTurn = (int32_t *)devAlloc(sizeof(int32_t) * kMakeTurnSlots * W);
-    MW_HIP_CHECK(hipMemsetAsync(d.makeTurn, 0, sizeof(int32_t) * kMakeTurnSlots * W, stream));
+    const size_t turn_bytes = sizeof(int32_t) * kMakeTurnSlots * kMakeTurnWaves * W;
+    d.makeTurn = (int32_t *)devAlloc(turn_bytes);
+    MW_HIP_CHECK(hipMemsetAsync(d.makeTurn, 0, turn_bytes, stream));
+    d.makeEpoch = (int32_t *)devAlloc(sizeof(int32_t));
+    {
+        const int32_t first_epoch = 1;
+        copy(d.makeEpoch, &first_epoch, sizeof(int32_t));
+    }
     if (d.tmpBytesPerWorld > 0) {
         d.tmpArena = devAlloc((size_t)d.tmpBytesPerWorld * W);
         copy(d.tmpArena, I.host.tmpArena, (size_t)d.tmpBytesPerWorld * W);

@@ -149,9 +149,15 @@ public:
     // Row-parallel mode (set by the row-parallel node kernels): the lane's
     // position in the reference's serial walk, (query archetype << 24) | row.
     MW_INLINE void setRowParallel(uint32_t row_key) { rowKey_ = row_key; seq_ = 0; }
-    // The lane's wave index among the waves covering this world's rows and
-    // the world's finished-wave counter (StateView::makeTurn).
-    MW_INLINE void setMakeTurn(int32_t *turn, int32_t chunk) { turn_ = turn; turnChunk_ = chunk; }
+    // The lane's wave index among the waves covering this world's rows, the
+    // world's finished-wave marks (StateView::makeTurn) and the node's epoch.
+    MW_INLINE void setMakeTurn(int32_t *marks, int32_t chunk, int32_t epoch)
+    {
+        turn_ = marks;
+        turnChunk_ = chunk;
+        turnEpoch_ = epoch;
+    }
+    MW_INLINE bool madeEntities() const { return made_; }
     MW_INLINE bool rowParallel() const { return rowKey_ != kSerialRowKey; }
 
     template <typename ArchetypeT, typename... Args>
@@ -235,6 +241,8 @@ protected:
     uint32_t seq_ = 0;
     int32_t *turn_ = nullptr;
     int32_t turnChunk_ = 0;
+    int32_t turnEpoch_ = 0;
+    bool made_ = false;
     int32_t jobDepth_ = 0;      // nesting of the job being run (0: none)
     // Job API bookkeeping (only touched by job-API worlds).
     uint64_t jobKeys_[kMaxJobDepth];
@@ -260,12 +268,27 @@ public:
 // Row-parallel makeEntityNow: the world's ID store is serial
 // (id_map_impl.inl:69-182), so lanes take it one at a time, in row order:
 // the lanes of a wave in lane order, and a wave only once every lower wave
-// covering the world's rows has finished (StateView::makeTurn; the row
-// kernel counts finished waves per world).  The IDs are therefore the same
-// run to run, and the reference's when every row makes at most one entity
-// (its serial walk hands them out in row order).  Lower waves are dispatched
-// before higher ones and never wait on them, so the wait always ends.
-// Without a turn counter (other callers) waves go through a per-world lock.
+// covering the world's rows has finished (StateView::makeTurn: each wave
+// marks itself done with the node's epoch -- a count would also count higher
+// waves that finished first).  The IDs are therefore the same run to run,
+// and the reference's when every row makes at most one entity (its serial
+// walk hands them out in row order).  Lower waves are dispatched before
+// higher ones and never wait on them, so the wait always ends.  Without the
+// marks (other callers, worlds past kMakeTurnWaves waves) waves go through a
+// per-world lock.
+MW_INLINE bool lowerWavesDone(const int32_t *marks, int32_t chunk, int32_t epoch)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    for (int32_t i = 0; i < chunk; i++) {
+        if (__hip_atomic_load(marks + i, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) return false;
+    }
+    return true;
+#else
+    (void)marks; (void)chunk; (void)epoch;
+    return true;
+#endif
+}
+
 MW_INLINE Entity Context::lockedAcquire(int32_t arch, int32_t row)
 {
     IDMapView ids = state_->ids(world_);
@@ -277,8 +300,16 @@ MW_INLINE Entity Context::lockedAcquire(int32_t arch, int32_t row)
         const uint32_t leader = (uint32_t)__builtin_ctzll(pending);
         if (lane == leader) {
             if (turn_) {
-                while (__hip_atomic_load(turn_, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != turnChunk_)
+                // bounded: a wait that never ends is flagged and the ID taken
+                uint32_t spins = 0;
+                while (!lowerWavesDone(turn_, turnChunk_, turnEpoch_)) {
                     __builtin_amdgcn_s_sleep(2);
+                    if (++spins == (1u << 20)) {
+                        atomicOr(state_->errorFlags + world_, kErrFlagMakeOrder);
+                        break;
+                    }
+                }
+                made_ = true;
                 e = ids.acquire(ids.st->worldCache);
                 if (e.id >= 0) ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
             } else {

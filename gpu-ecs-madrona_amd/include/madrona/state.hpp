@@ -237,6 +237,7 @@ inline constexpr int32_t kErrFlagTmpAllocFull = 1 << 17;   // per-world tmpAlloc
 inline constexpr int32_t kErrFlagDeferredFull = 1 << 18;   // deferred destroy log full
 inline constexpr int32_t kErrFlagRowParallelOp = 1 << 19;  // op not available in a row-parallel node
 inline constexpr int32_t kErrFlagCommitLimit = 1 << 20;    // archetype too large for the ordered commit
+inline constexpr int32_t kErrFlagMakeOrder = 1 << 22;      // a row-parallel make gave up waiting for its turn
 
 // Ordered structural commit (see Context, row-parallel mode): an append key
 // orders a row made by a row-parallel lane exactly where the reference's
@@ -273,6 +274,7 @@ struct ArchetypeView {
 };
 
 inline constexpr int32_t kMakeTurnSlots = 8;     // = kMaxQueryArchetypes (context.hpp)
+inline constexpr int32_t kMakeTurnWaves = 64;    // waves per world with ordered makes
 
 struct StateView {
     int32_t numWorlds;
@@ -289,11 +291,14 @@ struct StateView {
     int32_t *deferCount;        // [numWorlds] deferred destroys of the running node
     DeferredDestroy *deferLog;  // [numWorlds][deferCap]
     int32_t deferCap;
-    // Waves of the running row-parallel node that have finished their rows,
-    // per (query archetype, world): a wave's makeEntityNow calls wait until
-    // every lower wave of the world is done, so IDs are taken in row order
-    // (Context::lockedAcquire); reset by the ordered commit.
-    int32_t *makeTurn;          // [kMakeTurnSlots][numWorlds]
+    // Waves of the running row-parallel node that have finished their rows:
+    // per (query archetype, world, wave covering the world) the node's epoch
+    // once the wave is done.  A wave's makeEntityNow calls wait until every
+    // lower wave of the world is done, so IDs are taken in row order
+    // (Context::lockedAcquire).  The ordered commit after each node advances
+    // the epoch, so nothing is ever reset.
+    int32_t *makeTurn;          // [kMakeTurnSlots][numWorlds][kMakeTurnWaves]
+    int32_t *makeEpoch;         // [1]
     // Per-world bump allocator (Context::tmpAlloc, reference
     // StateManager::tmpAlloc, src/core/state.cpp:584-602): 256-byte
     // granules, reset by ResetTmpAllocNode.

@@ -445,32 +445,49 @@ parallelForKernel(const StateView *__restrict__ st_in, int32_t arch, int32_t que
     // launch configuration caps the grid (LaunchCtx::capGrid)
     // finished waves per world (row-ordered makeEntityNow, Context::lockedAcquire)
     int32_t *turn = st->makeTurn && query_arch < kMakeTurnSlots
-                        ? st->makeTurn + (size_t)query_arch * st->numWorlds : nullptr;
+                        ? st->makeTurn + (size_t)query_arch * st->numWorlds * kMakeTurnWaves : nullptr;
+    const int32_t epoch = turn ? st->makeEpoch[0] : 0;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t inv = t / threads;
         const int32_t w = (int32_t)(inv / inv_per_world);
         const int32_t first = (int32_t)(inv - (int64_t)w * inv_per_world) * items;
         const int32_t n = st->arch[arch].numRows[w];
+        // this wave's index among the waves covering world w
+        const int64_t t_w0 = (int64_t)w * inv_per_world * threads;
+        const int64_t chunk = (t >> 6) - (t_w0 >> 6);
+        int32_t *marks = turn ? turn + (size_t)w * kMakeTurnWaves : nullptr;
+        bool made = false;
         if (first < n) {
             ContextT ctx = worldContext<ContextT>(st, w);
-            // this wave's index among the waves covering world w
-            const int64_t t_w0 = (int64_t)w * inv_per_world * threads;
-            if (turn) ctx.setMakeTurn(turn + w, (int32_t)((t >> 6) - (t_w0 >> 6)));
+            if (marks && chunk < kMakeTurnWaves) ctx.setMakeTurn(marks, (int32_t)chunk, epoch);
 #pragma unroll 1
             for (int32_t k = 0; k < items && first + k < n; k++) {
                 ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k));
                 invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, first + k,
                                                         std::index_sequence_for<ComponentTs...> {});
             }
+            made = ctx.madeEntities();
         }
+#if !defined(MW_NO_MAKE_TURN_SIGNAL)      // (A/B experiments only: breaks row-ordered makes)
         if (turn) {
-            // the wave is done with its rows of each world it covers: the
-            // active lanes are a prefix of the wave (t ascends with the lane)
+            // The wave is done with its rows of each world it covers (the
+            // active lanes are a prefix of the wave: t ascends with the
+            // lane).  Only a world's later waves wait on the count, so the
+            // world's last wave does not signal; release ordering (an L2
+            // write-back) only when the wave took IDs the next one must see.
             const int32_t pw = __shfl_up(w, 1, 64);
-            if (__lane_id() == 0 || pw != w)
-                __hip_atomic_fetch_add(turn + w, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            const int64_t t_w_last = t_w0 + (int64_t)inv_per_world * threads - 1;
+            const bool signal = (__lane_id() == 0 || pw != w) && (t >> 6) < (t_w_last >> 6) &&
+                                chunk < kMakeTurnWaves;
+            // a plain store of the epoch (no read-modify-write)
+            if (__ballot(made) != 0) {
+                if (signal) __hip_atomic_store(marks + chunk, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            } else if (signal) {
+                __hip_atomic_store(marks + chunk, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
+#endif
     }
 }
 #endif
