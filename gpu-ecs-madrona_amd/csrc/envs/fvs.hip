@@ -4,9 +4,9 @@
 // and row compaction.  Restated from the reference's job-API example
 // (examples/fantasy_vs/fvs.cpp:111-240, fvs.hpp) onto the TaskGraph API:
 //   actionSelect  ParallelForNode<Entity, Position, Action>   (fvs.cpp:111-151)
-//   caster        CustomParallelForNode<.., 16, 1, Entity, Action, Mana>
-//                 (fvs.cpp:153-190): the blast's scan of every Position /
-//                 Health row is split over the invocation's 16 lanes
+//   caster        ParallelForNode<Entity, Action, Mana>       (fvs.cpp:153-190;
+//                 a blast's scan of every Position / Health row is shared by
+//                 the lanes of the caster's wave)
 //   archer        ParallelForNode<Entity, Action, Quiver>     (fvs.cpp:192-214)
 //   cleanup       ParallelForNode<Entity, Health> marks the dead, a
 //                 PerWorldNode makes their trackers, a ParallelForNode over
@@ -65,11 +65,6 @@ struct Config {
 
 class Engine;
 
-// Lanes per casting dragon: a blast tests every Position / Health row of the
-// world (250 at the benchmark size) against its radius; one lane per dragon
-// made that a serial chain of ~250 dependent cache reads.
-constexpr int32_t kCastLanes = 16;
-
 struct Game : public WorldBase {
     static void registerTypes(ECSRegistry &reg, const Config &cfg)
     {
@@ -90,7 +85,7 @@ struct Game : public WorldBase {
         auto act = builder.addToGraph<
             ParallelForNode<Engine, actionSelectSystem, Entity, Position, Action>>({});
         auto cast = builder.addToGraph<
-            CustomParallelForNode<Engine, casterSystem, kCastLanes, 1, Entity, Action, Mana>>({ act });
+            ParallelForNode<Engine, casterSystem, Entity, Action, Mana>>({ act });
         auto shoot = builder.addToGraph<
             ParallelForNode<Engine, archerSystem, Entity, Action, Quiver>>({ act });
         auto mark = builder.addToGraph<
@@ -167,50 +162,60 @@ MW_HD void Game::actionSelectSystem(Engine &ctx, Entity &e, Position &pos, Actio
     }
 }
 
-MW_HD static inline int32_t castLane()
+// A blast tests every Position / Health row of the world (250 at the
+// benchmark size) against its radius.  A dragon casts about once per 1200
+// ticks, so one lane per dragon keeps the common path cheap, but a caster's
+// serial scan set the kernel's length (a chain of ~250 dependent cache
+// reads).  On the device the active lanes of the caster's wave share each
+// blast's scan; damage is an integer atomic subtraction, so every hp ends as
+// after the reference's serial scan.
+MW_HD static inline void blast(Engine &ctx, const Game &g, int32_t w, const Vector3 &target, int32_t first,
+                               int32_t stride)
 {
-#if defined(__HIP_DEVICE_COMPILE__) || !defined(__HIPCC__)
-    return mwGPU::invocationLane<kCastLanes>();
-#else
-    return 0;                              // hipcc's host pass: never run
-#endif
-}
-
-// The reference's serial body, cooperatively: every lane of the invocation
-// decides from the row's values (regenerated mana, remaining time), the last
-// lane writes them back (on the device the lanes read in lockstep before the
-// store; on the CPU back end the lanes run in order, so lanes 0..14 read
-// before lane 15 writes), and the lanes share the blast's row scan.  Blast
-// damage is an integer atomic subtraction, so the split leaves every hp as
-// the serial scan does.
-MW_HD void Game::casterSystem(Engine &ctx, Entity &e, Action &action, Mana &mana)
-{                                                          // fvs.cpp:153-190
-    const Game &g = ctx.data();
-    const int32_t lane = castLane();
-    const float mp = mana.mp + kManaRegenRate * kDeltaT;
-    const bool cast = !(action.remainingTime > 0) && !(mp < kCastCost);
-    if (lane == kCastLanes - 1) {
-        mana.mp = cast ? mp - kCastCost : mp;
-        if (cast) action.remainingTime = kCastTime;
-    }
-    if (!cast) return;
-    const Draw d { g.worldSeed, (uint32_t)e.id, g.tickCount };
-    const Vector3 target {
-        d.uniform(kDrawTargetX, g.worldBounds.pMin.x, g.worldBounds.pMax.x),
-        d.uniform(kDrawTargetY, g.worldBounds.pMin.y, g.worldBounds.pMax.y),
-        d.uniform(kDrawTargetZ, g.worldBounds.pMin.z, g.worldBounds.pMax.z),
-    };
     StateView &st = ctx.state();
-    const int32_t w = ctx.worldID().idx;
     for (int32_t a = 0; a < g.healthQuery.numArchetypes; a++) {
         const int32_t arch = g.healthQuery.archetypes[a];
         const Position *pos = st.column<Position>(arch, g.healthQuery.cols[a][0], w);
         Health *hp = st.column<Health>(arch, g.healthQuery.cols[a][1], w);
         const int32_t n = st.arch[arch].numRows[w];
-        for (int32_t r = lane; r < n; r += kCastLanes) {
+        for (int32_t r = first; r < n; r += stride) {
             if (target.distance(rowRef(pos, r)) <= kBlastRadius) damage(rowRef(hp, r), kBlastDamage);
         }
     }
+}
+
+MW_HD void Game::casterSystem(Engine &ctx, Entity &e, Action &action, Mana &mana)
+{                                                          // fvs.cpp:153-190
+    const Game &g = ctx.data();
+    mana.mp += kManaRegenRate * kDeltaT;
+    const bool cast = !(action.remainingTime > 0) && !(mana.mp < kCastCost);
+    Vector3 target {};
+    if (cast) {
+        mana.mp -= kCastCost;
+        const Draw d { g.worldSeed, (uint32_t)e.id, g.tickCount };
+        target = Vector3 {
+            d.uniform(kDrawTargetX, g.worldBounds.pMin.x, g.worldBounds.pMax.x),
+            d.uniform(kDrawTargetY, g.worldBounds.pMin.y, g.worldBounds.pMax.y),
+            d.uniform(kDrawTargetZ, g.worldBounds.pMin.z, g.worldBounds.pMax.z),
+        };
+        action.remainingTime = kCastTime;
+    }
+    const int32_t w = ctx.worldID().idx;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // every active lane of the wave helps with each of its casters' blasts
+    const uint64_t active = __ballot(1);
+    const int32_t rank = __popcll(active & ((1ull << __lane_id()) - 1));
+    const int32_t lanes = __popcll(active);
+    uint64_t casters = __ballot(cast);
+    while (casters) {
+        const int32_t src = __builtin_ctzll(casters);
+        casters &= casters - 1;
+        const Vector3 t { __shfl(target.x, src), __shfl(target.y, src), __shfl(target.z, src) };
+        blast(ctx, g, __shfl(w, src), t, rank, lanes);
+    }
+#elif !defined(__HIPCC__)
+    if (cast) blast(ctx, g, w, target, 0, 1);
+#endif
 }
 
 MW_HD void Game::archerSystem(Engine &ctx, Entity &e, Action &action, Quiver &quiver)
