@@ -45,10 +45,12 @@ void launchWorldKernel(const void *kernel, LaunchCtx &lc)
 // Row-parallel kernels: numWorlds x ceil(capacity / items) invocations of
 // `threads` lanes each, 256-lane blocks (grid-stride past capGrid).
 void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype, int32_t query_arch,
-                     int32_t threads, int32_t items, const void *cols, size_t)
+                     int32_t threads, int32_t items, const void *cols, size_t, bool world_waves)
 {
     const int32_t cap = lc.view->arch[archetype].capacity;
-    const int64_t lanes = (int64_t)lc.numWorlds * ((cap + items - 1) / items) * threads;
+    // world_waves: one wave per world (parallelForWorldKernel)
+    const int64_t lanes = world_waves ? (cap > 0 ? (int64_t)lc.numWorlds * 64 : 0)
+                                      : (int64_t)lc.numWorlds * ((cap + items - 1) / items) * threads;
     if (lanes == 0) return;
     dim3 block(256);
     const int64_t blocks = std::min<int64_t>((lanes + 255) / 256, 0x7fffffff);
@@ -624,6 +626,7 @@ static LaunchCtx makeLaunchCtx(Executor::Impl &I, Executor *exec)
     LaunchCtx lc { I.stream, I.mgr->deviceView(), &dv, I.cfg.numWorlds, exec };
     lc.nodeData = I.nodeDataDev;
     lc.serialNodes = I.cfg.serialNodes;
+    if (const char *e = getenv("MADRONA_MW_WORLD_WAVE_LANES")) lc.worldWaveLanes = atoi(e);
     return lc;
 }
 

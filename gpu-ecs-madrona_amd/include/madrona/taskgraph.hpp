@@ -64,6 +64,10 @@ struct LaunchCtx {
     // ParallelForNode / CustomParallelForNode walks each world's rows in
     // order on one invocation, as the reference's ParallelForNode::run does.
     int32_t serialNodes = 0;
+    // Row nodes whose tables need at most this many lanes per world run one
+    // wave per world (parallelForWorldKernel); env
+    // MADRONA_MW_WORLD_WAVE_LANES overrides the default (0: never).
+    int32_t worldWaveLanes = 256;
 
     // Grid for a grid-stride kernel that needs `blocks` blocks to cover its
     // work in one pass: capped at numCUs x blocksPerCU when configured.
@@ -348,7 +352,7 @@ struct ColArgs {
 // Launch helpers (csrc/runtime/executor.hip).
 void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype, int32_t query_arch,
                      int32_t threads_per_invocation, int32_t items_per_invocation,
-                     const void *cols, size_t cols_bytes);
+                     const void *cols, size_t cols_bytes, bool world_waves);
 void launchWorldKernel(const void *kernel, LaunchCtx &lc);
 void launchNodeFnKernel(const void *kernel, LaunchCtx &lc, void *node_dev, uint32_t fixed_count,
                         uint32_t threads_per_invocation);
@@ -490,6 +494,45 @@ parallelForKernel(const StateView *__restrict__ st_in, int32_t arch, int32_t que
 #endif
     }
 }
+
+// Small tables (at most LaunchCtx::worldWaveLanes lanes of invocations per
+// world, 256 by default): one
+// wave per world walks the world's invocations 64 lanes at a time, stopping
+// at the world's row count.  Rows of one world never span waves, so
+// row-parallel makeEntityNow needs no cross-wave ordering (the wave's lanes
+// take IDs in lane order, chunk after chunk), and a sparse table (fantasy_vs'
+// cleanup trackers: a few rows of 250) costs one wave per world instead of
+// one per 64 rows of capacity.
+template <typename ContextT, auto Fn, int32_t threads, int32_t items, typename... ComponentTs>
+__global__ void __launch_bounds__(256)
+parallelForWorldKernel(const StateView *__restrict__ st_in, int32_t arch, int32_t query_arch,
+                       ColArgs<sizeof...(ComponentTs)> cols)
+{
+    MW_TRACE_BLOCK(arch);
+    StateView *st = const_cast<StateView *>(st_in);
+    const int32_t cap = st->arch[arch].capacity;
+    const int32_t inv_per_world = (cap + items - 1) / items;
+    const int32_t lanes_per_world = inv_per_world * threads;
+    const int32_t lane = (int32_t)(threadIdx.x & 63);
+    const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wv < st->numWorlds; wv += waves) {
+        const int32_t w = (int32_t)wv;
+        const int32_t n = st->arch[arch].numRows[w];
+        for (int32_t base = 0; base < lanes_per_world && (base / threads) * items < n; base += 64) {
+            const int32_t l = base + lane;
+            const int32_t first = (l / threads) * items;
+            if (l < lanes_per_world && first < n) {
+                ContextT ctx = worldContext<ContextT>(st, w);
+#pragma unroll 1
+                for (int32_t k = 0; k < items && first + k < n; k++) {
+                    ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k));
+                    invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, first + k,
+                                                            std::index_sequence_for<ComponentTs...> {});
+                }
+            }
+        }
+    }
+}
 #endif
 
 }
@@ -575,11 +618,17 @@ public:
             for (int32_t c = 0; c < (int32_t)sizeof...(ComponentTs); c++) {
                 cols.c[c] = self->query_.cols[a][c];
             }
-            detail::launchRowKernel(
-                (const void *)&detail::parallelForKernel<ContextT, Fn, threads_per_invocation,
-                                                         items_per_invocation, ComponentTs...>,
-                lc, self->query_.archetypes[a], a, threads_per_invocation, items_per_invocation,
-                &cols, sizeof(cols));
+            const int32_t arch = self->query_.archetypes[a];
+            const int64_t lanes = (int64_t)(lc.view->arch[arch].capacity + items_per_invocation - 1) /
+                                  items_per_invocation * threads_per_invocation;
+            const bool world_waves = lanes <= lc.worldWaveLanes;
+            const void *kernel =
+                world_waves ? (const void *)&detail::parallelForWorldKernel<
+                                  ContextT, Fn, threads_per_invocation, items_per_invocation, ComponentTs...>
+                            : (const void *)&detail::parallelForKernel<
+                                  ContextT, Fn, threads_per_invocation, items_per_invocation, ComponentTs...>;
+            detail::launchRowKernel(kernel, lc, arch, a, threads_per_invocation, items_per_invocation,
+                                    &cols, sizeof(cols), world_waves);
         }
         detail::launchStructuralCommit(lc);
 #else

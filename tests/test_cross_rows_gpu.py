@@ -102,12 +102,18 @@ def test_ecs_ops_serial_nodes_entity_ids_exact_and_repeatable():
             assert a.spawns(w).tobytes() == b.spawns(w).tobytes()
 
 
-def test_ecs_ops_row_parallel_entity_ids_repeatable():
-    """Row-parallel makeEntityNow takes IDs in row order (a wave's lanes in
-    order, a world's waves one after another: StateView::makeTurn), so two
-    runs of the same worlds are byte-identical, ID columns included.  40
-    agent rows per world put most worlds across two waves, so the waves of a
-    world race for the ID store unless they are ordered."""
+@pytest.mark.parametrize("world_wave_lanes", [None, "0"])
+def test_ecs_ops_row_parallel_entity_ids_repeatable(monkeypatch, world_wave_lanes):
+    """Row-parallel makeEntityNow takes IDs in row order, so two runs of the
+    same worlds are byte-identical, ID columns included.  By default the 40
+    agent rows of a world are walked by one wave (parallelForWorldKernel:
+    lane order, chunk after chunk); MADRONA_MW_WORLD_WAVE_LANES=0 maps rows
+    to lanes across the grid, which puts most worlds across two waves, and
+    the waves of a world then take IDs one after another (their finished-wave
+    marks, StateView::makeTurn) -- without that ordering they race for the
+    ID store."""
+    if world_wave_lanes is not None:
+        monkeypatch.setenv("MADRONA_MW_WORLD_WAVE_LANES", world_wave_lanes)
     W, steps = 2048, 30
     a = el.EcsOpsSim(W)
     b = el.EcsOpsSim(W)
