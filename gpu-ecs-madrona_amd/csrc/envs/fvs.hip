@@ -178,8 +178,20 @@ MW_HD static inline void blast(Engine &ctx, const Game &g, int32_t w, const Vect
         const Position *pos = st.column<Position>(arch, g.healthQuery.cols[a][0], w);
         Health *hp = st.column<Health>(arch, g.healthQuery.cols[a][1], w);
         const int32_t n = st.arch[arch].numRows[w];
-        for (int32_t r = first; r < n; r += stride) {
-            if (target.distance(rowRef(pos, r)) <= kBlastRadius) damage(rowRef(hp, r), kBlastDamage);
+        // four rows' positions loaded before any damage is applied (the
+        // atomics would otherwise order each row's load after the last one)
+        for (int32_t r0 = first; r0 < n; r0 += 4 * stride) {
+            Vector3 p[4];
+#pragma unroll
+            for (int32_t k = 0; k < 4; k++) {
+                const int32_t r = r0 + k * stride;
+                if (r < n) p[k] = rowRef(pos, r);
+            }
+#pragma unroll
+            for (int32_t k = 0; k < 4; k++) {
+                const int32_t r = r0 + k * stride;
+                if (r < n && target.distance(p[k]) <= kBlastRadius) damage(rowRef(hp, r), kBlastDamage);
+            }
         }
     }
 }

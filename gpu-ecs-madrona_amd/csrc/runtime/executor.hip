@@ -137,7 +137,7 @@ constexpr int32_t kCommitStageWords = 1024;
 
 static size_t commitSharedBytes(const CommitArgs &A)
 {
-    return (size_t)A.capMax * 8 + (size_t)(A.sortA + A.sortO) * 8 + (size_t)kCommitStageWords * 4;
+    return (size_t)A.capMax * 8 + (size_t)(A.sortA + 2 * A.sortO) * 8 + (size_t)kCommitStageWords * 4;
 }
 
 static constexpr uint64_t kAppliedOp = 0xFFFF'FFFE'FFFF'FFFFull;
@@ -184,6 +184,7 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
     uint64_t *akeys = (uint64_t *)(where + A.capMax);
     uint64_t *okeys = akeys + A.sortA;
     uint32_t *stage = (uint32_t *)(okeys + A.sortO);     // [kCommitStageWords]
+    uint64_t *dloc = (uint64_t *)(stage + kCommitStageWords);   // [sortO] resolved destroy targets
     __shared__ int32_t n_moved;
     __shared__ int32_t col_words[kMaxColumns + 1];     // prefix of dwords per row by column
     __shared__ unsigned long long arch_mask;
@@ -200,9 +201,15 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
     // resident grid) and walks only those with work.  (A block per 256-world
     // chunk walked its chunk's worlds one after another: 64 busy blocks for
     // 16384 worlds, 0.2 ms per fantasy_vs destroy commit.)
-    for (int32_t w = blockIdx.x; w < st.numWorlds; w += gridDim.x) {
+    // The block's lanes check 64 of its worlds at once (one round of loads),
+    // then the block walks the ones with work.
+    static_assert(kCommitThreads == 64, "one wave per block: the ballot covers the block");
+    for (int64_t base = blockIdx.x; base < st.numWorlds; base += (int64_t)gridDim.x * 64) {
+    const int64_t mine = base + (int64_t)tid * gridDim.x;
+    const bool has_work = mine < st.numWorlds && (st.appendDirty[mine] != 0 || st.deferCount[mine] != 0);
+    for (uint64_t todo = __ballot(has_work); todo != 0; todo &= todo - 1) {
+        const int32_t w = (int32_t)(base + (int64_t)__builtin_ctzll(todo) * gridDim.x);
         const uint64_t dirty = st.appendDirty[w];
-        if (dirty == 0 && st.deferCount[w] == 0) continue;
         int32_t nops = st.deferCount[w];
         nops = min(nops, st.deferCap);
         DeferredDestroy *log = st.deferLog + (size_t)w * st.deferCap;
@@ -218,7 +225,7 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
         bitonicSortLDS(okeys, so);
         for (int32_t i = tid; i < nops; i += blockDim.x) {
             const Loc l = ids.lookup(log[i].e);
-            log[i].key = l.valid() ? (((uint64_t)l.archetype << 32) | (uint32_t)l.row) : ~0ull;
+            dloc[i] = l.valid() ? (((uint64_t)l.archetype << 32) | (uint32_t)l.row) : ~0ull;
             if (l.valid()) atomicOr(&arch_mask, 1ull << l.archetype);
         }
         __syncthreads();
@@ -257,8 +264,8 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
                 int32_t n = n0, ia = 0, io = 0;
                 for (;;) {
                     while (io < so && okeys[io] != ~0ull &&
-                           (log[okeys[io] & 0xFFFF].key == ~0ull ||
-                            (int32_t)(log[okeys[io] & 0xFFFF].key >> 32) != a)) {
+                           (dloc[okeys[io] & 0xFFFF] == ~0ull ||
+                            (int32_t)(dloc[okeys[io] & 0xFFFF] >> 32) != a)) {
                         io++;
                     }
                     const uint64_t ka = ia < m ? akeys[ia] : ~0ull;
@@ -273,7 +280,7 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
                         n++;
                     } else {
                         const int32_t i = (int32_t)(ko & 0xFFFF);
-                        const int32_t r = (int32_t)(uint32_t)log[i].key;
+                        const int32_t r = (int32_t)(uint32_t)dloc[i];
                         io++;
                         if (r < 0 || r >= n_end || where[r] < 0) continue;
                         const int32_t p = where[r];
@@ -282,7 +289,7 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
                         where[q] = p;
                         where[r] = -1;
                         n--;
-                        log[i].key = kAppliedOp;
+                        dloc[i] = kAppliedOp;
                     }
                 }
                 n_final = n;
@@ -390,12 +397,13 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
         if (tid == 0) {
             for (int32_t s = 0; s < nops; s++) {
                 const int32_t i = (int32_t)(okeys[s] & 0xFFFF);
-                if (log[i].key == kAppliedOp) ids.release(ids.st->worldCache, log[i].e.id);
+                if (dloc[i] == kAppliedOp) ids.release(ids.st->worldCache, log[i].e.id);
             }
             st.appendDirty[w] = 0;
             st.deferCount[w] = 0;
         }
         __syncthreads();
+    }
     }
 }
 
