@@ -44,9 +44,15 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E 8.0 TB/s spec
 # BVH node is not counted (lower bound).
 BYTES = {
     "UpdateLeafPositionsNode": {"body": 96 + 68},
-    "RefitNode": {"body": 32 + 2 * 24},
+    # whole BVH nodes read and written back (0.69 nodes of 116 B per body: the
+    # oracle's trees hold 81-97 nodes per 129-body world in the timed window)
+    # + the leaf AABB, parent and LeafID per body; PMC (calibrated): 1.0x
+    "RefitNode": {"body": 32 + 160},
     "UpdateBVHNode": {"body": 0},
-    "FindOverlappingNode": {"body": 8 + 4 + 4 + 12, "cand": 16},
+    # per body: its leaf's node slot (the node's lines, 80 B per body), leaf
+    # parent / order / entity, the entity's IDNode, ResponseType, LeafID and
+    # leaf AABB; per candidate: the pair (16 B) and its packed slots (8 B)
+    "FindOverlappingNode": {"body": 80 + 4 + 4 + 8 + 12 + 4 + 4 + 24, "cand": 16 + 8},
     "SubstepRigidBodiesNode": {"body": 84 + 108},
     "NarrowphaseNode": {"cand": 16 + 2 * 44, "contact": 112},
     "SolverNode": {"body": 56 + 24, "contact": (112 + 2 * 92 + 2 * 28 + 16) + (112 + 2 * 100 + 2 * 24)},
