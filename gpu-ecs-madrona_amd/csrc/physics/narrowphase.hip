@@ -865,7 +865,8 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
     }
     __shared__ int32_t s_pre[kNarrowBins + 1];
     loadBinPrefix(P, 0, s_pre);
-    const int32_t total = s_pre[kNarrowBins];
+    // the SAT verdicts (hhJobs) are indexed by list position: never past them
+    const int32_t total = min(s_pre[kNarrowBins], P.numWorlds * P.candCapacity);
     const int32_t stride = gridDim.x * kGroupsPerBlock;
     for (int32_t idx = blockIdx.x * kGroupsPerBlock + group; idx < total; idx += stride) {
         const SatWork wk = P.satWork[binEntry(P, s_pre, idx, 0)];
@@ -946,12 +947,17 @@ __device__ __forceinline__ void narrowContactBlock(const PhysArgs &P)
 
     __shared__ int32_t s_pre[kNarrowBins + 1];
     loadBinPrefix(P, 0, s_pre);
-    const int32_t total = s_pre[kNarrowBins];
+    const int32_t total = min(s_pre[kNarrowBins], P.numWorlds * P.candCapacity);
     for (int32_t i = blockIdx.x * kContactBlock + threadIdx.x; i < total;
          i += gridDim.x * kContactBlock) {
         const ContactJob job = P.hhJobs[i];
         if (job.kind == kJobNone) continue;
         const SatWork &wk = job.pair;
+        if ((uint32_t)wk.world >= (uint32_t)P.numWorlds || (uint32_t)wk.slot >= (uint32_t)P.candCapacity ||
+            (uint32_t)wk.aObj >= (uint32_t)P.objs.numObjects || (uint32_t)wk.bObj >= (uint32_t)P.objs.numObjects) {
+            atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
+            continue;
+        }
         const int32_t w = wk.world;
         int32_t *flags = P.errorFlags + w;
         Contact &out = P.candContacts[(size_t)w * P.candCapacity + wk.slot];
