@@ -41,6 +41,17 @@ def world_bytes(node, nd, nk):
     return (nd + nk) * (8 + 64)                     # cleanup scan: Entity + Health
 
 
+def pmc_traffic(node):
+    """HBM bytes per launch of the node kind from the committed rocprofv3 PMC
+    passes (profiles/r03_fvs_traffic.json, tools/gpu_fvs_pmc.sh); None if
+    absent."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r03_fvs_traffic.json")) as f:
+            return json.load(f)["nodes"][node]["bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--worlds", type=int, default=16384)
@@ -172,7 +183,7 @@ def main():
                    "timed_ticks": f"{args.preroll + 1}-{args.preroll + args.steps}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": None, "ms_per_launch": round(launch_ms, 4),
+                     "traffic": pmc_traffic(dom), "ms_per_launch": round(launch_ms, 4),
                      "timing": "HIP events around every launch of the node kind over 100 "
                                "ticks right after the timed region (executor stream)",
                      "bytes_per_launch": int(nbytes)},
