@@ -838,9 +838,6 @@ __device__ __forceinline__ void sortWorldsForSolver(const PhysArgs &P, int32_t *
 // and leaves its verdict in the job at the same index (kind kJobNone when
 // separated).  The grid is what is resident at once; every group reaches
 // the end of the list and exits.
-#ifndef MW_SAT_PREFETCH
-#define MW_SAT_PREFETCH 1
-#endif
 #ifndef MW_SAT_MIN_BLOCKS
 #define MW_SAT_MIN_BLOCKS 4
 #endif
@@ -871,31 +868,8 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
     // the SAT verdicts (hhJobs) are indexed by list position: never past them
     const int32_t total = min(s_pre[kNarrowBins], P.numWorlds * P.candCapacity);
     const int32_t stride = gridDim.x * kGroupsPerBlock;
-#if MW_SAT_PREFETCH
-    // The next pair's 48-byte work entry is loaded while this pair is
-    // tested, 8 bytes on each of the group's first six lanes (2 registers a
-    // lane), and parked in LDS after the test: the group then starts its
-    // next pair without a global round trip.
-    static_assert(sizeof(SatWork) == 48 && kGroup >= 6, "six 8-byte pieces per entry");
-    __shared__ uint2 s_next[kGroupsPerBlock][6];
-    int32_t idx = blockIdx.x * kGroupsPerBlock + group;
-    if (idx < total && lane < 6)
-        s_next[group][lane] = ((const uint2 *)&P.satWork[binEntry(P, s_pre, idx, 0)])[lane];
-    groupSync();
-    for (; idx < total; idx += stride) {
-        SatWork wk;
-        {
-            uint2 *dst = (uint2 *)&wk;
-#pragma unroll
-            for (int32_t k = 0; k < 6; k++) dst[k] = s_next[group][k];
-        }
-        uint2 nx { 0u, 0u };
-        if (idx + stride < total && lane < 6)
-            nx = ((const uint2 *)&P.satWork[binEntry(P, s_pre, idx + stride, 0)])[lane];
-#else
     for (int32_t idx = blockIdx.x * kGroupsPerBlock + group; idx < total; idx += stride) {
         const SatWork wk = P.satWork[binEntry(P, s_pre, idx, 0)];
-#endif
         const bool ok = (uint32_t)wk.world < (uint32_t)P.numWorlds &&
                         (uint32_t)wk.slot < (uint32_t)P.candCapacity &&
                         (uint32_t)wk.aObj < (uint32_t)P.objs.numObjects &&
@@ -913,10 +887,6 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
         }
         if (lane == 0) P.hhJobs[idx] = job;
         groupSync();
-#if MW_SAT_PREFETCH
-        if (lane < 6) s_next[group][lane] = nx;
-        groupSync();
-#endif
     }
 }
 
