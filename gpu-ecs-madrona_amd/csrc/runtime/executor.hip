@@ -4,6 +4,7 @@
 // src/mw/cuda_exec.cpp:1519-1815 (run graph, getExported, export kernels).
 #include <madrona/mw_gpu.hpp>
 #include <madrona/tracing.hpp>
+#include <madrona/commit.hpp>
 #include <madrona/launch_config.hpp>
 
 #include <hip/hip_runtime.h>
@@ -105,68 +106,22 @@ void launchNodeFnKernel(const void *kernel, LaunchCtx &lc, void *node_dev, uint3
 }
 
 // ---------------------------------------------------------------------------
-// Ordered structural commit of a row-parallel node (Context, row-parallel
-// mode).  One block per world with work (others exit on two loads):
-//   1. the world's deferred destroys are sorted by append key (LDS bitonic
-//      sort) and their targets looked up (before anything moves);
-//   2. per touched archetype: the rows appended past the (unchanged) row
-//      count are sorted by key; one lane replays appends and
-//      swap-removes in key order on row INDICES only (slot[final position]
-//      = source row, where[source row] = position: O(1) per event in LDS),
-//      which is the reference's serial order (state.inl:398-472,
-//      src/core/state.cpp:181-202); then all lanes move the rows that
-//      changed position, column by column through a per-block scratch
-//      (wave-parallel compaction: coalesced copies), remap moved entities
-//      and clear the keys;
-//   3. one lane releases the destroyed IDs in key order (IDMap::releaseID).
+// Ordered structural commit of a row-parallel node (madrona/commit.hpp) as
+// its own kernel: one-wave blocks strided over the worlds, each world's
+// working set in LDS.  Nodes whose every query table is walked one wave per
+// world commit inside their row kernel instead (taskgraph.hpp).
 // ---------------------------------------------------------------------------
 struct CommitArgs {
     StateView *st;
     char *scratch;                 // [gridDim.x][scratchPerBlock]
     uint64_t scratchPerBlock;
-    int32_t capMax;                // rows per world the LDS index arrays hold
-    int32_t sortA;                 // pow2 >= capMax
-    int32_t sortO;                 // pow2 >= deferCap
+    detail::CommitShape shape;
     int32_t grid;                  // blocks (all resident): worlds are strided over them
 };
 
-// LDS of one commit block: slot / where per row, the append keys and the
-// destroy keys (each padded to a power of two for the bitonic sort), and a
-// staging buffer for the moved rows' words.
-constexpr int32_t kCommitStageWords = 1024;
-
 static size_t commitSharedBytes(const CommitArgs &A)
 {
-    return (size_t)A.capMax * 8 + (size_t)(A.sortA + 2 * A.sortO) * 8 + (size_t)kCommitStageWords * 4;
-}
-
-static constexpr uint64_t kAppliedOp = 0xFFFF'FFFE'FFFF'FFFFull;
-
-__device__ static inline void bitonicSortLDS(uint64_t *keys, int32_t n)
-{
-    for (int32_t k = 2; k <= n; k <<= 1) {
-        for (int32_t j = k >> 1; j > 0; j >>= 1) {
-            for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
-                const int32_t ixj = i ^ j;
-                if (ixj > i) {
-                    const uint64_t a = keys[i], b = keys[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) {
-                        keys[i] = b;
-                        keys[ixj] = a;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
-__device__ static inline int32_t pow2Ceil(int32_t n)
-{
-    int32_t p = 1;
-    while (p < n) p <<= 1;
-    return p;
+    return detail::commitWorkingBytes(A.shape);
 }
 
 // One wave per block: a world's commit is a chain of small steps (sorts of a
@@ -179,17 +134,6 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
 {
     MW_TRACE_BLOCK(0);
     extern __shared__ __align__(16) char commit_lds[];
-    int32_t *slot = (int32_t *)commit_lds;
-    int32_t *where = slot + A.capMax;
-    uint64_t *akeys = (uint64_t *)(where + A.capMax);
-    uint64_t *okeys = akeys + A.sortA;
-    uint32_t *stage = (uint32_t *)(okeys + A.sortO);     // [kCommitStageWords]
-    uint64_t *dloc = (uint64_t *)(stage + kCommitStageWords);   // [sortO] resolved destroy targets
-    __shared__ int32_t n_moved;
-    __shared__ int32_t col_words[kMaxColumns + 1];     // prefix of dwords per row by column
-    __shared__ unsigned long long arch_mask;
-    __shared__ int32_t n_final;
-
     StateView &st = *A.st;
     char *scratch = A.scratch + (size_t)blockIdx.x * A.scratchPerBlock;
     const int32_t tid = threadIdx.x;
@@ -197,213 +141,19 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
     // the next node's waves mark themselves done with a new epoch
     // (row-ordered makeEntityNow); the next kernel sees the store
     if (st.makeEpoch && blockIdx.x == 0 && tid == 0) st.makeEpoch[0] = st.makeEpoch[0] + 1;
-    // Most nodes mutate nothing: a block checks its worlds (strided over the
-    // resident grid) and walks only those with work.  (A block per 256-world
-    // chunk walked its chunk's worlds one after another: 64 busy blocks for
-    // 16384 worlds, 0.2 ms per fantasy_vs destroy commit.)
-    // The block's lanes check 64 of its worlds at once (one round of loads),
-    // then the block walks the ones with work.
+    // Most nodes mutate nothing: a block's lanes check 64 of its worlds
+    // (strided over the resident grid) in one round of loads, then the block
+    // walks the ones with work.  (A block per 256-world chunk walked its
+    // chunk's worlds one after another: 64 busy blocks for 16384 worlds,
+    // 0.2 ms per fantasy_vs destroy commit.)
     static_assert(kCommitThreads == 64, "one wave per block: the ballot covers the block");
     for (int64_t base = blockIdx.x; base < st.numWorlds; base += (int64_t)gridDim.x * 64) {
-    const int64_t mine = base + (int64_t)tid * gridDim.x;
-    const bool has_work = mine < st.numWorlds && (st.appendDirty[mine] != 0 || st.deferCount[mine] != 0);
-    for (uint64_t todo = __ballot(has_work); todo != 0; todo &= todo - 1) {
-        const int32_t w = (int32_t)(base + (int64_t)__builtin_ctzll(todo) * gridDim.x);
-        const uint64_t dirty = st.appendDirty[w];
-        int32_t nops = st.deferCount[w];
-        nops = min(nops, st.deferCap);
-        DeferredDestroy *log = st.deferLog + (size_t)w * st.deferCap;
-        IDMapView ids = st.ids(w);
-
-        // 1. deferred destroys: sort by key, resolve targets
-        const int32_t so = pow2Ceil(max(nops, 1));
-        for (int32_t i = tid; i < so; i += blockDim.x) {
-            okeys[i] = i < nops ? ((log[i].key & ~0xFFFFull) | (uint64_t)i) : ~0ull;
+        const int64_t mine = base + (int64_t)tid * gridDim.x;
+        const bool has_work = mine < st.numWorlds && (st.appendDirty[mine] != 0 || st.deferCount[mine] != 0);
+        for (uint64_t todo = __ballot(has_work); todo != 0; todo &= todo - 1) {
+            const int32_t w = (int32_t)(base + (int64_t)__builtin_ctzll(todo) * gridDim.x);
+            detail::commitWorld(st, A.shape, commit_lds, scratch, w);
         }
-        if (tid == 0) arch_mask = dirty;
-        __syncthreads();
-        bitonicSortLDS(okeys, so);
-        for (int32_t i = tid; i < nops; i += blockDim.x) {
-            const Loc l = ids.lookup(log[i].e);
-            dloc[i] = l.valid() ? (((uint64_t)l.archetype << 32) | (uint32_t)l.row) : ~0ull;
-            if (l.valid()) atomicOr(&arch_mask, 1ull << l.archetype);
-        }
-        __syncthreads();
-        const uint64_t mask = arch_mask;
-
-        // 2. per archetype, in index order
-        for (int32_t a = 0; a < st.numArchetypes; a++) {
-            if (!(mask & (1ull << a))) continue;
-            ArchetypeView &av = st.arch[a];
-            const int32_t cap = av.capacity;
-            if (cap > A.capMax) {
-                if (tid == 0) atomicOr(st.errorFlags + w, kErrFlagCommitLimit);
-                __syncthreads();
-                continue;
-            }
-            uint64_t *keys = av.appendKeys ? av.appendKeys + (size_t)w * cap : nullptr;
-            // rows appended by the node: [numRows, numRows + pending), the
-            // ones past the capacity were refused (kErrTableFull)
-            const int32_t n0 = min(av.numRows[w], cap);
-            const int32_t m = keys ? min(av.pendingRows[w], cap - n0) : 0;
-            const int32_t n_end = n0 + m;
-            const int32_t sa = pow2Ceil(max(m, 1));
-            for (int32_t j = tid; j < sa; j += blockDim.x) {
-                akeys[j] = j < m ? ((keys[n0 + j] & ~0xFFFFull) | (uint64_t)j) : ~0ull;
-            }
-            for (int32_t p = tid; p < n_end; p += blockDim.x) {
-                slot[p] = p < n0 ? p : -1;
-                where[p] = p < n0 ? p : -1;
-            }
-            __syncthreads();
-            bitonicSortLDS(akeys, sa);
-
-            const bool temporary = (av.flags & kArchTemporary) != 0;
-            const Entity *ecol = (const Entity *)(av.cols[0] + (size_t)w * cap * sizeof(Entity));
-            if (tid == 0) {
-                int32_t n = n0, ia = 0, io = 0;
-                for (;;) {
-                    while (io < so && okeys[io] != ~0ull &&
-                           (dloc[okeys[io] & 0xFFFF] == ~0ull ||
-                            (int32_t)(dloc[okeys[io] & 0xFFFF] >> 32) != a)) {
-                        io++;
-                    }
-                    const uint64_t ka = ia < m ? akeys[ia] : ~0ull;
-                    const uint64_t ko = io < so ? okeys[io] : ~0ull;
-                    if (ka == ~0ull && ko == ~0ull) break;
-                    if (ka < ko) {
-                        const int32_t r = n0 + (int32_t)(ka & 0xFFFF);
-                        ia++;
-                        if (!temporary && ecol[r].id < 0) continue;   // ID store was full
-                        slot[n] = r;
-                        where[r] = n;
-                        n++;
-                    } else {
-                        const int32_t i = (int32_t)(ko & 0xFFFF);
-                        const int32_t r = (int32_t)(uint32_t)dloc[i];
-                        io++;
-                        if (r < 0 || r >= n_end || where[r] < 0) continue;
-                        const int32_t p = where[r];
-                        const int32_t q = slot[n - 1];
-                        slot[p] = q;
-                        where[q] = p;
-                        where[r] = -1;
-                        n--;
-                        dloc[i] = kAppliedOp;
-                    }
-                }
-                n_final = n;
-            }
-            __syncthreads();
-            const int32_t nf = n_final;
-
-            // Rows that changed position.  Few rows move per commit (a
-            // destroy moves the last row into the hole), so their words
-            // go through LDS in one gather and one scatter for all columns
-            // (two barriers); a move too large for the stage goes column by
-            // column through the block's global scratch.
-            int32_t *moved = (int32_t *)akeys;           // the append keys are replayed
-            if (tid == 0) {
-                n_moved = 0;
-                int32_t words = 0;
-                bool dwords = true;
-                for (int32_t c = 0; c < av.numColumns; c++) {
-                    col_words[c] = words;
-                    words += (int32_t)(av.colBytes[c] / 4);
-                    dwords = dwords && av.colBytes[c] % 4 == 0;
-                }
-                col_words[av.numColumns] = dwords ? words : -1;
-            }
-            __syncthreads();
-            for (int32_t p = tid; p < nf; p += blockDim.x) {
-                if (slot[p] != p) moved[atomicAdd(&n_moved, 1)] = p;
-            }
-            __syncthreads();
-            const int32_t nm = n_moved;
-            const int32_t row_words = col_words[av.numColumns];
-            const bool staged = row_words > 0 && (int64_t)nm * row_words <= kCommitStageWords;
-            if (staged) {
-                const int32_t total = nm * row_words;
-                for (int32_t t = tid; t < total; t += blockDim.x) {
-                    const int32_t m = t / row_words, k = t - m * row_words;
-                    int32_t c = 0;
-                    while (col_words[c + 1] <= k) c++;
-                    const uint32_t nw = av.colBytes[c] / 4;
-                    const uint32_t *base = (const uint32_t *)(av.cols[c] + (size_t)w * cap * av.colBytes[c]);
-                    stage[t] = base[(size_t)slot[moved[m]] * nw + (k - col_words[c])];
-                }
-                __syncthreads();
-                for (int32_t t = tid; t < total; t += blockDim.x) {
-                    const int32_t m = t / row_words, k = t - m * row_words;
-                    int32_t c = 0;
-                    while (col_words[c + 1] <= k) c++;
-                    const uint32_t nw = av.colBytes[c] / 4;
-                    uint32_t *base = (uint32_t *)(av.cols[c] + (size_t)w * cap * av.colBytes[c]);
-                    base[(size_t)moved[m] * nw + (k - col_words[c])] = stage[t];
-                }
-                __syncthreads();
-            }
-            for (int32_t c = 0; c < av.numColumns && !staged; c++) {
-                const uint32_t nb = av.colBytes[c];
-                char *base = av.cols[c] + (size_t)w * cap * nb;
-                if (nb % 4 == 0) {
-                    const uint32_t words = nb / 4;
-                    const int64_t total = (int64_t)nf * words;
-                    for (int64_t t = tid; t < total; t += blockDim.x) {
-                        const int32_t p = (int32_t)(t / words), k = (int32_t)(t - (int64_t)p * words);
-                        const int32_t src = slot[p];
-                        if (src != p) ((uint32_t *)scratch)[t] = ((const uint32_t *)(base + (size_t)src * nb))[k];
-                    }
-                    __syncthreads();
-                    for (int64_t t = tid; t < total; t += blockDim.x) {
-                        const int32_t p = (int32_t)(t / words), k = (int32_t)(t - (int64_t)p * words);
-                        if (slot[p] != p) ((uint32_t *)(base + (size_t)p * nb))[k] = ((const uint32_t *)scratch)[t];
-                    }
-                } else {
-                    const int64_t total = (int64_t)nf * nb;
-                    for (int64_t t = tid; t < total; t += blockDim.x) {
-                        const int32_t p = (int32_t)(t / nb), k = (int32_t)(t - (int64_t)p * nb);
-                        const int32_t src = slot[p];
-                        if (src != p) scratch[t] = base[(size_t)src * nb + k];
-                    }
-                    __syncthreads();
-                    for (int64_t t = tid; t < total; t += blockDim.x) {
-                        const int32_t p = (int32_t)(t / nb), k = (int32_t)(t - (int64_t)p * nb);
-                        if (slot[p] != p) base[(size_t)p * nb + k] = scratch[t];
-                    }
-                }
-                __syncthreads();
-            }
-            // remap moved / appended entities, settle the keys and the count
-            if (!temporary) {
-                for (int32_t p = tid; p < nf; p += blockDim.x) {
-                    if (slot[p] != p || p >= n0) {
-                        const Entity e = ecol[p];
-                        ids.nodes[e.id].val = Loc { (uint32_t)a, p };
-                    }
-                }
-            }
-            if (keys) {
-                for (int32_t r = n0 + tid; r < n_end; r += blockDim.x) keys[r] = kNoAppendKey;
-            }
-            if (tid == 0) {
-                av.numRows[w] = nf;
-                if (av.pendingRows) av.pendingRows[w] = 0;
-            }
-            __syncthreads();
-        }
-
-        // 3. ID releases of the applied destroys, in key order
-        if (tid == 0) {
-            for (int32_t s = 0; s < nops; s++) {
-                const int32_t i = (int32_t)(okeys[s] & 0xFFFF);
-                if (dloc[i] == kAppliedOp) ids.release(ids.st->worldCache, log[i].e.id);
-            }
-            st.appendDirty[w] = 0;
-            st.deferCount[w] = 0;
-        }
-        __syncthreads();
-    }
     }
 }
 
@@ -412,7 +162,7 @@ namespace detail {
 void launchStructuralCommit(LaunchCtx &lc)
 {
     const CommitArgs *A = lc.exec ? (const CommitArgs *)lc.exec->commitArgs() : nullptr;
-    if (!A || A->capMax <= 0) return;
+    if (!A || A->shape.capMax <= 0) return;
     const size_t lds = commitSharedBytes(*A);
     MW_LAUNCH(structuralCommitKernel, dim3((uint32_t)A->grid), dim3(kCommitThreads), lds,
                        (hipStream_t)lc.stream, *A);
@@ -710,31 +460,17 @@ void Executor::uploadState()
 {
     impl_->mgr->uploadToDevice(impl_->stream);
 
-    // Ordered-commit sizing: the LDS index arrays hold the largest table
-    // that takes entity rows or row-parallel appends (at most 4096 rows per
-    // world; larger tables raise kErrFlagCommitLimit if a row-parallel node
-    // mutates them); one scratch slab per commit block holds a column of it.
+    // Ordered-commit sizing (StateManager: the largest table that takes
+    // entity rows or row-parallel appends); one scratch slab per commit block
+    // holds a column of it.
     {
         const StateView &dv = impl_->mgr->deviceViewHost();
-        int32_t cap_max = 0;
-        uint32_t col_max = 4;
-        for (int32_t a = 0; a < dv.numArchetypes; a++) {
-            const ArchetypeView &av = dv.arch[a];
-            if (av.flags & kArchModuleRows) continue;
-            if (av.capacity > kCommitMaxRows) continue;
-            cap_max = std::max(cap_max, av.capacity);
-            for (int32_t c = 0; c < av.numColumns; c++) col_max = std::max(col_max, av.colBytes[c]);
-        }
         CommitArgs &A = impl_->commit;
         A.st = impl_->mgr->deviceView();
-        A.capMax = (cap_max + 63) / 64 * 64;
-        A.sortA = 1;
-        while (A.sortA < A.capMax) A.sortA <<= 1;
-        A.sortO = 1;
-        while (A.sortO < dv.deferCap) A.sortO <<= 1;
-        A.scratchPerBlock = ((uint64_t)A.capMax * col_max + 255) / 256 * 256;
+        A.shape = detail::CommitShape { dv.commitCapMax, dv.commitSortA, dv.commitSortO };
+        A.scratchPerBlock = ((uint64_t)dv.commitCapMax * dv.commitColMax + 255) / 256 * 256;
         A.grid = 1;
-        if (A.capMax > 0) {
+        if (A.shape.capMax > 0) {
             // refuse a configuration whose commit cannot launch (it would
             // silently drop every structural op of a row-parallel node)
             const size_t lds = commitSharedBytes(A);
@@ -743,7 +479,7 @@ void Executor::uploadState()
             if (per_cu <= 0) {
                 throw std::runtime_error(
                     "ordered commit needs " + std::to_string(lds) + " B of LDS per block (" +
-                    std::to_string(A.capMax) + " table rows, " + std::to_string(dv.deferCap) +
+                    std::to_string(A.shape.capMax) + " table rows, " + std::to_string(dv.deferCap) +
                     " deferred destroys per world) but a workgroup holds " +
                     std::to_string(hipx::maxLDSPerBlock()) +
                     " B: lower max_deferred_destroys or the table capacities");

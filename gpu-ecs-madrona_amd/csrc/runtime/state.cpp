@@ -402,6 +402,26 @@ void StateManager::uploadToDevice(void *stream_ptr)
     d.makeTurn = (int32_t *)devAlloc(turn_bytes);
     MW_HIP_CHECK(hipMemsetAsync(d.makeTurn, 0, turn_bytes, stream));
     d.makeEpoch = (int32_t *)devAlloc(sizeof(int32_t));
+    // Ordered-commit shape: the largest table that takes entity rows or
+    // row-parallel appends (at most kCommitMaxRows rows per world; larger
+    // tables raise kErrFlagCommitLimit if a row-parallel node mutates them).
+    {
+        int32_t cap_max = 0;
+        uint32_t col_max = 4;
+        for (int32_t a = 0; a < d.numArchetypes; a++) {
+            const ArchetypeView &av = d.arch[a];
+            if (av.flags & kArchModuleRows) continue;
+            if (av.capacity > kCommitMaxRows) continue;
+            cap_max = std::max(cap_max, av.capacity);
+            for (int32_t c = 0; c < av.numColumns; c++) col_max = std::max(col_max, av.colBytes[c]);
+        }
+        d.commitCapMax = (cap_max + 63) / 64 * 64;
+        d.commitSortA = 1;
+        while (d.commitSortA < d.commitCapMax) d.commitSortA <<= 1;
+        d.commitSortO = 1;
+        while (d.commitSortO < d.deferCap) d.commitSortO <<= 1;
+        d.commitColMax = col_max;
+    }
     {
         const int32_t first_epoch = 1;
         copy(d.makeEpoch, &first_epoch, sizeof(int32_t));

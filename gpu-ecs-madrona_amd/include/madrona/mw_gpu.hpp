@@ -25,7 +25,6 @@ namespace madrona {
 
 inline constexpr int32_t kDefaultTmpAllocBytes = 16 * 1024;    // Context::tmpAlloc per world
 inline constexpr int32_t kDefaultDeferredPerWorld = 256;        // deferred destroys per node per world
-inline constexpr int32_t kCommitMaxRows = 4096;                 // ordered-commit table limit
 
 // Default chained tmpAlloc pool (device): twice the worlds' arenas, at least
 // 16 MiB, at most 1 GiB.

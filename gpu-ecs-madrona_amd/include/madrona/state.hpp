@@ -274,6 +274,7 @@ struct ArchetypeView {
 };
 
 inline constexpr int32_t kMakeTurnSlots = 8;     // = kMaxQueryArchetypes (context.hpp)
+inline constexpr int32_t kCommitMaxRows = 4096;  // ordered-commit table limit
 inline constexpr int32_t kMakeTurnWaves = 64;    // waves per world with ordered makes
 
 struct StateView {
@@ -299,6 +300,12 @@ struct StateView {
     // the epoch, so nothing is ever reset.
     int32_t *makeTurn;          // [kMakeTurnSlots][numWorlds][kMakeTurnWaves]
     int32_t *makeEpoch;         // [1]
+    // Ordered-commit shape (madrona/commit.hpp): rows per world the index
+    // arrays hold, the key sorts' sizes, the widest column.
+    int32_t commitCapMax;
+    int32_t commitSortA;
+    int32_t commitSortO;
+    uint32_t commitColMax;
     // Per-world bump allocator (Context::tmpAlloc, reference
     // StateManager::tmpAlloc, src/core/state.cpp:584-602): 256-byte
     // granules, reset by ResetTmpAllocNode.

@@ -13,6 +13,7 @@
 #pragma once
 
 #include <madrona/context.hpp>
+#include <madrona/commit.hpp>
 #include <madrona/optional.hpp>
 #include <madrona/tracing.hpp>
 
