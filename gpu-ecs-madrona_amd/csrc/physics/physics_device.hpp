@@ -495,7 +495,7 @@ constexpr int32_t kNarrowBlock = 256;
 constexpr int32_t kContactBlock = MW_CONTACT_BLOCK;   // plane / contact kernels
 constexpr int32_t kSolverBlock = 64;      // lanes per world (one wave)
 #ifndef MW_SOLVER_WORLDS
-#define MW_SOLVER_WORLDS 2
+#define MW_SOLVER_WORLDS 1
 #endif
 constexpr int32_t kSolverWorlds = MW_SOLVER_WORLDS;       // worlds per solver block
 constexpr int32_t kSolverThreads = kSolverBlock * kSolverWorlds;
