@@ -621,8 +621,12 @@ __host__ __device__ inline size_t solverWorldLDSBytes(int32_t nb)
 // kind), so one pass over a level keeps all of the block's lanes on that
 // level's items from all of its worlds.
 constexpr int32_t kSolverItems = kSolverWorlds * kSolverLDSContacts;
+// Dependency levels the block's bucket table holds; a deeper world (a tall
+// stack: the benchmark's worlds average 1.7 levels) solves from the global
+// records instead.  48, not 128: one world's LDS drops to 12.1 KB and 12
+// single-world blocks fit a CU (the VGPR limit) instead of 11.
 #ifndef MW_SOLVER_MAX_LEVELS
-#define MW_SOLVER_MAX_LEVELS kSolverLDSContacts
+#define MW_SOLVER_MAX_LEVELS 48
 #endif
 constexpr int32_t kSolverBuckets = kNumKinds * (MW_SOLVER_MAX_LEVELS + 2);
 
@@ -1231,27 +1235,36 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     const bool fits = BL.scalars[1] <= kSolverLDSContacts;
     MW_SOLVER_MARK(0);
 
-    if (!fits) {
-        // some world of the block overflows the LDS records: every world
-        // of the block solves on its own wave with global records
+    // Levels of the world's items (contacts, then joints) in LDS, unless the
+    // items overflow the LDS records or the levels the bucket table holds:
+    // then every world of the block solves on its own wave from the global
+    // records (same bits).  One call site for that path (a second inlined
+    // copy sent the kernel arguments to scratch).
+    const int32_t N = K + J;
+    int32_t max_level = 0;
+    if (fits) {
+        int32_t my_levels = 0;
         if (live) {
+            appendJoints(P, w, L.recs, K, J, lane);
+            waveSync();
+            my_levels = scheduleLevels(L, N, L.recs, L.prevs, lane);
+        }
+        if (live && lane == 0) atomicMax(&BL.scalars[2], my_levels);
+        __syncthreads();
+        max_level = BL.scalars[2];
+    }
+    MW_SOLVER_MARK(1);
+    if (!fits || max_level > MW_SOLVER_MAX_LEVELS) {
+        if (live) {
+            if (fits) {                       // scheduled once already: afresh
+                for (int32_t b = lane; b < nb; b += kSolverBlock) L.lastItem[b] = -1;
+                waveSync();
+            }
             solveWorldGlobal(P, w, L, J, lane);
             writeWorldBodies(P, w, L, lane, integrate_next != 0);
         }
         return;
     }
-
-    const int32_t N = K + J;     // contacts, then joints
-    int32_t my_levels = 0;
-    if (live) {
-        appendJoints(P, w, L.recs, K, J, lane);
-        waveSync();
-        my_levels = scheduleLevels(L, N, L.recs, L.prevs, lane);
-    }
-    if (live && lane == 0) atomicMax(&BL.scalars[2], my_levels);
-    __syncthreads();
-    const int32_t max_level = BL.scalars[2];
-    MW_SOLVER_MARK(1);
 
     // counting sort of the block's items by (level, kind)
     const int32_t nbk = (max_level + 2) * kNumKinds;
