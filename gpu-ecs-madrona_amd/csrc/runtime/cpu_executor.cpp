@@ -374,7 +374,7 @@ void Executor::runSteps(int32_t n)
     // runs of neighbouring worlds per claim: a world's rows share cache lines
     // with its neighbours' at the edges of every column slab, and two
     // workers stepping neighbours n times each would trade those lines
-    const int64_t chunk = std::max<int64_t>(1, I.cfg.numWorlds / (4 * (int64_t)I.pool->numThreads()));
+    const int64_t chunk = std::max<int64_t>(1, I.cfg.numWorlds / (16 * (int64_t)I.pool->numThreads()));
     I.pool->parallelFor(I.cfg.numWorlds, chunk, [](void *a, int64_t begin, int64_t end) {
         MultiArg &m = *(MultiArg *)a;
         for (int64_t w = begin; w < end; w++) {
