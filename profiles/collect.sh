@@ -6,7 +6,7 @@
 set -euo pipefail
 R=${1:-r01}
 OUT=$PWD/gpurun_out/prof_$R
-B="$PWD/bench.py --no-cpu-baseline --steps 10 --warmup 2"
+B="$PWD/bench.py --no-cpu-baseline --no-cpu-executor --steps 10 --warmup 2"
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1
