@@ -377,7 +377,8 @@ def main():
             "traffic": pmc_traffic(dom),
             "bytes_per_launch": int(nbytes), "ms_per_launch": round(ms, 4),
             "timed_launches": int(ev_n1 - ev_n0),
-            "timing": ("HIP events on the executor stream around every launch of the kernel in "
+            "timing": ("a HIP event pair bound to the kernel (hipExtLaunchKernelGGL: kernel start to "
+                       "kernel end, no dispatch gap) on every launch of the node in "
                        + ("every timed step" if args.timed_every <= 1 else
                           f"every {args.timed_every}th timed step (the first of each run of "
                           f"{args.timed_every}; the step graph is split at that node in those "

@@ -627,6 +627,15 @@ int32_t mw_set_timed_node_every(mw_exec *exec, const char *node_name, int32_t ev
     }, -1)
 }
 
+int32_t mw_set_timed_node_index(mw_exec *exec, int32_t node, int32_t every)
+{
+    MW_TRY({
+        if (every < 1) throw std::invalid_argument("mw_set_timed_node_index: every must be >= 1");
+        exec->exec->setTimedNodeIndex(node, every);
+        return 0;
+    }, -1)
+}
+
 double mw_timed_node_ms(mw_exec *exec, int64_t *launches)
 {
     MW_TRY({ return exec->exec->timedNodeMs(launches); }, -1.0)

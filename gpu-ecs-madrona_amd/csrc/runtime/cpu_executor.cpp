@@ -184,6 +184,12 @@ struct Executor::Impl {
     // timing of one node kind (setTimedNode / timeNode): wall time of every
     // run of that node, summed over worlds
     std::string timedName;
+    int32_t timedIndex = -1;        // setTimedNodeIndex: one node only
+    bool timedMatch(int32_t n) const
+    {
+        if (timedIndex >= 0) return n == timedIndex;
+        return !timedName.empty() && timedName == graph.nodeName(n);
+    }
     std::atomic<int64_t> timedNs { 0 };
     int64_t timedLaunches = 0;
 };
@@ -333,7 +339,7 @@ void Executor::runAsync()
             const int32_t n = sg.nodes[0];
             const auto t0 = std::chrono::steady_clock::now();
             I.graph.nodeFns(n).cpuGlobal(I.graph.nodeState(n), rc);
-            if (timing && I.timedName == I.graph.nodeName(n)) {
+            if (timing && I.timedMatch(n)) {
                 I.timedNs += std::chrono::duration_cast<std::chrono::nanoseconds>(
                     std::chrono::steady_clock::now() - t0).count();
                 I.timedLaunches++;
@@ -343,7 +349,7 @@ void Executor::runAsync()
         std::vector<uint8_t> timed;
         if (timing) {
             for (int32_t n : sg.nodes) {
-                timed.push_back(I.timedName == I.graph.nodeName(n));
+                timed.push_back(I.timedMatch(n));
                 I.timedLaunches += timed.back();
             }
         }
@@ -459,13 +465,16 @@ double Executor::timeNode(const char *name, int32_t num_steps)
 {
     Impl &I = *impl_;
     const std::string saved = I.timedName;
+    const int32_t saved_index = I.timedIndex;
     const int64_t ns0 = I.timedNs.load(), l0 = I.timedLaunches;
     I.timedName = name ? name : "";
+    I.timedIndex = -1;
     for (int32_t s = 0; s < num_steps; s++) runAsync();
     const int64_t ns = I.timedNs.load() - ns0, l = I.timedLaunches - l0;
     I.timedNs = ns0;
     I.timedLaunches = l0;
     I.timedName = saved;
+    I.timedIndex = saved_index;
     // per launch = one run of the node over every world (summed worker time)
     return l > 0 ? (double)ns * 1e-6 / (double)l : -1.0;
 }
@@ -474,8 +483,18 @@ void Executor::setTimedNode(const char *name, int32_t every)
 {
     (void)every;   // host timing costs no graph split: every step is timed
     impl_->timedName = name ? name : "";
+    impl_->timedIndex = -1;
     impl_->timedNs = 0;
     impl_->timedLaunches = 0;
+}
+
+void Executor::setTimedNodeIndex(int32_t node, int32_t every)
+{
+    if (node < 0 || node >= impl_->graph.numNodes()) {
+        throw std::runtime_error("setTimedNodeIndex: node index past the graph");
+    }
+    setTimedNode(impl_->graph.nodeName(node), every);
+    impl_->timedIndex = node;
 }
 
 double Executor::timedNodeMs(int64_t *launches)

@@ -39,7 +39,7 @@ void launchWorldKernel(const void *kernel, LaunchCtx &lc)
     const uint32_t blocks = lc.capGrid((uint32_t)((lc.numWorlds + 63) / 64));
     if (blocks == 0) return;
     hipx::residentBlocks(kernel, "perWorldKernel", 64, 0);
-    MW_HIP_CHECK(hipLaunchKernel(kernel, dim3(blocks), dim3(64), args, 0,
+    MW_HIP_CHECK(hipx::launchKernel(kernel, dim3(blocks), dim3(64), args, 0,
                                  (hipStream_t)lc.stream));
 }
 
@@ -67,7 +67,7 @@ void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype, int32
     StateView *st = lc.devState;
     int32_t arch = archetype, qa = query_arch;
     void *kargs[] = { &st, &arch, &qa, const_cast<void *>(cols) };
-    MW_HIP_CHECK(hipLaunchKernel(kernel, grid, block, kargs, 0, (hipStream_t)lc.stream));
+    MW_HIP_CHECK(hipx::launchKernel(kernel, grid, block, kargs, 0, (hipStream_t)lc.stream));
 }
 
 // World-serial row nodes: numWorlds invocations of `threads` lanes.
@@ -79,7 +79,7 @@ void launchSerialKernel(const void *kernel, LaunchCtx &lc, int32_t threads, cons
     StateView *st = lc.devState;
     void *kargs[] = { &st, const_cast<void *>(query) };
     hipx::residentBlocks(kernel, "serialForKernel", 256, 0);
-    MW_HIP_CHECK(hipLaunchKernel(kernel, dim3(blocks), dim3(256), kargs, 0, (hipStream_t)lc.stream));
+    MW_HIP_CHECK(hipx::launchKernel(kernel, dim3(blocks), dim3(256), kargs, 0, (hipStream_t)lc.stream));
 }
 
 // addNodeFn nodes: a fixed count per world sizes the grid; a dynamic count
@@ -99,7 +99,7 @@ void launchNodeFnKernel(const void *kernel, LaunchCtx &lc, void *node_dev, uint3
     if (blocks == 0) return;
     void *kargs[] = { &node_dev, &fixed_count, &threads };
     hipx::residentBlocks(kernel, "nodeFnKernel", 256, 0);
-    MW_HIP_CHECK(hipLaunchKernel(kernel, dim3(blocks), dim3(256), kargs, 0,
+    MW_HIP_CHECK(hipx::launchKernel(kernel, dim3(blocks), dim3(256), kargs, 0,
                                  (hipStream_t)lc.stream));
 }
 
@@ -329,7 +329,7 @@ struct Executor::Impl {
     // The step as replayable hipGraph segments.  Normally one segment holds
     // every node plus the export gathers; with live node timing enabled the
     // step is split at each timed node, which is launched directly on the
-    // stream between its segments, bracketed by HIP events.
+    // stream between its segments, its kernels bound to a HIP event pair.
     struct Segment {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
@@ -344,9 +344,11 @@ struct Executor::Impl {
     std::vector<ExportBuf> exports;
     int64_t *hostRowsTotal = nullptr;
 
-    // Live per-node timing: HIP events recorded around every launch of one
-    // node kind inside each step, accumulated at each sync.
+    // Live per-node timing: a HIP event pair bound to the kernels of every
+    // launch of one node kind inside each step (launchNodeTimed: first
+    // kernel start to last kernel end), accumulated at each sync.
     std::string timedName;
+    int32_t timedIndex = -1;        // setTimedNodeIndex: one node only
     // One event pair per timed launch per enqueued step: a burst of
     // runAsync steps keeps every step's pairs until the next sync.
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timedPool;
@@ -568,6 +570,7 @@ static void launchExports(Executor::Impl &I, const StateView &dv)
 
 static bool isTimed(const Executor::Impl &I, int32_t node)
 {
+    if (I.timedIndex >= 0) return node == I.timedIndex;
     return !I.timedName.empty() && I.timedName == I.graph.nodeName(node);
 }
 
@@ -630,6 +633,26 @@ static std::pair<hipEvent_t, hipEvent_t> &timedPair(Executor::Impl &I, int32_t e
     return I.timedPool[i];
 }
 
+// Node `i` with its kernels bound to the event pair (hipx::TimedLaunch):
+// `start` is first recorded in stream order and then re-bound to the first
+// kernel's start; a node none of whose kernels took the binding (a world
+// library launching through its own calls) keeps the stream-order pair.
+static void launchNodeTimed(Executor::Impl &I, int32_t i, LaunchCtx &lc,
+                            hipEvent_t start, hipEvent_t stop)
+{
+    MW_HIP_CHECK(hipEventRecord(start, I.stream));
+    hipx::TimedLaunch t { start, stop };
+    hipx::tlTimed = &t;
+    try {
+        launchNode(I, i, lc);
+    } catch (...) {
+        hipx::tlTimed = nullptr;
+        throw;
+    }
+    hipx::tlTimed = nullptr;
+    if (t.start) MW_HIP_CHECK(hipEventRecord(stop, I.stream));
+}
+
 // One step's launch sequence: every node in sorted order, then the export
 // gathers.  Nodes of the timed kind are bracketed by their own event pair.
 static void launchStep(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
@@ -637,10 +660,12 @@ static void launchStep(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
     int32_t ev = 0;
     traceStepBegin(I);
     for (int32_t i = 0; i < I.graph.numNodes(); i++) {
-        const bool timed = isTimed(I, i);
-        if (timed) MW_HIP_CHECK(hipEventRecord(timedPair(I, ev).first, I.stream));
-        launchNode(I, i, lc);
-        if (timed) MW_HIP_CHECK(hipEventRecord(timedPair(I, ev++).second, I.stream));
+        if (isTimed(I, i)) {
+            const auto &pr = timedPair(I, ev++);
+            launchNodeTimed(I, i, lc, pr.first, pr.second);
+        } else {
+            launchNode(I, i, lc);
+        }
     }
     launchExports(I, dv);
     traceStepEnd(I);
@@ -834,10 +859,8 @@ void Executor::runAsync()
         for (auto &sg : sampled ? I.segs : I.plainSegs) {
             if (sg.exec) MW_HIP_CHECK(hipGraphLaunch(sg.exec, I.stream));
             if (sg.timedNode >= 0) {
-                MW_HIP_CHECK(hipEventRecord(timedPair(I, ev).first, I.stream));
-                launchNode(I, sg.timedNode, lc);
-                MW_HIP_CHECK(hipEventRecord(timedPair(I, ev).second, I.stream));
-                ev++;
+                const auto &pr = timedPair(I, ev++);
+                launchNodeTimed(I, sg.timedNode, lc, pr.first, pr.second);
             }
         }
     } else {
@@ -872,23 +895,33 @@ void Executor::run()
     sync();
 }
 
+static void setTimed(Executor &E, Executor::Impl &I, const char *name, int32_t index, int32_t every)
+{
+    E.sync();
+    I.timedName = name ? name : "";
+    I.timedIndex = index;
+    I.timedEvery = std::max(1, every);
+    I.stepIndex = 0;
+    I.timedMs = 0.0;
+    I.timedLaunches = 0;
+    I.timedPerStep = 0;
+    for (int32_t i = 0; i < I.graph.numNodes(); i++) I.timedPerStep += isTimed(I, i);
+    const StateView &dv = I.mgr->deviceViewHost();
+    LaunchCtx lc = makeLaunchCtx(I, &E);
+    if (I.cfg.useGraph) captureGraph(I, lc, dv);
+}
+
 void Executor::setTimedNode(const char *name, int32_t every)
 {
-    sync();
-    impl_->timedName = name ? name : "";
-    impl_->timedEvery = std::max(1, every);
-    impl_->stepIndex = 0;
-    impl_->timedMs = 0.0;
-    impl_->timedLaunches = 0;
-    impl_->timedPerStep = 0;
-    if (!impl_->timedName.empty()) {
-        for (int32_t i = 0; i < impl_->graph.numNodes(); i++) {
-            if (impl_->timedName == impl_->graph.nodeName(i)) impl_->timedPerStep++;
-        }
+    setTimed(*this, *impl_, name, -1, every);
+}
+
+void Executor::setTimedNodeIndex(int32_t node, int32_t every)
+{
+    if (node < 0 || node >= impl_->graph.numNodes()) {
+        throw std::runtime_error("setTimedNodeIndex: node index past the graph");
     }
-    const StateView &dv = impl_->mgr->deviceViewHost();
-    LaunchCtx lc = makeLaunchCtx(*impl_, this);
-    if (impl_->cfg.useGraph) captureGraph(*impl_, lc, dv);
+    setTimed(*this, *impl_, impl_->graph.nodeName(node), node, every);
 }
 
 void Executor::enableTracing(int64_t max_records)
@@ -1079,16 +1112,14 @@ double Executor::timeNode(const char *name, int32_t num_steps)
     for (int32_t s = 0; s < num_steps; s++) {
         for (int32_t i = 0; i < impl_->graph.numNodes(); i++) {
             bool match = strcmp(impl_->graph.nodeName(i), name) == 0;
-            hipEvent_t a = nullptr, b = nullptr;
             if (match) {
+                hipEvent_t a = nullptr, b = nullptr;
                 MW_HIP_CHECK(hipEventCreate(&a));
                 MW_HIP_CHECK(hipEventCreate(&b));
-                MW_HIP_CHECK(hipEventRecord(a, impl_->stream));
-            }
-            launchNode(*impl_, i, lc);
-            if (match) {
-                MW_HIP_CHECK(hipEventRecord(b, impl_->stream));
                 evs.push_back({ a, b });
+                launchNodeTimed(*impl_, i, lc, a, b);
+            } else {
+                launchNode(*impl_, i, lc);
             }
         }
         launchExports(*impl_, dv);

@@ -14,6 +14,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstddef>
 #include <cstdint>
@@ -35,6 +36,32 @@ int32_t residentBlocksNoThrow(const void *fn, int32_t threads, size_t dyn_lds);
 // hipGetLastError after a launch; throws naming the kernel.
 void checkLaunched(const char *name);
 
+// Live node timing (Executor::setTimedNode / timeNode).  While a
+// TimedLaunch is installed on this thread, MW_LAUNCH binds its events to the
+// kernels it launches (hipExtLaunchKernelGGL): `start` to the first kernel's
+// start (then cleared), `stop` to every kernel's end, the last one winning.
+// The pair then spans the node's kernels only, not the dispatch gap between
+// the preceding graph segment and the node's first kernel that stream-order
+// hipEventRecord markers include (≈30 us per solver launch on the MI355X box).
+struct TimedLaunch {
+    hipEvent_t start = nullptr;
+    hipEvent_t stop = nullptr;
+};
+inline thread_local TimedLaunch *tlTimed = nullptr;
+
+// hipLaunchKernel for the type-erased launchers (row / serial / node-function
+// kernels), with the TimedLaunch binding of MW_LAUNCH.
+inline hipError_t launchKernel(const void *fn, dim3 grid, dim3 block, void **args, size_t lds,
+                               hipStream_t stream)
+{
+    if (TimedLaunch *t = tlTimed) {
+        const hipEvent_t start = t->start;
+        t->start = nullptr;
+        return hipExtLaunchKernel(fn, grid, block, args, lds, stream, start, t->stop, 0);
+    }
+    return hipLaunchKernel(fn, grid, block, args, lds, stream);
+}
+
 }
 
 #define MW_HIP_CHECK(expr)                                                          \
@@ -49,6 +76,13 @@ void checkLaunched(const char *name);
         const dim3 blk__ = (block);                                                     \
         ::madrona::hipx::residentBlocks((const void *)&(kernel), #kernel,              \
                                         (int32_t)(blk__.x * blk__.y * blk__.z), (lds)); \
-        hipLaunchKernelGGL(kernel, grid, blk__, lds, stream, __VA_ARGS__);             \
+        if (::madrona::hipx::TimedLaunch *tl__ = ::madrona::hipx::tlTimed) {             \
+            const hipEvent_t start__ = tl__->start;                                     \
+            tl__->start = nullptr;                                                      \
+            hipExtLaunchKernelGGL(kernel, grid, blk__, lds, stream, start__, tl__->stop, \
+                                  0u, __VA_ARGS__);                                     \
+        } else {                                                                        \
+            hipLaunchKernelGGL(kernel, grid, blk__, lds, stream, __VA_ARGS__);         \
+        }                                                                               \
         ::madrona::hipx::checkLaunched(#kernel);                                       \
     } while (0)

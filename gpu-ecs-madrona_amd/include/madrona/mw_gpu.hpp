@@ -138,6 +138,9 @@ public:
     // every > 1: only every every-th step (the first of each run of
     // `every`) is split and timed, the others replay the unsplit graph.
     void setTimedNode(const char *name, int32_t every = 1);
+    // The same for one node of the graph (its index in sorted order), e.g.
+    // one of several ParallelForNodes; throws on an index past the graph.
+    void setTimedNodeIndex(int32_t node, int32_t every = 1);
     double timedNodeMs(int64_t *launches);
 
     // Device tracing (reference mw_gpu/tracing.hpp): records of every step

@@ -160,6 +160,8 @@ def _declare(lib):
     lib.mw_set_timed_node.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     lib.mw_set_timed_node_every.restype = ctypes.c_int32
     lib.mw_set_timed_node_every.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int32]
+    lib.mw_set_timed_node_index.restype = ctypes.c_int32
+    lib.mw_set_timed_node_index.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
     lib.mw_timed_node_ms.restype = ctypes.c_double
     lib.mw_timed_node_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
     lib.mw_num_nodes.argtypes = [ctypes.c_void_p]
@@ -201,7 +203,7 @@ C_ABI_SYMBOLS = (
     "mw_destroy", "mw_last_error", "mw_num_worlds", "mw_error_flags", "mw_num_archetypes",
     "mw_read_column", "mw_column_info", "mw_phys_read_candidates", "mw_phys_read_contacts",
     "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_copy_exported",
-    "mw_gen_collisions_inits", "mw_set_timed_node", "mw_set_timed_node_every", "mw_timed_node_ms",
+    "mw_gen_collisions_inits", "mw_set_timed_node", "mw_set_timed_node_every", "mw_set_timed_node_index", "mw_timed_node_ms",
     "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
     "mw_device_free", "mw_gen_fvs_inits", "mw_stream_wait", "mw_load_hull",
     "mw_trace_enable", "mw_trace_read", "mw_trace_func_name", "mw_trace_block_records",
@@ -514,6 +516,11 @@ class Executor:
         only the first step of every run of `every` steps is timed."""
         if self._lib.mw_set_timed_node_every(self.h, name.encode() if name else None,
                                              int(every)) != 0:
+            raise _err(self._lib)
+
+    def set_timed_node_index(self, node, every=1):
+        """set_timed_node for the one node at index `node` of node_names()."""
+        if self._lib.mw_set_timed_node_index(self.h, int(node), int(every)) != 0:
             raise _err(self._lib)
 
     def timed_node(self):

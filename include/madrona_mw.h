@@ -222,14 +222,16 @@ int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *contacts_out)
  * MADRONA_MW_FORCE_GLOBAL_IMAGES=1 at mw_create forces the global variants. */
 int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t n);
 
-/* physics kernel timing hook for the bench: records HIP events around each
- * launch of the named node kind on the executor stream ("SolverNode", ...).
+/* physics kernel timing hook for the bench: binds a HIP event pair to the
+ * kernels of each launch of the named node kind ("SolverNode", ...): first
+ * kernel start to last kernel end.
  * Returns the mean duration in ms over `num_steps` fresh steps.            */
 double mw_phys_time_node(mw_exec *exec, const char *node_name, int32_t num_steps);
 
 /* live timing inside the replayed step: the step graph is split at every
  * launch of the named node kind, which then runs directly on the executor
- * stream between graph segments, bracketed by HIP events; mw_timed_node_ms
+ * stream between graph segments with a HIP event pair bound to its kernels
+ * (first kernel start to last kernel end); mw_timed_node_ms
  * returns the accumulated ms and the number of timed launches since the
  * last mw_set_timed_node (NULL/"" disables and restores the single graph). */
 int32_t mw_set_timed_node(mw_exec *exec, const char *node_name);
@@ -237,6 +239,10 @@ int32_t mw_set_timed_node(mw_exec *exec, const char *node_name);
  * `every` steps is split and timed; the others replay the unsplit graph, so
  * the timing costs 1/every of the split's overhead). every >= 1.          */
 int32_t mw_set_timed_node_every(mw_exec *exec, const char *node_name, int32_t every);
+/* the same for one node of the step graph: `node` is its index in sorted
+ * order (mw_node_name), e.g. one of several ParallelForNodes.  -1 and a
+ * message on an index past the graph.                                      */
+int32_t mw_set_timed_node_index(mw_exec *exec, int32_t node, int32_t every);
 double mw_timed_node_ms(mw_exec *exec, int64_t *launches);
 
 /* ---- job-API environments -----------------------------

@@ -207,6 +207,29 @@ def test_sampled_node_timing_counts_and_does_not_perturb_state():
         assert a.contacts(w).tobytes() == b.contacts(w).tobytes()
 
 
+def test_node_index_timing_times_one_node():
+    # set_timed_node_index: only the one node (the first of the four
+    # SolverNodes) is split and timed; its event pair is bound to the
+    # node's kernels, so the per-launch time stays within the step's.
+    mw = _mw()
+    gcfg, _ = _cfg_pair()
+    pos, rot = gen_collisions_inits(16, 128, seed=5)
+    a = mw.CollisionsSim(16, pos, rot, gcfg)
+    b = mw.CollisionsSim(16, pos, rot, gcfg)
+    kinds = a.nodes()
+    first = kinds.index("SolverNode")
+    assert kinds.count("SolverNode") == gcfg.num_substeps
+    a.set_timed_node_index(first)
+    a.step(6)
+    b.step(6)
+    ms, n = a.timed_node()
+    assert n == 6 and ms > 0
+    for w in range(16):
+        assert a.bodies(w).tobytes() == b.bodies(w).tobytes()
+    with pytest.raises(RuntimeError, match="past the graph"):
+        a.set_timed_node_index(len(kinds))
+
+
 def test_episode_return_export_matches_oracle():
     # CustomParallelForNode (one wave per world) over the EpisodeReturn
     # singleton + the packed export buffer (getExported slot 2, a singleton:

@@ -159,3 +159,21 @@ def test_fvs_bit_exact_vs_live_reference(cpu):
                 assert a.tobytes() == b.tobytes(), f"tick {100 * t} world {w} arch {arch}"
     assert sum(len(ref.table(w, 0)) for w in range(W)) < 50 * W      # dragons died
 
+
+
+def test_node_index_timing_on_cpu_backend(cpu):
+    # set_timed_node_index times one node of the graph (here the markDead
+    # ParallelForNode, the fourth of five), not every node of its kind.
+    inits = ol.gen_fvs_inits(4, 50, 200, seed=1)
+    sim = cpu.FvsSim(4, inits, backend="cpu", num_workers=2)
+    kinds = sim.nodes()
+    mark = [i for i, k in enumerate(kinds) if k == "ParallelForNode"][3]
+    sim.set_timed_node_index(mark)
+    sim.step(3)
+    ms, n = sim.timed_node()
+    assert n == 3 and ms > 0
+    sim.set_timed_node("ParallelForNode")
+    sim.step(2)
+    assert sim.timed_node()[1] == 2 * kinds.count("ParallelForNode")
+    with pytest.raises(RuntimeError, match="past the graph"):
+        sim.set_timed_node_index(len(kinds))

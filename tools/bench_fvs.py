@@ -8,9 +8,9 @@ Timed window: the CHURN window, ticks preroll+1 .. preroll+K (default
 most of them die before tick 1200 (oracle run of the same init: 3197 of the
 sampled 3200 alive at 600, ~490 at 1200), so every timed tick destroys
 entities, releases IDs and compacts rows (the ordered commit's wave-parallel
-swap-removes) up to the window's end.  The sampled worlds' dragons alive
-after every chunk of ticks are reported (read between chunks, outside the
-timed steps).  The CPU
+swap-removes) up to the window's end.  The live dragons and knights of 256
+sampled worlds are read after every chunk of ticks (outside the timed
+steps); their window mean sizes the dominant node's algorithmic bytes.  The CPU
 baseline is the reference's own ECS (oracle/_ref) on the same tick window,
 one pinned worker per usable core, batches of 2048 worlds (the reference
 reserves 48 GiB of address space per world) until ~4 s is timed.
@@ -29,25 +29,41 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
 
 HBM_PEAK_GBS = 8000.0
-# Algorithmic bytes per launch and world (Entity 8,
-# Position 12, Health 64 (cache-line aligned), Action 4, Mana / Quiver 4).
-# The three ParallelForNodes are timed together, so their bytes are averaged:
-# actionSelect reads Entity + Position + Action and writes Position + Action
-# on every row, the caster reads Entity + Action + Mana and writes Mana on
-# dragon rows, the archer reads Entity + Action + Quiver on knight rows.
-def world_bytes(node, nd, nk):
-    if node == "ParallelForNode":
-        return ((nd + nk) * (8 + 2 * 12 + 2 * 4) + nd * (8 + 4 + 2 * 4) + nk * (8 + 4 + 4)) / 3
-    return (nd + nk) * (8 + 64)                     # cleanup scan: Entity + Health
+# The tick graph's nodes in sorted order (fvs.hip): the ParallelForNodes and
+# the PerWorldNodes, by system.
+ROW_SYSTEMS = ["actionSelectSystem", "casterSystem", "archerSystem", "markDeadSystem",
+               "destroyTrackedSystem"]
+WORLD_SYSTEMS = ["trackDeadSystem", "finishTickSystem"]
+# Algorithmic bytes per launch and world of a node (SURVEY.md §8(d) C5:
+# Entity 8, Position 12, Health 64 -- alignas(MADRONA_CACHE_LINE) --,
+# Action 4, Mana / Quiver 4), nd / nk = live dragons / knights of the world:
+# every column of the node's query read once per row, every column it
+# modifies written once.  The caster's blasts re-read Position / Health of the
+# world (L2-resident after the first) and are not counted; the cleanup nodes
+# touch a few tracker rows.
+SYS_BYTES = {
+    "actionSelectSystem": lambda nd, nk: (nd + nk) * (8 + 2 * 12 + 2 * 4),
+    "casterSystem": lambda nd, nk: nd * (8 + 4 + 2 * 4),
+    "archerSystem": lambda nd, nk: nk * (8 + 4 + 2 * 4),
+    "markDeadSystem": lambda nd, nk: (nd + nk) * (8 + 64),
+}
 
 
-def pmc_traffic(node):
-    """HBM bytes per launch of the node kind from the committed rocprofv3 PMC
-    passes (profiles/r03_fvs_traffic.json, tools/gpu_fvs_pmc.sh); None if
-    absent."""
+def node_systems(kinds):
+    """{node index: system} from the executor's node kinds."""
+    rows, worlds = iter(ROW_SYSTEMS), iter(WORLD_SYSTEMS)
+    return {i: next(rows) if k == "ParallelForNode" else next(worlds)
+            for i, k in enumerate(kinds)}
+
+
+def pmc_traffic(system):
+    """HBM bytes per launch of the system's node (row kernels + commit) over
+    the timed window, from the committed rocprofv3 PMC passes
+    (profiles/r03_fvs_traffic.json, tools/gpu_fvs_pmc.sh +
+    tools/fvs_prof_summary.py); None if absent."""
     try:
         with open(os.path.join(ROOT, "profiles", "r03_fvs_traffic.json")) as f:
-            return json.load(f)["nodes"][node]["bytes_per_launch"]
+            return json.load(f)["nodes"][system]["bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         return None
 
@@ -127,26 +143,42 @@ def main():
     inits = mw.gen_fvs_inits(W, args.dragons, args.knights, seed=0)
     sim = mw.FvsSim(W, inits)
 
+    systems = node_systems(sim.nodes())
+    # untimed pre-roll: the first ticks time each modelled node in turn (its
+    # kernels bound to an event pair) to pick the dominant one
     node_ms = {}
-    for name in ("ParallelForNode", "PerWorldNode"):
-        node_ms[name] = sim.time_node(name, 1)     # untimed pre-roll (2 ticks)
-    # restart from the init so the timed window is ticks warmup+1..warmup+K
-    sim.close()
-    sim = mw.FvsSim(W, inits)
-    dom = max(node_ms, key=lambda n: node_ms[n] * (4 if n == "ParallelForNode" else 1))
-    left = args.preroll
+    for i, sysname in systems.items():
+        if sysname not in SYS_BYTES:
+            continue
+        sim.set_timed_node_index(i)
+        sim.step(5)
+        ms, n = sim.timed_node()
+        node_ms[i] = ms / max(1, n)
+    sim.set_timed_node(None)
+    dom = max(node_ms, key=node_ms.get)
+    dom_sys = systems[dom]
+    left = args.preroll - 5 * len(node_ms)
+    if left < 0:
+        raise SystemExit("--preroll too short for the node timing")
     while left > 0:
         n = min(args.chunk, left)
         sim.step(n)
         left -= n
     sim.sync()
-    sampled = range(0, W, max(1, W // 64))
-    alive0 = sum(sim.num_rows(w, 0) for w in sampled)
-    # throughput: the plain step graph, chunks of ticks per host sync; only
-    # the stepping is timed (the sampled alive counts are read between chunks)
+    sampled = range(0, W, max(1, W // 256))
+
+    def live():
+        return (sum(sim.num_rows(w, 0) for w in sampled) / len(sampled),
+                sum(sim.num_rows(w, 1) for w in sampled) / len(sampled))
+
+    # throughput: the step graph, chunks of ticks per host sync; only the
+    # stepping is timed (the sampled row counts are read between chunks).
+    # The dominant node is timed live in the window: every 10th tick runs the
+    # graph split at that node with an event pair bound to its kernels.
+    sim.set_timed_node_index(dom, every=10)
     elapsed = 0.0
     left, tick = args.steps, args.preroll
-    alive_by_tick = [[tick, int(alive0)]]
+    rows_by_tick = [[tick, *live()]]
     while left > 0:
         n = min(args.chunk, left)
         t0 = time.perf_counter()
@@ -155,20 +187,18 @@ def main():
         elapsed += time.perf_counter() - t0
         left -= n
         tick += n
-        alive_by_tick.append([tick, int(sum(sim.num_rows(w, 0) for w in sampled))])
-    alive = alive_by_tick[-1][1]
-    # per-launch kernel time: HIP events around every launch of the dominant
-    # node kind (graph split at that node), one tick per sync, 100 ticks
-    sim.set_timed_node(dom)
-    for _ in range(100):
-        sim.step(1)
+        rows_by_tick.append([tick, *live()])
     ms1, n1 = sim.timed_node()
     ms0, n0 = 0.0, 0
     sim.set_timed_node(None)
     flags = sim.error_flags()
+    # mean live rows over the window (trapezoid over the chunk boundaries)
+    span = rows_by_tick[-1][0] - rows_by_tick[0][0]
+    nd_mean = sum((b[0] - a[0]) * (a[1] + b[1]) / 2 for a, b in zip(rows_by_tick, rows_by_tick[1:])) / span
+    nk_mean = sum((b[0] - a[0]) * (a[2] + b[2]) / 2 for a, b in zip(rows_by_tick, rows_by_tick[1:])) / span
 
     launch_ms = (ms1 - ms0) / max(1, n1 - n0)
-    nbytes = W * world_bytes(dom, args.dragons, args.knights)
+    nbytes = W * SYS_BYTES[dom_sys](nd_mean, nk_mean)
     achieved = nbytes / (launch_ms * 1e-3) / 1e9
     cpu = None if args.no_cpu_baseline else cpu_baseline(args)
     out = {
@@ -181,18 +211,23 @@ def main():
         "config": {"workload": f"examples/fantasy_vs restated: {W} worlds x ({args.dragons} "
                                f"dragons + {args.knights} knights), Game::tick with cleanup",
                    "timed_ticks": f"{args.preroll + 1}-{args.preroll + args.steps}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+        "roofline": {"bound": "hbm", "kernel": f"{dom_sys} (node {dom}: row kernels + ordered commit)",
+                     "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": pmc_traffic(dom), "ms_per_launch": round(launch_ms, 4),
-                     "timing": "HIP events around every launch of the node kind over 100 "
-                               "ticks right after the timed region (executor stream)",
-                     "bytes_per_launch": int(nbytes)},
+                     "traffic": pmc_traffic(dom_sys), "ms_per_launch": round(launch_ms, 4),
+                     "timed_launches": int(n1 - n0),
+                     "timing": "a HIP event pair bound to the node's kernels (first kernel start to "
+                               "last kernel end) on every 10th tick of the timed window (the step "
+                               "graph is split at that node on those ticks only)",
+                     "bytes_per_launch": int(nbytes),
+                     "bytes_model": f"{W} worlds x SYS_BYTES['{dom_sys}'] at the window's mean live "
+                                    f"rows per world: {nd_mean:.1f} dragons, {nk_mean:.1f} knights"},
         "cpu_baseline": cpu, "error_flags": flags,
-        "nodes_ms_per_launch_preroll": {k: round(v, 4) for k, v in node_ms.items()},
-        "dragons_alive_sampled_worlds": {"window_start": int(alive0), "window_end": int(alive),
-                                          "sampled_worlds": len(sampled),
-                                          "at_init": args.dragons * len(sampled),
-                                          "by_tick": alive_by_tick},
+        "nodes_ms_per_launch_preroll": {systems[i]: round(v, 4) for i, v in node_ms.items()},
+        "live_rows_sampled_worlds": {"sampled_worlds": len(sampled),
+                                     "at_init": [args.dragons, args.knights],
+                                     "by_tick_dragons_knights_per_world":
+                                         [[t, round(d, 2), round(k, 2)] for t, d, k in rows_by_tick]},
     }
     print(json.dumps(out))
     sim.close()

@@ -2,7 +2,9 @@
 """Per-tick kernel breakdown of a fantasy_vs kernel trace (rocprofv3
 --kernel-trace csv of tools/bench_fvs.py): kernels are labelled by system,
 commits by the node they follow; averages over ticks [A, B) of the run
-(counted by finishTickSystem launches).
+(counted by finishTickSystem launches).  The runtime's copy kernels (the
+bench reads sampled row counts between chunks of ticks) are left out; the
+wall time per tick includes those reads.
 
     python tools/fvs_trace_ticks.py run_kernel_trace.csv [A B]
 """
@@ -23,6 +25,8 @@ def main():
     fin = []
     for r in rows:
         name = r["Kernel_Name"]
+        if name.startswith("__amd_rocclr"):
+            continue       # the bench's row-count reads between chunks, not the tick
         k = next((x for x in KEYS if x in name), name[:40])
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
         if k == "structuralCommit":
@@ -39,7 +43,7 @@ def main():
     for k, v in sorted(agg.items(), key=lambda x: -sum(x[1])):
         print(f"{k:45s} launches={len(v):6d} avg={sum(v) / len(v):8.2f} us  per-tick={sum(v) / n:8.2f} us")
         total += sum(v) / n
-    print(f"kernel time per tick {total:.2f} us; wall per tick {(fin[b] - fin[a]) / n / 1000:.2f} us")
+    print(f"kernel time per tick {total:.2f} us; wall per tick {(fin[b - 1] - fin[a - 1]) / n / 1000:.2f} us")
 
 
 if __name__ == "__main__":

@@ -1,11 +1,23 @@
 #!/bin/bash
-# FETCH_SIZE / WRITE_SIZE of the fantasy_vs tick kernels (separate passes):
-#   bash tools/gpu_fvs_pmc.sh TAG
+# fantasy_vs kernel trace, then FETCH_SIZE and WRITE_SIZE in separate PMC
+# passes (no sys/runtime trace with --pmc), each bounded by its own timeout,
+# summarised per node over the bench's timed window (ticks 601-1200) by
+# tools/fvs_prof_summary.py:   bash tools/gpu_fvs_pmc.sh TAG
 set -o pipefail
 T=${1:-fvs_pmc}
 R=$PWD
-mkdir -p gpurun_out/$T
+O=$R/gpurun_out/$T
+mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-B="$R/tools/bench_fvs.py --no-cpu-baseline --worlds 16384 --preroll 600 --steps 100 --chunk 50"
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "FantasyVS|structuralCommit" --output-format csv -d $R/gpurun_out/$T/fetch -o run -- python3 $B > $R/gpurun_out/$T/fetch.log 2>&1 || exit 1
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "FantasyVS|structuralCommit" --output-format csv -d $R/gpurun_out/$T/write -o run -- python3 $B > $R/gpurun_out/$T/write.log 2>&1 || exit 2
+B="$R/tools/bench_fvs.py --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $B > $O/trace.log 2>&1 || { echo TRACEFAIL; tail -20 $O/trace.log; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "FantasyVS|structuralCommit" --output-format csv -d $O/fetch -o run -- python3 $B > $O/fetch.log 2>&1 || { echo FETCHFAIL; tail -20 $O/fetch.log; exit 2; }
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "FantasyVS|structuralCommit" --output-format csv -d $O/write -o run -- python3 $B > $O/write.log 2>&1 || { echo WRITEFAIL; tail -20 $O/write.log; exit 3; }
+cd $R
+python3 tools/fvs_prof_summary.py --trace $(find $O/trace -name "*kernel_trace.csv" | head -1) \
+    --fetch $(find $O/fetch -name "*counter_collection.csv" | head -1) \
+    --write $(find $O/write -name "*counter_collection.csv" | head -1) \
+    --out $O/fvs_traffic.json > /dev/null || exit 4
+python3 tools/fvs_trace_ticks.py $(find $O/trace -name "*kernel_trace.csv" | head -1) 600 1200 > $O/fvs_ticks.txt || exit 5
+cp $(find $O/trace -name "*kernel_stats.csv" | head -1) $O/fvs_kernel_stats.csv
+cat $O/fvs_ticks.txt
