@@ -647,6 +647,7 @@ __global__ void __launch_bounds__(kRefitBlock) refitGlobalKernel(PhysArgs P)
 // pass 2 writes them.
 
 constexpr int32_t kOverlapBuf = 12;     // candidates kept per body before a second sweep
+constexpr int32_t kOverlapMaskWords = 4; // worlds up to 256 leaves: hits as a register bitmask
 
 // findOverlappingEntry + BVH::findOverlaps (broadphase.cpp:897-932,
 // physics.inl:61-100) without a per-lane tree walk.  Every ancestor slot of
@@ -798,10 +799,57 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
             const int32_t e_id = me.id;
             const bool a_static = me.isStatic != 0;
             const bool active = row < rows;
-            // sweep 1: count hits, keep the first kOverlapBuf ranks.  The
-            // hit test is evaluated branch-free on one 32-byte broadcast read
-            // per leaf (short-circuit && became nested exec-mask branches with
-            // a dependent LDS read per field).
+            CandidateCollision *out = P.cands + (size_t)w * P.candCapacity;
+            uint64_t *out_slots = P.candSlots + (size_t)w * P.candCapacity;
+            int32_t total;
+            if (nleaves <= 64 * kOverlapMaskWords) {
+                // The hits as a leaf-rank bitmask in registers: the sweep
+                // stores nothing to LDS, so the broadcast leaf reads of
+                // successive iterations are not ordered behind a possibly
+                // aliasing store and stay in flight together; the writes walk
+                // the set bits in rank order (the reference's emission order).
+                uint64_t mask[kOverlapMaskWords];
+#pragma unroll
+                for (int32_t c = 0; c < kOverlapMaskWords; c++) {
+                    uint64_t bits = 0;
+                    const int32_t k0 = 64 * c, k1 = min(nleaves, k0 + 64);
+#pragma unroll 8
+                    for (int32_t k = k0; k < k1; k++) {
+                        bits |= (uint64_t)leafHit(leaves, k, q, e_id, a_static) << (k - k0);
+                    }
+                    mask[c] = active ? bits : 0;
+                    cnt += __popcll(mask[c]);
+                }
+                MW_OVERLAP_MARK(1);                       // sweep (thread 0's wave)
+                const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
+                MW_OVERLAP_MARK(2);                       // scan (waits for every wave)
+                if (cnt > 0) {
+                    const Loc a_loc = me.loc;
+                    const uint64_t a_slot = me.slot;
+                    int32_t slot = base + off;
+#pragma unroll
+                    for (int32_t c = 0; c < kOverlapMaskWords; c++) {
+                        uint64_t bits = mask[c];
+                        while (bits) {
+                            const int32_t k = 64 * c + __ffsll((unsigned long long)bits) - 1;
+                            bits &= bits - 1;
+                            const OrderedLeaf &o = leaves[k];
+                            if (slot < P.candCapacity) {
+                                out[slot] = CandidateCollision { a_loc, o.loc };
+                                out_slots[slot] = a_slot | (uint64_t)o.slot << 32;
+                            }
+                            slot++;
+                        }
+                    }
+                }
+                base += total;
+                MW_OVERLAP_MARK(3);                       // candidate writes (thread 0's)
+                continue;
+            }
+            // Worlds with more leaves: sweep 1 counts hits and keeps the
+            // first kOverlapBuf ranks in LDS, a second sweep covers a body
+            // with more.  The hit test is evaluated branch-free on one
+            // 32-byte broadcast read per leaf.
 #pragma unroll 4
             for (int32_t k = 0; k < nleaves; k++) {
                 const bool hit = active & leafHit(leaves, k, q, e_id, a_static);
@@ -811,11 +859,8 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
                 }
             }
             MW_OVERLAP_MARK(1);                           // sweep (thread 0's wave)
-            int32_t total;
             const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
             MW_OVERLAP_MARK(2);                           // scan (waits for every wave)
-            CandidateCollision *out = P.cands + (size_t)w * P.candCapacity;
-            uint64_t *out_slots = P.candSlots + (size_t)w * P.candCapacity;
             if (cnt > 0) {
                 const Loc a_loc = me.loc;
                 const uint64_t a_slot = me.slot;

@@ -488,15 +488,36 @@ __device__ __forceinline__ void writeFaceManifold(Contact &c, Vector3 n, const V
 // earlier choices replaced by p0).  Every walk recomputes the same vertices
 // with the same operations, so the chosen points are the reference's bits.
 // Returns true if a manifold was written.
+// The body columns a hull-plane pair reads: the hull's position, rotation
+// and scale, the plane body's position and rotation.
+struct PlaneIn {
+    Vector3 aPos;
+    Quat aRot;
+    Diag3x3 aScale;
+    Vector3 bPos;
+    Quat bRot;
+};
+
+__device__ __forceinline__ PlaneIn loadPlaneIn(const PhysArgs &P, const SatWork &wk)
+{
+    const BodyArch &BA = P.body[wk.aArch], &BB = P.body[wk.bArch];
+    const int32_t w = wk.world;
+    return PlaneIn { bcol<Vector3>(BA, Cols::Position, w, wk.a.row),
+                     bcol<Quat>(BA, Cols::Rotation, w, wk.a.row),
+                     bcol<Diag3x3>(BA, Cols::Scale, w, wk.a.row),
+                     bcol<Vector3>(BB, Cols::Position, w, wk.b.row),
+                     bcol<Quat>(BB, Cols::Rotation, w, wk.b.row) };
+}
+
 __device__ __forceinline__ bool planeContact(const PhysArgs &P, const ObjDev &O, int32_t w,
-                                             const SatWork &wk)
+                                             const SatWork &wk, const PlaneIn &in)
 {
     int32_t *flags = P.errorFlags + w;
     const HullDev ha = O.hulls[wk.aObj];
-    const HullXform xa = hullXform(P, w, P.body[wk.aArch], wk.a.row);
-    const BodyArch &BB = P.body[wk.bArch];
-    const Vector3 b_pos = bcol<Vector3>(BB, Cols::Position, w, wk.b.row);
-    const Quat b_rot = bcol<Quat>(BB, Cols::Rotation, w, wk.b.row);
+    const Mat3x3 unscaled_rot = Mat3x3::fromQuat(in.aRot);
+    const HullXform xa { unscaled_rot * in.aScale, unscaled_rot * in.aScale.inv(), in.aPos };
+    const Vector3 b_pos = in.bPos;
+    const Quat b_rot = in.bRot;
     const Vector3 pn = b_rot.rotateVec(Vector3 { 0, 0, 1 });
     const geometry::Plane plane { pn, dot(pn, b_pos) };
     float min_dot = FLT_MAX;
@@ -710,6 +731,18 @@ __device__ __forceinline__ void *stageTable(char *&dst, const void *src, size_t 
     return out;
 }
 
+// A plane work entry's indices are inside the tables its loads index.
+__device__ __forceinline__ bool planeWorkOk(const PhysArgs &P, const SatWork &wk)
+{
+    return (uint32_t)wk.world < (uint32_t)P.numWorlds &&
+           (uint32_t)wk.slot < (uint32_t)P.candCapacity &&
+           (uint32_t)wk.aObj < (uint32_t)P.objs.numObjects &&
+           (uint32_t)wk.aArch < (uint32_t)P.numBodyArchs &&
+           (uint32_t)wk.bArch < (uint32_t)P.numBodyArchs &&
+           (uint32_t)wk.a.row < (uint32_t)P.body[wk.aArch].capacity &&
+           (uint32_t)wk.b.row < (uint32_t)P.body[wk.bArch].capacity;
+}
+
 // Hull-plane contacts, one lane per pair of the bins' back parts.
 __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
 {
@@ -730,21 +763,36 @@ __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
     __shared__ int32_t s_pre[kNarrowBins + 1];
     loadBinPrefix(P, 1, s_pre);
     const int32_t total = s_pre[kNarrowBins];
-    for (int32_t i = blockIdx.x * kContactBlock + threadIdx.x; i < total;
-         i += gridDim.x * kContactBlock) {
-        const SatWork wk = P.satWork[binEntry(P, s_pre, i, 1)];
-        const bool ok = (uint32_t)wk.world < (uint32_t)P.numWorlds &&
-                        (uint32_t)wk.slot < (uint32_t)P.candCapacity &&
-                        (uint32_t)wk.aObj < (uint32_t)P.objs.numObjects &&
-                        (uint32_t)wk.aArch < (uint32_t)P.numBodyArchs &&
-                        (uint32_t)wk.bArch < (uint32_t)P.numBodyArchs &&
-                        (uint32_t)wk.a.row < (uint32_t)P.body[wk.aArch].capacity &&
-                        (uint32_t)wk.b.row < (uint32_t)P.body[wk.bArch].capacity;
+    // Two-deep software pipeline over the lane's pairs: while pair i is
+    // solved, the body columns of pair i + stride and the work entry of pair
+    // i + 2 stride are in flight (the contact stores would otherwise order
+    // every next load behind them).
+    const int32_t stride = gridDim.x * kContactBlock;
+    int32_t i = blockIdx.x * kContactBlock + threadIdx.x;
+    SatWork wk1, wk2;
+    bool ok1 = false;
+    PlaneIn in1;
+    if (i < total) {
+        wk1 = P.satWork[binEntry(P, s_pre, i, 1)];
+        ok1 = planeWorkOk(P, wk1);
+        if (ok1) in1 = loadPlaneIn(P, wk1);
+    }
+    if (i + stride < total) wk2 = P.satWork[binEntry(P, s_pre, i + stride, 1)];
+    for (; i < total; i += stride) {
+        const SatWork wk = wk1;
+        const bool ok = ok1;
+        const PlaneIn in = in1;
+        if (i + stride < total) {
+            wk1 = wk2;
+            ok1 = planeWorkOk(P, wk1);
+            if (ok1) in1 = loadPlaneIn(P, wk1);
+            if (i + 2 * stride < total) wk2 = P.satWork[binEntry(P, s_pre, i + 2 * stride, 1)];
+        }
         if (!ok) {
             atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
             continue;
         }
-        if (planeContact(P, O, wk.world, wk))
+        if (planeContact(P, O, wk.world, wk, in))
             recordManifold(P, wk.world, wk.slot, slotOf(P, wk.bArch, wk.b), slotOf(P, wk.aArch, wk.a));
     }
 }

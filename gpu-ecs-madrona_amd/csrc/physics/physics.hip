@@ -270,6 +270,17 @@ struct NarrowphaseNode : PhysNodeBase {
         hipStream_t stream = (hipStream_t)lc.stream;
         if (self->substep == 0)
             MW_LAUNCH(narrowFilterKernel, dim3(Q.numWorlds), dim3(kNarrowBlock), 0, stream, Q);
+        // The hull-plane pairs share nothing with the hull-hull ones (own
+        // list, own contact slots): their kernel runs on the side stream,
+        // beside SAT + contact clipping (a parallel branch of the graph).
+        hipStream_t side = (hipStream_t)lc.sideStream;
+        if (side) {
+            MW_HIP_CHECK(hipEventRecord((hipEvent_t)lc.forkEvent, stream));
+            MW_HIP_CHECK(hipStreamWaitEvent(side, (hipEvent_t)lc.forkEvent, 0));
+        }
+        MW_LAUNCH(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),
+                  dim3(kContactBlock), Q.planeGeoBytes, side ? side : stream, Q);
+        if (side) MW_HIP_CHECK(hipEventRecord((hipEvent_t)lc.joinEvent, side));
         if (Q.satImage) {       // the grid never exceeds the slabs of the image
             const uint32_t g = std::min<uint32_t>(lc.persistentGrid(Q.satGrid), Q.satImageBlocks);
             MW_LAUNCH(narrowSATGlobalKernel, dim3(g), dim3(kNarrowBlock),
@@ -278,8 +289,6 @@ struct NarrowphaseNode : PhysNodeBase {
             MW_LAUNCH(narrowSATKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
                       narrowphaseSharedBytes(Q), stream, Q);
         }
-        MW_LAUNCH(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),
-                           dim3(kContactBlock), Q.planeGeoBytes, stream, Q);
         if (Q.clipImage) {
             const uint32_t g = std::min<uint32_t>(lc.persistentGrid(Q.contactGrid), Q.clipImageBlocks);
             MW_LAUNCH(narrowContactGlobalKernel, dim3(g), dim3(kContactBlock), 0, stream, Q);
@@ -287,6 +296,7 @@ struct NarrowphaseNode : PhysNodeBase {
             MW_LAUNCH(narrowContactKernel, dim3(lc.persistentGrid(Q.contactGrid)),
                       dim3(kContactBlock), contactSharedBytes(Q), stream, Q);
         }
+        if (side) MW_HIP_CHECK(hipStreamWaitEvent(stream, (hipEvent_t)lc.joinEvent, 0));
     }
 };
 

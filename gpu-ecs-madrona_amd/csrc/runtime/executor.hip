@@ -325,6 +325,8 @@ struct Executor::Impl {
     ExecConfig cfg;
     std::unique_ptr<StateManager> mgr;
     hipStream_t stream = nullptr;
+    hipStream_t sideStream = nullptr;   // LaunchCtx::sideStream
+    hipEvent_t forkEvent = nullptr, joinEvent = nullptr;
     TaskGraph graph;
     // The step as replayable hipGraph segments.  Normally one segment holds
     // every node plus the export gathers; with live node timing enabled the
@@ -387,6 +389,14 @@ static LaunchCtx makeLaunchCtx(Executor::Impl &I, Executor *exec)
     lc.nodeData = I.nodeDataDev;
     lc.serialNodes = I.cfg.serialNodes;
     if (const char *e = getenv("MADRONA_MW_WORLD_WAVE_LANES")) lc.worldWaveLanes = atoi(e);
+    // opt-in: in the replayed graph the join costs more than the overlap
+    // saves (DESIGN.md round-3 dead ends)
+    const char *side = getenv("MADRONA_MW_SIDE_STREAM");
+    if (side && atoi(side) != 0) {
+        lc.sideStream = I.sideStream;
+        lc.forkEvent = I.forkEvent;
+        lc.joinEvent = I.joinEvent;
+    }
     return lc;
 }
 
@@ -397,6 +407,9 @@ Executor::Executor(const ExecConfig &cfg) : impl_(new Impl)
     impl_->cfg = cfg;
     MW_HIP_CHECK(hipSetDevice(cfg.gpuID));
     MW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking));
+    MW_HIP_CHECK(hipStreamCreateWithFlags(&impl_->sideStream, hipStreamNonBlocking));
+    MW_HIP_CHECK(hipEventCreateWithFlags(&impl_->forkEvent, hipEventDisableTiming));
+    MW_HIP_CHECK(hipEventCreateWithFlags(&impl_->joinEvent, hipEventDisableTiming));
     impl_->mgr.reset(new StateManager(StateManager::Config {
         cfg.numWorlds, cfg.defaultCapacity,
         cfg.tmpAllocBytesPerWorld >= 0 ? cfg.tmpAllocBytesPerWorld : kDefaultTmpAllocBytes,
@@ -434,6 +447,9 @@ Executor::~Executor()
     }
     impl_->mgr.reset();
     if (impl_->stream) (void)hipStreamDestroy(impl_->stream);
+    if (impl_->sideStream) (void)hipStreamDestroy(impl_->sideStream);
+    if (impl_->forkEvent) (void)hipEventDestroy(impl_->forkEvent);
+    if (impl_->joinEvent) (void)hipEventDestroy(impl_->joinEvent);
 }
 
 StateManager &Executor::stateManager() { return *impl_->mgr; }

@@ -69,6 +69,14 @@ struct LaunchCtx {
     // wave per world (parallelForWorldKernel); env
     // MADRONA_MW_WORLD_WAVE_LANES overrides the default (0: never).
     int32_t worldWaveLanes = 256;
+    // A second stream of the executor for a node's independent kernels
+    // (fork: record forkEvent on `stream`, the side stream waits on it; join:
+    // record joinEvent on the side stream, `stream` waits on it).  Inside the
+    // step graph's capture this makes parallel branches.  Null (the default;
+    // env MADRONA_MW_SIDE_STREAM=1 sets it): every kernel runs on `stream`.
+    void *sideStream = nullptr;     // hipStream_t
+    void *forkEvent = nullptr;      // hipEvent_t
+    void *joinEvent = nullptr;      // hipEvent_t
 
     // Grid for a grid-stride kernel that needs `blocks` blocks to cover its
     // work in one pass: capped at numCUs x blocksPerCU when configured.
