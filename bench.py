@@ -184,54 +184,69 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(args, executor=False):
-    """Reference CPU executor (oracle/_ref, built from the reference's own
-    src/core + src/physics) on a bounded sample of the same workload and the
-    same step window as the timed GPU region (steps warmup+1 .. warmup+K of
-    consecutive world batches); falls back to the parity-pinned restatement
-    (oracle/) when the reference build is absent."""
+def cpu_baselines(args, legs):
+    """CPU legs on a bounded sample of the same workload and the same step
+    window as the timed GPU region (steps warmup+1 .. warmup+K of consecutive
+    world batches): "reference" = the reference's own executor (oracle/_ref,
+    built from its src/core + src/physics; the parity-pinned restatement in
+    oracle/ when that build is absent), "executor" = the framework's CPU back
+    end (libmadrona_cpu.so).  With both legs their batches alternate over the
+    same worlds (reference batch i, then executor batch i), so the two rates
+    come from the same worlds in the same stretch of host load; batches are
+    added until every leg has cpu_target_s of timed work."""
     import subprocess
     threads = args.cpu_threads if args.cpu_threads > 0 else usable_cores()
     if args.cpu_worlds <= 0:
         args.cpu_worlds = max(256, 16 * threads)
     if args.cpu_steps <= 0:
         args.cpu_steps = args.steps
-    total_s, total_steps, kind, batches = 0.0, 0, None, 0
+    acc = {leg: {"s": 0.0, "steps": 0, "kind": None} for leg in legs}
+    batches = 0
     t_wall = time.perf_counter()
-    while batches < args.cpu_max_batches and total_s < args.cpu_target_s:
-        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child",
-               "--cpu-worlds", str(args.cpu_worlds),
-               "--cpu-first-world", str(batches * args.cpu_worlds),
-               "--cpu-threads", str(threads), "--cubes", str(args.cubes),
-               "--workload", args.workload,
-               "--substeps", str(args.substeps), "--cpu-steps", str(args.cpu_steps),
-               "--settle", str(args.settle), "--warmup", str(args.warmup)] + \
-              (["--cpu-port"] if args.cpu_port else []) + (["--cpu-executor"] if executor else [])
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
-        if r.returncode != 0:
-            raise RuntimeError(f"cpu baseline child failed: {r.stderr[-2000:]}")
-        res = json.loads(r.stdout.strip().splitlines()[-1])
-        kind = res["kind"]
-        total_s += res["seconds"]
-        total_steps += res["env_steps"]
+    while batches < args.cpu_max_batches and min(a["s"] for a in acc.values()) < args.cpu_target_s:
+        for leg in legs:
+            cmd = [sys.executable, os.path.abspath(__file__), "--cpu-child",
+                   "--cpu-worlds", str(args.cpu_worlds),
+                   "--cpu-first-world", str(batches * args.cpu_worlds),
+                   "--cpu-threads", str(threads), "--cubes", str(args.cubes),
+                   "--workload", args.workload,
+                   "--substeps", str(args.substeps), "--cpu-steps", str(args.cpu_steps),
+                   "--settle", str(args.settle), "--warmup", str(args.warmup)] + \
+                  (["--cpu-port"] if args.cpu_port else []) + \
+                  (["--cpu-executor"] if leg == "executor" else [])
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+            if r.returncode != 0:
+                raise RuntimeError(f"cpu {leg} child failed: {r.stderr[-2000:]}")
+            res = json.loads(r.stdout.strip().splitlines()[-1])
+            acc[leg]["kind"] = res["kind"]
+            acc[leg]["s"] += res["seconds"]
+            acc[leg]["steps"] += res["env_steps"]
         batches += 1
     wall = time.perf_counter() - t_wall
-    return {
-        "value": round(total_steps / total_s, 1),
-        "unit": "env-steps/s",
-        "cores": threads,
-        "cpu_model": cpu_model(),
-        "host_cpus_visible": os.cpu_count(),
-        "kind": kind,
-        "sample": f"{args.workload} {batches} batches x {args.cpu_worlds} worlds (worlds 0-"
-                  f"{batches * args.cpu_worlds - 1}) x {args.cubes} cubes, S={args.substeps}; "
-                  f"timed steps {args.settle + args.warmup + 1}-"
-                  f"{args.settle + args.warmup + args.cpu_steps} ("
-                  + ("the GPU's timed window" if args.cpu_steps == args.steps
-                     else "starts where the GPU's timed window starts")
-                  + f"), {threads} host threads pinned one per usable core, "
-                  f"{total_s:.2f} s timed / {wall:.1f} s wall",
-    }
+    out = {}
+    for leg in legs:
+        a = acc[leg]
+        out[leg] = {
+            "value": round(a["steps"] / a["s"], 1),
+            "unit": "env-steps/s",
+            "cores": threads,
+            "cpu_model": cpu_model(),
+            "host_cpus_visible": os.cpu_count(),
+            "kind": a["kind"],
+            "sample": ("libmadrona_cpu.so: " if leg == "executor" else "")
+                      + f"{args.workload} {batches} batches x {args.cpu_worlds} worlds (worlds 0-"
+                      f"{batches * args.cpu_worlds - 1}) x {args.cubes} cubes, S={args.substeps}; "
+                      f"timed steps {args.settle + args.warmup + 1}-"
+                      f"{args.settle + args.warmup + args.cpu_steps} ("
+                      + ("the GPU's timed window" if args.cpu_steps == args.steps
+                         else "starts where the GPU's timed window starts")
+                      + f"), {threads} host threads pinned one per usable core, "
+                      f"{a['s']:.2f} s timed"
+                      + (f"; batches alternated with the {' / '.join(l for l in legs if l != leg)} "
+                         f"leg over the same worlds, {wall:.1f} s wall for all legs"
+                         if len(legs) > 1 else f" / {wall:.1f} s wall"),
+        }
+    return out
 
 
 def main():
@@ -391,13 +406,12 @@ def main():
 
     cpu = cpu_exec = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args)
-        if not args.no_cpu_executor:
-            # the framework's own CPU back end (the reference's
-            # TaskGraphExecutor restated, libmadrona_cpu.so) on the same
-            # cores, worlds and step window, reported beside the reference
-            cpu_exec = cpu_baseline(args, executor=True)
-            cpu_exec["sample"] = "libmadrona_cpu.so: " + cpu_exec["sample"]
+        # the framework's own CPU back end (the reference's
+        # TaskGraphExecutor restated, libmadrona_cpu.so) on the same cores,
+        # worlds and step window, reported beside the reference
+        legs = ["reference"] + ([] if args.no_cpu_executor else ["executor"])
+        res = cpu_baselines(args, legs)
+        cpu, cpu_exec = res["reference"], res.get("executor")
 
     if rank == 0:
         out = {

@@ -655,11 +655,52 @@ geometry::Segment shortestSegmentBetween(const geometry::Segment &s1, const geom
     return { s1.p1 + s * v1, s2.p1 + t * v2 };
 }
 
+// Per-world narrowphase state of one substep.  Each body's world AABB and
+// hull state (makeHullState) are computed once, the first time a pair needs
+// them, instead of once per pair as runNarrowphase does: the same function
+// of the same pose, so the same bits, and no body moves during the pass.
 struct NarrowScratch {
     HullState a, b;
     std::vector<Vector3> tmp1, tmp2;
     std::vector<float> depths;
+    std::vector<AABB> box;            // [body slot]
+    std::vector<HullState> hull;      // [body slot]
+    std::vector<uint8_t> haveBox, haveHull;
+
+    void reset(int32_t bodies)
+    {
+        if ((int32_t)box.size() < bodies) {
+            box.resize(bodies);
+            hull.resize(bodies);
+        }
+        haveBox.assign(bodies, 0);
+        haveHull.assign(bodies, 0);
+    }
 };
+
+// Slot of a body in its world: the body archetypes' rows laid end to end.
+int32_t bodySlotOf(const PhysArgs &P, const Body &b, int32_t w)
+{
+    return b.B->slotBase + (int32_t)(b.i - (size_t)w * b.B->capacity);
+}
+
+const AABB &cachedWorldAABB(const PhysArgs &P, NarrowScratch &S, const Body &b, int32_t slot)
+{
+    if (!S.haveBox[slot]) {
+        S.box[slot] = P.objs.aabbs[b.obj()].applyTRS(b.pos(), b.rot(), b.scale());
+        S.haveBox[slot] = 1;
+    }
+    return S.box[slot];
+}
+
+const HullState &cachedHullState(NarrowScratch &S, HullView h, const Body &b, int32_t slot)
+{
+    if (!S.haveHull[slot]) {
+        makeHullState(S.hull[slot], h, b.pos(), b.rot(), b.scale());
+        S.haveHull[slot] = 1;
+    }
+    return S.hull[slot];
+}
 
 // generateContacts -> addManifoldToSolver (narrowphase.cpp:1123-1162,
 // 1366-1513): the world's contacts in append order.
@@ -693,23 +734,22 @@ void runNarrowphasePair(const PhysArgs &P, int32_t w, NarrowScratch &S, int32_t 
         std::swap(ba, bb);
         std::swap(ta, tb);
     }
-    AABB aw = O.aabbs[ba.obj()].applyTRS(ba.pos(), ba.rot(), ba.scale());
-    AABB bw = O.aabbs[bb.obj()].applyTRS(bb.pos(), bb.rot(), bb.scale());
-    if (!aw.overlaps(bw)) return;
+    const int32_t sa = bodySlotOf(P, ba, w), sb = bodySlotOf(P, bb, w);
+    if (!cachedWorldAABB(P, S, ba, sa).overlaps(cachedWorldAABB(P, S, bb, sb))) return;
 
     const uint32_t hull_t = (uint32_t)CollisionPrimitive::Type::Hull;
     const uint32_t plane_t = (uint32_t)CollisionPrimitive::Type::Plane;
     const uint32_t test = ta | tb;
     if (test == hull_t) {                                  // HullHull
         HullView ha { &O.hulls[ba.obj()], &O }, hb { &O.hulls[bb.obj()], &O };
-        makeHullState(S.a, ha, ba.pos(), ba.rot(), ba.scale());
-        makeHullState(S.b, hb, bb.pos(), bb.rot(), bb.scale());
+        const HullState &A = cachedHullState(S, ha, ba, sa);
+        const HullState &B = cachedHullState(S, hb, bb, sb);
         // doSAT (narrowphase.cpp:678-758)
-        FaceQuery fa = queryFaceDirections(S.a, S.b);
+        FaceQuery fa = queryFaceDirections(A, B);
         if (fa.separation > 0.0f) return;
-        FaceQuery fb = queryFaceDirections(S.b, S.a);
+        FaceQuery fb = queryFaceDirections(B, A);
         if (fb.separation > 0.0f) return;
-        EdgeQuery eq = queryEdgeDirections(S.a, S.b);
+        EdgeQuery eq = queryEdgeDirections(A, B);
         if (eq.separation > 0.0f) return;
 
         const bool face_a = fa.separation > eq.separation;
@@ -720,8 +760,8 @@ void runNarrowphasePair(const PhysArgs &P, int32_t w, NarrowScratch &S, int32_t 
             const bool a_is_ref = fa.separation >= fb.separation;
             const geometry::Plane ref_plane = a_is_ref ? fa.plane : fb.plane;
             const int32_t ref_face = a_is_ref ? fa.faceIdx : fb.faceIdx;
-            const HullState &ref = a_is_ref ? S.a : S.b;
-            const HullState &inc = a_is_ref ? S.b : S.a;
+            const HullState &ref = a_is_ref ? A : B;
+            const HullState &inc = a_is_ref ? B : A;
             const int32_t inc_face = findIncidentFace(inc, ref_plane.normal);
             ref_loc = a_is_ref ? a_loc : b_loc;
             other_loc = a_is_ref ? b_loc : a_loc;
@@ -773,9 +813,9 @@ void runNarrowphasePair(const PhysArgs &P, int32_t w, NarrowScratch &S, int32_t 
             other_loc = b_loc;
             const geometry::HalfEdge &ea = ha.hedge(eq.edgeA);
             const geometry::HalfEdge &eb = hb.hedge(eq.edgeB);
-            geometry::Segment sa { S.a.vertices[ea.rootVertex], S.a.vertices[ha.hedge(ea.next).rootVertex] };
-            geometry::Segment sb { S.b.vertices[eb.rootVertex], S.b.vertices[hb.hedge(eb.next).rootVertex] };
-            geometry::Segment s = shortestSegmentBetween(sa, sb);
+            geometry::Segment ga { A.vertices[ea.rootVertex], A.vertices[ha.hedge(ea.next).rootVertex] };
+            geometry::Segment gb { B.vertices[eb.rootVertex], B.vertices[hb.hedge(eb.next).rootVertex] };
+            geometry::Segment s = shortestSegmentBetween(ga, gb);
             const Quat ident { 1, 0, 0, 0 };
             m = Manifold {};
             m.cp[0] = ident.rotateVec(s.p1) + Vector3::zero();
@@ -786,13 +826,13 @@ void runNarrowphasePair(const PhysArgs &P, int32_t w, NarrowScratch &S, int32_t 
         if (m.num > 0) addManifold(P, w, num_contacts, m, ref_loc, other_loc);
     } else if (test == (hull_t | plane_t)) {               // HullPlane
         HullView ha { &O.hulls[ba.obj()], &O };
-        makeHullState(S.a, ha, ba.pos(), ba.rot(), ba.scale());
+        const HullState &A = cachedHullState(S, ha, ba, sa);
         Vector3 pn = bb.rot().rotateVec(Vector3 { 0, 0, 1 });
         geometry::Plane plane { pn, dot(pn, bb.pos()) };
         // doSATPlane (narrowphase.cpp:760-788)
-        float sep = hullDistFromPlane(plane, S.a);
+        float sep = hullDistFromPlane(plane, A);
         if (sep > 0.0f) return;
-        const int32_t inc_face = findIncidentFace(S.a, plane.normal);
+        const int32_t inc_face = findIncidentFace(A, plane.normal);
         // createFacePlaneContact (narrowphase.cpp:974-1017)
         const size_t cap = (size_t)ha.h->numHedges + 8;
         if (S.tmp1.size() < cap) { S.tmp1.resize(cap); S.tmp2.resize(cap); S.depths.resize(cap); }
@@ -801,7 +841,7 @@ void runNarrowphasePair(const PhysArgs &P, int32_t w, NarrowScratch &S, int32_t 
         do {
             const geometry::HalfEdge &he = ha.hedge(hidx);
             hidx = he.next;
-            Vector3 v = S.a.vertices[he.rootVertex];
+            Vector3 v = A.vertices[he.rootVertex];
             float d = distFromPlane(plane, v);
             if (d < 0.0f) {
                 S.tmp1[n] = v - d * plane.normal;
@@ -819,6 +859,7 @@ void runNarrowphasePair(const PhysArgs &P, int32_t w, NarrowScratch &S, int32_t 
 void narrowphase(const PhysArgs &P, int32_t w)
 {
     thread_local NarrowScratch S;
+    S.reset(P.maxBodiesPerWorld);
     int32_t num_contacts = 0;
     const CandidateCollision *cands = P.cands + (size_t)w * P.candCapacity;
     const int32_t n = P.numCands[w];
