@@ -643,8 +643,8 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
     const BodyBox *boxes = P.bodyBoxes + (size_t)w * P.maxBodiesPerWorld;
     uint32_t *info = P.survInfo + (size_t)w * cap;
     const int32_t bin = w % kNarrowBins;
-    SatWork *list = P.satWork + (size_t)bin * P.binCap;
-    SatWork *list_back = list + P.binCap - 1;              // plane entries grow down
+    PackedSatWork *list = P.satWork + (size_t)bin * P.binCap;
+    PackedSatWork *list_back = list + P.binCap - 1;        // plane entries grow down
     constexpr uint32_t kHull = (uint32_t)CollisionPrimitive::Type::Hull;
     constexpr uint32_t kHullPlane = kHull | (uint32_t)CollisionPrimitive::Type::Plane;
 
@@ -689,9 +689,9 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
             wk[j].slot = slot;
             info[slot] = kNoManifold;
             if (wk[j].test == kHull) {
-                list[hpos++] = wk[j];
+                list[hpos++] = packWork(wk[j]);
             } else if (wk[j].test == kHullPlane) {
-                *(list_back - ppos++) = wk[j];
+                *(list_back - ppos++) = packWork(wk[j]);
             }
             // sphere / plane-plane survivors get a slot but no manifold:
             // the reference asserts on them (narrowphase.cpp:1197-1313)
@@ -769,11 +769,12 @@ __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
     // every next load behind them).
     const int32_t stride = gridDim.x * kContactBlock;
     int32_t i = blockIdx.x * kContactBlock + threadIdx.x;
-    SatWork wk1, wk2;
+    SatWork wk1;
+    PackedSatWork wk2;
     bool ok1 = false;
     PlaneIn in1;
     if (i < total) {
-        wk1 = P.satWork[binEntry(P, s_pre, i, 1)];
+        wk1 = unpackWork(P, P.satWork[binEntry(P, s_pre, i, 1)]);
         ok1 = planeWorkOk(P, wk1);
         if (ok1) in1 = loadPlaneIn(P, wk1);
     }
@@ -783,7 +784,7 @@ __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
         const bool ok = ok1;
         const PlaneIn in = in1;
         if (i + stride < total) {
-            wk1 = wk2;
+            wk1 = unpackWork(P, wk2);
             ok1 = planeWorkOk(P, wk1);
             if (ok1) in1 = loadPlaneIn(P, wk1);
             if (i + 2 * stride < total) wk2 = P.satWork[binEntry(P, s_pre, i + 2 * stride, 1)];
@@ -917,7 +918,7 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
     const int32_t total = min(s_pre[kNarrowBins], P.numWorlds * P.candCapacity);
     const int32_t stride = gridDim.x * kGroupsPerBlock;
     for (int32_t idx = blockIdx.x * kGroupsPerBlock + group; idx < total; idx += stride) {
-        const SatWork wk = P.satWork[binEntry(P, s_pre, idx, 0)];
+        const SatWork wk = unpackWork(P, P.satWork[binEntry(P, s_pre, idx, 0)]);
         const bool ok = (uint32_t)wk.world < (uint32_t)P.numWorlds &&
                         (uint32_t)wk.slot < (uint32_t)P.candCapacity &&
                         (uint32_t)wk.aObj < (uint32_t)P.objs.numObjects &&

@@ -336,6 +336,33 @@ __device__ __forceinline__ bool candOverlaps(const PhysArgs &P, int32_t w, uint6
     return A.box.overlaps(B.box);
 }
 
+// SatWork <-> the lists' 16-byte entries (PackedSatWork).
+__device__ __forceinline__ PackedSatWork packWork(const SatWork &w)
+{
+    return PackedSatWork { w.world,
+                           ((uint32_t)w.slot & 0xffffu) | (w.test & 7u) << 16 |
+                               ((uint32_t)w.aArch & 63u) << 19 | ((uint32_t)w.bArch & 63u) << 25,
+                           ((uint32_t)w.a.row & 0xffffu) | ((uint32_t)w.b.row & 0xffffu) << 16,
+                           ((uint32_t)w.aObj & 0xffffu) | ((uint32_t)w.bObj & 0xffffu) << 16 };
+}
+
+__device__ __forceinline__ SatWork unpackWork(const PhysArgs &P, const PackedSatWork &p)
+{
+    SatWork w;
+    w.world = p.world;
+    w.slot = (int32_t)(p.slotTest & 0xffffu);
+    w.test = (p.slotTest >> 16) & 7u;
+    w.aArch = (int32_t)((p.slotTest >> 19) & 63u);
+    w.bArch = (int32_t)((p.slotTest >> 25) & 63u);
+    w.pad = 0;
+    const int32_t na = P.numBodyArchs;
+    w.a = Loc { (uint32_t)(w.aArch < na ? P.body[w.aArch].archetype : -1), (int32_t)(p.rows & 0xffffu) };
+    w.b = Loc { (uint32_t)(w.bArch < na ? P.body[w.bArch].archetype : -1), (int32_t)(p.rows >> 16) };
+    w.aObj = (int32_t)(p.objs & 0xffffu);
+    w.bObj = (int32_t)(p.objs >> 16);
+    return w;
+}
+
 // A surviving candidate's work entry, in runNarrowphase's type order
 // (narrowphase.cpp:1574-1580).
 __device__ __forceinline__ SatWork candWork(const CandidateCollision &cand, uint64_t cs,
@@ -378,8 +405,8 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
     const uint64_t *slots = P.candSlots + (size_t)w * cap;
     uint32_t *info = P.survInfo + (size_t)w * cap;
     const int32_t bin = w % kNarrowBins;
-    SatWork *list = P.nextSatWork + (size_t)bin * P.binCap;
-    SatWork *list_back = list + P.binCap - 1;              // plane entries grow down
+    PackedSatWork *list = P.nextSatWork + (size_t)bin * P.binCap;
+    PackedSatWork *list_back = list + P.binCap - 1;        // plane entries grow down
     int32_t *counts = P.nextSatWorkCount + bin * kBinStride;
     constexpr uint32_t kHull = (uint32_t)CollisionPrimitive::Type::Hull;
     constexpr uint32_t kHullPlane = kHull | (uint32_t)CollisionPrimitive::Type::Plane;
@@ -458,8 +485,8 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
                 SatWork wk = candWork(c[j], s[j], A, B, w);
                 wk.slot = S + __popcll(mk & lt);
                 info[wk.slot] = kNoManifold;
-                if (hh) list[b_hh + __popcll(mh & lt)] = wk;
-                if (hp) *(list_back - (b_hp + __popcll(mp & lt))) = wk;
+                if (hh) list[b_hh + __popcll(mh & lt)] = packWork(wk);
+                if (hp) *(list_back - (b_hp + __popcll(mp & lt))) = packWork(wk);
             }
             S += __popcll(mk);
             b_hh += __popcll(mh);

@@ -207,6 +207,10 @@ void PhysicsModule::buildArgs(void *stream)
 
     ObjDev &O = P.objs;
     O.numObjects = (int32_t)metadata.size();
+    if (O.numObjects > 65535) {
+        // narrowphase work entries hold object ids in 16 bits (PackedSatWork)
+        throw std::runtime_error("physics: more than 65535 collision objects");
+    }
     O.maxVerts = 0;
     O.maxFaces = 0;
     O.maxEdges = 0;
@@ -237,7 +241,7 @@ void PhysicsModule::buildArgs(void *stream)
     P.solverOrder = alloc<int32_t>(W, stream);
     P.binCap = (W + kNarrowBins - 1) / kNarrowBins * P.candCapacity;
     for (int32_t set = 0; set < 2; set++) {
-        P.satWorkSet[set] = alloc<SatWork>((size_t)kNarrowBins * P.binCap, stream);
+        P.satWorkSet[set] = alloc<PackedSatWork>((size_t)kNarrowBins * P.binCap, stream);
         P.satWorkCountSet[set] = alloc<int32_t>(kNarrowBins * kBinStride, stream);
     }
     P.satWork = P.satWorkSet[0];

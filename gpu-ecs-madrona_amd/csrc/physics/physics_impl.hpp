@@ -95,6 +95,22 @@ struct SatWork {
 };
 static_assert(sizeof(SatWork) == 48);
 
+// A SatWork as the work lists store it: 16 B instead of 48.  The lists are
+// written once by the filters and read once by the SAT / plane kernels (4.7 M
+// entries per substep at the benchmark size, most of narrowphase's HBM
+// traffic); a Loc's archetype is its body archetype's (body[arch].archetype).
+// Rows and survivor slots fit 16 bits (<= 32767, physics_host.cpp), object
+// ids 16 bits and body archetype indices 6 bits (checked at upload), the
+// type test 3 bits.
+struct PackedSatWork {
+    int32_t world;
+    uint32_t slotTest;            // slot | test << 16 | aArch << 19 | bArch << 25
+    uint32_t rows;                // a.row | b.row << 16
+    uint32_t objs;                // aObj | bObj << 16
+};
+static_assert(sizeof(PackedSatWork) == 16);
+static_assert(kMaxBodyArchetypes <= 64, "6-bit body archetype indices");
+
 // A narrowphase pair that needs a contact manifold, with the feature the SAT
 // chose: hull-plane (from the filter), reference/incident face or edge pair
 // (from the SAT kernel).
@@ -150,7 +166,7 @@ struct PhysArgs {
     int32_t *survCount;           // [W] survivors per world
     int32_t *solverOrder;         // [W] worlds by descending survivor count: the solver
                                   // grid's world order (heaviest blocks dispatched first)
-    struct SatWork *satWork;      // [kNarrowBins][binCap] SAT / plane work lists: bin
+    struct PackedSatWork *satWork; // [kNarrowBins][binCap] SAT / plane work lists: bin
                                   // w % kNarrowBins holds world w's hull-hull survivors
                                   // from its front and hull-plane survivors from its back
     int32_t *satWorkCount;        // [kNarrowBins][kBinStride] per-bin counters: [0] hull-hull,
@@ -162,9 +178,9 @@ struct PhysArgs {
     // tail (integrating substep s + 1) filters into set (s + 1) % 2.  The
     // node launches point satWork / satWorkCount at the set a kernel reads
     // and nextSatWork / nextSatWorkCount at the set it fills or resets.
-    struct SatWork *satWorkSet[2];
+    struct PackedSatWork *satWorkSet[2];
     int32_t *satWorkCountSet[2];
-    struct SatWork *nextSatWork;
+    struct PackedSatWork *nextSatWork;
     int32_t *nextSatWorkCount;
     ContactJob *hhJobs;           // [W * candCapacity] SAT verdict per satWork entry
     int32_t contactGrid;          // persistent contact-kernel grid (blocks)
