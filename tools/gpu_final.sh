@@ -12,7 +12,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -1 $O/gputest.log
 timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1 || { echo BENCHFAIL; tail -30 $O/bench.log; exit 2; }
 tail -1 $O/bench.log
-timeout -k 10 300 python -u bench.py --workload simple --no-cpu-executor > $O/simple.log 2>&1 || { echo SIMPLEFAIL; tail -30 $O/simple.log; exit 3; }
+timeout -k 10 300 python -u bench.py --workload simple > $O/simple.log 2>&1 || { echo SIMPLEFAIL; tail -30 $O/simple.log; exit 3; }
 tail -1 $O/simple.log
 timeout -k 10 400 python -u tools/bench_fvs.py > $O/fvs.log 2>&1 || { echo FVSFAIL; tail -30 $O/fvs.log; exit 4; }
 tail -1 $O/fvs.log
