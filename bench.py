@@ -60,12 +60,18 @@ BYTES = {
 NODE_KINDS = list(BYTES.keys()) + ["CustomParallelForNode", "ParallelForNode"]
 
 
-def pmc_traffic(kernel_node):
+def pmc_traffic(kernel_node, workload="collisions"):
     """HBM bytes per launch of the node's kernel from the committed rocprofv3
-    PMC passes (profiles/*_traffic.json, written by profiles/pmc_traffic.py:
-    FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE).  None if absent."""
+    PMC passes of the same workload (profiles/rNN_traffic.json for
+    collisions, profiles/rNN_<workload>_traffic.json otherwise, written by
+    profiles/pmc_traffic.py via profiles/collect.sh: FETCH_SIZE x 2 (gfx950
+    correction) + WRITE_SIZE; the latest round's file).  None if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))
+    import re
+    tag = "" if workload == "collisions" else workload + "_"
+    pat = re.compile(r"r\d+_" + tag + r"traffic\.json$")
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json"))
+                   if pat.search(os.path.basename(f)))
     if not files:
         return None
     try:
@@ -389,7 +395,7 @@ def main():
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": pmc_traffic(dom),
+            "traffic": pmc_traffic(dom, args.workload),
             "bytes_per_launch": int(nbytes), "ms_per_launch": round(ms, 4),
             "timed_launches": int(ev_n1 - ev_n0),
             "timing": ("a HIP event pair bound to the kernel (hipExtLaunchKernelGGL: kernel start to "

@@ -1,13 +1,14 @@
 #!/bin/bash
 # Round profile collection on the GPU box (run from the repo root):
-#   bash profiles/collect.sh rNN
+#   bash profiles/collect.sh rNN [workload]   (collisions by default; simple)
 # kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in separate PMC passes
 # (no sys/runtime trace with --pmc), each bounded by its own timeout; the
 # bench's default window (steps 131-330), summarised over its 200 steps.
 set -euo pipefail
 R=${1:-r01}
-OUT=$PWD/gpurun_out/prof_$R
-B="$PWD/bench.py --no-cpu-baseline --no-cpu-executor"
+WL=${2:-collisions}
+OUT=$PWD/gpurun_out/prof_$R${2:+_$2}
+B="$PWD/bench.py --no-cpu-baseline --no-cpu-executor --workload $WL"
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1
