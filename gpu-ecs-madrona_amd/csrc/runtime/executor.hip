@@ -389,6 +389,7 @@ static LaunchCtx makeLaunchCtx(Executor::Impl &I, Executor *exec)
     lc.nodeData = I.nodeDataDev;
     lc.serialNodes = I.cfg.serialNodes;
     if (const char *e = getenv("MADRONA_MW_WORLD_WAVE_LANES")) lc.worldWaveLanes = atoi(e);
+    if (const char *e = getenv("MADRONA_MW_FUSE_ARCHETYPES")) lc.fuseArchetypes = atoi(e);
     // opt-in: in the replayed graph the join costs more than the overlap
     // saves (DESIGN.md round-3 dead ends)
     const char *side = getenv("MADRONA_MW_SIDE_STREAM");

@@ -69,6 +69,10 @@ struct LaunchCtx {
     // wave per world (parallelForWorldKernel); env
     // MADRONA_MW_WORLD_WAVE_LANES overrides the default (0: never).
     int32_t worldWaveLanes = 256;
+    // Row nodes over several small tables launch once for all of them
+    // (parallelForWorldMultiKernel); env MADRONA_MW_FUSE_ARCHETYPES=0: one
+    // launch per archetype.
+    int32_t fuseArchetypes = 1;
     // A second stream of the executor for a node's independent kernels
     // (fork: record forkEvent on `stream`, the side stream waits on it; join:
     // record joinEvent on the side stream, `stream` waits on it).  Inside the
@@ -358,6 +362,18 @@ struct ColArgs {
     int32_t c[N > 0 ? N : 1];
 };
 
+// A row node's archetypes run by one world-wave launch
+// (parallelForWorldMultiKernel): up to kFusedArchetypes of them, in query
+// order, each with its query index and column indices.
+inline constexpr int32_t kFusedArchetypes = 4;
+template <int32_t N>
+struct MultiColArgs {
+    int32_t n;
+    int32_t arch[kFusedArchetypes];
+    int32_t queryArch[kFusedArchetypes];
+    ColArgs<N> cols[kFusedArchetypes];
+};
+
 // Launch helpers (csrc/runtime/executor.hip).
 void launchRowKernel(const void *kernel, LaunchCtx &lc, int32_t archetype, int32_t query_arch,
                      int32_t threads_per_invocation, int32_t items_per_invocation,
@@ -542,6 +558,46 @@ parallelForWorldKernel(const StateView *__restrict__ st_in, int32_t arch, int32_
         }
     }
 }
+
+// The same for every archetype of the query in one launch (all of them
+// small tables): each world's wave walks the archetypes in query order, so a
+// world's rows run in the order the per-archetype launches gave them (its
+// first archetype's rows, then the next one's), one launch instead of one per
+// archetype.
+template <typename ContextT, auto Fn, int32_t threads, int32_t items, typename... ComponentTs>
+__global__ void __launch_bounds__(256)
+parallelForWorldMultiKernel(const StateView *__restrict__ st_in, int32_t, int32_t,
+                            MultiColArgs<sizeof...(ComponentTs)> m)
+{
+    MW_TRACE_BLOCK(m.arch[0]);
+    StateView *st = const_cast<StateView *>(st_in);
+    const int32_t lane = (int32_t)(threadIdx.x & 63);
+    const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wv < st->numWorlds; wv += waves) {
+        const int32_t w = (int32_t)wv;
+        for (int32_t a = 0; a < m.n; a++) {
+            const int32_t arch = m.arch[a];
+            const int32_t query_arch = m.queryArch[a];
+            const int32_t cap = st->arch[arch].capacity;
+            const int32_t inv_per_world = (cap + items - 1) / items;
+            const int32_t lanes_per_world = inv_per_world * threads;
+            const int32_t n = st->arch[arch].numRows[w];
+            for (int32_t base = 0; base < lanes_per_world && (base / threads) * items < n; base += 64) {
+                const int32_t l = base + lane;
+                const int32_t first = (l / threads) * items;
+                if (l < lanes_per_world && first < n) {
+                    ContextT ctx = worldContext<ContextT>(st, w);
+#pragma unroll 1
+                    for (int32_t k = 0; k < items && first + k < n; k++) {
+                        ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k));
+                        invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, m.cols[a], w, first + k,
+                                                                std::index_sequence_for<ComponentTs...> {});
+                    }
+                }
+            }
+        }
+    }
+}
 #endif
 
 }
@@ -620,6 +676,36 @@ public:
                 (const void *)&detail::serialForKernel<ContextT, Fn, threads_per_invocation,
                                                        ComponentTs...>,
                 lc, threads_per_invocation, &self->query_);
+            return;
+        }
+        // every archetype a small table: one world-wave launch for all
+        const int32_t na = self->query_.numArchetypes;
+        bool all_small = na >= 2 && na <= kFusedArchetypes && lc.fuseArchetypes;
+        int32_t widest = 0;
+        for (int32_t a = 0; all_small && a < na; a++) {
+            const int32_t arch = self->query_.archetypes[a];
+            const int64_t lanes = (int64_t)(lc.view->arch[arch].capacity + items_per_invocation - 1) /
+                                  items_per_invocation * threads_per_invocation;
+            all_small = lanes <= lc.worldWaveLanes;
+            if (lc.view->arch[arch].capacity > lc.view->arch[self->query_.archetypes[widest]].capacity)
+                widest = a;
+        }
+        if (all_small) {
+            detail::MultiColArgs<sizeof...(ComponentTs)> m {};
+            m.n = na;
+            for (int32_t a = 0; a < na; a++) {
+                m.arch[a] = self->query_.archetypes[a];
+                m.queryArch[a] = a;
+                for (int32_t c = 0; c < (int32_t)sizeof...(ComponentTs); c++) {
+                    m.cols[a].c[c] = self->query_.cols[a][c];
+                }
+            }
+            detail::launchRowKernel(
+                (const void *)&detail::parallelForWorldMultiKernel<
+                    ContextT, Fn, threads_per_invocation, items_per_invocation, ComponentTs...>,
+                lc, self->query_.archetypes[widest], 0, threads_per_invocation, items_per_invocation,
+                &m, sizeof(m), true);
+            detail::launchStructuralCommit(lc);
             return;
         }
         for (int32_t a = 0; a < self->query_.numArchetypes; a++) {
