@@ -21,6 +21,7 @@
 #include <initializer_list>
 #include <memory>
 #include <stdexcept>
+#include <tuple>
 #include <type_traits>
 #include <vector>
 
@@ -745,10 +746,18 @@ public:
             const int32_t n = st->arch[arch].numRows[w];
             const int32_t *cols = self->query_.cols[a];
             [&]<size_t... Is>(std::index_sequence<Is...>) {
+                // the world's column bases, once per archetype (Fn's stores
+                // could alias the StateView, so the loop would reload them)
+                const auto bases = std::make_tuple(
+                    st->column<std::remove_const_t<ComponentTs>>(arch, cols[Is], w)...);
                 for (int32_t r = 0; r < n; r++) {
-                    for (int32_t t = 0; t < threads_per_invocation; t++) {
-                        mwGPU::detail::cpuInvocationLane = t;
-                        Fn(ctx, st->column<std::remove_const_t<ComponentTs>>(arch, cols[Is], w)[r]...);
+                    if constexpr (threads_per_invocation == 1) {
+                        Fn(ctx, std::get<Is>(bases)[r]...);
+                    } else {
+                        for (int32_t t = 0; t < threads_per_invocation; t++) {
+                            mwGPU::detail::cpuInvocationLane = t;
+                            Fn(ctx, std::get<Is>(bases)[r]...);
+                        }
                     }
                 }
             }(std::index_sequence_for<ComponentTs...> {});

@@ -87,6 +87,9 @@ def parse():
                    help="ticks launched back-to-back per host sync (the reference "
                         "benchmark runs all ticks in one go)")
     p.add_argument("--cpu-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--cpu-executor", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--no-cpu-executor", action="store_true",
+                   help="skip the framework's CPU back end leg")
     return p.parse_args()
 
 
@@ -97,6 +100,17 @@ def cpu_child(args):
     inits = {k: v[first:] for k, v in
              ol.gen_fvs_inits(first + args.cpu_worlds, args.dragons, args.knights, seed=0).items()}
     threads = max(1, args.cpu_threads)
+    if args.cpu_executor:
+        # the framework's CPU back end (libmadrona_cpu.so) on the same worlds
+        os.environ["MADRONA_MW_NO_TORCH"] = "1"
+        import madrona_mi355x as mw
+        sim = mw.FvsSim(args.cpu_worlds, inits, first_world=first, backend="cpu", num_workers=threads)
+        sim.step(args.preroll)
+        t0 = time.perf_counter()
+        sim.step(args.steps)
+        dt = time.perf_counter() - t0
+        print(json.dumps({"kind": "port", "seconds": dt, "threads": threads}))
+        return
     ref = ol.ReferenceFvs(inits, first_world_index=args.cpu_first_world)
     ref.lib.ref_fvs_step_mt.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
     ref.lib.ref_fvs_step_mt(ref.h, args.preroll, threads)
@@ -107,31 +121,43 @@ def cpu_child(args):
     print(json.dumps({"kind": "reference", "seconds": dt, "threads": threads, "alive": alive}))
 
 
-def cpu_baseline(args):
+def cpu_baselines(args, legs):
+    """CPU legs on the same tick window: "reference" = the reference's own ECS
+    (oracle/_ref), "executor" = the framework's CPU back end; with both, their
+    batches alternate over the same worlds (one stretch of host load)."""
     sys.path.insert(0, ROOT)
     from bench import cpu_model, usable_cores
     threads = args.cpu_threads if args.cpu_threads > 0 else usable_cores()
-    total_s, batches, t_wall = 0.0, 0, time.perf_counter()
-    while batches < args.cpu_max_batches and total_s < args.cpu_target_s:
-        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child",
-                            "--cpu-worlds", str(args.cpu_worlds), "--cpu-threads", str(threads),
-                            "--cpu-first-world", str(batches * args.cpu_worlds),
-                            "--steps", str(args.steps), "--preroll", str(args.preroll),
-                            "--dragons", str(args.dragons), "--knights", str(args.knights)],
-                           capture_output=True, text=True, timeout=1200)
-        if r.returncode != 0:
-            raise RuntimeError(f"cpu baseline child failed: {r.stderr[-2000:]}")
-        res = json.loads(r.stdout.strip().splitlines()[-1])
-        total_s += res["seconds"]
+    acc = {leg: 0.0 for leg in legs}
+    batches, t_wall = 0, time.perf_counter()
+    while batches < args.cpu_max_batches and min(acc.values()) < args.cpu_target_s:
+        for leg in legs:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child",
+                                "--cpu-worlds", str(args.cpu_worlds), "--cpu-threads", str(threads),
+                                "--cpu-first-world", str(batches * args.cpu_worlds),
+                                "--steps", str(args.steps), "--preroll", str(args.preroll),
+                                "--dragons", str(args.dragons), "--knights", str(args.knights)] +
+                               (["--cpu-executor"] if leg == "executor" else []),
+                               capture_output=True, text=True, timeout=1200)
+            if r.returncode != 0:
+                raise RuntimeError(f"cpu {leg} child failed: {r.stderr[-2000:]}")
+            acc[leg] += json.loads(r.stdout.strip().splitlines()[-1])["seconds"]
         batches += 1
     worlds = batches * args.cpu_worlds
-    return {"value": round(worlds * args.steps / total_s, 1), "unit": "env-steps/s",
-            "cores": threads, "cpu_model": cpu_model(), "kind": "reference",
-            "sample": f"fantasy_vs {batches} batches x {args.cpu_worlds} worlds (worlds 0-{worlds - 1}) "
-                      f"x ({args.dragons} dragons + {args.knights} knights), ticks "
-                      f"{args.preroll + 1}-{args.preroll + args.steps} (the GPU's timed window), "
-                      f"{threads} host threads pinned one per usable core, {total_s:.2f} s timed / "
-                      f"{time.perf_counter() - t_wall:.1f} s wall"}
+    wall = time.perf_counter() - t_wall
+    out = {}
+    for leg in legs:
+        out[leg] = {"value": round(worlds * args.steps / acc[leg], 1), "unit": "env-steps/s",
+                    "cores": threads, "cpu_model": cpu_model(),
+                    "kind": "reference" if leg == "reference" else "port",
+                    "sample": ("libmadrona_cpu.so: " if leg == "executor" else "")
+                              + f"fantasy_vs {batches} batches x {args.cpu_worlds} worlds (worlds 0-"
+                              f"{worlds - 1}) x ({args.dragons} dragons + {args.knights} knights), ticks "
+                              f"{args.preroll + 1}-{args.preroll + args.steps} (the GPU's timed window), "
+                              f"{threads} host threads pinned one per usable core, {acc[leg]:.2f} s timed"
+                              + (f"; batches alternated with the other leg over the same worlds, "
+                                 f"{wall:.1f} s wall for both" if len(legs) > 1 else f" / {wall:.1f} s wall")}
+    return out
 
 
 def main():
@@ -200,7 +226,11 @@ def main():
     launch_ms = (ms1 - ms0) / max(1, n1 - n0)
     nbytes = W * SYS_BYTES[dom_sys](nd_mean, nk_mean)
     achieved = nbytes / (launch_ms * 1e-3) / 1e9
-    cpu = None if args.no_cpu_baseline else cpu_baseline(args)
+    cpu = cpu_exec = None
+    if not args.no_cpu_baseline:
+        legs = ["reference"] + ([] if args.no_cpu_executor else ["executor"])
+        res = cpu_baselines(args, legs)
+        cpu, cpu_exec = res["reference"], res.get("executor")
     out = {
         "metric": "env-steps/sec (summed worlds)", "value": round(W * args.steps / elapsed, 1),
         "unit": "env-steps/s", "n_gpus": 1, "steps": args.steps, "warmup": args.preroll,
@@ -222,7 +252,7 @@ def main():
                      "bytes_per_launch": int(nbytes),
                      "bytes_model": f"{W} worlds x SYS_BYTES['{dom_sys}'] at the window's mean live "
                                     f"rows per world: {nd_mean:.1f} dragons, {nk_mean:.1f} knights"},
-        "cpu_baseline": cpu, "error_flags": flags,
+        "cpu_baseline": cpu, "cpu_executor": cpu_exec, "error_flags": flags,
         "nodes_ms_per_launch_preroll": {systems[i]: round(v, 4) for i, v in node_ms.items()},
         "live_rows_sampled_worlds": {"sampled_worlds": len(sampled),
                                      "at_init": [args.dragons, args.knights],
