@@ -167,6 +167,24 @@ def test_collisions_full_size_sampled_worlds():
                 assert _contacts_equal(ka[k], kb[k]), f"step {checkpoint} world {w}: contact {k}"
 
 
+def test_side_stream_plane_branch_is_bit_identical(monkeypatch):
+    # MADRONA_MW_SIDE_STREAM=1 runs the hull-plane kernel on a second stream
+    # beside SAT + contact clipping (a parallel branch of the step graph);
+    # every body and contact stays bit-identical to the single-stream step.
+    mw = _mw()
+    gcfg, _ = _cfg_pair()
+    pos, rot = gen_collisions_inits(16, 128, seed=6)
+    b = mw.CollisionsSim(16, pos, rot, gcfg)
+    monkeypatch.setenv("MADRONA_MW_SIDE_STREAM", "1")
+    a = mw.CollisionsSim(16, pos, rot, gcfg)
+    a.step(40)
+    b.step(40)
+    assert a.error_flags() == 0
+    for w in range(16):
+        assert a.bodies(w).tobytes() == b.bodies(w).tobytes()
+        assert a.contacts(w).tobytes() == b.contacts(w).tobytes()
+
+
 def test_live_node_timing_does_not_perturb_state():
     # set_timed_node splits the step graph at the named node kind and times
     # its launches with HIP events; state must stay bit-identical to an

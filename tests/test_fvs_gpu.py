@@ -86,3 +86,21 @@ def test_fvs_full_size_sampled_worlds():
         orcs[i].step(1200)
         for arch in (0, 1):
             assert sim.table(w, arch).tobytes() == orcs[i].table(0, arch).tobytes(), (w, arch)
+
+
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_fvs_fused_and_per_archetype_launches_match_oracle(monkeypatch, fuse):
+    # MADRONA_MW_FUSE_ARCHETYPES=1 (default): actionSelect / markDead run one
+    # world-wave launch over dragons and knights (parallelForWorldMultiKernel);
+    # 0: one launch per archetype.  Both bit-exact through the deaths.
+    monkeypatch.setenv("MADRONA_MW_FUSE_ARCHETYPES", fuse)
+    mw = _mw()
+    W = 5
+    inits = ol.gen_fvs_inits(W, 50, 200, seed=3)
+    sim = mw.FvsSim(W, inits)
+    orc = ol.OracleFvs(inits)
+    for t in range(1, 9):
+        sim.step(150)
+        orc.step(150)
+        assert sim.error_flags() == 0
+        _compare(sim, orc, range(W), f"fuse={fuse} tick {150 * t}")
