@@ -737,7 +737,7 @@ public:
     // 63-71) -- the world's matching rows in query order, rows counted when
     // each archetype's walk starts, structural ops immediate (world-serial).
     // A cooperative Fn runs once per invocation lane, lanes in order.
-    static void runWorld(RowForNode *self, CpuRunCtx &rc, int32_t w)
+    [[gnu::flatten]] static void runWorld(RowForNode *self, CpuRunCtx &rc, int32_t w)
     {
         ContextT ctx = detail::worldContext<ContextT>(rc.state, w, rc.mgr);
         StateView *st = rc.state;
