@@ -29,6 +29,12 @@ def make_sim(mw, env, worlds):
         sim = mw.CollisionsSim(worlds, pos, rot, g)
         sim.step(120)                 # the bench's settled contact regime
         return sim
+    if env == "simple":
+        g = mw.default_collisions_config(100, 4, 4096, 4096)
+        pos, rot = mw.gen_collisions_inits(worlds, 100, seed=0)
+        sim = mw.SimpleSim(worlds, pos, rot, g)
+        sim.step(120)                 # bench.py --workload simple's settled window
+        return sim
     if env == "fvs":
         from madrona_mi355x import gen_fvs_inits
         sim = mw.FvsSim(worlds, gen_fvs_inits(worlds, 50, 200, seed=0))
@@ -49,7 +55,7 @@ def time_kind(sim, kind, steps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--env", default="collisions", choices=("collisions", "fvs"))
+    ap.add_argument("--env", default="collisions", choices=("collisions", "simple", "fvs"))
     ap.add_argument("--worlds", type=int, default=8192)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--candidates", default="0,1,2,4,8,16")
