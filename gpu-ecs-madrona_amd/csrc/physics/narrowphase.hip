@@ -669,10 +669,9 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
         const int32_t off = blockExclusiveScan(packed, s_scan, &total);
         if (threadIdx.x == 0) {
             const int32_t thh = (total >> 10) & 1023, tpl = total >> 20;
-            s_base[0] = thh > 0 ? atomicAdd(binCounter(P, bin, 0), thh) : 0;
-            s_base[1] = tpl > 0 ? atomicAdd(binCounter(P, bin, 1), tpl) : 0;
-            // an overrun of the bin is refused and flagged (filterWorldOnWave)
-            s_base[2] = s_base[0] + thh > P.binCap || s_base[1] + tpl > P.binCap;
+            // one reservation in both lists; an overrun of the bin is
+            // refused and flagged (reserveBin, filterWorldOnWave)
+            s_base[2] = !reserveBin(binCounter(P, bin, 0), thh, tpl, P.binCap, s_base[0], s_base[1]);
             if (s_base[2]) atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardList << 8));
         }
         __syncthreads();

@@ -269,7 +269,24 @@ __device__ __forceinline__ BodyBox integrateBody(const PhysArgs &P, const BodyAr
 
 __device__ __forceinline__ int32_t *binCounter(const PhysArgs &P, int32_t bin, int32_t which)
 {
-    return P.satWorkCount + bin * kBinStride + which * (kBinStride / 2);
+    return P.satWorkCount + bin * kBinStride + which;
+}
+
+// One reservation in both lists of a bin: the two counts are the halves of
+// one 64-bit counter (hull-hull low, hull-plane high), so a single atomic
+// returns both bases at one point of the bin's reservation order.  The
+// hull-hull list grows up from the bin's front and the hull-plane list down
+// from its back; every reservation sees all earlier ones of both lists, so
+// refusing any whose two ends would cross (b_hh + n_hh + b_hp + n_hp >
+// binCap) keeps the two lists from ever overwriting each other.
+__device__ __forceinline__ bool reserveBin(int32_t *counts, int32_t n_hh, int32_t n_hp,
+                                           int32_t bin_cap, int32_t &b_hh, int32_t &b_hp)
+{
+    const unsigned long long add = ((unsigned long long)(uint32_t)n_hp << 32) | (uint32_t)n_hh;
+    const unsigned long long old = add ? atomicAdd((unsigned long long *)counts, add) : 0ull;
+    b_hh = (int32_t)(uint32_t)old;
+    b_hp = (int32_t)(uint32_t)(old >> 32);
+    return (int64_t)b_hh + n_hh + b_hp + n_hp <= (int64_t)bin_cap;
 }
 
 // Reset the counters of a list set (`counts`: satWorkCount or
@@ -278,7 +295,7 @@ __device__ __forceinline__ int32_t *binCounter(const PhysArgs &P, int32_t bin, i
 __device__ __forceinline__ void resetNarrowLists(int32_t *counts, int32_t tid, int32_t nthreads)
 {
     for (int32_t i = tid; i < 2 * kNarrowBins; i += nthreads)
-        counts[(i >> 1) * kBinStride + (i & 1) * (kBinStride / 2)] = 0;
+        counts[(i >> 1) * kBinStride + (i & 1)] = 0;
 }
 
 // Exclusive prefix of the bins' counts of list `which` into s_pre[0..64]
@@ -431,18 +448,16 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
             n_hp += __popcll(__ballot(keep && t == kHullPlane));
         }
     }
-    int32_t b_hh = 0, b_hp = 0;
-    if (lane == 0) {
-        b_hh = n_hh > 0 ? atomicAdd(counts, n_hh) : 0;
-        b_hp = n_hp > 0 ? atomicAdd(counts + kBinStride / 2, n_hp) : 0;
-    }
+    int32_t b_hh = 0, b_hp = 0, fits = 1;
+    if (lane == 0) fits = reserveBin(counts, n_hh, n_hp, P.binCap, b_hh, b_hp);
     b_hh = __shfl(b_hh, 0);
     b_hp = __shfl(b_hp, 0);
-    // Each list stays inside its bin whatever its counter says (the
+    fits = __shfl(fits, 0);
+    // The two lists stay inside their bin whatever the counter says (the
     // reservations fit by construction -- binCap = worlds per bin x
     // candCapacity -- while the counters were reset before this filter):
     // an overrun is refused and flagged, never written.
-    if (b_hh + n_hh > P.binCap || b_hp + n_hp > P.binCap) {
+    if (!fits) {
         if (lane == 0) {
             atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardList << 8));
             P.survCount[w] = 0;

@@ -170,7 +170,8 @@ struct PhysArgs {
                                   // w % kNarrowBins holds world w's hull-hull survivors
                                   // from its front and hull-plane survivors from its back
     int32_t *satWorkCount;        // [kNarrowBins][kBinStride] per-bin counters: [0] hull-hull,
-                                  // [kBinStride/2] hull-plane entries this substep; the
+                                  // [1] hull-plane entries this substep (one 64-bit
+                                  // counter, reserveBin); the
                                   // filter appends, the integrate kernel / fused solver
                                   // tail resets
     int32_t binCap;               // entries per bin (worlds per bin x candCapacity)
@@ -230,7 +231,7 @@ MW_INLINE int32_t numInternalNodes(int32_t num_leaves)   // broadphase.cpp:33-40
 
 // Narrowphase work-list bins (narrowphase.hip; world w in bin w % kNarrowBins).
 constexpr int32_t kNarrowBins = 64;
-constexpr int32_t kBinStride = 32;        // ints per bin: hull-hull at 0, hull-plane at 16
+constexpr int32_t kBinStride = 32;        // ints per bin (own cache lines): hull-hull at 0, hull-plane at 1 (one 64-bit counter)
 
 // Error flag bits (StateView::errorFlags)
 inline constexpr int32_t kErrIDStoreFull = 1;

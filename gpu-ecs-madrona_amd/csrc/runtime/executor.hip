@@ -157,12 +157,23 @@ __global__ void __launch_bounds__(kCommitThreads) structuralCommitKernel(CommitA
     }
 }
 
+// A graph with no committable table still advances the epoch after every
+// row node, so the next node's row-ordered makes wait on fresh marks.
+__global__ void __launch_bounds__(64) bumpMakeEpochKernel(StateView *st)
+{
+    if (threadIdx.x == 0 && st->makeEpoch) st->makeEpoch[0] = st->makeEpoch[0] + 1;
+}
+
 namespace detail {
 
 void launchStructuralCommit(LaunchCtx &lc)
 {
     const CommitArgs *A = lc.exec ? (const CommitArgs *)lc.exec->commitArgs() : nullptr;
-    if (!A || A->shape.capMax <= 0) return;
+    if (!A) return;
+    if (A->shape.capMax <= 0) {
+        MW_LAUNCH(bumpMakeEpochKernel, dim3(1), dim3(64), 0, (hipStream_t)lc.stream, A->st);
+        return;
+    }
     const size_t lds = commitSharedBytes(*A);
     MW_LAUNCH(structuralCommitKernel, dim3((uint32_t)A->grid), dim3(kCommitThreads), lds,
                        (hipStream_t)lc.stream, *A);

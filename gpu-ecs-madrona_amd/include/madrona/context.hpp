@@ -147,8 +147,18 @@ public:
     {}
 
     // Row-parallel mode (set by the row-parallel node kernels): the lane's
-    // position in the reference's serial walk, (query archetype << 24) | row.
-    MW_INLINE void setRowParallel(uint32_t row_key) { rowKey_ = row_key; seq_ = 0; }
+    // position in the reference's serial walk, (query archetype << 24) | row,
+    // the archetype the lane's row lives in and the node's query-component
+    // mask (queryComponentMask): get / getUnsafe of one of those components
+    // at another row is a cross-row access the serial walk would order and
+    // the row-parallel launch does not, so it raises kErrFlagCrossRow.
+    MW_INLINE void setRowParallel(uint32_t row_key, int32_t own_arch = -1, uint64_t query_mask = 0)
+    {
+        rowKey_ = row_key;
+        seq_ = 0;
+        ownArch_ = own_arch;
+        queryMask_ = query_mask;
+    }
     // The lane's wave index among the waves covering this world's rows, the
     // world's finished-wave marks (StateView::makeTurn) and the node's epoch.
     MW_INLINE void setMakeTurn(int32_t *marks, int32_t chunk, int32_t epoch)
@@ -223,6 +233,7 @@ protected:
     MW_INLINE uint64_t nextAppendKey() { return ((uint64_t)rowKey_ << 32) | ((uint64_t)(seq_++ & 0xFFFFu) << 16); }
     MW_INLINE Entity lockedAcquire(int32_t arch, int32_t row);
     MW_INLINE void raiseFlag(int32_t bit);
+    template <typename ComponentT> MW_INLINE void checkCrossRow(Loc loc);
     template <typename Fn> MW_INLINE void runJob(Fn &fn);
     MW_INLINE void drainDeferredJobs();
     MW_INLINE bool jobRunning(uint64_t key) const
@@ -239,6 +250,8 @@ protected:
     StateManager *mgr_;
     uint32_t rowKey_ = kSerialRowKey;
     uint32_t seq_ = 0;
+    int32_t ownArch_ = -1;
+    uint64_t queryMask_ = 0;
     int32_t *turn_ = nullptr;
     int32_t turnChunk_ = 0;
     int32_t turnEpoch_ = 0;
@@ -271,11 +284,19 @@ public:
 // covering the world's rows has finished (StateView::makeTurn: each wave
 // marks itself done with the node's epoch -- a count would also count higher
 // waves that finished first).  The IDs are therefore the same run to run,
-// and the reference's when every row makes at most one entity (its serial
-// walk hands them out in row order).  Lower waves are dispatched before
+// and the reference's when every row makes at most one entity and the node
+// walks one row per invocation (its serial walk hands them out in row
+// order).  With items_per_invocation = k > 1 a wave's lanes take IDs in
+// lockstep per item -- rows 0, k, 2k, ... first, then 1, k + 1, ... -- so
+// the IDs are deterministic but not in row order; the rows themselves still
+// land in the reference's order (the ordered commit sorts the append keys).
+// Lower waves are dispatched before
 // higher ones and never wait on them, so the wait always ends.  Without the
-// marks (other callers, worlds past kMakeTurnWaves waves) waves go through a
-// per-world lock.
+// marks (other callers, worlds past kMakeTurnWaves waves) waves go through
+// the per-world lock alone.  The ordered path takes the same lock after its
+// turn: a world whose walked table spans more than kMakeTurnWaves waves
+// mixes ordered and unordered waves, and a turn wait that timed out must
+// still not race another wave inside the ID store.
 MW_INLINE bool lowerWavesDone(const int32_t *marks, int32_t chunk, int32_t epoch)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -310,16 +331,13 @@ MW_INLINE Entity Context::lockedAcquire(int32_t arch, int32_t row)
                     }
                 }
                 made_ = true;
-                e = ids.acquire(ids.st->worldCache);
-                if (e.id >= 0) ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
-            } else {
-                while (atomicCAS(&ids.st->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
-                __threadfence();
-                e = ids.acquire(ids.st->worldCache);
-                if (e.id >= 0) ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
-                __threadfence();
-                atomicExch(&ids.st->lock, 0);
             }
+            while (atomicCAS(&ids.st->lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
+            __threadfence();
+            e = ids.acquire(ids.st->worldCache);
+            if (e.id >= 0) ids.nodes[e.id].val = Loc { (uint32_t)arch, row };
+            __threadfence();
+            atomicExch(&ids.st->lock, 0);
         }
         pending &= pending - 1;
     }
@@ -471,9 +489,41 @@ MW_INLINE void Context::resetTmpAlloc()
 #endif
 }
 
+// One bit per component type (its type key mod 64): the components a
+// row-parallel node's query iterates (the Entity column is the engine's).
+template <typename ComponentT>
+constexpr MW_INLINE uint64_t componentBit()
+{
+    return std::is_same_v<std::remove_cv_t<ComponentT>, Entity> ? 0
+               : (1ull << (typeKey<std::remove_cv_t<ComponentT>>() & 63));
+}
+
+template <typename... ComponentTs>
+constexpr MW_INLINE uint64_t queryComponentMask()
+{
+    return (uint64_t(0) | ... | componentBit<ComponentTs>());
+}
+
+template <typename ComponentT>
+MW_INLINE void Context::checkCrossRow(Loc loc)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Another lane of the same launch owns that row and may be writing it
+    // (the reference walks the world's rows serially, taskgraph.inl:63-71):
+    // flag it so an unported world fails loudly instead of racing.
+    if ((queryMask_ & componentBit<ComponentT>()) != 0 && rowParallel() &&
+        ((int32_t)loc.archetype != ownArch_ || loc.row != (int32_t)(rowKey_ & 0xFFFFFFu))) {
+        raiseFlag(kErrFlagCrossRow);
+    }
+#else
+    (void)loc;
+#endif
+}
+
 template <typename ComponentT>
 MW_INLINE ResultRef<ComponentT> Context::get(Loc loc)
 {
+    checkCrossRow<ComponentT>(loc);
     int32_t col = state_->findColumn(loc.archetype, typeKey<ComponentT>());
     if (col < 0) return ResultRef<ComponentT>(nullptr);
     return ResultRef<ComponentT>(&rowRef(state_->column<ComponentT>(loc.archetype, col, world_), loc.row));
@@ -497,6 +547,7 @@ MW_INLINE ComponentT &Context::getUnsafe(int32_t e_id)
 template <typename ComponentT>
 MW_INLINE ComponentT &Context::getUnsafe(Loc loc)
 {
+    checkCrossRow<ComponentT>(loc);
     int32_t col = state_->findColumn(loc.archetype, typeKey<ComponentT>());
     return rowRef(state_->column<ComponentT>(loc.archetype, col, world_), loc.row);
 }

@@ -238,6 +238,7 @@ inline constexpr int32_t kErrFlagDeferredFull = 1 << 18;   // deferred destroy l
 inline constexpr int32_t kErrFlagRowParallelOp = 1 << 19;  // op not available in a row-parallel node
 inline constexpr int32_t kErrFlagCommitLimit = 1 << 20;    // archetype too large for the ordered commit
 inline constexpr int32_t kErrFlagMakeOrder = 1 << 22;      // a row-parallel make gave up waiting for its turn
+inline constexpr int32_t kErrFlagCrossRow = 1 << 23;       // row-parallel get/getUnsafe of a query component at another row
 
 // Ordered structural commit (see Context, row-parallel mode): an append key
 // orders a row made by a row-parallel lane exactly where the reference's

@@ -493,7 +493,8 @@ parallelForKernel(const StateView *__restrict__ st_in, int32_t arch, int32_t que
             if (marks && chunk < kMakeTurnWaves) ctx.setMakeTurn(marks, (int32_t)chunk, epoch);
 #pragma unroll 1
             for (int32_t k = 0; k < items && first + k < n; k++) {
-                ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k));
+                ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k), arch,
+                                   queryComponentMask<ComponentTs...>());
                 invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, first + k,
                                                         std::index_sequence_for<ComponentTs...> {});
             }
@@ -551,7 +552,8 @@ parallelForWorldKernel(const StateView *__restrict__ st_in, int32_t arch, int32_
                 ContextT ctx = worldContext<ContextT>(st, w);
 #pragma unroll 1
                 for (int32_t k = 0; k < items && first + k < n; k++) {
-                    ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k));
+                    ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k), arch,
+                                       queryComponentMask<ComponentTs...>());
                     invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, first + k,
                                                             std::index_sequence_for<ComponentTs...> {});
                 }
@@ -590,7 +592,8 @@ parallelForWorldMultiKernel(const StateView *__restrict__ st_in, int32_t, int32_
                     ContextT ctx = worldContext<ContextT>(st, w);
 #pragma unroll 1
                     for (int32_t k = 0; k < items && first + k < n; k++) {
-                        ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k));
+                        ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k), arch,
+                                           queryComponentMask<ComponentTs...>());
                         invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, m.cols[a], w, first + k,
                                                                 std::index_sequence_for<ComponentTs...> {});
                     }

@@ -281,7 +281,10 @@ ERR_BITS = {1: "id store full", 2: "table full", 4: "candidate overflow",
             64: "index guard (site in bits 8..15)", 128: "joint overflow",
             1 << 16: "job dropped", 1 << 17: "tmpAlloc arena full", 1 << 18: "deferred log full",
             1 << 19: "op not available in a row-parallel node", 1 << 20: "commit limit",
-            1 << 21: "static body written by a non-finite solve"}
+            1 << 21: "static body written by a non-finite solve",
+            1 << 22: "row-parallel make gave up waiting for its turn",
+            1 << 23: "row-parallel get/getUnsafe of a query component at another row"}
+ERR_CROSS_ROW = 1 << 23
 
 
 # DeviceLog (include/madrona/tracing.hpp; reference mw_gpu/tracing.hpp:30-41).

@@ -327,7 +327,60 @@ struct RefWorld {
     PhysWorld *world;
     Engine *ctx;
     TaskGraph *graph;
+    bool logCandidates = false;
+    std::vector<CandidateCollision> candidates;   // logCandidates mode only
 };
+
+// Mirror of TaskGraph's private layout (include/madrona/taskgraph.hpp:15-27,
+// 89-94: HeapArray<Node> sorted_nodes_, HeapArray<NodeData> node_datas_) so
+// a logged step can walk the built graph node by node, exactly as
+// TaskGraph::run does (src/core/taskgraph.cpp:117-122), without editing the
+// reference headers.
+struct TaskGraphMirror {
+    struct Node {
+        void (*fn)(NodeBase *, Context *);
+        uint32_t dataIDX;
+        uint32_t numChildren;
+    };
+    struct alignas(128) NodeData {
+        char userData[128];
+    };
+    Node *nodes;
+    CountT numNodes;
+    NodeData *datas;
+    CountT numDatas;
+};
+static_assert(sizeof(TaskGraphMirror) == sizeof(TaskGraph));
+
+// One step of a logged world: TaskGraph::run's loop, plus a read-only copy
+// of the CandidateTemporary rows at the first node boundary where the table
+// is non-empty.  Only findOverlapping appends to it and only the
+// ClearTmpNode<CandidateTemporary> of setupSubstepTasks
+// (src/physics/physics.cpp:1184-1185) empties it (Table::clear,
+// src/common/table.cpp:83-86), so that copy is the step's full candidate
+// list in emission order.  Nothing is written to world state.
+static void runLogged(RefWorld *rw)
+{
+    auto *g = (TaskGraphMirror *)rw->graph;
+    Engine &ctx = *rw->ctx;
+    auto q = ctx.query<CandidateCollision>();
+    bool done = false;
+    rw->candidates.clear();
+    for (CountT i = 0; i < g->numNodes; i++) {
+        if (!done) {
+            ctx.forEach(q, [&](CandidateCollision &c) {
+                rw->candidates.push_back(c);
+            });
+            done = !rw->candidates.empty();
+        }
+        const auto &n = g->nodes[i];
+        n.fn((NodeBase *)&g->datas[n.dataIDX].userData[0], rw->ctx);
+    }
+}
+
+// Set before ref_phys_create: worlds created afterwards log their candidate
+// pairs (ref_phys_set_candidate_log).  Off for the CPU baseline.
+static bool g_logCandidates = false;
 
 struct RefPhys {
     RefPhysConfig cfg;
@@ -402,6 +455,7 @@ static void * createWorlds(bool simple, int32_t num_worlds,
             init_rot + (size_t)w * cfg->numCubes * 4,
         };
         new (rw->world) PhysWorld(*rw->ctx, h->mgr, *cfg, init, simple, num_hulls);
+        rw->logCandidates = g_logCandidates && !simple;
 
         TaskGraph::Builder builder(*rw->ctx);
         if (simple) setupSimpleTasks(builder, cfg->numSubsteps);
@@ -478,7 +532,8 @@ MADRONA_EXPORT void ref_phys_step(void *handle, int32_t num_steps)
             // the last substep wrote.
             memset((void *)solver.contacts, 0xFF,
                    sizeof(Contact) * solver.maxContacts);
-            rw->graph->run(rw->ctx);
+            if (rw->logCandidates) runLogged(rw);
+            else rw->graph->run(rw->ctx);
         }
     }
 }
@@ -604,6 +659,26 @@ MADRONA_EXPORT int32_t ref_phys_read_contacts(void *handle, int32_t world,
     SolverData &solver = rw->ctx->getSingleton<SolverData>();
     memcpy(out, (void *)solver.contacts, sizeof(Contact) * solver.maxContacts);
     return (int32_t)solver.maxContacts;
+}
+
+MADRONA_EXPORT void ref_phys_set_candidate_log(int32_t on)
+{
+    g_logCandidates = on != 0;
+}
+
+// The last step's candidate pairs (Loc a, Loc b) in the reference's
+// findOverlapping emission order; -1 when the worlds were created without
+// the candidate log.  Returns the total count (copies at most cap).
+MADRONA_EXPORT int32_t ref_phys_read_candidates(void *handle, int32_t world,
+                                                void *out, int32_t cap)
+{
+    auto *h = (RefPhys *)handle;
+    RefWorld *rw = h->worlds[world];
+    if (!rw->logCandidates) return -1;
+    int32_t n = (int32_t)rw->candidates.size();
+    memcpy(out, rw->candidates.data(),
+           sizeof(CandidateCollision) * (size_t)(n < cap ? n : cap));
+    return n;
 }
 
 MADRONA_EXPORT int32_t ref_sizeof(int32_t what)

@@ -254,6 +254,11 @@ def load_ref(image="main"):
         lib.ref_phys_read_bodies.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
         lib.ref_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32] + [ctypes.c_void_p] * 4
         lib.ref_phys_read_contacts.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p]
+        if hasattr(lib, "ref_phys_read_candidates"):
+            lib.ref_phys_set_candidate_log.argtypes = [ctypes.c_int32]
+            lib.ref_phys_read_candidates.restype = ctypes.c_int32
+            lib.ref_phys_read_candidates.argtypes = [ctypes.c_void_p, ctypes.c_int32,
+                                                     ctypes.c_void_p, ctypes.c_int32]
         _REF[key] = lib
     return _REF[key]
 
@@ -331,10 +336,15 @@ class OracleSimple(OraclePhys):
 
 
 class ReferencePhys:
-    """The reference itself (oracle/_ref/libmadrona_ref.so)."""
+    """The reference itself (oracle/_ref/libmadrona_ref.so).
 
-    def __init__(self, cfg, pos, rot, hulls=None):
+    log_candidates: add the harness's read-only candidate log node after the
+    reference broadphase (oracle/ref_harness.cpp setupTasks) so candidates()
+    returns each step's pairs; off by default (the CPU baseline)."""
+
+    def __init__(self, cfg, pos, rot, hulls=None, log_candidates=False):
         self.lib = load_ref()
+        self.lib.ref_phys_set_candidate_log(1 if log_candidates else 0)
         self.cfg = cfg
         self.num_worlds = pos.shape[0]
         self.nb = cfg.numCubes + 1
@@ -346,9 +356,20 @@ class ReferencePhys:
         else:
             self.h = self.lib.ref_phys_create_hulls(self.num_worlds, ctypes.byref(cfg),
                                                     _vp(self._pos), _vp(self._rot), *hulls.args())
+        self.lib.ref_phys_set_candidate_log(0)
 
     def step(self, n=1):
         self.lib.ref_phys_step(self.h, n)
+
+    def candidates(self, w, cap=1 << 16):
+        """The last step's candidate pairs as (n, 4) int32 rows (Loc a, Loc b),
+        the layout of OraclePhys.candidates; needs log_candidates=True."""
+        out = np.zeros((cap, 4), np.int32)
+        n = self.lib.ref_phys_read_candidates(self.h, w, _vp(out), cap)
+        if n < 0:
+            raise RuntimeError("ReferencePhys created without log_candidates")
+        assert n <= cap
+        return out[:n]
 
     def bodies(self, w):
         out = np.zeros(self.nb, BODY_DTYPE)

@@ -167,6 +167,41 @@ def test_collisions_full_size_sampled_worlds():
                 assert _contacts_equal(ka[k], kb[k]), f"step {checkpoint} world {w}: contact {k}"
 
 
+def test_collisions_full_size_vs_reference_window():
+    # BASELINE configs[2] at full size (8192 worlds) against the fixtures
+    # the reference itself wrote for worlds 0, 1, 4095 and 8191 at steps
+    # 130, 145 (the driver's timed steps 126-145) and 330 (the end of
+    # bench.py's default window): bodies, candidate pairs and the last
+    # substep's contacts, bit for bit (tests/golden/make_golden.py
+    # make_window).
+    import os
+    from oracle_lib import BODY_DTYPE, CONTACT_DTYPE
+    mw = _mw()
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "collisions_window_ref.npz"),
+                allow_pickle=False)
+    worlds = [int(w) for w in g["worlds"]]
+    W = int(g["num_worlds"])
+    gcfg, _ = _cfg_pair(max_contacts=int(g["cfg"][2]))
+    pos, rot = mw.gen_collisions_inits(W, 128, seed=0)
+    assert pos[worlds].tobytes() == g["init_pos"].tobytes()
+    sim = mw.CollisionsSim(W, pos, rot, gcfg)
+    done = 0
+    for step in (int(x) for x in g["snap_steps"]):
+        sim.step(step - done)
+        done = step
+        assert sim.error_flags() == 0, mw.ERR_BITS
+        for i, w in enumerate(worlds):
+            want = g[f"bodies_{step}_{i}"].view(BODY_DTYPE)
+            d = _diff(sim.bodies(w), want)
+            assert d is None, f"step {step} world {w}: {d}"
+            assert sim.candidates(w).tobytes() == g[f"candidates_{step}_{i}"].tobytes(), (step, w)
+            raw = g[f"contacts_{step}_{i}"].view(CONTACT_DTYPE).reshape(-1)
+            got = sim.contacts(w)
+            assert 0 < len(got) <= len(raw), (step, w, len(got), len(raw))
+            for k in range(len(got)):
+                assert _contacts_equal(got[k], raw[k]), f"step {step} world {w}: contact {k}"
+
+
 def test_side_stream_plane_branch_is_bit_identical(monkeypatch):
     # MADRONA_MW_SIDE_STREAM=1 runs the hull-plane kernel on a second stream
     # beside SAT + contact clipping (a parallel branch of the step graph);

@@ -68,15 +68,22 @@ def test_serial_nodes_many_worlds_sampled():
         assert sim.sparks(w).tobytes() == ref.sparks(0).tobytes(), f"world {w}: sparks differ"
 
 
-def test_row_parallel_mode_diverges_as_documented():
-    """Default mode: lanes of one world run concurrently, so the carried
-    running hash and the cross-row flow are not the serial walk's.  This is
-    the documented contract: such bodies need serial_nodes or
-    WorldSerialForNode."""
+def test_row_parallel_mode_raises_cross_row_flag():
+    """Default mode: lanes of one world run concurrently, so a row reading or
+    writing another row of a component its node iterates (flowSystem's
+    ctx.get<Cell>(c.next)) races with that row's own lane.  Such a world
+    fails loudly: kErrFlagCrossRow is raised on the first step
+    (Context::checkCrossRow), and its state is not the serial walk's.  The
+    contract: such bodies need serial_nodes or
+    WorldSerialForNode, which stay flag-free (the tests above)."""
+    import madrona_mi355x as mw
     W = 4
     sim, ref = cl.CrossSim(W), cl.RefCross(W)
-    diverged = False
-    for _ in range(5):
+    sim.step()
+    ref.step()
+    assert sim.error_flags() & mw.ERR_CROSS_ROW, sim.error_flags()
+    diverged = any(not cl.worlds_equal(sim, ref, w) for w in range(W))
+    for _ in range(4):
         sim.step()
         ref.step()
         diverged |= any(not cl.worlds_equal(sim, ref, w) for w in range(W))

@@ -67,3 +67,26 @@ def test_exported_tensor_zero_copy_dlpack():
     after = view.clone()            # ordered after the steps on torch's stream
     torch.cuda.synchronize()
     assert after.cpu().numpy().tobytes() == np.array(sim.exported_array(2, np.float32)).tobytes()
+
+
+def test_madrona_python_module_on_hip_memory():
+    # The reference's import name over HIP memory: a torch tensor on the
+    # device round-trips zero-copy, and CudaSync.wait orders a consumer
+    # stream after the executor's enqueued steps.
+    import madrona_python
+    import torch
+    a = torch.arange(1000, dtype=torch.int32, device="cuda")
+    t = madrona_python.Tensor(a)
+    assert t.is_on_gpu() and t.gpu_id() == a.device.index
+    b = t.to_torch()
+    assert b.device == a.device and b.data_ptr() == a.data_ptr()
+    b[7] = -1
+    assert int(a[7]) == -1
+    _, sim = _sim()
+    sim.step_async(2)
+    strm = torch.cuda.Stream()
+    madrona_python.CudaSync(sim).wait(strm.cuda_stream)
+    with torch.cuda.stream(strm):
+        ret = torch.from_numpy(sim.exported_array(2, np.float32)).to("cuda")
+    strm.synchronize()
+    assert ret.numel() == 4

@@ -74,21 +74,75 @@ def test_oracle_bit_exact_vs_golden_bodies_and_contacts():
                     assert contacts_equal(got_c[i], want_c[i]), (step, w, i)
 
 
+WINDOW = os.path.join(os.path.dirname(__file__), "golden", "collisions_window_ref.npz")
+
+
+def _contact_prefix_equal(got, raw_ref):
+    """Ours holds exactly the last substep's manifolds; the reference's array
+    holds them as a prefix (an earlier substep may have written more)."""
+    assert len(got) <= len(raw_ref), (len(got), len(raw_ref))
+    for i in range(len(got)):
+        if not contacts_equal(got[i], raw_ref[i]):
+            return i
+    return None
+
+
 @pytest.mark.skipif(not ref_available(), reason="reference build absent (GPU box)")
 def test_oracle_bit_exact_vs_live_reference():
+    # Every step through the end of bench.py's default window (131-330):
+    # bodies, the step's candidate pairs (harness candidate log), the last
+    # substep's contacts and the BVH.  Each world is compared up to its first
+    # manifold with an undefined reference value (DESIGN §4); the oracle
+    # counts them, and collisions worlds of this seed have none.
     cfg = default_phys_config(num_cubes=128, max_contacts=2048)
     pos, rot = gen_collisions_inits(2, 128, seed=7)
     orc = OraclePhys(cfg, pos, rot)
-    ref = ReferencePhys(cfg, pos, rot)
-    for step in range(60):
+    ref = ReferencePhys(cfg, pos, rot, log_candidates=True)
+    for step in range(330):
         orc.step()
         ref.step()
         for w in range(2):
+            assert orc.ub_manifolds(w) == 0, (step, w)
             assert orc.bodies(w).tobytes() == ref.bodies(w).tobytes(), (step, w)
-            n_o, a_o, p_o, s_o = orc.bvh(w)
-            n_r, a_r, p_r, s_r = ref.bvh(w)
-            assert n_o.tobytes() == n_r[:len(n_o)].tobytes()
-            assert a_o.tobytes() == a_r.tobytes()
+            assert orc.candidates(w).tobytes() == ref.candidates(w).tobytes(), (step, w)
+            raw = ref.contacts_raw(w)
+            raw = raw[raw["ref"][:, 0] != 0xFFFFFFFF]
+            assert _contact_prefix_equal(orc.contacts(w), raw) is None, (step, w)
+            if step % 10 == 0:
+                n_o, a_o, p_o, s_o = orc.bvh(w)
+                n_r, a_r, p_r, s_r = ref.bvh(w)
+                assert n_o.tobytes() == n_r[:len(n_o)].tobytes()
+                assert a_o.tobytes() == a_r.tobytes()
+
+
+def test_oracle_bit_exact_vs_reference_window_golden():
+    # BASELINE configs[2]'s own worlds (0, 1, 4095, 8191 of 8192, seed 0) at
+    # steps 130 / 145 / 330, the bench's timed windows, against fixtures the
+    # reference wrote (tests/golden/make_golden.py make_window).
+    g = np.load(WINDOW, allow_pickle=False)
+    worlds = [int(w) for w in g["worlds"]]
+    pos, rot = gen_collisions_inits(int(g["num_worlds"]), 128, seed=0)
+    assert pos[worlds].tobytes() == g["init_pos"].tobytes()
+    assert rot[worlds].tobytes() == g["init_rot"].tobytes()
+    ci = g["cfg"]
+    cfg = default_phys_config(num_cubes=int(ci[0]), num_substeps=int(ci[1]),
+                              max_contacts=int(ci[2]))
+    orc = OraclePhys(cfg, g["init_pos"], g["init_rot"])
+    done = 0
+    for step in g["snap_steps"]:
+        step = int(step)
+        orc.step(step - done, 4)
+        done = step
+        for i in range(len(worlds)):
+            # no undefined-manifold value in these worlds through step 330
+            assert orc.ub_manifolds(i) == 0, (step, worlds[i])
+            want = g[f"bodies_{step}_{i}"].view(BODY_DTYPE)
+            assert orc.bodies(i).tobytes() == want.tobytes(), (step, worlds[i])
+            assert orc.candidates(i).tobytes() == g[f"candidates_{step}_{i}"].tobytes()
+            raw = g[f"contacts_{step}_{i}"].view(CONTACT_DTYPE).reshape(-1)
+            got = orc.contacts(i)
+            assert len(got) > 0
+            assert _contact_prefix_equal(got, raw) is None, (step, worlds[i])
 
 
 def test_oracle_small_world_counts_and_threads_agree():

@@ -42,3 +42,14 @@ def test_pointer_view_and_deleter_release():
     del v
     gc.collect()
     assert len(mp._LIVE) == 0
+
+
+def test_madrona_python_import_name():
+    # A reference-side script: import madrona_python, Tensor(t).to_torch()
+    # (src/python/bindings.cpp:78-123), CudaSync present (:126-127).
+    import madrona_python
+    a = torch.arange(6, dtype=torch.float32).reshape(2, 3)
+    b = madrona_python.Tensor(a).to_torch()
+    assert b.data_ptr() == a.data_ptr() and torch.equal(a, b)
+    assert hasattr(madrona_python.CudaSync, "wait")
+    assert madrona_python.Tensor is Tensor
