@@ -38,10 +38,13 @@ sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E 8.0 TB/s spec
 
 # Algorithmic bytes each node moves per unit, per launch (SURVEY.md §8(d),
-# DESIGN.md §6): body = one physics body row, cand = one candidate pair,
-# contact = one contact manifold.  The solver node fuses solvePositions,
-# setVelocities and solveVelocities.  The overlap query's 116 B per visited
-# BVH node is not counted (lower bound).
+# DESIGN.md §3 "Roofline in bench.py"): body = one physics body row, cand =
+# one candidate pair, surv = one narrowphase survivor pair, contact = one
+# contact manifold; "fused" = the work a launch does only when it also runs
+# the next substep's integration + filter (SolverNode, substeps 0..S-2) or
+# the first substep's filter (NarrowphaseNode, substep 0), weighted by the
+# timed launches that did.  The overlap query's 116 B per visited BVH node
+# is not counted (lower bound).
 BYTES = {
     "UpdateLeafPositionsNode": {"body": 96 + 68},
     # whole BVH nodes read and written back (0.69 nodes of 116 B per body: the
@@ -54,33 +57,69 @@ BYTES = {
     # leaf AABB; per candidate: the pair (16 B) and its packed slots (8 B)
     "FindOverlappingNode": {"body": 80 + 4 + 4 + 8 + 12 + 4 + 4 + 24, "cand": 16 + 8},
     "SubstepRigidBodiesNode": {"body": 84 + 108},
-    "NarrowphaseNode": {"cand": 16 + 2 * 44, "contact": 112},
-    "SolverNode": {"body": 56 + 24, "contact": (112 + 2 * 92 + 2 * 28 + 16) + (112 + 2 * 100 + 2 * 24)},
+    # filter (substep 0 only): the candidate and both bodies' poses per
+    # candidate; SAT / plane: the packed work entry (16 B) and both bodies'
+    # poses (Position 12 + Rotation 16 + Scale 12 + ObjectID 4) per survivor
+    # pair; the manifold written per contact
+    "NarrowphaseNode": {"surv": 16 + 2 * 44, "contact": 112,
+                        "fused": {"cand": 16 + 2 * 44}},
+    # solverKernel (one wave per world): each body's image in once (Position
+    # 12, Rotation 16, Velocity 24, ObjectID 4, ResponseType 4) and out once
+    # (Position, Rotation, Velocity); per contact and per pass (positions,
+    # velocities) the 112-byte manifold and both bodies' read-only substep
+    # columns (positions: PreSolvePositional + SubstepPrevState, 2 x 56;
+    # velocities: PreSolvePositional + PreSolveVelocity, 2 x 52), lambdaN
+    # written (16), survivor info read and contact order written (4 + 4);
+    # fused tail: the next substep's integration (192 / body, as
+    # SubstepRigidBodiesNode) and narrowphase filter (104 / cand)
+    "SolverNode": {"body": 60 + 52,
+                   "contact": (112 + 2 * 56 + 16) + (112 + 2 * 52) + 4 + 4,
+                   "fused": {"body": 84 + 108, "cand": 16 + 2 * 44}},
 }
+
+
+def launch_bytes(node, units):
+    """Algorithmic bytes of one launch of `node` for `units` (per-launch
+    means; units["fused"] = fraction of launches that ran the fused work)."""
+    m = BYTES[node]
+    b = sum(v * units.get(u, 0.0) for u, v in m.items() if u != "fused")
+    b += units.get("fused", 0.0) * sum(v * units.get(u, 0.0) for u, v in m.get("fused", {}).items())
+    return b
+
+
 NODE_KINDS = list(BYTES.keys()) + ["CustomParallelForNode", "ParallelForNode"]
 
 
-def pmc_traffic(kernel_node, workload="collisions"):
+def pmc_traffic(kernel_node, workload="collisions", timed_steps=None):
     """HBM bytes per launch of the node's kernel from the committed rocprofv3
-    PMC passes of the same workload (profiles/rNN_traffic.json for
-    collisions, profiles/rNN_<workload>_traffic.json otherwise, written by
+    PMC passes of the same workload (profiles/rNN_traffic*.json for
+    collisions, profiles/rNN_<workload>_traffic*.json otherwise, written by
     profiles/pmc_traffic.py via profiles/collect.sh: FETCH_SIZE x 2 (gfx950
-    correction) + WRITE_SIZE; the latest round's file).  None if absent."""
+    correction) + WRITE_SIZE), from the latest file whose step window is
+    exactly `timed_steps` (the window this run timed).  (None, note) when no
+    committed profile covers that window."""
     import glob
     import re
     tag = "" if workload == "collisions" else workload + "_"
-    pat = re.compile(r"r\d+_" + tag + r"traffic\.json$")
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json"))
+    pat = re.compile(r"r\d+_" + tag + r"traffic(_w\d+-\d+)?\.json$")
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_traffic*.json"))
                    if pat.search(os.path.basename(f)))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            data = json.load(f)
+    seen = []
+    for path in reversed(files):
+        try:
+            with open(path) as f:
+                data = json.load(f)
+        except (OSError, ValueError):
+            continue
+        seen.append(f"{os.path.basename(path)}: {data.get('timed_steps')}")
+        if data.get("timed_steps") != timed_steps:
+            continue
         entry = data.get("nodes", {}).get(kernel_node)
-        return None if entry is None else entry["bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        return None
+        if entry is None or entry.get("bytes_per_launch") is None:
+            continue
+        return entry["bytes_per_launch"], f"profiles/{os.path.basename(path)}, steps {timed_steps}"
+    return None, (f"no committed PMC profile for steps {timed_steps} "
+                  f"(have: {'; '.join(seen) or 'none'})")
 
 
 def parse():
@@ -359,6 +398,8 @@ def main():
     for _ in range(args.warmup):
         step()
     ev_ms0, ev_n0 = sim.timed_node() if dom else (0.0, 0)
+    if dom:
+        sim.take_units()       # (syncs) units of the timed launches only
 
     # timed region: barrier + device sync on both sides (the framework's
     # stream is the only GPU work in this process), max over ranks
@@ -385,17 +426,32 @@ def main():
         if ev_n1 - ev_n0 <= 0:
             raise RuntimeError(f"bench: no timed launch of {dom} in {args.steps} steps")
         ms = (ev_ms1 - ev_ms0) / (ev_n1 - ev_n0)
-        cands, contacts = sim.counts()
-        units = {"body": W * (args.cubes + (2 if simple else 1)), "cand": float(cands.sum()),
-                 "contact": float(contacts.sum())}
-        nbytes = sum(BYTES[dom].get(u, 0) * units[u] for u in units)
+        # the work units of exactly the timed launches (their candidates,
+        # survivors and manifolds, summed on the device right after each
+        # timed launch; mw_phys_take_units)
+        n_l, u_cand, u_cont, n_fused, u_surv = sim.take_units()
+        if n_l != ev_n1 - ev_n0:
+            raise RuntimeError(f"bench: {n_l} unit probes for {ev_n1 - ev_n0} timed launches")
+        units = {"body": W * (args.cubes + (2 if simple else 1)), "cand": u_cand / n_l,
+                 "surv": u_surv / n_l, "contact": u_cont / n_l, "fused": n_fused / n_l}
+        nbytes = launch_bytes(dom, units)
         achieved = nbytes / (ms * 1e-3) / 1e9
-        step_bytes = sum(launches[n] * sum(BYTES[n].get(u, 0) * units[u] for u in units)
-                         for n in BYTES)
+        # whole step: every modelled node at the timed launches' mean units
+        # (NarrowphaseNode's survivors only when it was the timed node)
+        step_units = dict(units, fused=(args.substeps - 1) / args.substeps)
+        step_bytes = sum(launches[n] * launch_bytes(n, step_units) for n in BYTES
+                         if n not in ("SolverNode", "NarrowphaseNode"))
+        step_bytes += args.substeps * launch_bytes("SolverNode", step_units)
+        if dom == "NarrowphaseNode":
+            step_bytes += args.substeps * launch_bytes(
+                "NarrowphaseNode", dict(units, fused=1.0 / args.substeps))
+        timed_steps = f"{args.settle + args.warmup + 1}-{args.settle + args.warmup + args.steps}"
+        traffic, traffic_src = pmc_traffic(dom, args.workload, timed_steps)
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": pmc_traffic(dom, args.workload),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "bytes_per_launch": int(nbytes), "ms_per_launch": round(ms, 4),
             "timed_launches": int(ev_n1 - ev_n0),
             "timing": ("a HIP event pair bound to the kernel (hipExtLaunchKernelGGL: kernel start to "
@@ -404,10 +460,13 @@ def main():
                           f"every {args.timed_every}th timed step (the first of each run of "
                           f"{args.timed_every}; the step graph is split at that node in those "
                           "steps only, the others replay the unsplit graph)")),
+            "units_per_launch": {k: round(v, 3) for k, v in units.items()},
+            "units_source": (f"summed on the device after each of the {n_l} timed launches "
+                             "(mw_phys_take_units)"),
             "step_algorithmic_bytes": int(step_bytes),
             "step_achieved_gbs": round(step_bytes / (elapsed / args.steps) / 1e9, 2),
-            "mean_candidates_per_world": round(float(cands.mean()), 1),
-            "mean_contacts_per_world": round(float(contacts.mean()), 1),
+            "mean_candidates_per_world": round(units["cand"] / W, 1),
+            "mean_contacts_per_world": round(units["contact"] / W, 1),
         }
 
     cpu = cpu_exec = None

@@ -23,6 +23,7 @@
 
 #include "../runtime/hip_launch.hpp"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -206,6 +207,66 @@ MW_PHYS_NODE(FindOverlappingNode,
         MW_LAUNCH(findOverlapsKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
                   findOverlapsSharedBytes(P), stream, P);)
 
+// Work units of a live-timed launch (PhysArgs::unitAccum): the probe sums
+// the worlds' candidates and this substep's contact manifolds -- after a
+// solver launch the solver's own count (lastNumContacts), after a
+// narrowphase launch the survivor slots that got a manifold -- and adds
+// them to the accumulators.  Launched only behind a node whose kernels are
+// bound to a timing event pair (hipx::tlTimed), outside that pair, so the
+// replayed (untimed) steps never run it.
+__global__ void __launch_bounds__(256) unitProbeKernel(PhysArgs P, int32_t from_solver,
+                                                       int32_t fused_extra)
+{
+    // one wave per world (grid-stride), one pair of atomics per wave
+    const int32_t lane = threadIdx.x & 63;
+    const int32_t waves = (int32_t)(gridDim.x * blockDim.x) >> 6;
+    unsigned long long cands = 0, contacts = 0, survivors = 0;
+    for (int32_t w = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < P.numWorlds;
+         w += waves) {
+        if (lane == 0) {
+            cands += (unsigned long long)P.lastNumCands[w];
+            if (from_solver) contacts += (unsigned long long)P.lastNumContacts[w];
+        }
+        if (!from_solver) {
+            const int32_t n = min(P.survCount[w], P.candCapacity);
+            if (lane == 0) survivors += (unsigned long long)n;
+            const uint32_t *info = P.survInfo + (size_t)w * P.candCapacity;
+            for (int32_t i = lane; i < n; i += 64) contacts += info[i] != kNoManifold;
+        }
+    }
+#pragma unroll
+    for (int32_t o = 32; o > 0; o >>= 1) {
+        cands += __shfl_down(cands, o, 64);
+        contacts += __shfl_down(contacts, o, 64);
+        survivors += __shfl_down(survivors, o, 64);
+    }
+    if (lane == 0) {
+        if (cands) atomicAdd(P.unitAccum + 1, cands);
+        if (contacts) atomicAdd(P.unitAccum + 2, contacts);
+        if (survivors) atomicAdd(P.unitAccum + 4, survivors);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicAdd(P.unitAccum + 0, 1ull);
+        if (fused_extra) atomicAdd(P.unitAccum + 3, 1ull);
+    }
+}
+
+static void probeUnits(const PhysArgs &P, LaunchCtx &lc, bool from_solver, bool fused_extra)
+{
+    if (!hipx::tlTimed || !P.unitAccum) return;
+    hipx::TimedLaunch *t = hipx::tlTimed;
+    hipx::tlTimed = nullptr;        // not part of the node's timed span
+    try {
+        MW_LAUNCH(unitProbeKernel, dim3((uint32_t)std::min((P.numWorlds + 3) / 4, 2048)), dim3(256), 0,
+                  (hipStream_t)lc.stream, P,
+                  from_solver ? 1 : 0, fused_extra ? 1 : 0);
+    } catch (...) {
+        hipx::tlTimed = t;
+        throw;
+    }
+    hipx::tlTimed = t;
+}
+
 // The narrowphase work lists come in two sets (PhysArgs::satWorkSet):
 // substep i's narrowphase reads set i % 2, and its filter for substep i + 1
 // (fused into substep i's solver) appends to set (i + 1) % 2.  The launch
@@ -297,6 +358,7 @@ struct NarrowphaseNode : PhysNodeBase {
                       dim3(kContactBlock), contactSharedBytes(Q), stream, Q);
         }
         if (side) MW_HIP_CHECK(hipStreamWaitEvent(stream, (hipEvent_t)lc.joinEvent, 0));
+        probeUnits(Q, lc, false, self->substep == 0);
     }
 };
 
@@ -325,6 +387,7 @@ struct SolverNode : PhysNodeBase {
         else
             MW_LAUNCH(solverKernel, grid, dim3(kSolverThreads), solverSharedBytes(Q),
                       (hipStream_t)lc.stream, Q, self->integrateNext);
+        probeUnits(Q, lc, true, self->integrateNext != 0);
     }
 };
 

@@ -265,6 +265,7 @@ void PhysicsModule::buildArgs(void *stream)
     P.solverPrevs = alloc<int32_t>((size_t)W * P.recStride, stream);
     P.lastNumContacts = alloc<int32_t>(W, stream);
     P.lastNumCands = alloc<int32_t>(W, stream);
+    P.unitAccum = alloc<unsigned long long>(kUnitSlots, stream);
 
 }
 

@@ -207,6 +207,13 @@ struct PhysArgs {
     int32_t *numJointRows;        // [W]
     JointConstraint *joints;      // [W][jointCapacity]
     int32_t *lastNumCands;        // [W] debug: candidates of the last step
+    // Work units of the live-timed launches (bench roofline): after every
+    // launch of a node being timed, unitProbeKernel adds [0] 1, [1] the
+    // candidates, [2] the contact manifolds of that launch's substep, [3] 1 if
+    // the launch also ran the next substep's integration + filter (solver) /
+    // the first substep's filter (narrowphase), [4] the narrowphase's
+    // survivor pairs.  mw_phys_take_units reads and zeroes them.
+    unsigned long long *unitAccum;  // [kUnitSlots]
 
     // LDS images that do not fit a workgroup live in global slabs instead
     // (null: the kernel stages them in LDS); physics.hip upload() decides.
@@ -222,6 +229,7 @@ struct PhysArgs {
 };
 
 inline constexpr uint32_t kNoManifold = 0xFFFF'FFFFu;
+inline constexpr int32_t kUnitSlots = 5;      // PhysArgs::unitAccum
 
 MW_INLINE int32_t numInternalNodes(int32_t num_leaves)   // broadphase.cpp:33-40
 {

@@ -157,8 +157,13 @@ static void copyOut(void *dst, const void *src, size_t bytes)
 {
     MW_HIP_OK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
 }
+static void zeroArena(void *dst, size_t bytes)
+{
+    MW_HIP_OK(hipMemset(dst, 0, bytes));
+}
 #else
 static void copyOut(void *dst, const void *src, size_t bytes) { memcpy(dst, src, bytes); }
+static void zeroArena(void *dst, size_t bytes) { memset(dst, 0, bytes); }
 
 [[noreturn]] static void gfx950Only(const char *what)
 {
@@ -688,6 +693,18 @@ extern "C" int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *co
             copyOut(contacts_out, P->lastNumContacts, 4 * P->numWorlds);
         }
         return P->numWorlds;
+    }, -1)
+}
+
+extern "C" int32_t mw_phys_take_units(mw_exec *exec, int64_t *out)
+{
+    MW_TRY({
+        exec->exec->sync();
+        phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
+        if (!P || !P->unitAccum || !out) return -1;
+        copyOut(out, P->unitAccum, phys::kUnitSlots * sizeof(int64_t));
+        zeroArena(P->unitAccum, phys::kUnitSlots * sizeof(int64_t));
+        return phys::kUnitSlots;
     }, -1)
 }
 

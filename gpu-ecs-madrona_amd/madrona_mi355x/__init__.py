@@ -128,6 +128,7 @@ def _declare(lib):
     lib.mw_phys_read_bvh.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_int32]
     lib.mw_phys_counts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.mw_phys_take_units.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     lib.mw_phys_kernel_variants.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
     lib.mw_copy_exported.restype = ctypes.c_int64
     lib.mw_copy_exported.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64]
@@ -202,7 +203,8 @@ C_ABI_SYMBOLS = (
     "mw_create", "mw_step", "mw_step_async", "mw_sync", "mw_get_exported", "mw_stream",
     "mw_destroy", "mw_last_error", "mw_num_worlds", "mw_error_flags", "mw_num_archetypes",
     "mw_read_column", "mw_column_info", "mw_phys_read_candidates", "mw_phys_read_contacts",
-    "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_copy_exported",
+    "mw_phys_read_bvh", "mw_phys_time_node", "mw_phys_counts", "mw_phys_take_units",
+    "mw_copy_exported",
     "mw_gen_collisions_inits", "mw_set_timed_node", "mw_set_timed_node_every", "mw_set_timed_node_index", "mw_timed_node_ms",
     "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
     "mw_device_free", "mw_gen_fvs_inits", "mw_stream_wait", "mw_load_hull",
@@ -663,6 +665,16 @@ class CollisionsSim(Executor):
                                k.ctypes.data_as(ctypes.c_void_p)) < 0:
             raise _err(self._lib)
         return c, k
+
+    def take_units(self):
+        """(timed launches, candidates, contact manifolds, launches with the
+        fused next-substep / first-substep filter work, narrowphase survivor
+        pairs) summed over the live-timed physics launches since the last
+        call; zeroes them."""
+        out = np.zeros(5, np.int64)
+        if self._lib.mw_phys_take_units(self.h, out.ctypes.data_as(ctypes.c_void_p)) < 0:
+            raise _err(self._lib)
+        return tuple(int(x) for x in out)
 
     def kernel_variants(self):
         """{kernel: True when it runs its global-image variant} (mw_create

@@ -214,6 +214,16 @@ int32_t mw_phys_read_bvh(mw_exec *exec, int32_t world, void *nodes_out,
 /* per-world candidate / contact counts of the last step / substep. */
 int32_t mw_phys_counts(mw_exec *exec, int32_t *cands_out, int32_t *contacts_out);
 
+/* Work units of the live-timed physics launches since the last call (then
+ * zeroed): out[0] timed SolverNode / NarrowphaseNode launches, out[1] their
+ * candidates summed over worlds, out[2] their substeps' contact manifolds,
+ * out[3] how many of them also ran the next substep's integration + filter
+ * (solver) or the first substep's filter (narrowphase), out[4] the
+ * narrowphase launches' survivor pairs.  bench.py's roofline byte model uses
+ * them so its units are the timed launches' own.  out holds 5 int64;
+ * returns 5, or -1 without physics.  No reference counterpart.             */
+int32_t mw_phys_take_units(mw_exec *exec, int64_t *out);
+
 /* Which variant of each LDS-staging physics kernel the executor runs (mw_create
  * picks it: a world / hull image that does not fit a workgroup's LDS moves to
  * a global slab, same results).  out[0..5] = 1 for: refit on the global node

@@ -76,6 +76,9 @@ def main():
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--timed-steps", default=None,
+                    help="the bench's timed step range these K steps are (e.g. 131-330); "
+                         "bench.py uses a profile for `traffic` only when it equals its own")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -115,7 +118,8 @@ def main():
         if e["bytes_per_launch"]:
             e["hbm_gbs"] = round(e["bytes_per_launch"] / (e["ms_per_launch"] * 1e-3) / 1e9, 1)
     json.dump({"source": "rocprofv3 kernel trace + PMC FETCH_SIZE (x2, gfx950) / WRITE_SIZE",
-               "steps": a.steps, "nodes": nodes}, open(a.out, "w"), indent=1)
+               "steps": a.steps, "timed_steps": a.timed_steps, "nodes": nodes},
+              open(a.out, "w"), indent=1)
     print(json.dumps(nodes, indent=1))
 
 

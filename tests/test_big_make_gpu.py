@@ -40,7 +40,25 @@ def _sim(W, backend):
     if ENV_NAME not in mw.env_names(backend):
         assert mw.load_env(so, backend) == 1
     inits = (Init * W)(*[Init(w) for w in range(W)])
-    return mw.Executor(ENV_NAME, W, Cfg(NUM_CELLS), inits, ctypes.sizeof(Init), backend=backend)
+    # up to 261 destroys per world per tick (the drop node)
+    kw = {"num_workers": 4} if backend == "cpu" else {"max_deferred_destroys": 1024}
+    return mw.Executor(ENV_NAME, W, Cfg(NUM_CELLS), inits, ctypes.sizeof(Init), backend=backend,
+                       **kw)
+
+
+def cpu_rows(W, ticks, worlds):
+    """The same worlds on the CPU back end (world-serial: the reference's
+    walk): per tick and world, the Cell and Mark component rows."""
+    ex = _sim(W, "cpu")
+    out = {}
+    for t in range(ticks):
+        ex.step()
+        assert ex.error_flags() == 0, t
+        for w in worlds:
+            out[f"cells_{t}_{w}"] = _rows(ex, ARCH_CELL, 1, w, CELL_DTYPE)
+            out[f"marks_{t}_{w}"] = _rows(ex, ARCH_MARK, 1, w, MARK_DTYPE)
+    ex.close()
+    return out
 
 
 def _makes(k, tick):
@@ -51,22 +69,38 @@ def _rows(ex, arch, col, w, dtype):
     return ex.read_column(arch, col, w, np.uint8, max_rows=8192).view(dtype)
 
 
+def test_big_make_cpu_backend_invariants():
+    # the CPU reference side of the GPU test below: every tick makes the
+    # expected marks, two ticks of marks stay alive, no flag
+    rows = cpu_rows(8, 4, range(0, 8, 7))
+    for t in range(4):
+        cells, marks = rows[f"cells_{t}_0"], rows[f"marks_{t}_0"]
+        assert len(cells) == NUM_CELLS
+        made_now = int(sum(_makes(k, t) for k in cells["k"]))
+        assert made_now == int((marks["born"] == t).sum()) > 4 * 64
+        assert set(np.unique(marks["born"]).tolist()) == set(range(max(0, t - 1), t + 1))
+
+
 @pytest.mark.gpu
-def test_big_table_row_parallel_makes_unique_ids_and_serial_rows():
+def test_big_table_row_parallel_makes_unique_ids_and_serial_rows(tmp_path):
+    import subprocess
+    import sys
     W, ticks = 64, 6
+    ref = str(tmp_path / "cpu.npz")
+    subprocess.run([sys.executable, os.path.abspath(__file__), str(W), str(ticks), ref],
+                   check=True, timeout=120)
+    ref = np.load(ref)
     gpu = _sim(W, "gpu")
-    cpu = _sim(W, "cpu")
     for t in range(ticks):
         gpu.step()
-        cpu.step()
-        assert gpu.error_flags() == 0 and cpu.error_flags() == 0, t
+        assert gpu.error_flags() == 0, (t, hex(gpu.error_flags()))
         for w in range(0, W, 7):
             cells = _rows(gpu, ARCH_CELL, 1, w, CELL_DTYPE)
-            cells_c = _rows(cpu, ARCH_CELL, 1, w, CELL_DTYPE)
+            cells_c = ref[f"cells_{t}_{w}"]
             assert len(cells) == NUM_CELLS
             assert cells[["k", "made"]].tobytes() == cells_c[["k", "made"]].tobytes(), (t, w)
             marks = _rows(gpu, ARCH_MARK, 1, w, MARK_DTYPE)
-            marks_c = _rows(cpu, ARCH_MARK, 1, w, MARK_DTYPE)
+            marks_c = ref[f"marks_{t}_{w}"]
             # the ordered commit lands the marks in the serial walk's order
             assert marks.tobytes() == marks_c.tobytes(), (t, w)
             made_now = int(sum(_makes(k, t) for k in cells["k"]))
@@ -81,4 +115,10 @@ def test_big_table_row_parallel_makes_unique_ids_and_serial_rows():
             fresh = cells[np.array([_makes(k, t) for k in cells["k"]])]
             assert all((int(g), int(i)) in live for g, i in zip(fresh["mark_gen"], fresh["mark_id"]))
     gpu.close()
-    cpu.close()
+
+
+if __name__ == "__main__":           # child of the GPU test: no GPU in this process
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "gpu-ecs-madrona_amd"))
+    W, ticks, path = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+    np.savez(path, **cpu_rows(W, ticks, range(0, W, 7)))
