@@ -29,3 +29,15 @@ def _build_oracle():
         import subprocess
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     yield
+
+
+def pytest_assertrepr_compare(config, op, left, right):
+    """A failed `a.tobytes() == b.tobytes()` on large buffers: report the
+    lengths and the first differing byte instead of pytest's difflib
+    explanation, which is quadratic and takes minutes on megabyte buffers
+    (long enough for a GPU box to take the run for hung)."""
+    if op == "==" and isinstance(left, (bytes, bytearray)) and isinstance(right, (bytes, bytearray)):
+        n = min(len(left), len(right))
+        first = next((i for i in range(n) if left[i] != right[i]), n)
+        return [f"byte buffers differ: len {len(left)} vs {len(right)}, first difference at byte {first}"]
+    return None

@@ -1,14 +1,17 @@
 """configs[3] on the one GPU a test box has: the sharded HIP executor.
 
 BASELINE.json configs[3] is 65 536 collisions worlds over 8 GPUs, rank g
-owning worlds [8192 g, 8192 (g + 1)) (madrona_mi355x/sharding.py).  Two gloo
-ranks stand in for GPUs 0 and 7: both create the HIP executor on device 0
-for their shard (inits drawn with the GLOBAL world index, first_world =
-8192 g), step it, and all-gather the per-world episode returns with
-sharding.gather_world_returns (the gloo form of the RCCL hand-off; RCCL
-itself cannot put two ranks on one device).  Checks:
-  * the gathered returns equal one process stepping both shards;
-  * sampled worlds of each shard, replayed by the oracle from their global
+owning worlds [8192 g, 8192 (g + 1)) (madrona_mi355x/sharding.py).  Eight
+gloo ranks stand in for the node's 8 GPUs: each creates the HIP executor on
+device 0 for its shard (inits drawn with the GLOBAL world index,
+first_world = 8192 g; 8 x ~4.8 GB of HBM), steps it, and all-gathers the
+per-world episode returns with sharding.gather_world_returns (the gloo form
+of the RCCL hand-off; RCCL itself cannot put two ranks on one device, so the
+RCCL nranks > 1 path stays unmeasured until the driver's 8-GPU run).
+Checks:
+  * the gathered 65 536 returns equal one process stepping all 8 shards in
+    order;
+  * sampled worlds of every shard, replayed by the oracle from their global
     index, are bit-exact (bodies, candidates, contacts).
 Reference: SURVEY.md §8(e); per-executor init src/mw/cuda_exec.cpp:1692-1763.
 """
@@ -21,7 +24,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 WORLDS_PER_RANK = 8192
-SHARDS = (0, 7)          # the ranks of an 8-GPU node these processes play
+SHARDS = tuple(range(8))  # the ranks of an 8-GPU node these processes play
 STEPS = 48
 SAMPLE = (0, 1, 4095, 8191)   # local indices checked against the oracle
 
@@ -53,10 +56,10 @@ def _check_sample(mw, sim, shard):
     g = _cfg(mw)
     o = PhysConfig(128, 4, g.delta_t, g.gravity_z, 4096, g.cube_inv_mass, g.cube_inv_inertia,
                    g.mu_s, g.mu_d)
-    first, _ = world_shard(shard, WORLDS_PER_RANK)
-    glob = [first + i for i in SAMPLE]
-    pos, rot = mw.gen_collisions_inits(glob[-1] + 1, 128, seed=0)
-    orc = OraclePhys(o, np.ascontiguousarray(pos[glob]), np.ascontiguousarray(rot[glob]))
+    first, n = world_shard(shard, WORLDS_PER_RANK)
+    pos, rot = mw.gen_collisions_inits(n, 128, seed=0, first_world=first)
+    sel = list(SAMPLE)
+    orc = OraclePhys(o, np.ascontiguousarray(pos[sel]), np.ascontiguousarray(rot[sel]))
     orc.step(STEPS, 4)
     for k, w in enumerate(SAMPLE):
         d = tc._diff(sim.bodies(w), orc.bodies(k))
@@ -95,18 +98,24 @@ def test_configs3_shards_on_one_gpu_gather_and_oracle():
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    n = len(SHARDS)
+    procs = [ctx.Process(target=_rank_main, args=(r, n, port, q)) for r in range(n)]
     for p in procs:
         p.start()
     got = {}
-    for _ in procs:
-        r, g = q.get(timeout=110)
-        got[r] = g
-    for p in procs:
-        p.join(timeout=30)
-        assert p.exitcode == 0
-    assert got[0].tobytes() == got[1].tobytes()
-    # one process running both shards, in global world order
+    try:
+        for _ in procs:
+            r, g = q.get(timeout=150)
+            got[r] = g
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert all(got[r].tobytes() == got[0].tobytes() for r in range(n))
+    assert got[0].size == n * WORLDS_PER_RANK
+    # one process running every shard, in global world order
     import madrona_mi355x as mw
     want = []
     for shard in SHARDS:
