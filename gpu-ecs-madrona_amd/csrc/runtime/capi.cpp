@@ -575,6 +575,11 @@ int32_t mw_num_nodes(mw_exec *exec)
     MW_TRY({ return exec->exec->numNodes(); }, -1)
 }
 
+int32_t mw_world_walk_runs(mw_exec *exec)
+{
+    MW_TRY({ return exec->exec->worldWalkRuns(); }, -1)
+}
+
 const char *mw_node_name(mw_exec *exec, int32_t node)
 {
     MW_TRY({ return exec->exec->nodeName(node); }, nullptr)

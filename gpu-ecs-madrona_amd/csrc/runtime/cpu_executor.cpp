@@ -512,6 +512,7 @@ int64_t Executor::readTrace(void *, int64_t, int64_t *) { return -1; }
 const char *Executor::traceFuncName(int32_t) { return nullptr; }
 
 int32_t Executor::numNodes() const { return impl_->graph.numNodes(); }
+int32_t Executor::worldWalkRuns() const { return 0; }
 
 const char *Executor::nodeName(int32_t node) const
 {

@@ -166,6 +166,20 @@ __global__ void __launch_bounds__(64) bumpMakeEpochKernel(StateView *st)
 
 namespace detail {
 
+void readDeviceWord(const void *kernel, void *host_out)
+{
+    void *dev = nullptr;
+    MW_HIP_CHECK(hipMalloc(&dev, 16));
+    void *args[] = { &dev };
+    const hipError_t e = hipLaunchKernel(kernel, dim3(1), dim3(1), args, 0, nullptr);
+    if (e != hipSuccess) {
+        (void)hipFree(dev);
+        hipx::hipFail(e, "readDeviceWord launch", __FILE__, __LINE__);
+    }
+    MW_HIP_CHECK(hipMemcpy(host_out, dev, 8, hipMemcpyDeviceToHost));
+    MW_HIP_CHECK(hipFree(dev));
+}
+
 void launchStructuralCommit(LaunchCtx &lc)
 {
     const CommitArgs *A = lc.exec ? (const CommitArgs *)lc.exec->commitArgs() : nullptr;
@@ -391,6 +405,25 @@ struct Executor::Impl {
     char *nodeDataDev = nullptr;
     // Ordered structural commit of row-parallel nodes.
     CommitArgs commit {};
+
+    // World walk (TaskGraph::NodeFns::walk, planned when the graph is set):
+    // per node 1 = walkable with walkKernel[i] / resumeKernel[i] and entries
+    // [walkOff[i], walkOff[i + 1]) of walkEntriesDev, 2 = a no-op that may sit
+    // inside a run (an elided reset), 0 = launched on its own.
+    bool walkEnabled = false;
+    std::vector<uint8_t> walkable;
+    std::vector<uint8_t> walkCommits;        // the node's entries include a commit point
+    std::vector<const void *> walkKernel;
+    std::vector<const void *> resumeKernel;
+    std::vector<int32_t> walkOff;
+    detail::WalkEntry *walkEntriesDev = nullptr;
+    int32_t *walkResume = nullptr;           // [W] commit point a world stopped at, -1
+    // worldResumeKernel's per-block global scratch (commit working set +
+    // move scratch) and grids
+    char *walkScratch = nullptr;
+    uint64_t walkPerBlock = 0;
+    uint64_t walkWsBytes = 0;
+    std::vector<std::pair<const void *, int32_t>> walkGrid;   // kernel -> grid
 };
 
 static LaunchCtx makeLaunchCtx(Executor::Impl &I, Executor *exec)
@@ -453,6 +486,9 @@ Executor::~Executor()
     if (impl_->hostRowsTotal) (void)hipHostFree(impl_->hostRowsTotal);
     if (impl_->nodeDataDev) (void)hipFree(impl_->nodeDataDev);
     if (impl_->commit.scratch) (void)hipFree(impl_->commit.scratch);
+    if (impl_->walkEntriesDev) (void)hipFree(impl_->walkEntriesDev);
+    if (impl_->walkScratch) (void)hipFree(impl_->walkScratch);
+    if (impl_->walkResume) (void)hipFree(impl_->walkResume);
     for (auto &e : impl_->exports) {
         (void)hipFree(e.buf);
         if (e.scanOwner) (void)hipFree(e.offsets);
@@ -681,20 +717,165 @@ static void launchNodeTimed(Executor::Impl &I, int32_t i, LaunchCtx &lc,
     if (t.start) MW_HIP_CHECK(hipEventRecord(stop, I.stream));
 }
 
+// World walk planning (before any capture: a node's walk plan may read a
+// device address back with a synchronous launch).  Opt-in,
+// MADRONA_MW_WORLD_WALK=1: on fantasy_vs the walk is 0.25 ms per tick against
+// 0.14 for the per-node launches -- the world functions are
+// called through pointers and compiled with the function ABI, the heaviest
+// (the caster's row code) at ~100 VGPRs, so the walk holds 4-5 waves per
+// SIMD where the per-node world-wave kernels hold 8.
+static void planWorldWalk(Executor::Impl &I, LaunchCtx &lc)
+{
+    const int32_t n = I.graph.numNodes();
+    I.walkable.assign(n, 0);
+    I.walkCommits.assign(n, 0);
+    I.walkKernel.assign(n, nullptr);
+    I.resumeKernel.assign(n, nullptr);
+    I.walkOff.assign(n + 1, 0);
+    if (const char *e = getenv("MADRONA_MW_WORLD_WALK")) I.walkEnabled = atoi(e) != 0;
+    std::vector<detail::WalkEntry> all;
+    for (int32_t i = 0; i < n; i++) {
+        I.walkOff[i] = (int32_t)all.size();
+        if (!I.walkEnabled) continue;
+        if (i < (int32_t)I.nodeSkip.size() && I.nodeSkip[i]) {
+            I.walkable[i] = 2;
+            continue;
+        }
+        const TaskGraph::NodeFns &f = I.graph.nodeFns(i);
+        if (!f.walk) continue;
+        detail::WalkEntry tmp[detail::kMaxWalkEntriesPerNode];
+        const void *kernels[2] = { nullptr, nullptr };
+        const int32_t ne = f.walk(I.graph.nodeState(i), lc, tmp, kernels);
+        if (ne <= 0 || ne > detail::kMaxWalkEntriesPerNode || !kernels[0] || !kernels[1]) continue;
+        I.walkable[i] = 1;
+        I.walkKernel[i] = kernels[0];
+        I.resumeKernel[i] = kernels[1];
+        for (int32_t k = 0; k < ne; k++) I.walkCommits[i] |= tmp[k].kind == detail::kWalkCommit;
+        all.insert(all.end(), tmp, tmp + ne);
+    }
+    I.walkOff[n] = (int32_t)all.size();
+    if (I.walkEntriesDev) {
+        MW_HIP_CHECK(hipFree(I.walkEntriesDev));
+        I.walkEntriesDev = nullptr;
+    }
+    if (all.empty()) return;
+    MW_HIP_CHECK(hipMalloc(&I.walkEntriesDev, sizeof(detail::WalkEntry) * all.size()));
+    MW_HIP_CHECK(hipMemcpy(I.walkEntriesDev, all.data(), sizeof(detail::WalkEntry) * all.size(),
+                           hipMemcpyHostToDevice));
+    if (!I.walkResume) {
+        MW_HIP_CHECK(hipMalloc(&I.walkResume, sizeof(int32_t) * std::max(I.cfg.numWorlds, 1)));
+        MW_HIP_CHECK(hipMemset(I.walkResume, 0xFF, sizeof(int32_t) * std::max(I.cfg.numWorlds, 1)));
+    }
+    // resident grids (one wave per block); the resume kernel's blocks each
+    // own a global scratch slab for the commit
+    const CommitArgs &A = I.commit;
+    I.walkWsBytes = (detail::commitWorkingBytes(A.shape) + 255) / 256 * 256;
+    I.walkPerBlock = I.walkWsBytes + (A.scratchPerBlock + 255) / 256 * 256;
+    int64_t max_resume = 1;
+    I.walkGrid.clear();
+    auto add_grid = [&](const void *k, bool resume) {
+        for (auto &g : I.walkGrid) {
+            if (g.first == k) return;
+        }
+        const int32_t per_cu = hipx::residentBlocks(k, resume ? "worldResumeKernel" : "worldWalkKernel", 64, 0);
+        int64_t grid = std::min<int64_t>(I.cfg.numWorlds, (int64_t)per_cu * std::max(I.numCUs, 1));
+        if (resume) {
+            // enough blocks for the usual handful of stopped worlds; slabs
+            // bounded to 256 MiB
+            grid = std::min<int64_t>(grid, std::max<int64_t>(1, (256ll << 20) / (int64_t)I.walkPerBlock));
+            max_resume = std::max(max_resume, grid);
+        }
+        I.walkGrid.push_back({ k, (int32_t)std::max<int64_t>(grid, 1) });
+    };
+    for (int32_t i = 0; i < n; i++) {
+        if (I.walkable[i] != 1) continue;
+        add_grid(I.walkKernel[i], false);
+        add_grid(I.resumeKernel[i], true);
+    }
+    if (I.walkScratch) {
+        MW_HIP_CHECK(hipFree(I.walkScratch));
+        I.walkScratch = nullptr;
+    }
+    MW_HIP_CHECK(hipMalloc(&I.walkScratch, std::max<size_t>(I.walkPerBlock * max_resume, 256)));
+}
+
+static int32_t walkGridOf(const Executor::Impl &I, const void *kernel)
+{
+    for (auto &g : I.walkGrid) {
+        if (g.first == kernel) return g.second;
+    }
+    return 1;
+}
+
+// One walk run: the walk over every world, then (if the run has commit
+// points) the resume pass over the worlds that stopped at one.
+static void launchWorldWalk(Executor::Impl &I, LaunchCtx &lc, int32_t b, int32_t e, bool commits)
+{
+    const void *walk = I.walkKernel[b], *resume = I.resumeKernel[b];
+    const detail::WalkEntry *entries = I.walkEntriesDev + I.walkOff[b];
+    int32_t n = I.walkOff[e] - I.walkOff[b];
+    StateView *st = lc.devState;
+    int32_t *res = I.walkResume;
+    {
+        void *args[] = { &entries, &n, &st, &res };
+        hipx::residentBlocks(walk, "worldWalkKernel", 64, 0);
+        MW_HIP_CHECK(hipx::launchKernel(walk, dim3((uint32_t)walkGridOf(I, walk)), dim3(64), args, 0, I.stream));
+        hipx::checkLaunched("worldWalkKernel");
+    }
+    if (!commits) return;
+    char *scratch = I.walkScratch;
+    uint64_t per_block = I.walkPerBlock, ws_bytes = I.walkWsBytes;
+    detail::CommitShape shape = I.commit.shape;
+    void *args[] = { &entries, &n, &st, &res, &scratch, &per_block, &shape, &ws_bytes };
+    hipx::residentBlocks(resume, "worldResumeKernel", 64, 0);
+    MW_HIP_CHECK(hipx::launchKernel(resume, dim3((uint32_t)walkGridOf(I, resume)), dim3(64), args, 0,
+                                    I.stream));
+    hipx::checkLaunched("worldResumeKernel");
+}
+
+// Nodes [b, e) in order: maximal runs of walkable nodes of one walk kernel
+// with at least two real nodes become one walk launch each; the rest are
+// launched node by node.  Tracing keeps per-node launches (its markers).
+static void launchRange(Executor::Impl &I, int32_t b, int32_t e, LaunchCtx &lc)
+{
+    int32_t k = b;
+    while (k < e) {
+        if (!I.trace && k < (int32_t)I.walkable.size() && I.walkable[k] == 1) {
+            const void *kern = I.walkKernel[k];
+            int32_t j = k, real = 0;
+            while (j < e && (I.walkable[j] == 2 || (I.walkable[j] == 1 && I.walkKernel[j] == kern))) {
+                real += I.walkable[j] == 1;
+                j++;
+            }
+            if (real >= 2) {
+                bool commits = false;
+                for (int32_t q = k; q < j; q++) commits |= I.walkCommits[q] != 0;
+                launchWorldWalk(I, lc, k, j, commits);
+                k = j;
+                continue;
+            }
+        }
+        launchNode(I, k, lc);
+        k++;
+    }
+}
+
 // One step's launch sequence: every node in sorted order, then the export
 // gathers.  Nodes of the timed kind are bracketed by their own event pair.
 static void launchStep(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
 {
     int32_t ev = 0;
     traceStepBegin(I);
+    int32_t start = 0;
     for (int32_t i = 0; i < I.graph.numNodes(); i++) {
         if (isTimed(I, i)) {
+            launchRange(I, start, i, lc);
             const auto &pr = timedPair(I, ev++);
             launchNodeTimed(I, i, lc, pr.first, pr.second);
-        } else {
-            launchNode(I, i, lc);
+            start = i + 1;
         }
     }
+    launchRange(I, start, I.graph.numNodes(), lc);
     launchExports(I, dv);
     traceStepEnd(I);
 }
@@ -742,7 +923,7 @@ static void captureSegments(Executor::Impl &I, LaunchCtx &lc, const StateView &d
             MW_HIP_CHECK(hipStreamBeginCapture(I.stream, hipStreamCaptureModeThreadLocal));
             try {
                 if (start == 0) traceStepBegin(I);
-                for (int32_t k = start; k < i; k++) launchNode(I, k, lc);
+                launchRange(I, start, i, lc);
                 if (last) {
                     launchExports(I, dv);
                     traceStepEnd(I);
@@ -800,6 +981,30 @@ static void applyLaunchConfigEnv(Executor::Impl &I)
 }
 
 int32_t Executor::numNodes() const { return impl_->graph.numNodes(); }
+
+int32_t Executor::worldWalkRuns() const
+{
+    const Impl &I = *impl_;
+    const int32_t n = (int32_t)I.walkable.size();
+    int32_t runs = 0, k = 0;
+    while (k < n) {
+        if (I.walkable[k] == 1) {
+            int32_t j = k, real = 0;
+            while (j < n && (I.walkable[j] == 2 ||
+                             (I.walkable[j] == 1 && I.walkKernel[j] == I.walkKernel[k]))) {
+                real += I.walkable[j] == 1;
+                j++;
+            }
+            if (real >= 2) {
+                runs++;
+                k = j;
+                continue;
+            }
+        }
+        k++;
+    }
+    return runs;
+}
 const char *Executor::nodeName(int32_t node) const
 {
     if (node < 0 || node >= impl_->graph.numNodes()) return nullptr;
@@ -870,6 +1075,7 @@ void Executor::setGraph(TaskGraph &&graph)
     applyLaunchConfigEnv(*impl_);
     const StateView &dv = impl_->mgr->deviceViewHost();
     LaunchCtx lc = makeLaunchCtx(*impl_, this);
+    planWorldWalk(*impl_, lc);
     if (impl_->cfg.useGraph) captureGraph(*impl_, lc, dv);
 }
 

@@ -161,6 +161,10 @@ public:
     const void *commitArgs() const;
 
     int32_t numNodes() const;
+    // World-walk launches per step (runs of world-local nodes walked by one
+    // persistent kernel; MADRONA_MW_WORLD_WALK=1 when the graph is set).
+    // 0 when off or on the CPU back end.
+    int32_t worldWalkRuns() const;
     const char *nodeName(int32_t node) const;
     int32_t nodeBlocksPerCU(int32_t node) const;
     void setNodeBlocksPerCU(int32_t node, int32_t blocks_per_cu);

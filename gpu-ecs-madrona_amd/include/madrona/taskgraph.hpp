@@ -17,6 +17,11 @@
 #include <madrona/optional.hpp>
 #include <madrona/tracing.hpp>
 
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#endif
+
+#include <cstring>
 #include <functional>
 #include <initializer_list>
 #include <memory>
@@ -44,6 +49,40 @@ private:
 };
 
 class Executor;
+
+// ---------------------------------------------------------------------------
+// World walk: the persistent megakernel of the reference
+// (src/mw/device/megakernel_impl.inl:29-55: each block walks the task graph,
+// dispatch(funcID) per node).  A run of consecutive world-local nodes -- row
+// nodes over small tables with their ordered commits, world-serial row nodes,
+// per-world nodes, fixed-count device nodes -- becomes ONE launch: a wave
+// takes a world and calls every node's world function for it in graph order
+// (device function pointers: the node kinds of a world are known only when
+// setupTasks runs, as the reference's are only known to its NVRTC build).
+// Worlds are independent, so the result is that of the per-node launches;
+// the launch floors and inter-kernel drains between the nodes go away.
+// ---------------------------------------------------------------------------
+namespace detail {
+inline constexpr int32_t kWalkParamBytes = 240;
+inline constexpr int32_t kMaxWalkEntriesPerNode = 2;
+struct WalkEntry;
+// What a world function gets besides its entry: the device state.
+struct WalkCtx {
+    StateView *st;
+};
+using WalkFn = void (*)(const WalkEntry &, const WalkCtx &, int32_t);
+// kind: a node's world function, or the ordered-commit point after a
+// row-parallel node.
+inline constexpr int32_t kWalkCall = 0;
+inline constexpr int32_t kWalkCommit = 1;
+struct alignas(16) WalkEntry {
+    WalkFn fn;                     // device address (same code object as the walk kernels)
+    int32_t kind;
+    int32_t pad;
+    char params[kWalkParamBytes];  // the node's launch arguments
+};
+static_assert(sizeof(WalkEntry) == 256);
+}
 
 // Everything a node's launch function needs.  Captured into a hipGraph, so a
 // launch must be a pure function of its node data and this struct.
@@ -167,10 +206,17 @@ public:
 
     // How a node runs: kernels (LaunchFn, hipcc builds) and / or on host
     // threads (CPU back end, g++ builds) -- per world or once per step.
+    // walk: the node's world-walk entries (at most kMaxWalkEntriesPerNode)
+    // and the walk / resume kernels of its code object (kernels[0], [1]), or
+    // 0 when the node cannot run inside a walk in this configuration (called
+    // before capture).
+    using WalkPlanFn = int32_t (*)(void *node, LaunchCtx &lc, detail::WalkEntry *out,
+                                   const void **kernels);
     struct NodeFns {
         LaunchFn launch = nullptr;
         CpuWorldFn cpuWorld = nullptr;
         CpuGlobalFn cpuGlobal = nullptr;
+        WalkPlanFn walk = nullptr;
     };
 
     // Node flags: a framework node whose kernels never call Context::tmpAlloc
@@ -261,6 +307,12 @@ public:
                 if constexpr (requires { NodeT::kTmpAllocReset; }) flags |= kNodeTmpAllocReset;
                 NodeFns fns;
                 fns.launch = [](void *n, LaunchCtx &lc) { NodeT::launch((NodeT *)n, lc); };
+                if constexpr (requires(NodeT *n, LaunchCtx &lc, detail::WalkEntry *e, const void **k) {
+                                  NodeT::walkPlan(n, lc, e, k); }) {   // k: const void *[2]
+                    fns.walk = [](void *n, LaunchCtx &lc, detail::WalkEntry *e, const void **k) {
+                        return NodeT::walkPlan((NodeT *)n, lc, e, k);
+                    };
+                }
                 if constexpr (requires(NodeT *n, CpuRunCtx &rc, int32_t w) { NodeT::runWorld(n, rc, w); }) {
                     fns.cpuWorld = [](void *n, CpuRunCtx &rc, int32_t w) { NodeT::runWorld((NodeT *)n, rc, w); };
                 }
@@ -389,6 +441,10 @@ void launchSerialKernel(const void *kernel, LaunchCtx &lc, int32_t threads_per_i
 // The ordered structural commit of a row-parallel node (see Context): a
 // no-op for worlds whose lanes made / destroyed nothing.
 void launchStructuralCommit(LaunchCtx &lc);
+// Runs `kernel(out_dev)` (one lane) and copies the 8-byte word it stores
+// back to the host: the device address of a world function (plan time only,
+// never during a capture).
+void readDeviceWord(const void *kernel, void *host_out);
 
 template <typename ContextT>
 MW_INLINE ContextT worldContext(StateView *st, int32_t w, StateManager *mgr = nullptr)
@@ -567,6 +623,37 @@ parallelForWorldKernel(const StateView *__restrict__ st_in, int32_t arch, int32_
 // world's rows run in the order the per-archetype launches gave them (its
 // first archetype's rows, then the next one's), one launch instead of one per
 // archetype.
+// One world's rows of every archetype of a small-table query, walked by the
+// calling wave (all 64 lanes, wave-uniform w): the body of
+// parallelForWorldMultiKernel and of the world walk's row entries.
+template <typename ContextT, auto Fn, int32_t threads, int32_t items, typename... ComponentTs>
+__device__ inline void rowWorldMulti(StateView *st, const MultiColArgs<sizeof...(ComponentTs)> &m,
+                                     int32_t w, int32_t lane)
+{
+    for (int32_t a = 0; a < m.n; a++) {
+        const int32_t arch = m.arch[a];
+        const int32_t query_arch = m.queryArch[a];
+        const int32_t cap = st->arch[arch].capacity;
+        const int32_t inv_per_world = (cap + items - 1) / items;
+        const int32_t lanes_per_world = inv_per_world * threads;
+        const int32_t n = st->arch[arch].numRows[w];
+        for (int32_t base = 0; base < lanes_per_world && (base / threads) * items < n; base += 64) {
+            const int32_t l = base + lane;
+            const int32_t first = (l / threads) * items;
+            if (l < lanes_per_world && first < n) {
+                ContextT ctx = worldContext<ContextT>(st, w);
+#pragma unroll 1
+                for (int32_t k = 0; k < items && first + k < n; k++) {
+                    ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k), arch,
+                                       queryComponentMask<ComponentTs...>());
+                    invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, m.cols[a], w, first + k,
+                                                            std::index_sequence_for<ComponentTs...> {});
+                }
+            }
+        }
+    }
+}
+
 template <typename ContextT, auto Fn, int32_t threads, int32_t items, typename... ComponentTs>
 __global__ void __launch_bounds__(256)
 parallelForWorldMultiKernel(const StateView *__restrict__ st_in, int32_t, int32_t,
@@ -577,29 +664,7 @@ parallelForWorldMultiKernel(const StateView *__restrict__ st_in, int32_t, int32_
     const int32_t lane = (int32_t)(threadIdx.x & 63);
     const int64_t waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     for (int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wv < st->numWorlds; wv += waves) {
-        const int32_t w = (int32_t)wv;
-        for (int32_t a = 0; a < m.n; a++) {
-            const int32_t arch = m.arch[a];
-            const int32_t query_arch = m.queryArch[a];
-            const int32_t cap = st->arch[arch].capacity;
-            const int32_t inv_per_world = (cap + items - 1) / items;
-            const int32_t lanes_per_world = inv_per_world * threads;
-            const int32_t n = st->arch[arch].numRows[w];
-            for (int32_t base = 0; base < lanes_per_world && (base / threads) * items < n; base += 64) {
-                const int32_t l = base + lane;
-                const int32_t first = (l / threads) * items;
-                if (l < lanes_per_world && first < n) {
-                    ContextT ctx = worldContext<ContextT>(st, w);
-#pragma unroll 1
-                    for (int32_t k = 0; k < items && first + k < n; k++) {
-                        ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k), arch,
-                                           queryComponentMask<ComponentTs...>());
-                        invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, m.cols[a], w, first + k,
-                                                                std::index_sequence_for<ComponentTs...> {});
-                    }
-                }
-            }
-        }
+        rowWorldMulti<ContextT, Fn, threads, items, ComponentTs...>(st, m, (int32_t)wv, lane);
     }
 }
 #endif
@@ -644,6 +709,206 @@ serialForKernel(const StateView *__restrict__ st_in, Query<ComponentTs...> q)
                 }
             }
         }
+    }
+}
+#endif
+
+#if defined(__HIPCC__)
+// ---------------------------------------------------------------------------
+// World walk (see WalkEntry): the kernel and the world functions.  Every
+// world function is called by a whole wave (lanes 0..63, wave-uniform w).
+// Each translation unit gets its own walk kernel (WalkTU is internal), so a
+// run's world functions and the kernel calling them share one code object,
+// and the kernel's register budget covers every function it can call.
+namespace {
+struct WalkTU {};
+}
+
+// A world function is called through a pointer, so its arguments arrive in
+// vector registers even though every lane passes the same values; reading
+// them back through readfirstlane makes them scalar again (uniform
+// addresses and loop bounds in SGPRs: fewer VGPRs, scalar loads).
+template <typename T>
+__device__ inline T *walkUniform(T *p)
+{
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T *)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ inline int32_t walkUniform(int32_t x)
+{
+    return __builtin_amdgcn_readfirstlane(x);
+}
+
+__device__ inline void walkSync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// The walk: one wave per block, blocks strided over the worlds; a world's
+// entries run in graph order with a wave barrier between them (the next node
+// sees every lane's writes).  At a commit point a world whose lanes made or
+// destroyed nothing goes on; a world with structural work stops there and
+// leaves the entry index in resume[w] for worldResumeKernel.  The commit code
+// is not reachable from this kernel, so its register budget is the world
+// functions' (the commit alone needs ~120 VGPRs; most nodes of most worlds
+// never reach it).
+template <typename Tag>
+__global__ void __launch_bounds__(64)
+worldWalkKernel(const WalkEntry *__restrict__ entries, int32_t n, StateView *st, int32_t *resume)
+{
+    MW_TRACE_BLOCK(0);
+    const WalkCtx c { st };
+    for (int32_t w = (int32_t)blockIdx.x; w < st->numWorlds; w += (int32_t)gridDim.x) {
+#pragma unroll 1
+        for (int32_t i = 0; i < n; i++) {
+            const WalkEntry &e = entries[i];
+            if (e.kind == kWalkCommit) {
+                if (commitLoad(st->appendDirty + w) != 0 || commitLoad(st->deferCount + w) != 0) {
+                    if (threadIdx.x == 0) resume[w] = i;
+                    break;
+                }
+                continue;
+            }
+            e.fn(e, c, w);
+            walkSync();
+        }
+    }
+}
+
+// The worlds a walk stopped at a commit point: commit (the executor's ordered
+// commit, working set in this block's global slab), then the rest of the
+// world's entries, committing again wherever the world is dirty.  Blocks
+// (one wave) check 64 worlds per round with one ballot, as the commit kernel
+// does; a step where no world stopped costs one pass of loads.
+template <typename Tag>
+__global__ void __launch_bounds__(64)
+worldResumeKernel(const WalkEntry *__restrict__ entries, int32_t n, StateView *st, int32_t *resume,
+                  char *scratch, uint64_t per_block, CommitShape shape, uint64_t ws_bytes)
+{
+    MW_TRACE_BLOCK(0);
+    char *ws = scratch + (size_t)blockIdx.x * per_block;
+    char *moves = ws + ws_bytes;
+    const WalkCtx c { st };
+    const int32_t lane = (int32_t)(threadIdx.x & 63);
+    for (int64_t base = blockIdx.x; base < st->numWorlds; base += (int64_t)gridDim.x * 64) {
+        const int64_t mine = base + (int64_t)lane * gridDim.x;
+        const bool stopped = mine < st->numWorlds && resume[mine] >= 0;
+        for (uint64_t todo = __ballot(stopped); todo != 0; todo &= todo - 1) {
+            const int32_t w = (int32_t)(base + (int64_t)__builtin_ctzll(todo) * gridDim.x);
+            const int32_t from = resume[w];
+            walkSync();
+            for (int32_t i = from; i < n; i++) {
+                const WalkEntry &e = entries[i];
+                if (e.kind == kWalkCommit) {
+                    if (shape.capMax > 0 &&
+                        (commitLoad(st->appendDirty + w) != 0 || commitLoad(st->deferCount + w) != 0)) {
+                        commitWorld(*st, shape, ws, moves, w);
+                    }
+                } else {
+                    e.fn(e, c, w);
+                }
+                walkSync();
+            }
+            if (lane == 0) resume[w] = -1;
+        }
+    }
+}
+
+template <typename Tag, auto F>
+__global__ void walkFnAddrKernel(WalkFn *out)
+{
+    *out = F;
+}
+
+// Device address of world function F in this translation unit's code object
+// (per device: each device loads its own copy of the code object).
+template <typename Tag, auto F>
+WalkFn walkFnAddr()
+{
+    static WalkFn cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        throw std::runtime_error("world walk: no current HIP device");
+    }
+    if (!cache[dev]) readDeviceWord((const void *)&walkFnAddrKernel<Tag, F>, &cache[dev]);
+    return cache[dev];
+}
+
+template <int32_t N>
+struct RowWalkParams {
+    MultiColArgs<N> m;
+    int32_t serial;
+    int32_t threads;
+};
+
+// A row node's world: row-parallel lanes over the world's small tables
+// (rowWorldMulti, as parallelForWorldMultiKernel), or the world-serial walk
+// on threads_per_invocation lanes (serialForKernel's body).
+template <typename ContextT, auto Fn, int32_t threads, int32_t items, typename... ComponentTs>
+__device__ void rowWalkEntry(const WalkEntry &e_in, const WalkCtx &c, int32_t w_in)
+{
+    const WalkEntry &e = *walkUniform(&e_in);
+    const int32_t w = walkUniform(w_in);
+    const auto &p = *reinterpret_cast<const RowWalkParams<sizeof...(ComponentTs)> *>(e.params);
+    const int32_t lane = (int32_t)(threadIdx.x & 63);
+    StateView *st = walkUniform(c.st);
+    if (!p.serial) {
+        rowWorldMulti<ContextT, Fn, threads, items, ComponentTs...>(st, p.m, w, lane);
+        return;
+    }
+    if (lane >= threads) return;
+    ContextT ctx = worldContext<ContextT>(st, w);
+    for (int32_t a = 0; a < p.m.n; a++) {
+        const int32_t arch = p.m.arch[a];
+        const int32_t n = st->arch[arch].numRows[w];
+#pragma unroll 1
+        for (int32_t r = 0; r < n; r++) {
+            invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, p.m.cols[a], w, r,
+                                                    std::index_sequence_for<ComponentTs...> {});
+            if constexpr (threads > 1) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+    }
+}
+
+// PerWorldNode: Fn(ctx) on the world's lane 0 (world-serial context).
+template <typename ContextT, auto Fn>
+__device__ void perWorldWalkEntry(const WalkEntry &, const WalkCtx &c, int32_t w_in)
+{
+    const int32_t w = walkUniform(w_in);
+    StateView *st = walkUniform(c.st);
+    if ((threadIdx.x & 63) != 0) return;
+    ContextT ctx = worldContext<ContextT>(st, w);
+    Fn(ctx);
+}
+
+// addNodeFn with a fixed count per world: the world's invocations w * count
+// + k, threads lanes each (nodeFnKernel's numbering).
+template <typename NodeT>
+struct NodeFnWalkParams {
+    NodeT *node;
+    uint32_t count;
+    uint32_t threads;
+};
+
+template <typename NodeT, auto fn>
+__device__ void nodeFnWalkEntry(const WalkEntry &e_in, const WalkCtx &, int32_t w_in)
+{
+    const WalkEntry &e = *walkUniform(&e_in);
+    const int32_t w = walkUniform(w_in);
+    const auto &p = *reinterpret_cast<const NodeFnWalkParams<NodeT> *>(e.params);
+    const int32_t total = (int32_t)(p.count * p.threads);
+    for (int32_t base = 0; base < total; base += 64) {
+        const int32_t t = base + (int32_t)(threadIdx.x & 63);
+        if (t < total) std::invoke(fn, p.node, (int32_t)((int64_t)w * p.count + t / (int32_t)p.threads));
     }
 }
 #endif
@@ -732,6 +997,48 @@ public:
         detail::launchStructuralCommit(lc);
 #else
         (void)self; (void)lc;
+#endif
+    }
+
+    // World walk: the node's rows (and its ordered commit) for one world at a
+    // time, when every archetype of the query is a small table (as for
+    // parallelForWorldMultiKernel) or the node is world-serial.
+    static int32_t walkPlan(RowForNode *self, LaunchCtx &lc, detail::WalkEntry *out, const void **kernels)
+    {
+#if defined(__HIPCC__)
+        const int32_t na = self->query_.numArchetypes;
+        if (na < 1 || na > detail::kFusedArchetypes) return 0;
+        const bool serial = kSerial || lc.serialNodes;
+        for (int32_t a = 0; a < na && !serial; a++) {
+            const int64_t lanes = (int64_t)(lc.view->arch[self->query_.archetypes[a]].capacity +
+                                            items_per_invocation - 1) /
+                                  items_per_invocation * threads_per_invocation;
+            if (lanes > lc.worldWaveLanes) return 0;
+        }
+        detail::RowWalkParams<sizeof...(ComponentTs)> p {};
+        static_assert(sizeof(p) <= detail::kWalkParamBytes, "row walk parameters");
+        p.m.n = na;
+        for (int32_t a = 0; a < na; a++) {
+            p.m.arch[a] = self->query_.archetypes[a];
+            p.m.queryArch[a] = a;
+            for (int32_t c = 0; c < (int32_t)sizeof...(ComponentTs); c++) p.m.cols[a].c[c] = self->query_.cols[a][c];
+        }
+        p.serial = serial ? 1 : 0;
+        p.threads = threads_per_invocation;
+        out[0] = detail::WalkEntry {};
+        out[0].fn = detail::walkFnAddr<detail::WalkTU,
+                                       &detail::rowWalkEntry<ContextT, Fn, threads_per_invocation,
+                                                             items_per_invocation, ComponentTs...>>();
+        memcpy(out[0].params, &p, sizeof(p));
+        kernels[0] = (const void *)&detail::worldWalkKernel<detail::WalkTU>;
+        kernels[1] = (const void *)&detail::worldResumeKernel<detail::WalkTU>;
+        if (serial) return 1;
+        out[1] = detail::WalkEntry {};
+        out[1].kind = detail::kWalkCommit;
+        return 2;
+#else
+        (void)self; (void)lc; (void)out; (void)kernels;
+        return 0;
 #endif
     }
 
@@ -863,6 +1170,22 @@ TaskGraph::NodeID TaskGraph::Builder::addNodeFn(TypedDataID<NodeT> data,
         (void)d; (void)lc;
 #endif
     };
+#if defined(__HIPCC__)
+    if (fixed_num_invocations > 0 && fixed_num_invocations != 0xFFFF'FFFFu) {
+        fns.walk = [](void *d, LaunchCtx &lc, detail::WalkEntry *out, const void **kernels) -> int32_t {
+            const Desc &dd = *(const Desc *)d;
+            detail::NodeFnWalkParams<NodeT> p { (NodeT *)(lc.nodeData + (size_t)dd.dataIdx * maxNodeDataBytes),
+                                                dd.fixedCount, dd.threads };
+            static_assert(sizeof(p) <= detail::kWalkParamBytes);
+            out[0] = detail::WalkEntry {};
+            out[0].fn = detail::walkFnAddr<detail::WalkTU, &detail::nodeFnWalkEntry<NodeT, fn>>();
+            memcpy(out[0].params, &p, sizeof(p));
+            kernels[0] = (const void *)&detail::worldWalkKernel<detail::WalkTU>;
+            kernels[1] = (const void *)&detail::worldResumeKernel<detail::WalkTU>;
+            return 1;
+        };
+    }
+#endif
 #if !defined(__HIPCC__)
     // CPU back end.  A fixed count per world is world-local (invocation
     // world * count + k, k in order, each by every one of its lanes in
@@ -947,6 +1270,19 @@ public:
         detail::launchWorldKernel((const void *)&detail::perWorldKernel<ContextT, Fn>, lc);
 #else
         (void)lc;
+#endif
+    }
+    static int32_t walkPlan(PerWorldNode *, LaunchCtx &, detail::WalkEntry *out, const void **kernels)
+    {
+#if defined(__HIPCC__)
+        out[0] = detail::WalkEntry {};
+        out[0].fn = detail::walkFnAddr<detail::WalkTU, &detail::perWorldWalkEntry<ContextT, Fn>>();
+        kernels[0] = (const void *)&detail::worldWalkKernel<detail::WalkTU>;
+        kernels[1] = (const void *)&detail::worldResumeKernel<detail::WalkTU>;
+        return 1;
+#else
+        (void)out; (void)kernels;
+        return 0;
 #endif
     }
 #if !defined(__HIPCC__)

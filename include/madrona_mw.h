@@ -281,6 +281,14 @@ typedef struct mw_jobs_collisions_config {
  * it.  mw_set_node_blocks_per_cu: node -1 sets the default, value -1 on a
  * node reverts it to the default; re-captures the step graph.             */
 int32_t mw_num_nodes(mw_exec *exec);
+/* World walk (the persistent megakernel, reference src/mw/device/
+ * megakernel_impl.inl:29-55): with MADRONA_MW_WORLD_WALK=1 in the
+ * environment at mw_create, runs of consecutive world-local nodes (row nodes
+ * over small tables with their ordered commits, world-serial row nodes,
+ * per-world nodes, fixed-count device nodes) are walked by one kernel, a
+ * wave per world calling each node's world function in graph order; same
+ * results.  Returns the walk launches per step (0: off / CPU back end).    */
+int32_t mw_world_walk_runs(mw_exec *exec);
 const char *mw_node_name(mw_exec *exec, int32_t node);
 int32_t mw_node_blocks_per_cu(mw_exec *exec, int32_t node);
 int mw_set_node_blocks_per_cu(mw_exec *exec, int32_t node, int32_t blocks_per_cu);

@@ -83,6 +83,8 @@ def parse():
     p.add_argument("--cpu-max-batches", type=int, default=48)
     p.add_argument("--cpu-first-world", type=int, default=0, help=argparse.SUPPRESS)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-node-timing", action="store_true",
+                   help="no live node timing in the window (every tick replays the whole graph)")
     p.add_argument("--chunk", type=int, default=50,
                    help="ticks launched back-to-back per host sync (the reference "
                         "benchmark runs all ticks in one go)")
@@ -201,7 +203,8 @@ def main():
     # stepping is timed (the sampled row counts are read between chunks).
     # The dominant node is timed live in the window: every 10th tick runs the
     # graph split at that node with an event pair bound to its kernels.
-    sim.set_timed_node_index(dom, every=10)
+    if not args.no_node_timing:
+        sim.set_timed_node_index(dom, every=10)
     elapsed = 0.0
     left, tick = args.steps, args.preroll
     rows_by_tick = [[tick, *live()]]
@@ -225,7 +228,7 @@ def main():
 
     launch_ms = (ms1 - ms0) / max(1, n1 - n0)
     nbytes = W * SYS_BYTES[dom_sys](nd_mean, nk_mean)
-    achieved = nbytes / (launch_ms * 1e-3) / 1e9
+    achieved = nbytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
     cpu = cpu_exec = None
     if not args.no_cpu_baseline:
         legs = ["reference"] + ([] if args.no_cpu_executor else ["executor"])
