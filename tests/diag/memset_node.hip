@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <vector>
 
@@ -45,6 +46,56 @@ __global__ void resetKernel(uint32_t *c, int32_t n)
 
 }
 
+// The graph as the executor builds it: captured inside a helper whose
+// stack frame is gone when the graph replays (the executor captures in
+// captureSegments and replays from runAsync).
+__attribute__((noinline)) static hipError_t captureInHelper(int32_t reset, uint32_t *c, int32_t n,
+                                                            hipStream_t s, hipGraphExec_t *ge,
+                                                            hipGraph_t *g)
+{
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) return e;
+    volatile uint32_t value = 0;               // a stack local, as a caller's would be
+    if (reset == 0) {
+        hipLaunchKernelGGL(resetKernel, grid, block, 0, s, c, n);
+    } else if (reset == 1) {
+        (void)hipMemsetAsync(c, (int)value, sizeof(uint32_t) * (size_t)n, s);
+    } else {
+        (void)hipMemsetD32Async((hipDeviceptr_t)c, (int)value, (size_t)n, s);
+    }
+    hipLaunchKernelGGL(bumpKernel, grid, block, 0, s, c, n, 1u, 0);
+    hipLaunchKernelGGL(bumpKernel, grid, block, 0, s, c, n, 2u, 1);
+    e = hipStreamEndCapture(s, g);
+    if (e != hipSuccess) return e;
+    return hipGraphInstantiate(ge, *g, nullptr, nullptr, 0);
+}
+
+// Overwrites a large stretch of the host stack with the pattern the fault
+// log showed in every counter (0x7657500C), then returns.
+__attribute__((noinline)) static uint32_t scribbleStack(uint32_t pattern)
+{
+    volatile uint32_t junk[16384];
+    for (int32_t i = 0; i < 16384; i++) junk[i] = pattern;
+    return junk[pattern & 1023];
+}
+
+// Allocates and fills many small host blocks with the pattern, then frees
+// them: a runtime that kept a pointer to a freed parameter block of the
+// captured node would read the pattern back at replay (the fault log's
+// 0x7657500C looks like the low half of a host heap pointer).
+__attribute__((noinline)) static void scribbleHeap(uint32_t pattern)
+{
+    std::vector<uint32_t *> blocks;
+    for (int32_t k = 0; k < 4096; k++) {
+        const size_t words = 4 + (size_t)(k % 128);
+        uint32_t *b = (uint32_t *)malloc(words * 4);
+        for (size_t i = 0; i < words; i++) b[i] = pattern;
+        blocks.push_back(b);
+    }
+    for (uint32_t *b : blocks) free(b);
+}
+
 // Returns the number of replays after which at least one counter was wrong
 // (out[0]), the first such replay (out[1], -1 if none) and the number of
 // wrong counters summed over replays (out[2]); -1 on a HIP error.
@@ -60,21 +111,9 @@ extern "C" int memset_node_run(int32_t reset, int32_t n, int32_t replays, int32_
     hipStream_t s;
     DIAG_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
 
-    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-    DIAG_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    if (reset == 0) {
-        hipLaunchKernelGGL(resetKernel, grid, block, 0, s, c, n);
-    } else if (reset == 1) {
-        (void)hipMemsetAsync(c, 0, sizeof(uint32_t) * (size_t)n, s);
-    } else {
-        (void)hipMemsetD32Async((hipDeviceptr_t)c, 0, (size_t)n, s);
-    }
-    hipLaunchKernelGGL(bumpKernel, grid, block, 0, s, c, n, 1u, 0);
-    hipLaunchKernelGGL(bumpKernel, grid, block, 0, s, c, n, 2u, 1);
     hipGraph_t g = nullptr;
-    DIAG_CHECK(hipStreamEndCapture(s, &g));
     hipGraphExec_t ge = nullptr;
-    DIAG_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    DIAG_CHECK(captureInHelper(reset, c, n, s, &ge, &g));
 
     std::vector<uint32_t> host(n);
     std::vector<uint8_t> hs(scratch_bytes, 1);
@@ -82,6 +121,17 @@ extern "C" int memset_node_run(int32_t reset, int32_t n, int32_t replays, int32_
     for (int32_t r = 0; r < replays; r++) {
         DIAG_CHECK(hipGraphLaunch(ge, s));
         DIAG_CHECK(hipStreamSynchronize(s));
+        if (host_copies >= 2) (void)scribbleStack(0x7657500Cu + (uint32_t)r);
+        if (host_copies >= 4) scribbleHeap(0x7657500Cu);
+        if (host_copies >= 3) {
+            // the executor's sequence between replays: a D2H read-back of a
+            // column (mw_read_column: hipMemcpy on the null stream) and a
+            // fresh device allocation (hipMalloc, as a late export buffer)
+            void *extra = nullptr;
+            DIAG_CHECK(hipMalloc(&extra, 4096));
+            DIAG_CHECK(hipMemcpy(hs.data(), c, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost));
+            DIAG_CHECK(hipFree(extra));
+        }
         if (host_copies) {
             // what tests and exports do between steps: synchronous copies on
             // the null stream

@@ -1,6 +1,11 @@
 """Prints, for each reset method x size x host-copy setting, how many of the
 graph replays left a counter wrong (tests/diag/memset_node.hip).  TEST
-INFRASTRUCTURE: a diagnosis run, results recorded in DESIGN.md."""
+INFRASTRUCTURE: a diagnosis run, results recorded in DESIGN.md.
+host_copies: 0 none, 1 synchronous H2D / D2H copies between replays, 2 the
+same after scribbling the host stack with the fault log's counter value
+(the graph is captured in a helper whose frame is gone by then), 3 also a
+D2H read-back and a hipMalloc / hipFree between replays, 4 also 4096 host
+heap blocks filled with that value and freed between replays."""
 import ctypes
 import json
 import os
@@ -30,7 +35,7 @@ if __name__ == "__main__":
     rows = []
     for reset in (0, 1, 2):
         for n in (1, 2, 64, 8192, 8193):
-            for hc in (0, 1):
+            for hc in (0, 1, 2, 3, 4):
                 r = run(lib, reset, n, 200, hc)
                 r.update(reset=["kernel", "hipMemsetAsync", "hipMemsetD32Async"][reset], n=n, host_copies=hc)
                 rows.append(r)
