@@ -801,9 +801,28 @@ __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
 // Returns true (on every lane of the group) if the pair is not separated;
 // the leader's `job` then holds createFaceContact's / createEdgeContact's
 // inputs.
+#if defined(MW_SAT_PROFILE)
+// Profiling build only (make BUILD=build_prof EXTRA=-DMW_SAT_PROFILE): per
+// hull-hull pair, where the SAT ended ([0] pairs, [1] separated by a face of
+// a, [2] of b, [3] by an edge pair, [4] face contact, [5] edge contact) and
+// the group leader's clock in each phase ([8] staging, [9] faces of a,
+// [10] faces of b, [11] edge pairs, [12] contact job).
+static __device__ unsigned long long g_satStage[16];
+#define MW_SAT_COUNT(i) do { if (lane == 0) atomicAdd(&g_satStage[i], 1ull); } while (0)
+#define MW_SAT_TICK(i) do { if (lane == 0) { const long long t__ = wall_clock64(); \
+    atomicAdd(&g_satStage[i], (unsigned long long)(t__ - prof_t)); prof_t = t__; } } while (0)
+#else
+#define MW_SAT_COUNT(i) do {} while (0)
+#define MW_SAT_TICK(i) do {} while (0)
+#endif
+
 __device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS &g,
                             int32_t lane, ContactJob &job)
 {
+#if defined(MW_SAT_PROFILE)
+    long long prof_t = wall_clock64();
+#endif
+    MW_SAT_COUNT(0);
     const ObjDev &O = P.objs;
     const int32_t w = wk.world;
     HullRef ha, hb;
@@ -814,13 +833,17 @@ __device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS
     ha.center = stageHull(P, w, P.body[wk.aArch], wk.a.row, ha.hd, g.vA, g.pA, g.qA, lane);
     hb.center = stageHull(P, w, P.body[wk.bArch], wk.b.row, hb.hd, g.vB, g.pB, g.qB, lane);
     groupSync();
+    MW_SAT_TICK(8);
 
     const FaceQuery fa = groupFaceQuery(ha, hb, lane);
-    if (fa.separation > 0.0f) return false;
+    MW_SAT_TICK(9);
+    if (fa.separation > 0.0f) { MW_SAT_COUNT(1); return false; }
     const FaceQuery fb = groupFaceQuery(hb, ha, lane);
-    if (fb.separation > 0.0f) return false;
+    MW_SAT_TICK(10);
+    if (fb.separation > 0.0f) { MW_SAT_COUNT(2); return false; }
     const EdgeQuery eq = groupEdgeQuery(ha, hb, lane);
-    if (eq.separation > 0.0f) return false;
+    MW_SAT_TICK(11);
+    if (eq.separation > 0.0f) { MW_SAT_COUNT(3); return false; }
 
     job.pair = wk;
     if (fa.separation > eq.separation || fb.separation > eq.separation) {
@@ -830,15 +853,27 @@ __device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS
         job.plane = a_is_ref ? fa.plane : fb.plane;
         job.feature0 = a_is_ref ? fa.faceIdx : fb.faceIdx;
         job.feature1 = findIncidentFace(a_is_ref ? hb : ha, job.plane.normal);
+        MW_SAT_COUNT(4);
     } else {
         job.kind = kJobEdge;
         job.refIsA = 1;
         job.feature0 = eq.edgeA;
         job.feature1 = eq.edgeB;
         job.plane = geometry::Plane { eq.normal, eq.separation };
+        MW_SAT_COUNT(5);
     }
+    MW_SAT_TICK(12);
     return true;
 }
+
+#if defined(MW_SAT_PROFILE)
+extern "C" int mw_debug_sat_stages(unsigned long long *out)
+{
+    unsigned long long z[16] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_satStage), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_satStage), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // Solver world order.  Block durations follow the worlds' contact counts
 // (p50 / p99 ~ 1 : 3), so with the grid in world-index order the heavy

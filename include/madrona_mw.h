@@ -186,8 +186,14 @@ const char *mw_last_error(void);
 
 /* ---- introspection (tests, tooling) ------------------------------------ */
 int32_t mw_num_worlds(mw_exec *exec);
-/* OR of per-world error flags (1 id store full, 2 table full, 4 candidate
- * overflow, 8 contact overflow, 16 BVH stack overflow).                    */
+/* OR of per-world error flags: 1 id store full, 2 table full, 4 candidate
+ * overflow, 8 contact overflow, 16 BVH stack overflow, 32 solver body
+ * overflow, 64 index guard (site in bits 8..15), 128 joint overflow,
+ * 1<<16 job dropped, 1<<17 tmpAlloc arena full, 1<<18 deferred log full,
+ * 1<<19 op not available in a row-parallel node, 1<<20 commit limit,
+ * 1<<21 static body written by a non-finite solve, 1<<22 row-parallel make
+ * gave up waiting for its turn, 1<<23 row-parallel get of a query component
+ * at another row (kErrFlagCrossRow, include/madrona/state.hpp).            */
 int32_t mw_error_flags(mw_exec *exec);
 int32_t mw_num_archetypes(mw_exec *exec);
 /* Copy rows of (archetype, column) of one world to host `out` (capacity
