@@ -116,12 +116,19 @@ struct GroupLDS {
     Vector3 *vA, *vB;
     geometry::Plane *pA, *pB;
     EdgeQuad *qA, *qB;
+    float *sA;                     // [maxEdges][minkStride]: edge i of a x face f of b
+    float *tB;                     // [maxEdges][minkStride]: edge j of b x face f of a
 };
+
+__host__ __device__ inline size_t minkTableBytes(const ObjDev &O)
+{
+    return a16(sizeof(float) * O.maxEdges * O.minkStride);
+}
 
 __host__ __device__ inline size_t groupLDSBytes(const ObjDev &O)
 {
     return 2 * a16(sizeof(Vector3) * O.maxVerts) + 2 * a16(sizeof(geometry::Plane) * O.maxFaces) +
-           2 * a16(sizeof(EdgeQuad) * O.maxEdges);
+           2 * a16(sizeof(EdgeQuad) * O.maxEdges) + 2 * minkTableBytes(O);
 }
 
 // The group staging area; block 0 first uses it for the solver's world
@@ -131,7 +138,7 @@ constexpr size_t kOrderSortBytes = 1024 * sizeof(int32_t);
 
 size_t narrowphaseSharedBytes(const PhysArgs &P)
 {
-    return std::max(kGroupsPerBlock * groupLDSBytes(P.objs), kOrderSortBytes);
+    return std::max(kGroupsPerBlock * groupLDSBytes(P.objs), kOrderSortBytes) + P.satGeoBytes;
 }
 
 __device__ __forceinline__ GroupLDS groupLDS(char *smem, int32_t group, const ObjDev &O)
@@ -143,7 +150,9 @@ __device__ __forceinline__ GroupLDS groupLDS(char *smem, int32_t group, const Ob
     g.pA = (geometry::Plane *)p; p += a16(sizeof(geometry::Plane) * O.maxFaces);
     g.pB = (geometry::Plane *)p; p += a16(sizeof(geometry::Plane) * O.maxFaces);
     g.qA = (EdgeQuad *)p; p += a16(sizeof(EdgeQuad) * O.maxEdges);
-    g.qB = (EdgeQuad *)p;
+    g.qB = (EdgeQuad *)p; p += a16(sizeof(EdgeQuad) * O.maxEdges);
+    g.sA = (float *)p; p += minkTableBytes(O);
+    g.tB = (float *)p;
     return g;
 }
 
@@ -176,55 +185,48 @@ __device__ __forceinline__ void groupArgMax(float &v, int32_t &k)
     }
 }
 
-// Transform one body's hull into the group's LDS and copy its edge topology.
-// Not inlined: the two transforms, interleaved into the SAT body by the
-// scheduler, set the kernel's register peak (156 -> ~110 VGPRs apart), and
-// the call only takes scalars and pointers (aggregates would be passed
-// byval through scratch).
-__device__ __noinline__ void stageHullRaw(const Vector3 *obj_verts,
-                                          const geometry::Plane *obj_planes,
-                                          const EdgeQuad *obj_quads, int32_t vert_off,
-                                          int32_t num_verts, int32_t face_off, int32_t num_faces,
-                                          int32_t edge_off, int32_t num_edges,
-                                          float xx, float xy, float xz, float qw, float qx,
-                                          float qy, float qz, float s0, float s1, float s2,
+// Body columns a SAT group stages a hull from, per body archetype: an LDS
+// copy of PhysArgs::body's entries (the kernel-argument array indexed by a
+// per-group value is a vector load from the argument segment at every use).
+struct SatArch {
+    const Vector3 *pos;
+    const Quat *rot;
+    const Diag3x3 *scale;
+    int32_t capacity;
+    int32_t archetype;
+};
+
+// A body's position, rotation and scale: what its hull's world transform
+// (hullXform) is made of.
+struct BodyPose {
+    Vector3 x;
+    Quat q;
+    Diag3x3 s;
+};
+
+__device__ __forceinline__ BodyPose loadPose(const SatArch &A, int32_t w, int32_t row)
+{
+    const size_t i = (size_t)w * A.capacity + row;
+    return BodyPose { A.pos[i], A.rot[i], A.scale[i] };
+}
+
+// Transform one body's hull into the group's LDS and copy its edge topology
+// (hullXform / worldVertex / worldPlane, the same operations).
+__device__ __forceinline__ void stageHull(const ObjDev &O, const HullDev &hd, const BodyPose &p,
                                           Vector3 *v, geometry::Plane *pl, EdgeQuad *q,
                                           int32_t lane)
 {
-    const Vector3 x { xx, xy, xz };
-    const Diag3x3 scale { s0, s1, s2 };
-    const Mat3x3 unscaled_rot = Mat3x3::fromQuat(Quat { qw, qx, qy, qz });
-    const HullXform xf { unscaled_rot * scale, unscaled_rot * scale.inv(), x };
-    HullDev hd {};
-    hd.vertOffset = vert_off;
-    hd.numVerts = num_verts;
-    hd.faceOffset = face_off;
-    hd.numFaces = num_faces;
-    hd.edgeOffset = edge_off;
-    hd.numEdges = num_edges;
+    const Mat3x3 unscaled_rot = Mat3x3::fromQuat(p.q);
+    const HullXform xf { unscaled_rot * p.s, unscaled_rot * p.s.inv(), p.x };
     for (int32_t i = lane; i < hd.numVerts; i += kGroup)
-        v[i] = xf.vtx * obj_verts[hd.vertOffset + i] + xf.x;
+        v[i] = xf.vtx * O.vertices[hd.vertOffset + i] + xf.x;
     for (int32_t i = lane; i < hd.numFaces; i += kGroup) {
-        const geometry::Plane op = obj_planes[hd.faceOffset + i];
+        const geometry::Plane op = O.planes[hd.faceOffset + i];
         const Vector3 origin = xf.vtx * (op.normal * op.d) + xf.x;
         const Vector3 n = (xf.nrm * op.normal).normalize();
         pl[i] = geometry::Plane { n, dot(n, origin) };
     }
-    for (int32_t i = lane; i < hd.numEdges; i += kGroup) q[i] = obj_quads[hd.edgeOffset + i];
-}
-
-__device__ __forceinline__ Vector3 stageHull(const PhysArgs &P, int32_t w, const BodyArch &B,
-                                             int32_t row, const HullDev &hd, Vector3 *v,
-                                             geometry::Plane *pl, EdgeQuad *q, int32_t lane)
-{
-    const ObjDev &O = P.objs;
-    const Vector3 x = bcol<Vector3>(B, Cols::Position, w, row);
-    const Quat r = bcol<Quat>(B, Cols::Rotation, w, row);
-    const Diag3x3 sc = bcol<Diag3x3>(B, Cols::Scale, w, row);
-    stageHullRaw(O.vertices, O.planes, O.edgeQuads, hd.vertOffset, hd.numVerts, hd.faceOffset,
-                 hd.numFaces, hd.edgeOffset, hd.numEdges, x.x, x.y, x.z, r.w, r.x, r.y, r.z,
-                 sc.d0, sc.d1, sc.d2, v, pl, q, lane);
-    return x;
+    for (int32_t i = lane; i < hd.numEdges; i += kGroup) q[i] = O.edgeQuads[hd.edgeOffset + i];
 }
 
 __device__ __forceinline__ float hullDistFromPlane(const geometry::Plane &p, const HullRef &h)
@@ -237,10 +239,12 @@ __device__ __forceinline__ float hullDistFromPlane(const geometry::Plane &p, con
     return min_dot - p.d;
 }
 
+// A face query's result: the deepest face's separation and index (-1 when
+// no face scored above -FLT_MAX); its plane is re-read from the staged hull
+// when a contact job needs it.
 struct FaceQuery {
     float separation;
     int32_t faceIdx;
-    geometry::Plane plane;
 };
 
 // queryFaceDirections (narrowphase.cpp:395-431).  The reference stops at the
@@ -256,8 +260,13 @@ __device__ FaceQuery groupFaceQuery(const HullRef &a, const HullRef &b, int32_t 
         if (scanWins(d, f, v, k)) { v = d; k = f; }
     }
     groupArgMax(v, k);
-    if (v > -FLT_MAX) return { v, k, a.planes[k] };
-    return { -FLT_MAX, -1, geometry::Plane { { 0, 0, 0 }, 0 } };
+    if (v > -FLT_MAX) return { v, k };
+    return { -FLT_MAX, -1 };
+}
+
+__device__ __forceinline__ geometry::Plane facePlane(const geometry::Plane *planes, int32_t f)
+{
+    return f >= 0 ? planes[f] : geometry::Plane { { 0, 0, 0 }, 0 };
 }
 
 __device__ __forceinline__ bool isMinkowskiFace(const Vector3 &a, const Vector3 &b,
@@ -298,41 +307,157 @@ __device__ __forceinline__ float edgePairSeparation(const HullRef &a, const Hull
     return sep;
 }
 
+// An edge query's result: the best pair index p = i * nB + j and its
+// separation (-FLT_MAX, p = 0 when no pair scored); the contact normal is
+// recomputed from the pair when an edge job needs it.
 struct EdgeQuery {
     float separation;
-    Vector3 normal;
-    int32_t edgeA;                 // edge indices (into the hull's edge list)
-    int32_t edgeB;
+    int32_t pair;
 };
 
 // queryEdgeDirections (narrowphase.cpp:474-540).  Pair index p = i * nB + j
 // is the reference's loop order; the early return on a positive separation
-// only ever rejects the pair.
+// only ever rejects the pair.  A lane walks its pairs (i, j) incrementally
+// and keeps edge i of a (its face normals and their cross product, the
+// Minkowski test's a-side) while only j changes: the same operations as
+// edgePairSeparation, fewer LDS reads and no division per pair.
 __device__ EdgeQuery groupEdgeQuery(const HullRef &a, const HullRef &b, int32_t lane)
 {
     const int32_t nA = a.hd.numEdges, nB = b.hd.numEdges;
     float v = __builtin_nanf("");
     int32_t k = INT32_MAX;
-    for (int32_t p = lane; p < nA * nB; p += kGroup) {
-        const int32_t i = p / nB, j = p - i * nB;
-        const float sep = edgePairSeparation(a, b, i, j, nullptr);
-        if (scanWins(sep, p, v, k)) { v = sep; k = p; }
+    if (nB > 0) {
+        int32_t i = lane / nB, j = lane - (lane / nB) * nB;
+        int32_t cur = -1;
+        EdgeQuad ea {};
+        Vector3 an1 {}, an2 {}, bxa {};
+        for (int32_t p = lane; p < nA * nB; p += kGroup) {
+            if (i != cur) {
+                cur = i;
+                ea = a.quads[i];
+                an1 = a.planes[ea.face1].normal;
+                an2 = a.planes[ea.face2].normal;
+                bxa = an2.cross(an1);
+            }
+            const EdgeQuad eb = b.quads[j];
+            const Vector3 c = -b.planes[eb.face1].normal, d = -b.planes[eb.face2].normal;
+            // isMinkowskiFace(an1, an2, c, d)
+            const Vector3 dxc = d.cross(c);
+            const float cba = c.dot(bxa), dba = d.dot(bxa);
+            const float adc = an1.dot(dxc), bdc = an2.dot(dxc);
+            float sep = -FLT_MAX;
+            if (cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f) {
+                const Vector3 pa1 = a.verts[ea.v1], pb1 = b.verts[eb.v1];
+                Vector3 da = a.verts[ea.v2] - pa1, db = b.verts[eb.v2] - pb1;
+                Vector3 uc = da.cross(db);
+                float l2 = uc.length2();
+                if (l2 != 0) {
+                    float inv = 1.f / sqrtf(l2);
+                    Vector3 n = uc * inv;
+                    if (n.dot(pa1 - a.center) < 0.0f) n = -n;
+                    sep = n.dot(pb1 - pa1);
+                }
+            }
+            if (scanWins(sep, p, v, k)) { v = sep; k = p; }
+            j += kGroup;
+            while (j >= nB) { j -= nB; i++; }
+        }
     }
     groupArgMax(v, k);
-    if (!(v > -FLT_MAX)) return { -FLT_MAX, { 0, 0, 0 }, 0, 0 };
-    EdgeQuery q;
-    q.edgeA = k / nB;
-    q.edgeB = k - q.edgeA * nB;
-    q.separation = edgePairSeparation(a, b, q.edgeA, q.edgeB, &q.normal);
-    return q;
+    if (!(v > -FLT_MAX)) return { -FLT_MAX, 0 };
+    return { v, k };
 }
 
-__device__ __forceinline__ int32_t findIncidentFace(const HullRef &h, Vector3 ref_normal)
+// The Minkowski-face test of edge pair (i, j) (isMinkowskiFace(a1, a2, -b1,
+// -b2) with a1 / a2 the faces of edge i of a, b1 / b2 those of edge j of b)
+// reads four dot products, each a function of one edge and one face:
+//   cba = -b1 . (a2 x a1),  dba = -b2 . (a2 x a1)   row i of sA, columns b1 / b2
+//   adc = a1 . ((-b2) x (-b1)),  bdc = a2 . ((-b2) x (-b1))   row j of tB
+// so the group evaluates them once per (edge, face), not four times per
+// edge pair; each entry is the same expression as in edgePairSeparation, so
+// the test's verdicts are the same bits.
+__device__ __forceinline__ void buildMinkTables(const HullRef &a, const HullRef &b, float *sA, float *tB,
+                                                int32_t stride, int32_t lane)
+{
+    for (int32_t i = lane; i < a.hd.numEdges; i += kGroup) {
+        const EdgeQuad ea = a.quads[i];
+        const Vector3 bxa = a.planes[ea.face2].normal.cross(a.planes[ea.face1].normal);
+        for (int32_t f = 0; f < b.hd.numFaces; f++) sA[i * stride + f] = (-b.planes[f].normal).dot(bxa);
+    }
+    for (int32_t j = lane; j < b.hd.numEdges; j += kGroup) {
+        const EdgeQuad eb = b.quads[j];
+        const Vector3 c = -b.planes[eb.face1].normal, d = -b.planes[eb.face2].normal;
+        const Vector3 dxc = d.cross(c);
+        for (int32_t f = 0; f < a.hd.numFaces; f++) tB[j * stride + f] = a.planes[f].normal.dot(dxc);
+    }
+}
+
+// groupEdgeQuery with the tables: the lanes first test their edge pairs
+// (four LDS reads each, in chunks of 32 pairs per lane, a bit per pair),
+// then compute the separation of the pairs that passed.  In the per-pair
+// form nearly every step of a wave runs the separation branch for the few
+// lanes whose pair passed; here a lane runs it only for its own passes.
+// The (separation, p) scan sees the same values in the same order, the
+// failed pairs' -FLT_MAX included.
+__device__ EdgeQuery groupEdgeQueryTables(const HullRef &a, const HullRef &b, const float *sA,
+                                          const float *tB, int32_t stride, int32_t lane)
+{
+    const int32_t nA = a.hd.numEdges, nB = b.hd.numEdges, n = nA * nB;
+    float v = __builtin_nanf("");
+    int32_t k = INT32_MAX;
+    if (nB > 0) {
+        int32_t i = lane / nB, j = lane - (lane / nB) * nB;
+        for (int32_t base = lane; base < n; base += 32 * kGroup) {
+            uint32_t pass = 0;
+            int32_t t = 0;
+            for (int32_t p = base; p < n && t < 32; p += kGroup, t++) {
+                const EdgeQuad ea = a.quads[i], eb = b.quads[j];
+                const float *si = sA + i * stride, *tj = tB + j * stride;
+                const float cba = si[eb.face1], dba = si[eb.face2];
+                const float adc = tj[ea.face1], bdc = tj[ea.face2];
+                if (cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f) pass |= 1u << t;
+                j += kGroup;
+                while (j >= nB) { j -= nB; i++; }
+            }
+            // failed pairs score -FLT_MAX: the scan keeps the first of them
+            const uint32_t all = t == 32 ? ~0u : (1u << t) - 1u;
+            if (pass != all) {
+                const int32_t p0 = base + kGroup * __builtin_ctz(~pass);
+                if (scanWins(-FLT_MAX, p0, v, k)) { v = -FLT_MAX; k = p0; }
+            }
+            while (pass) {
+                const int32_t bit = __builtin_ctz(pass);
+                pass &= pass - 1;
+                const int32_t p = base + kGroup * bit;
+                const int32_t pi = p / nB, pj = p - pi * nB;
+                const EdgeQuad ea = a.quads[pi], eb = b.quads[pj];
+                float sep = -FLT_MAX;
+                const Vector3 pa1 = a.verts[ea.v1], pb1 = b.verts[eb.v1];
+                Vector3 da = a.verts[ea.v2] - pa1, db = b.verts[eb.v2] - pb1;
+                Vector3 uc = da.cross(db);
+                float l2 = uc.length2();
+                if (l2 != 0) {
+                    float inv = 1.f / sqrtf(l2);
+                    Vector3 nrm = uc * inv;
+                    if (nrm.dot(pa1 - a.center) < 0.0f) nrm = -nrm;
+                    sep = nrm.dot(pb1 - pa1);
+                }
+                if (scanWins(sep, p, v, k)) { v = sep; k = p; }
+            }
+        }
+    }
+    groupArgMax(v, k);
+    if (!(v > -FLT_MAX)) return { -FLT_MAX, 0 };
+    return { v, k };
+}
+
+__device__ __forceinline__ int32_t findIncidentFace(const geometry::Plane *planes, int32_t num_faces,
+                                                    Vector3 ref_normal)
 {
     float min_dot = FLT_MAX;
     int32_t face = -1;
-    for (int32_t f = 0; f < h.hd.numFaces; f++) {
-        float d = dot(h.planes[f].normal, ref_normal);
+    for (int32_t f = 0; f < num_faces; f++) {
+        float d = dot(planes[f].normal, ref_normal);
         if (d < min_dot) { min_dot = d; face = f; }
     }
     return face;
@@ -808,6 +933,7 @@ __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
 // the group leader's clock in each phase ([8] staging, [9] faces of a,
 // [10] faces of b, [11] edge pairs, [12] contact job).
 static __device__ unsigned long long g_satStage[16];
+
 #define MW_SAT_COUNT(i) do { if (lane == 0) atomicAdd(&g_satStage[i], 1ull); } while (0)
 #define MW_SAT_TICK(i) do { if (lane == 0) { const long long t__ = wall_clock64(); \
     atomicAdd(&g_satStage[i], (unsigned long long)(t__ - prof_t)); prof_t = t__; } } while (0)
@@ -815,25 +941,37 @@ static __device__ unsigned long long g_satStage[16];
 #define MW_SAT_COUNT(i) do {} while (0)
 #define MW_SAT_TICK(i) do {} while (0)
 #endif
+#if defined(MW_SAT_CUTS)
+// Timing build only (make BUILD=build_cut EXTRA=-DMW_SAT_CUTS): with
+// mw_debug_set_sat_exp(c), c > 0, every pair is declared separated after
+// staging (1), the face queries (2), the Minkowski tables (3) or the edge
+// query (4); the phases' times by difference (eager node timing).
+static __device__ int32_t g_satExp;
+#define MW_SAT_CUT(i) do { if (g_satExp == (i)) return false; } while (0)
+#else
+#define MW_SAT_CUT(i) do {} while (0)
+#endif
 
-__device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS &g,
-                            int32_t lane, ContactJob &job)
+__device__ __forceinline__ bool hullHullSAT(const ObjDev &O, int32_t a_obj, int32_t b_obj,
+                                            const BodyPose &pa, const BodyPose &pb,
+                                            const GroupLDS &g, int32_t lane, ContactJob &job)
 {
 #if defined(MW_SAT_PROFILE)
     long long prof_t = wall_clock64();
 #endif
     MW_SAT_COUNT(0);
-    const ObjDev &O = P.objs;
-    const int32_t w = wk.world;
     HullRef ha, hb;
-    ha.hd = O.hulls[wk.aObj];
-    hb.hd = O.hulls[wk.bObj];
+    ha.hd = O.hulls[a_obj];
+    hb.hd = O.hulls[b_obj];
     ha.verts = g.vA; ha.planes = g.pA; ha.quads = g.qA;
     hb.verts = g.vB; hb.planes = g.pB; hb.quads = g.qB;
-    ha.center = stageHull(P, w, P.body[wk.aArch], wk.a.row, ha.hd, g.vA, g.pA, g.qA, lane);
-    hb.center = stageHull(P, w, P.body[wk.bArch], wk.b.row, hb.hd, g.vB, g.pB, g.qB, lane);
+    ha.center = pa.x;
+    hb.center = pb.x;
+    stageHull(O, ha.hd, pa, g.vA, g.pA, g.qA, lane);
+    stageHull(O, hb.hd, pb, g.vB, g.pB, g.qB, lane);
     groupSync();
     MW_SAT_TICK(8);
+    MW_SAT_CUT(1);
 
     const FaceQuery fa = groupFaceQuery(ha, hb, lane);
     MW_SAT_TICK(9);
@@ -841,25 +979,43 @@ __device__ bool hullHullSAT(const PhysArgs &P, const SatWork &wk, const GroupLDS
     const FaceQuery fb = groupFaceQuery(hb, ha, lane);
     MW_SAT_TICK(10);
     if (fb.separation > 0.0f) { MW_SAT_COUNT(2); return false; }
-    const EdgeQuery eq = groupEdgeQuery(ha, hb, lane);
+    MW_SAT_CUT(2);
+    EdgeQuery eq;
+    if (O.minkStride > 0) {
+        buildMinkTables(ha, hb, g.sA, g.tB, O.minkStride, lane);
+        groupSync();
+        MW_SAT_CUT(3);
+        eq = groupEdgeQueryTables(ha, hb, g.sA, g.tB, O.minkStride, lane);
+    } else {
+        eq = groupEdgeQuery(ha, hb, lane);
+    }
     MW_SAT_TICK(11);
     if (eq.separation > 0.0f) { MW_SAT_COUNT(3); return false; }
+    MW_SAT_CUT(4);
 
-    job.pair = wk;
     if (fa.separation > eq.separation || fb.separation > eq.separation) {
         const bool a_is_ref = fa.separation >= fb.separation;
         job.kind = kJobFace;
         job.refIsA = a_is_ref ? 1 : 0;
-        job.plane = a_is_ref ? fa.plane : fb.plane;
-        job.feature0 = a_is_ref ? fa.faceIdx : fb.faceIdx;
-        job.feature1 = findIncidentFace(a_is_ref ? hb : ha, job.plane.normal);
+        const int32_t ref_face = a_is_ref ? fa.faceIdx : fb.faceIdx;
+        job.plane = facePlane(a_is_ref ? ha.planes : hb.planes, ref_face);
+        job.feature0 = ref_face;
+        job.feature1 = findIncidentFace(a_is_ref ? hb.planes : ha.planes,
+                                        a_is_ref ? hb.hd.numFaces : ha.hd.numFaces, job.plane.normal);
         MW_SAT_COUNT(4);
     } else {
         job.kind = kJobEdge;
         job.refIsA = 1;
-        job.feature0 = eq.edgeA;
-        job.feature1 = eq.edgeB;
-        job.plane = geometry::Plane { eq.normal, eq.separation };
+        const int32_t nB = hb.hd.numEdges;
+        job.feature0 = nB > 0 ? eq.pair / nB : 0;
+        job.feature1 = eq.pair - job.feature0 * nB;
+        if (eq.separation > -FLT_MAX) {
+            Vector3 n;
+            const float sep = edgePairSeparation(ha, hb, job.feature0, job.feature1, &n);
+            job.plane = geometry::Plane { n, sep };
+        } else {
+            job.plane = geometry::Plane { { 0, 0, 0 }, -FLT_MAX };
+        }
         MW_SAT_COUNT(5);
     }
     MW_SAT_TICK(12);
@@ -872,6 +1028,12 @@ extern "C" int mw_debug_sat_stages(unsigned long long *out)
     unsigned long long z[16] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_satStage), sizeof(z)) != hipSuccess) return -1;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_satStage), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+#if defined(MW_SAT_CUTS)
+extern "C" int mw_debug_set_sat_exp(int32_t cut)
+{
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_satExp), &cut, sizeof(cut)) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -917,12 +1079,70 @@ __device__ __forceinline__ void sortWorldsForSolver(const PhysArgs &P, int32_t *
     __syncthreads();
 }
 
+// The SAT kernel's LDS copy of the hull tables it stages from (hulls,
+// vertices, face planes, edge quads): every pair reads a few hundred bytes
+// of them, shared by all pairs.  It follows the group staging area (or, in
+// the global-image variant, the world sort's scratch).
+__host__ __device__ inline size_t satGeoBytesFor(const ObjDev &O)
+{
+    return a16(sizeof(HullDev) * O.numObjects) + a16(sizeof(Vector3) * O.numVertsTotal) +
+           a16(sizeof(geometry::Plane) * O.numPlanesTotal) + a16(sizeof(EdgeQuad) * O.numEdgesTotal);
+}
+
+size_t satGeoSharedBytes(const PhysArgs &P)
+{
+    const size_t b = satGeoBytesFor(P.objs);
+    return b <= 16 * 1024 ? b : 0;
+}
+
+__host__ __device__ inline size_t satStageBytes(const ObjDev &O)
+{
+    return kOrderSortBytes > kGroupsPerBlock * groupLDSBytes(O) ? kOrderSortBytes
+                                                                 : kGroupsPerBlock * groupLDSBytes(O);
+}
+
+// A work entry's indices are inside the tables the SAT indexes.
+__device__ __forceinline__ bool satWorkOk(const PhysArgs &P, const SatArch *arch,
+                                          const PackedSatWork &p)
+{
+    const uint32_t a_arch = (p.slotTest >> 19) & 63u, b_arch = (p.slotTest >> 25) & 63u;
+    return (uint32_t)p.world < (uint32_t)P.numWorlds &&
+           (p.slotTest & 0xffffu) < (uint32_t)P.candCapacity &&
+           (p.objs & 0xffffu) < (uint32_t)P.objs.numObjects &&
+           (p.objs >> 16) < (uint32_t)P.objs.numObjects &&
+           a_arch < (uint32_t)P.numBodyArchs && b_arch < (uint32_t)P.numBodyArchs &&
+           (p.rows & 0xffffu) < (uint32_t)arch[a_arch].capacity &&
+           (p.rows >> 16) < (uint32_t)arch[b_arch].capacity;
+}
+
+// unpackWork with the archetypes from the LDS table.
+__device__ __forceinline__ SatWork unpackSat(const PhysArgs &P, const SatArch *arch,
+                                             const PackedSatWork &p)
+{
+    SatWork w;
+    w.world = p.world;
+    w.slot = (int32_t)(p.slotTest & 0xffffu);
+    w.test = (p.slotTest >> 16) & 7u;
+    w.aArch = (int32_t)((p.slotTest >> 19) & 63u);
+    w.bArch = (int32_t)((p.slotTest >> 25) & 63u);
+    w.pad = 0;
+    const int32_t na = P.numBodyArchs;
+    w.a = Loc { (uint32_t)(w.aArch < na ? arch[w.aArch].archetype : -1), (int32_t)(p.rows & 0xffffu) };
+    w.b = Loc { (uint32_t)(w.bArch < na ? arch[w.bArch].archetype : -1), (int32_t)(p.rows >> 16) };
+    w.aObj = (int32_t)(p.objs & 0xffffu);
+    w.bObj = (int32_t)(p.objs >> 16);
+    return w;
+}
+
 // Stage 4, persistent: each group takes hull-hull pairs off the flat list
 // and leaves its verdict in the job at the same index (kind kJobNone when
-// separated).  The grid is what is resident at once; every group reaches
-// the end of the list and exits.
+// separated: only the kind is written).  The grid is what is resident at
+// once; every group reaches the end of the list and exits.
 #ifndef MW_SAT_MIN_BLOCKS
 #define MW_SAT_MIN_BLOCKS 4
+#endif
+#ifndef MW_SAT_PIPE
+#define MW_SAT_PIPE 2        // software pipeline depth: 2, or 0 (loads at use)
 #endif
 // kGlobal: the groups' hull staging exceeds a workgroup's LDS and lives in
 // the block's slab of P.satImage (narrowSATGlobalKernel); the world sort
@@ -946,29 +1166,80 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
         __shared__ int32_t s_sort_scan[kNarrowBlock / 64];
         sortWorldsForSolver(P, (int32_t *)smem, s_sort_scan);
     }
+    ObjDev O = P.objs;
+    if (P.satGeoBytes > 0) {
+        char *dst = smem + (kGlobal ? kOrderSortBytes : satStageBytes(P.objs));
+        O.hulls = (HullDev *)stageTable(dst, P.objs.hulls, sizeof(HullDev) * O.numObjects);
+        O.vertices = (Vector3 *)stageTable(dst, P.objs.vertices, sizeof(Vector3) * O.numVertsTotal);
+        O.planes = (geometry::Plane *)stageTable(dst, P.objs.planes,
+                                                 sizeof(geometry::Plane) * O.numPlanesTotal);
+        O.edgeQuads = (EdgeQuad *)stageTable(dst, P.objs.edgeQuads, sizeof(EdgeQuad) * O.numEdgesTotal);
+    }
+    __shared__ SatArch s_arch[kMaxBodyArchetypes];
+    if (threadIdx.x < kMaxBodyArchetypes) {
+        const BodyArch &B = P.body[threadIdx.x];
+        s_arch[threadIdx.x] = SatArch { (const Vector3 *)B.cols[Cols::Position],
+                                        (const Quat *)B.cols[Cols::Rotation],
+                                        (const Diag3x3 *)B.cols[Cols::Scale], B.capacity,
+                                        B.archetype };
+    }
     __shared__ int32_t s_pre[kNarrowBins + 1];
-    loadBinPrefix(P, 0, s_pre);
+    loadBinPrefix(P, 0, s_pre);            // (its barrier publishes the tables)
     // the SAT verdicts (hhJobs) are indexed by list position: never past them
     const int32_t total = min(s_pre[kNarrowBins], P.numWorlds * P.candCapacity);
     const int32_t stride = gridDim.x * kGroupsPerBlock;
-    for (int32_t idx = blockIdx.x * kGroupsPerBlock + group; idx < total; idx += stride) {
-        const SatWork wk = unpackWork(P, P.satWork[binEntry(P, s_pre, idx, 0)]);
-        const bool ok = (uint32_t)wk.world < (uint32_t)P.numWorlds &&
-                        (uint32_t)wk.slot < (uint32_t)P.candCapacity &&
-                        (uint32_t)wk.aObj < (uint32_t)P.objs.numObjects &&
-                        (uint32_t)wk.bObj < (uint32_t)P.objs.numObjects &&
-                        (uint32_t)wk.aArch < (uint32_t)P.numBodyArchs &&
-                        (uint32_t)wk.bArch < (uint32_t)P.numBodyArchs &&
-                        (uint32_t)wk.a.row < (uint32_t)P.body[wk.aArch].capacity &&
-                        (uint32_t)wk.b.row < (uint32_t)P.body[wk.bArch].capacity;
+    // Two-deep software pipeline over the group's pairs (as the plane
+    // kernel's): while pair idx is tested, the body poses of pair
+    // idx + stride and the work entry of pair idx + 2 stride are in flight.
+    int32_t idx = blockIdx.x * kGroupsPerBlock + group;
+    PackedSatWork w1 {}, w2 {};
+    BodyPose pa1 {}, pb1 {};
+    bool ok1 = false;
+    if (MW_SAT_PIPE != 0 && idx < total) {
+        w1 = P.satWork[binEntry(P, s_pre, idx, 0)];
+        ok1 = satWorkOk(P, s_arch, w1);
+        if (ok1) {
+            pa1 = loadPose(s_arch[(w1.slotTest >> 19) & 63u], w1.world, (int32_t)(w1.rows & 0xffffu));
+            pb1 = loadPose(s_arch[(w1.slotTest >> 25) & 63u], w1.world, (int32_t)(w1.rows >> 16));
+        }
+    }
+    if (MW_SAT_PIPE != 0 && idx + stride < total) w2 = P.satWork[binEntry(P, s_pre, idx + stride, 0)];
+    for (; idx < total; idx += stride) {
+#if MW_SAT_PIPE == 0
+        w1 = P.satWork[binEntry(P, s_pre, idx, 0)];
+        ok1 = satWorkOk(P, s_arch, w1);
+        if (ok1) {
+            pa1 = loadPose(s_arch[(w1.slotTest >> 19) & 63u], w1.world, (int32_t)(w1.rows & 0xffffu));
+            pb1 = loadPose(s_arch[(w1.slotTest >> 25) & 63u], w1.world, (int32_t)(w1.rows >> 16));
+        }
+#endif
+        const PackedSatWork pw = w1;
+        const bool ok = ok1;
+        const BodyPose pa = pa1, pb = pb1;
+        if (MW_SAT_PIPE != 0 && idx + stride < total) {
+            w1 = w2;
+            ok1 = satWorkOk(P, s_arch, w1);
+            if (ok1) {
+                pa1 = loadPose(s_arch[(w1.slotTest >> 19) & 63u], w1.world, (int32_t)(w1.rows & 0xffffu));
+                pb1 = loadPose(s_arch[(w1.slotTest >> 25) & 63u], w1.world, (int32_t)(w1.rows >> 16));
+            }
+            if (idx + 2 * stride < total) w2 = P.satWork[binEntry(P, s_pre, idx + 2 * stride, 0)];
+        }
         ContactJob job;
         job.kind = kJobNone;
         if (ok) {
-            hullHullSAT(P, wk, g, lane, job);
+            hullHullSAT(O, (int32_t)(pw.objs & 0xffffu), (int32_t)(pw.objs >> 16), pa, pb, g, lane, job);
         } else if (lane == 0) {
             atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
         }
-        if (lane == 0) P.hhJobs[idx] = job;
+        if (lane == 0) {
+            if (job.kind == kJobNone) {
+                P.hhJobs[idx].kind = kJobNone;
+            } else {
+                job.pair = unpackSat(P, s_arch, pw);
+                P.hhJobs[idx] = job;
+            }
+        }
         groupSync();
     }
 }
@@ -990,9 +1261,9 @@ size_t narrowphaseImageBytes(const PhysArgs &P)
     return kGroupsPerBlock * groupLDSBytes(P.objs);
 }
 
-size_t narrowphaseGlobalSharedBytes(const PhysArgs &)
+size_t narrowphaseGlobalSharedBytes(const PhysArgs &P)
 {
-    return kOrderSortBytes;
+    return kOrderSortBytes + P.satGeoBytes;
 }
 
 __host__ __device__ inline size_t contactLDSBytes(int32_t clip_cap)
@@ -1033,8 +1304,8 @@ __device__ __forceinline__ void narrowContactBlock(const PhysArgs &P)
     const int32_t total = min(s_pre[kNarrowBins], P.numWorlds * P.candCapacity);
     for (int32_t i = blockIdx.x * kContactBlock + threadIdx.x; i < total;
          i += gridDim.x * kContactBlock) {
+        if (P.hhJobs[i].kind == kJobNone) continue;   // separated: only the kind was written
         const ContactJob job = P.hhJobs[i];
-        if (job.kind == kJobNone) continue;
         const SatWork &wk = job.pair;
         if ((uint32_t)wk.world >= (uint32_t)P.numWorlds || (uint32_t)wk.slot >= (uint32_t)P.candCapacity ||
             (uint32_t)wk.aObj >= (uint32_t)P.objs.numObjects || (uint32_t)wk.bObj >= (uint32_t)P.objs.numObjects) {

@@ -32,6 +32,10 @@ namespace madrona::phys {
 using namespace math;
 using namespace base;
 
+#if defined(MW_SAT_CUTS)
+static const PhysArgs *g_cutArgs = nullptr;     // mw_debug_time_sat
+#endif
+
 
 PhysicsModule::~PhysicsModule()
 {
@@ -85,7 +89,16 @@ void PhysicsModule::upload(void *stream_ptr)
         P.overlapImage = alloc<char>((size_t)W * findOverlapsImageBytes(P), stream_ptr);
     }
 
-    // SAT: persistent grid of exactly the blocks that can be resident
+    // SAT: persistent grid of exactly the blocks that can be resident (hull
+    // tables in LDS up to 16 KB, else read from HBM; from HBM under
+    // MADRONA_MW_FORCE_GLOBAL_IMAGES, so the fallback tests cover both)
+    P.satGeoBytes = force ? 0 : (int32_t)satGeoSharedBytes(P);
+#if defined(MW_SAT_CUTS)
+    g_cutArgs = &args;
+#endif
+    // MADRONA_MW_SAT_TABLES=0: the SAT edge query without its Minkowski-test
+    // tables (the per-pair form; parity tests of both)
+    if (const char *t = std::getenv("MADRONA_MW_SAT_TABLES"); t && t[0] == '0') P.objs.minkStride = 0;
     P.satImage = nullptr;
     P.satImageBlocks = 0;
     if (fitsLDS((const void *)&narrowSATKernel, kNarrowBlock, narrowphaseSharedBytes(P))) {
@@ -281,6 +294,36 @@ static PhysArgs substepArgs(const PhysArgs &P, int32_t i, bool reset_next)
     Q.nextSatWorkCount = reset_next || i > 0 ? P.satWorkCountSet[(i + 1) & 1] : nullptr;
     return Q;
 }
+
+#if defined(MW_SAT_CUTS)
+// Timing build only (narrowphase.hip MW_SAT_CUTS): the SAT kernel relaunched
+// `reps` times on the list substep `substep` of the last step read, cut after
+// phase `cut` (0: whole SAT); the mean ms per launch.  The relaunches rewrite
+// hhJobs and solverOrder only (rewritten again before their next reads) and
+// reset no list.
+extern "C" int mw_debug_set_sat_exp(int32_t cut);
+extern "C" double mw_debug_time_sat(int32_t cut, int32_t reps, int32_t substep)
+{
+    if (!g_cutArgs || g_cutArgs->satImage) return -1.0;
+    PhysArgs Q = substepArgs(*g_cutArgs, substep, false);
+    Q.nextSatWorkCount = nullptr;
+    if (hipDeviceSynchronize() != hipSuccess || mw_debug_set_sat_exp(cut) != 0) return -1.0;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a, nullptr);
+    for (int32_t r = 0; r < reps; r++)
+        hipLaunchKernelGGL(narrowSATKernel, dim3(Q.satGrid), dim3(kNarrowBlock),
+                           narrowphaseSharedBytes(Q), nullptr, Q);
+    (void)hipEventRecord(b, nullptr);
+    float ms = -1.f;
+    if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = -1.f;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    mw_debug_set_sat_exp(0);
+    return ms / reps;
+}
+#endif
 
 // substepRigidBodies.  Substeps after the first are integrated by the
 // previous substep's solver kernel as it writes its bodies back (fused: the

@@ -515,6 +515,7 @@ size_t findOverlapsSharedBytes(const PhysArgs &P);
 size_t refitSharedBytes(const PhysArgs &P);
 size_t solverSharedBytes(const PhysArgs &P);
 size_t narrowphaseSharedBytes(const PhysArgs &P);
+size_t satGeoSharedBytes(const PhysArgs &P);
 size_t contactSharedBytes(const PhysArgs &P);
 size_t planeSharedBytes(const PhysArgs &P);
 // Global-image variants: dynamic LDS they still use, and image bytes per

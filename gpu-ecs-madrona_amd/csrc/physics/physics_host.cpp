@@ -219,6 +219,7 @@ void PhysicsModule::buildArgs(void *stream)
         O.maxFaces = std::max(O.maxFaces, h.numFaces);
         O.maxEdges = std::max(O.maxEdges, h.numEdges);
     }
+    O.minkStride = O.maxEdges * O.maxFaces <= 128 ? O.maxFaces : 0;
     O.metadata = upload(metadata, stream);
     O.aabbs = upload(aabbs, stream);
     O.types = upload(types, stream);
@@ -233,6 +234,7 @@ void PhysicsModule::buildArgs(void *stream)
     O.numPlanesTotal = (int32_t)planes.size();
     O.numHedgesTotal = (int32_t)hedges.size();
     O.numPolygonsTotal = (int32_t)polygons.size();
+    O.numEdgesTotal = (int32_t)edgeQuads.size();
 
     P.bodyBoxes = alloc<BodyBox>((size_t)W * std::max(P.maxBodiesPerWorld, 1), stream);
     P.survInfo = alloc<uint32_t>((size_t)W * P.candCapacity, stream);

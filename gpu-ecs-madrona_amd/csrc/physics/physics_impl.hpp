@@ -58,7 +58,11 @@ struct ObjDev {
     uint32_t *polygons;           // half-edge index per face
     EdgeQuad *edgeQuads;          // per edge (same offsets as edges)
     // table sizes (entries), for the kernels that stage the geometry in LDS
-    int32_t numVertsTotal, numPlanesTotal, numHedgesTotal, numPolygonsTotal;
+    int32_t numVertsTotal, numPlanesTotal, numHedgesTotal, numPolygonsTotal, numEdgesTotal;
+    // SAT edge query: row stride (maxFaces) of the per-pair Minkowski-test
+    // tables in the group's staging area, 0 when they would not fit
+    // (maxEdges x maxFaces > 128) and the test is evaluated per edge pair
+    int32_t minkStride;
 };
 
 inline constexpr int32_t kMaxBodyArchetypes = 4;
@@ -189,6 +193,8 @@ struct PhysArgs {
                                   // them from HBM; tables too large)
     int32_t clipCap;              // clip polygon capacity (2 x largest face)
     int32_t satGrid;              // persistent SAT grid (blocks)
+    int32_t satGeoBytes;          // SAT kernel's LDS copy of the hull tables (0: read
+                                  // them from HBM; tables too large)
     int32_t planeGrid;            // persistent plane-contact grid (blocks)
     Contact *candContacts;        // [W][candCapacity] manifold per survivor slot
     int32_t maxContacts;          // SolverData::maxContacts (reference assert)

@@ -718,14 +718,16 @@ extern "C" int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t 
     MW_TRY({
         phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
         if (!P || !out) return -1;
-        int32_t v[6];
+        int32_t v[8];
         v[0] = P->refitGlobal != 0;
         v[1] = P->overlapImage != nullptr;
         v[2] = P->satImage != nullptr;
         v[3] = P->clipImage != nullptr;
         v[4] = P->solverImage != nullptr;
         v[5] = P->planeGeoBytes > 0;
-        for (int32_t i = 0; i < n && i < 6; i++) out[i] = v[i];
-        return 6;
+        v[6] = P->satGeoBytes > 0;
+        v[7] = P->objs.minkStride > 0;
+        for (int32_t i = 0; i < n && i < 8; i++) out[i] = v[i];
+        return 8;
     }, -1)
 }

@@ -686,11 +686,12 @@ class CollisionsSim(Executor):
 
     def kernel_variants(self):
         """{kernel: True when it runs its global-image variant} (mw_create
-        decides per LDS image; plane_lds: the plane kernel's LDS hull tables)."""
-        out = np.zeros(6, np.int32)
-        if self._lib.mw_phys_kernel_variants(self.h, out.ctypes.data_as(ctypes.c_void_p), 6) < 0:
+        decides per LDS image; plane_lds / sat_lds: the plane / SAT kernel's
+        LDS hull tables; sat_mink: the SAT edge query's Minkowski tables)."""
+        out = np.zeros(8, np.int32)
+        if self._lib.mw_phys_kernel_variants(self.h, out.ctypes.data_as(ctypes.c_void_p), 8) < 0:
             raise _err(self._lib)
-        keys = ("refit", "find_overlaps", "sat", "contact", "solver", "plane_lds")
+        keys = ("refit", "find_overlaps", "sat", "contact", "solver", "plane_lds", "sat_lds", "sat_mink")
         return {k: bool(v) for k, v in zip(keys, out)}
 
     def bvh(self, w, cap=4096):

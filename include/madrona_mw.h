@@ -233,8 +233,11 @@ int32_t mw_phys_take_units(mw_exec *exec, int64_t *out);
 /* Which variant of each LDS-staging physics kernel the executor runs (mw_create
  * picks it: a world / hull image that does not fit a workgroup's LDS moves to
  * a global slab, same results).  out[0..5] = 1 for: refit on the global node
- * slab, findOverlaps / SAT / contact / solver with a global image, and (last)
- * the plane kernel's LDS hull tables.  Returns 6, or -1 without physics.
+ * slab, findOverlaps / SAT / contact / solver with a global image, then the
+ * plane kernel's and the SAT kernel's LDS hull tables, and (last) the SAT
+ * edge query's Minkowski-test tables (hulls small enough; environment
+ * MADRONA_MW_SAT_TABLES=0 at mw_create turns them off).  Returns 8, or -1
+ * without physics.
  * MADRONA_MW_FORCE_GLOBAL_IMAGES=1 at mw_create forces the global variants. */
 int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t n);
 

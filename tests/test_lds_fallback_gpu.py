@@ -94,6 +94,28 @@ def test_forced_global_images_bit_exact(monkeypatch):
     _lockstep(sim, orc, W, 40)
 
 
+@pytest.mark.parametrize("tables", ["1", "0"])
+def test_sat_edge_query_forms_bit_exact(monkeypatch, tables):
+    """The SAT edge query's two forms (narrowphase.hip groupEdgeQueryTables:
+    the Minkowski-test dot products tabulated per (edge, face), passes
+    compacted per lane; groupEdgeQuery: the test per edge pair) on cube
+    worlds and on a cube + wedge hull set: the same bits as the oracle every
+    step (MADRONA_MW_SAT_TABLES=0 selects the per-pair form)."""
+    monkeypatch.setenv("MADRONA_MW_SAT_TABLES", tables)
+    W, n = 4, 128
+    pos, rot = gen_collisions_inits(W, n, seed=11)
+    sim, orc = _pair(W, n, pos, rot)
+    v = sim.kernel_variants()
+    assert v["sat_mink"] == (tables == "1") and v["sat_lds"], v
+    _lockstep(sim, orc, W, 30)
+
+    W, n = 3, 24
+    pos, rot = gen_collisions_inits(W, n, seed=7)
+    sim, orc = _pair(W, n, pos, rot, names=("cube", "wedge"))
+    assert sim.kernel_variants()["sat_mink"] == (tables == "1")
+    _lockstep(sim, orc, W, 40)
+
+
 def _grid_world(W, n, spacing=3.0, z=0.95):
     side = int(np.ceil(np.sqrt(n)))
     pos = np.zeros((W, n, 3), np.float32)

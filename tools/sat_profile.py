@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
-"""SAT stage profile (experiment tool) with the profiling build:
+"""SAT stage profile (experiment tool).
   make -C gpu-ecs-madrona_amd BUILD=build_prof EXTRA=-DMW_SAT_PROFILE
   MADRONA_MW_LIB=gpu-ecs-madrona_amd/build_prof/libmadrona_mw.so python tools/sat_profile.py [simple|collisions]
-Where the hull-hull SAT of each pair ends and the group leader's clock per
-phase, over 10 settled steps."""
+      where the hull-hull SAT of each pair ends and the group leader's clock
+      per phase over 10 settled steps (the counters' atomics slow the kernel
+      several-fold: shares only);
+  make -C gpu-ecs-madrona_amd BUILD=build_cut EXTRA=-DMW_SAT_CUTS
+  MADRONA_MW_LIB=gpu-ecs-madrona_amd/build_cut/libmadrona_mw.so python tools/sat_profile.py [simple|collisions] --cuts
+      NarrowphaseNode time with the SAT cut after each phase."""
 import ctypes
 import os
 import sys
@@ -23,9 +27,18 @@ def main():
     pos, rot = mw.gen_collisions_inits(W, n, seed=0)
     sim = (mw.SimpleSim if wl == "simple" else mw.CollisionsSim)(W, pos, rot, cfg)
     lib = mw.library()
+    sim.step(130)
+    if "--cuts" in sys.argv:
+        lib.mw_debug_time_sat.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+        lib.mw_debug_time_sat.restype = ctypes.c_double
+        sim.sync()
+        names = ["full", "staging", "+faces", "+tables", "+edges", "full"]
+        for cut, nm in zip((0, 1, 2, 3, 4, 0), names):
+            ms = lib.mw_debug_time_sat(cut, 20, 3)
+            print(f"narrowSATKernel cut {cut} ({nm:8s}) {ms:.4f} ms/launch (last substep's list, 20 launches)")
+        return
     lib.mw_debug_sat_stages.argtypes = [ctypes.c_void_p]
     out = np.zeros(16, np.uint64)
-    sim.step(130)
     lib.mw_debug_sat_stages(out.ctypes.data_as(ctypes.c_void_p))
     sim.step(10)
     lib.mw_debug_sat_stages(out.ctypes.data_as(ctypes.c_void_p))
