@@ -120,15 +120,29 @@ struct GroupLDS {
     float *tB;                     // [maxEdges][minkStride]: edge j of b x face f of a
 };
 
+#ifndef MW_SAT_BANK_PAD
+#define MW_SAT_BANK_PAD 1
+#endif
+
 __host__ __device__ inline size_t minkTableBytes(const ObjDev &O)
 {
     return a16(sizeof(float) * O.maxEdges * O.minkStride);
 }
 
+// A group's staging area, padded to 16 B past a multiple of 128 B: the
+// groups of a wave read the same element of their own hulls together, and
+// with areas a multiple of 128 B apart those reads all fall on one LDS bank
+// (4-way conflicts in each 32-lane half); 16 B more per group puts
+// consecutive groups 4 banks apart.
 __host__ __device__ inline size_t groupLDSBytes(const ObjDev &O)
 {
-    return 2 * a16(sizeof(Vector3) * O.maxVerts) + 2 * a16(sizeof(geometry::Plane) * O.maxFaces) +
-           2 * a16(sizeof(EdgeQuad) * O.maxEdges) + 2 * minkTableBytes(O);
+    const size_t raw = 2 * a16(sizeof(Vector3) * O.maxVerts) + 2 * a16(sizeof(geometry::Plane) * O.maxFaces) +
+                       2 * a16(sizeof(EdgeQuad) * O.maxEdges) + 2 * minkTableBytes(O);
+#if MW_SAT_BANK_PAD
+    return raw + (16 + 128 - raw % 128) % 128;
+#else
+    return raw;
+#endif
 }
 
 // The group staging area; block 0 first uses it for the solver's world
@@ -212,21 +226,48 @@ __device__ __forceinline__ BodyPose loadPose(const SatArch &A, int32_t w, int32_
 
 // Transform one body's hull into the group's LDS and copy its edge topology
 // (hullXform / worldVertex / worldPlane, the same operations).
+// `first` / `step`: the lanes of the group that stage this hull.
 __device__ __forceinline__ void stageHull(const ObjDev &O, const HullDev &hd, const BodyPose &p,
                                           Vector3 *v, geometry::Plane *pl, EdgeQuad *q,
-                                          int32_t lane)
+                                          int32_t first, int32_t step)
 {
     const Mat3x3 unscaled_rot = Mat3x3::fromQuat(p.q);
     const HullXform xf { unscaled_rot * p.s, unscaled_rot * p.s.inv(), p.x };
-    for (int32_t i = lane; i < hd.numVerts; i += kGroup)
+    for (int32_t i = first; i < hd.numVerts; i += step)
         v[i] = xf.vtx * O.vertices[hd.vertOffset + i] + xf.x;
-    for (int32_t i = lane; i < hd.numFaces; i += kGroup) {
+    for (int32_t i = first; i < hd.numFaces; i += step) {
         const geometry::Plane op = O.planes[hd.faceOffset + i];
         const Vector3 origin = xf.vtx * (op.normal * op.d) + xf.x;
         const Vector3 n = (xf.nrm * op.normal).normalize();
         pl[i] = geometry::Plane { n, dot(n, origin) };
     }
-    for (int32_t i = lane; i < hd.numEdges; i += kGroup) q[i] = O.edgeQuads[hd.edgeOffset + i];
+    for (int32_t i = first; i < hd.numEdges; i += step) q[i] = O.edgeQuads[hd.edgeOffset + i];
+}
+
+// Both hulls of a pair staged at once: the group's first half transforms
+// hull a, the second half hull b, so each lane builds one hull transform
+// instead of two (the inputs are picked per lane field by field; selecting
+// whole aggregates would go through scratch).
+__device__ __forceinline__ void stagePair(const ObjDev &O, const HullRef &ha, const HullRef &hb,
+                                          const BodyPose &pa, const BodyPose &pb, const GroupLDS &g,
+                                          int32_t lane)
+{
+    constexpr int32_t kHalf = kGroup / 2;
+    const bool second = lane >= kHalf;
+    HullDev hd;
+    hd.vertOffset = second ? hb.hd.vertOffset : ha.hd.vertOffset;
+    hd.numVerts = second ? hb.hd.numVerts : ha.hd.numVerts;
+    hd.faceOffset = second ? hb.hd.faceOffset : ha.hd.faceOffset;
+    hd.numFaces = second ? hb.hd.numFaces : ha.hd.numFaces;
+    hd.edgeOffset = second ? hb.hd.edgeOffset : ha.hd.edgeOffset;
+    hd.numEdges = second ? hb.hd.numEdges : ha.hd.numEdges;
+    BodyPose p;
+    p.x = Vector3 { second ? pb.x.x : pa.x.x, second ? pb.x.y : pa.x.y, second ? pb.x.z : pa.x.z };
+    p.q = Quat { second ? pb.q.w : pa.q.w, second ? pb.q.x : pa.q.x, second ? pb.q.y : pa.q.y,
+                 second ? pb.q.z : pa.q.z };
+    p.s = Diag3x3 { second ? pb.s.d0 : pa.s.d0, second ? pb.s.d1 : pa.s.d1, second ? pb.s.d2 : pa.s.d2 };
+    stageHull(O, hd, p, second ? g.vB : g.vA, second ? g.pB : g.pA, second ? g.qB : g.qA,
+              second ? lane - kHalf : lane, kHalf);
 }
 
 __device__ __forceinline__ float hullDistFromPlane(const geometry::Plane &p, const HullRef &h)
@@ -251,7 +292,7 @@ struct FaceQuery {
 // first face with positive distance; any positive result rejects the pair,
 // so the group evaluates every face and only the non-positive case needs the
 // serial argmax, which groupArgMax reproduces.
-__device__ FaceQuery groupFaceQuery(const HullRef &a, const HullRef &b, int32_t lane)
+__device__ __forceinline__ FaceQuery groupFaceQuery(const HullRef &a, const HullRef &b, int32_t lane)
 {
     float v = __builtin_nanf("");
     int32_t k = INT32_MAX;
@@ -399,25 +440,38 @@ __device__ __forceinline__ void buildMinkTables(const HullRef &a, const HullRef 
 // lanes whose pair passed; here a lane runs it only for its own passes.
 // The (separation, p) scan sees the same values in the same order, the
 // failed pairs' -FLT_MAX included.
-__device__ EdgeQuery groupEdgeQueryTables(const HullRef &a, const HullRef &b, const float *sA,
+__device__ __forceinline__ EdgeQuery groupEdgeQueryTables(const HullRef &a, const HullRef &b, const float *sA,
                                           const float *tB, int32_t stride, int32_t lane)
 {
     const int32_t nA = a.hd.numEdges, nB = b.hd.numEdges, n = nA * nB;
     float v = __builtin_nanf("");
     int32_t k = INT32_MAX;
     if (nB > 0) {
+        // (i, j) of p = lane, lane + kGroup, ...: each step adds (di, dj)
+        // with a carry; the table rows follow incrementally
+        const int32_t di = kGroup / nB, dj = kGroup - di * nB;
         int32_t i = lane / nB, j = lane - (lane / nB) * nB;
+        int32_t irow = i * stride, jrow = j * stride;
         for (int32_t base = lane; base < n; base += 32 * kGroup) {
             uint32_t pass = 0;
             int32_t t = 0;
             for (int32_t p = base; p < n && t < 32; p += kGroup, t++) {
                 const EdgeQuad ea = a.quads[i], eb = b.quads[j];
-                const float *si = sA + i * stride, *tj = tB + j * stride;
-                const float cba = si[eb.face1], dba = si[eb.face2];
-                const float adc = tj[ea.face1], bdc = tj[ea.face2];
-                if (cba * dba < 0.0f && adc * bdc < 0.0f && cba * bdc > 0.0f) pass |= 1u << t;
-                j += kGroup;
-                while (j >= nB) { j -= nB; i++; }
+                const float cba = sA[irow + eb.face1], dba = sA[irow + eb.face2];
+                const float adc = tB[jrow + ea.face1], bdc = tB[jrow + ea.face2];
+                // all three products, no short circuit: the same verdict
+                const bool m = (cba * dba < 0.0f) & (adc * bdc < 0.0f) & (cba * bdc > 0.0f);
+                pass |= (uint32_t)m << t;
+                i += di;
+                j += dj;
+                irow += di * stride;
+                jrow += dj * stride;
+                if (j >= nB) {
+                    j -= nB;
+                    jrow -= nB * stride;
+                    i++;
+                    irow += stride;
+                }
             }
             // failed pairs score -FLT_MAX: the scan keeps the first of them
             const uint32_t all = t == 32 ? ~0u : (1u << t) - 1u;
@@ -804,7 +858,24 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
             S = 0;
             break;
         }
-        int32_t hpos = s_base[0] + ((off >> 10) & 1023);
+        // hull-hull pairs whose last SAT passed the face queries (satHint)
+        // take the back of the chunk's reservation, the others its front
+        const int32_t thh = (total >> 10) & 1023;
+        int32_t heavy = 0;
+        {
+            int32_t sl = S + (off & 1023);
+#pragma unroll
+            for (int32_t j = 0; j < kFilterPer; j++) {
+                if (!keep[j]) continue;
+                if (wk[j].test == kHull && P.satHint && P.satHint[(size_t)w * cap + sl] != 0)
+                    heavy |= 1 << j;
+                sl++;
+            }
+        }
+        int32_t heavy_total;
+        const int32_t hoff = blockExclusiveScan(__popc((uint32_t)heavy), s_scan, &heavy_total);
+        int32_t lpos = s_base[0] + ((off >> 10) & 1023) - hoff;      // light pairs before mine
+        int32_t hpos = s_base[0] + thh - 1 - hoff;
         int32_t ppos = s_base[1] + (off >> 20);
         int32_t slot = S + (off & 1023);
 #pragma unroll
@@ -813,7 +884,8 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
             wk[j].slot = slot;
             info[slot] = kNoManifold;
             if (wk[j].test == kHull) {
-                list[hpos++] = packWork(wk[j]);
+                if ((heavy >> j) & 1) list[hpos--] = packWork(wk[j]);
+                else list[lpos++] = packWork(wk[j]);
             } else if (wk[j].test == kHullPlane) {
                 *(list_back - ppos++) = packWork(wk[j]);
             }
@@ -922,10 +994,6 @@ __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
     }
 }
 
-// Hull-hull SAT (doSAT, narrowphase.cpp:678-758) for one pair on one group.
-// Returns true (on every lane of the group) if the pair is not separated;
-// the leader's `job` then holds createFaceContact's / createEdgeContact's
-// inputs.
 #if defined(MW_SAT_PROFILE)
 // Profiling build only (make BUILD=build_prof EXTRA=-DMW_SAT_PROFILE): per
 // hull-hull pair, where the SAT ended ([0] pairs, [1] separated by a face of
@@ -947,50 +1015,57 @@ static __device__ unsigned long long g_satStage[16];
 // staging (1), the face queries (2), the Minkowski tables (3) or the edge
 // query (4); the phases' times by difference (eager node timing).
 static __device__ int32_t g_satExp;
-#define MW_SAT_CUT(i) do { if (g_satExp == (i)) return false; } while (0)
+#define MW_SAT_CUT(i) do { if (g_satExp == (i)) return kSatFaceSeparated; } while (0)
 #else
 #define MW_SAT_CUT(i) do {} while (0)
 #endif
 
-__device__ __forceinline__ bool hullHullSAT(const ObjDev &O, int32_t a_obj, int32_t b_obj,
-                                            const BodyPose &pa, const BodyPose &pb,
-                                            const GroupLDS &g, int32_t lane, ContactJob &job)
+#ifndef MW_SAT_SPLIT_STAGE
+#define MW_SAT_SPLIT_STAGE 0
+#endif
+
+// How a pair's SAT ended (satHint: the pairs that got past the face queries
+// are the expensive ones).
+enum : int32_t { kSatFaceSeparated = 0, kSatEdgeSeparated = 1, kSatContact = 2 };
+
+// The SAT of one pair after its hulls are known (doSAT, narrowphase.cpp:
+// 678-758): staging, face queries, edge query, contact job.  `stride` is the
+// Minkowski tables' row stride (0: the per-pair edge query).
+__device__ __forceinline__ int32_t satPair(const ObjDev &O, const HullRef &ha, const HullRef &hb,
+                                        const BodyPose &pa, const BodyPose &pb, const GroupLDS &g,
+                                        int32_t stride, int32_t lane, ContactJob &job)
 {
 #if defined(MW_SAT_PROFILE)
     long long prof_t = wall_clock64();
 #endif
-    MW_SAT_COUNT(0);
-    HullRef ha, hb;
-    ha.hd = O.hulls[a_obj];
-    hb.hd = O.hulls[b_obj];
-    ha.verts = g.vA; ha.planes = g.pA; ha.quads = g.qA;
-    hb.verts = g.vB; hb.planes = g.pB; hb.quads = g.qB;
-    ha.center = pa.x;
-    hb.center = pb.x;
-    stageHull(O, ha.hd, pa, g.vA, g.pA, g.qA, lane);
-    stageHull(O, hb.hd, pb, g.vB, g.pB, g.qB, lane);
+#if MW_SAT_SPLIT_STAGE
+    stagePair(O, ha, hb, pa, pb, g, lane);
+#else
+    stageHull(O, ha.hd, pa, g.vA, g.pA, g.qA, lane, kGroup);
+    stageHull(O, hb.hd, pb, g.vB, g.pB, g.qB, lane, kGroup);
+#endif
     groupSync();
     MW_SAT_TICK(8);
     MW_SAT_CUT(1);
 
     const FaceQuery fa = groupFaceQuery(ha, hb, lane);
     MW_SAT_TICK(9);
-    if (fa.separation > 0.0f) { MW_SAT_COUNT(1); return false; }
+    if (fa.separation > 0.0f) { MW_SAT_COUNT(1); return kSatFaceSeparated; }
     const FaceQuery fb = groupFaceQuery(hb, ha, lane);
     MW_SAT_TICK(10);
-    if (fb.separation > 0.0f) { MW_SAT_COUNT(2); return false; }
+    if (fb.separation > 0.0f) { MW_SAT_COUNT(2); return kSatFaceSeparated; }
     MW_SAT_CUT(2);
     EdgeQuery eq;
-    if (O.minkStride > 0) {
-        buildMinkTables(ha, hb, g.sA, g.tB, O.minkStride, lane);
+    if (stride > 0) {
+        buildMinkTables(ha, hb, g.sA, g.tB, stride, lane);
         groupSync();
         MW_SAT_CUT(3);
-        eq = groupEdgeQueryTables(ha, hb, g.sA, g.tB, O.minkStride, lane);
+        eq = groupEdgeQueryTables(ha, hb, g.sA, g.tB, stride, lane);
     } else {
         eq = groupEdgeQuery(ha, hb, lane);
     }
     MW_SAT_TICK(11);
-    if (eq.separation > 0.0f) { MW_SAT_COUNT(3); return false; }
+    if (eq.separation > 0.0f) { MW_SAT_COUNT(3); return kSatEdgeSeparated; }
     MW_SAT_CUT(4);
 
     if (fa.separation > eq.separation || fb.separation > eq.separation) {
@@ -1019,7 +1094,47 @@ __device__ __forceinline__ bool hullHullSAT(const ObjDev &O, int32_t a_obj, int3
         MW_SAT_COUNT(5);
     }
     MW_SAT_TICK(12);
-    return true;
+    return kSatContact;
+}
+
+
+#ifndef MW_SAT_BOX
+#define MW_SAT_BOX 1
+#endif
+
+__device__ __forceinline__ bool isBoxHull(const HullDev &h)
+{
+    return h.numVerts == 8 && h.numFaces == 6 && h.numEdges == 12;
+}
+
+// Hull-hull SAT (doSAT, narrowphase.cpp:678-758) for one pair on one
+// group.  Returns how it ended (on every lane of the group); for
+// kSatContact the leader's `job` holds createFaceContact's /
+// createEdgeContact's inputs.  A pair of box hulls
+// (8 vertices, 6 faces, 12 edges: every pair of the benchmarks) runs a copy
+// of satPair with those counts as constants -- its loops unrolled, the same
+// operations in the same order.
+__device__ __forceinline__ int32_t hullHullSAT(const ObjDev &O, int32_t a_obj, int32_t b_obj,
+                                            const BodyPose &pa, const BodyPose &pb,
+                                            const GroupLDS &g, int32_t lane, ContactJob &job)
+{
+    MW_SAT_COUNT(0);
+    HullRef ha, hb;
+    ha.hd = O.hulls[a_obj];
+    hb.hd = O.hulls[b_obj];
+    ha.verts = g.vA; ha.planes = g.pA; ha.quads = g.qA;
+    hb.verts = g.vB; hb.planes = g.pB; hb.quads = g.qB;
+    ha.center = pa.x;
+    hb.center = pb.x;
+#if MW_SAT_BOX
+    if (O.minkStride >= 6 && isBoxHull(ha.hd) && isBoxHull(hb.hd)) {
+        ha.hd.numVerts = hb.hd.numVerts = 8;
+        ha.hd.numFaces = hb.hd.numFaces = 6;
+        ha.hd.numEdges = hb.hd.numEdges = 12;
+        return satPair(O, ha, hb, pa, pb, g, 6, lane, job);
+    }
+#endif
+    return satPair(O, ha, hb, pa, pb, g, O.minkStride, lane, job);
 }
 
 #if defined(MW_SAT_PROFILE)
@@ -1142,7 +1257,7 @@ __device__ __forceinline__ SatWork unpackSat(const PhysArgs &P, const SatArch *a
 #define MW_SAT_MIN_BLOCKS 4
 #endif
 #ifndef MW_SAT_PIPE
-#define MW_SAT_PIPE 2        // software pipeline depth: 2, or 0 (loads at use)
+#define MW_SAT_PIPE 0        // software pipeline depth: 0 (loads at use) or 2
 #endif
 // kGlobal: the groups' hull staging exceeds a workgroup's LDS and lives in
 // the block's slab of P.satImage (narrowSATGlobalKernel); the world sort
@@ -1228,11 +1343,15 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
         ContactJob job;
         job.kind = kJobNone;
         if (ok) {
-            hullHullSAT(O, (int32_t)(pw.objs & 0xffffu), (int32_t)(pw.objs >> 16), pa, pb, g, lane, job);
+            const int32_t how = hullHullSAT(O, (int32_t)(pw.objs & 0xffffu), (int32_t)(pw.objs >> 16),
+                                            pa, pb, g, lane, job);
+            if (lane == 0 && P.hhJobs && P.satHint)
+                P.satHint[(size_t)pw.world * P.candCapacity + (pw.slotTest & 0xffffu)] =
+                    how != kSatFaceSeparated;
         } else if (lane == 0) {
             atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
         }
-        if (lane == 0) {
+        if (lane == 0 && P.hhJobs) {
             if (job.kind == kJobNone) {
                 P.hhJobs[idx].kind = kJobNone;
             } else {

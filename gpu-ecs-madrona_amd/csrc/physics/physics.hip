@@ -99,6 +99,9 @@ void PhysicsModule::upload(void *stream_ptr)
     // MADRONA_MW_SAT_TABLES=0: the SAT edge query without its Minkowski-test
     // tables (the per-pair form; parity tests of both)
     if (const char *t = std::getenv("MADRONA_MW_SAT_TABLES"); t && t[0] == '0') P.objs.minkStride = 0;
+    // MADRONA_MW_SAT_HINTS=0: work lists in candidate order, without the
+    // last SAT's outcome ordering them (satHint; A/B and parity of both)
+    if (const char *t = std::getenv("MADRONA_MW_SAT_HINTS"); t && t[0] == '0') P.satHint = nullptr;
     P.satImage = nullptr;
     P.satImageBlocks = 0;
     if (fitsLDS((const void *)&narrowSATKernel, kNarrowBlock, narrowphaseSharedBytes(P))) {
@@ -299,14 +302,15 @@ static PhysArgs substepArgs(const PhysArgs &P, int32_t i, bool reset_next)
 // Timing build only (narrowphase.hip MW_SAT_CUTS): the SAT kernel relaunched
 // `reps` times on the list substep `substep` of the last step read, cut after
 // phase `cut` (0: whole SAT); the mean ms per launch.  The relaunches rewrite
-// hhJobs and solverOrder only (rewritten again before their next reads) and
-// reset no list.
+// solverOrder only (rewritten again before its next read), write no
+// verdict and reset no list.
 extern "C" int mw_debug_set_sat_exp(int32_t cut);
 extern "C" double mw_debug_time_sat(int32_t cut, int32_t reps, int32_t substep)
 {
     if (!g_cutArgs || g_cutArgs->satImage) return -1.0;
     PhysArgs Q = substepArgs(*g_cutArgs, substep, false);
     Q.nextSatWorkCount = nullptr;
+    Q.hhJobs = nullptr;                // no verdicts written
     if (hipDeviceSynchronize() != hipSuccess || mw_debug_set_sat_exp(cut) != 0) return -1.0;
     hipEvent_t a, b;
     (void)hipEventCreate(&a);

@@ -15,12 +15,14 @@ for lib in build ${TEST_LIBS}; do
     if [ $rc -gt 1 ]; then exit $rc; fi
 done
 python -u tools/ab_bench.py --workload simple --out gpurun_out/${T} $VARIANTS || exit $?
-if [ -f gpu-ecs-madrona_amd/build_cut/libmadrona_mw.so ]; then
+for cut in ${CUT_LIBS:-build_cut}; do
+    [ -f gpu-ecs-madrona_amd/$cut/libmadrona_mw.so ] || continue
     for wl in simple collisions; do
-        MADRONA_MW_LIB=gpu-ecs-madrona_amd/build_cut/libmadrona_mw.so timeout -k 10 120 \
-            python -u tools/sat_profile.py $wl --cuts > gpurun_out/${T}_cuts_$wl.txt 2>&1
+        echo "== $cut $wl"
+        MADRONA_MW_LIB=gpu-ecs-madrona_amd/$cut/libmadrona_mw.so timeout -k 10 120 \
+            python -u tools/sat_profile.py $wl --cuts > gpurun_out/${T}_${cut}_$wl.txt 2>&1
         rc=$?
-        grep -v amdgpu.ids gpurun_out/${T}_cuts_$wl.txt
+        grep -v amdgpu.ids gpurun_out/${T}_${cut}_$wl.txt
         [ $rc -eq 0 ] || exit $rc
     done
-fi
+done
