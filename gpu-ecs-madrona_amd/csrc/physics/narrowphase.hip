@@ -48,6 +48,17 @@ __global__ void __launch_bounds__(256) integrateKernel(PhysArgs P)
 #define MW_SAT_GROUP 8
 #endif
 constexpr int32_t kGroup = MW_SAT_GROUP;               // lanes per hull-hull pair
+#if defined(MW_SAT_CUTS)
+// Timing build only (make BUILD=build_cut EXTRA=-DMW_SAT_CUTS): with
+// mw_debug_set_sat_exp(c), c > 0, every pair is declared separated after
+// staging (1), the face queries (2), the Minkowski tables (3), the edge
+// query's pass masks (5) or the whole edge query (4); the phases' times by
+// difference (mw_debug_time_sat).
+static __device__ int32_t g_satExp;
+#endif
+#ifndef MW_SAT_DPP
+#define MW_SAT_DPP (MW_SAT_GROUP == 8)
+#endif
 constexpr int32_t kGroupsPerBlock = kNarrowBlock / kGroup;
 
 __host__ __device__ inline size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
@@ -111,6 +122,23 @@ struct HullRef {
     HullDev hd;
     Vector3 center;
 };
+
+// An edge's four 16-bit indices read as one 8-byte word (one LDS load
+// instead of one per field).
+#ifndef MW_SAT_QUAD64
+#define MW_SAT_QUAD64 1
+#endif
+static_assert(sizeof(EdgeQuad) == 8 && alignof(EdgeQuad) == 2, "four 16-bit fields");
+__device__ __forceinline__ EdgeQuad ldQuad(const EdgeQuad *q, int32_t i)
+{
+#if MW_SAT_QUAD64
+    const uint64_t t = *(const uint64_t *)(q + i);
+    return EdgeQuad { (uint16_t)(t & 0xffffu), (uint16_t)((t >> 16) & 0xffffu),
+                      (uint16_t)((t >> 32) & 0xffffu), (uint16_t)(t >> 48) };
+#else
+    return q[i];
+#endif
+}
 
 struct GroupLDS {
     Vector3 *vA, *vB;
@@ -189,14 +217,39 @@ __device__ __forceinline__ bool scanWins(float v1, int32_t k1, float v2, int32_t
     return v1 > v2 || (v1 == v2 && k1 < k2);
 }
 
+// The (value, index) maximum of the group on every lane.  scanWins is a
+// total order (value, then lower index; NaN never wins), so the pairing
+// order of the reduction does not change the result.  For 8-lane groups the
+// exchanges are DPP moves within each 8-lane row half (mirror, then the
+// quad's xor 2 and xor 1 -- every lane ends with all eight), VALU
+// instructions instead of the LDS permute unit that __shfl_xor uses.
+__device__ __forceinline__ int32_t dppMove(int32_t x, int32_t ctrl_sel)
+{
+    switch (ctrl_sel) {
+    case 0: return __builtin_amdgcn_update_dpp(x, x, 0x141, 0xf, 0xf, false);   // row_half_mirror
+    case 1: return __builtin_amdgcn_update_dpp(x, x, 0x4e, 0xf, 0xf, false);    // quad_perm [2,3,0,1]
+    default: return __builtin_amdgcn_update_dpp(x, x, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    }
+}
+
 __device__ __forceinline__ void groupArgMax(float &v, int32_t &k)
 {
+#if MW_SAT_DPP
+    static_assert(kGroup == 8, "DPP reduction over 8-lane groups");
+#pragma unroll
+    for (int32_t step = 0; step < 3; step++) {
+        const float ov = __int_as_float(dppMove(__float_as_int(v), step));
+        const int32_t ok = dppMove(k, step);
+        if (scanWins(ov, ok, v, k)) { v = ov; k = ok; }
+    }
+#else
 #pragma unroll
     for (int32_t off = kGroup / 2; off > 0; off >>= 1) {
         const float ov = __shfl_xor(v, off, kGroup);
         const int32_t ok = __shfl_xor(k, off, kGroup);
         if (scanWins(ov, ok, v, k)) { v = ov; k = ok; }
     }
+#endif
 }
 
 // Body columns a SAT group stages a hull from, per body archetype: an LDS
@@ -241,7 +294,8 @@ __device__ __forceinline__ void stageHull(const ObjDev &O, const HullDev &hd, co
         const Vector3 n = (xf.nrm * op.normal).normalize();
         pl[i] = geometry::Plane { n, dot(n, origin) };
     }
-    for (int32_t i = first; i < hd.numEdges; i += step) q[i] = O.edgeQuads[hd.edgeOffset + i];
+    for (int32_t i = first; i < hd.numEdges; i += step)
+        *(uint64_t *)(q + i) = *(const uint64_t *)(O.edgeQuads + hd.edgeOffset + i);
 }
 
 // Both hulls of a pair staged at once: the group's first half transforms
@@ -328,7 +382,7 @@ __device__ __forceinline__ bool isMinkowskiFace(const Vector3 &a, const Vector3 
 __device__ __forceinline__ float edgePairSeparation(const HullRef &a, const HullRef &b,
                                                     int32_t i, int32_t j, Vector3 *normal_out)
 {
-    const EdgeQuad ea = a.quads[i], eb = b.quads[j];
+    const EdgeQuad ea = ldQuad(a.quads, i), eb = ldQuad(b.quads, j);
     float sep = -FLT_MAX;
     Vector3 n { 0, 0, 0 };
     if (isMinkowskiFace(a.planes[ea.face1].normal, a.planes[ea.face2].normal,
@@ -375,12 +429,12 @@ __device__ EdgeQuery groupEdgeQuery(const HullRef &a, const HullRef &b, int32_t 
         for (int32_t p = lane; p < nA * nB; p += kGroup) {
             if (i != cur) {
                 cur = i;
-                ea = a.quads[i];
+                ea = ldQuad(a.quads, i);
                 an1 = a.planes[ea.face1].normal;
                 an2 = a.planes[ea.face2].normal;
                 bxa = an2.cross(an1);
             }
-            const EdgeQuad eb = b.quads[j];
+            const EdgeQuad eb = ldQuad(b.quads, j);
             const Vector3 c = -b.planes[eb.face1].normal, d = -b.planes[eb.face2].normal;
             // isMinkowskiFace(an1, an2, c, d)
             const Vector3 dxc = d.cross(c);
@@ -421,12 +475,12 @@ __device__ __forceinline__ void buildMinkTables(const HullRef &a, const HullRef 
                                                 int32_t stride, int32_t lane)
 {
     for (int32_t i = lane; i < a.hd.numEdges; i += kGroup) {
-        const EdgeQuad ea = a.quads[i];
+        const EdgeQuad ea = ldQuad(a.quads, i);
         const Vector3 bxa = a.planes[ea.face2].normal.cross(a.planes[ea.face1].normal);
         for (int32_t f = 0; f < b.hd.numFaces; f++) sA[i * stride + f] = (-b.planes[f].normal).dot(bxa);
     }
     for (int32_t j = lane; j < b.hd.numEdges; j += kGroup) {
-        const EdgeQuad eb = b.quads[j];
+        const EdgeQuad eb = ldQuad(b.quads, j);
         const Vector3 c = -b.planes[eb.face1].normal, d = -b.planes[eb.face2].normal;
         const Vector3 dxc = d.cross(c);
         for (int32_t f = 0; f < a.hd.numFaces; f++) tB[j * stride + f] = a.planes[f].normal.dot(dxc);
@@ -440,6 +494,40 @@ __device__ __forceinline__ void buildMinkTables(const HullRef &a, const HullRef 
 // lanes whose pair passed; here a lane runs it only for its own passes.
 // The (separation, p) scan sees the same values in the same order, the
 // failed pairs' -FLT_MAX included.
+// The lane's (separation, p) scan over one chunk of its pairs p = base +
+// kGroup t, t < count, given which passed the Minkowski-face test: failed
+// pairs score -FLT_MAX (the scan keeps the first of them), passed ones
+// edgePairSeparation's value.
+__device__ __forceinline__ void scanPasses(const HullRef &a, const HullRef &b, uint32_t pass, int32_t count,
+                                           int32_t base, float &v, int32_t &k)
+{
+    const int32_t nB = b.hd.numEdges;
+    const uint32_t all = count == 32 ? ~0u : (1u << count) - 1u;
+    if (pass != all) {
+        const int32_t p0 = base + kGroup * __builtin_ctz(~pass);
+        if (scanWins(-FLT_MAX, p0, v, k)) { v = -FLT_MAX; k = p0; }
+    }
+    while (pass) {
+        const int32_t bit = __builtin_ctz(pass);
+        pass &= pass - 1;
+        const int32_t p = base + kGroup * bit;
+        const int32_t pi = p / nB, pj = p - pi * nB;
+        const EdgeQuad ea = ldQuad(a.quads, pi), eb = ldQuad(b.quads, pj);
+        float sep = -FLT_MAX;
+        const Vector3 pa1 = a.verts[ea.v1], pb1 = b.verts[eb.v1];
+        Vector3 da = a.verts[ea.v2] - pa1, db = b.verts[eb.v2] - pb1;
+        Vector3 uc = da.cross(db);
+        float l2 = uc.length2();
+        if (l2 != 0) {
+            float inv = 1.f / sqrtf(l2);
+            Vector3 nrm = uc * inv;
+            if (nrm.dot(pa1 - a.center) < 0.0f) nrm = -nrm;
+            sep = nrm.dot(pb1 - pa1);
+        }
+        if (scanWins(sep, p, v, k)) { v = sep; k = p; }
+    }
+}
+
 __device__ __forceinline__ EdgeQuery groupEdgeQueryTables(const HullRef &a, const HullRef &b, const float *sA,
                                           const float *tB, int32_t stride, int32_t lane)
 {
@@ -456,7 +544,7 @@ __device__ __forceinline__ EdgeQuery groupEdgeQueryTables(const HullRef &a, cons
             uint32_t pass = 0;
             int32_t t = 0;
             for (int32_t p = base; p < n && t < 32; p += kGroup, t++) {
-                const EdgeQuad ea = a.quads[i], eb = b.quads[j];
+                const EdgeQuad ea = ldQuad(a.quads, i), eb = ldQuad(b.quads, j);
                 const float cba = sA[irow + eb.face1], dba = sA[irow + eb.face2];
                 const float adc = tB[jrow + ea.face1], bdc = tB[jrow + ea.face2];
                 // all three products, no short circuit: the same verdict
@@ -473,31 +561,13 @@ __device__ __forceinline__ EdgeQuery groupEdgeQueryTables(const HullRef &a, cons
                     irow += stride;
                 }
             }
-            // failed pairs score -FLT_MAX: the scan keeps the first of them
-            const uint32_t all = t == 32 ? ~0u : (1u << t) - 1u;
-            if (pass != all) {
-                const int32_t p0 = base + kGroup * __builtin_ctz(~pass);
-                if (scanWins(-FLT_MAX, p0, v, k)) { v = -FLT_MAX; k = p0; }
+#if defined(MW_SAT_CUTS)
+            if (g_satExp == 5) {                 // masks only (kept alive)
+                if (pass == 0x7fffffffu) v = 0.0f;
+                continue;
             }
-            while (pass) {
-                const int32_t bit = __builtin_ctz(pass);
-                pass &= pass - 1;
-                const int32_t p = base + kGroup * bit;
-                const int32_t pi = p / nB, pj = p - pi * nB;
-                const EdgeQuad ea = a.quads[pi], eb = b.quads[pj];
-                float sep = -FLT_MAX;
-                const Vector3 pa1 = a.verts[ea.v1], pb1 = b.verts[eb.v1];
-                Vector3 da = a.verts[ea.v2] - pa1, db = b.verts[eb.v2] - pb1;
-                Vector3 uc = da.cross(db);
-                float l2 = uc.length2();
-                if (l2 != 0) {
-                    float inv = 1.f / sqrtf(l2);
-                    Vector3 nrm = uc * inv;
-                    if (nrm.dot(pa1 - a.center) < 0.0f) nrm = -nrm;
-                    sep = nrm.dot(pb1 - pa1);
-                }
-                if (scanWins(sep, p, v, k)) { v = sep; k = p; }
-            }
+#endif
+            scanPasses(a, b, pass, t, base, v, k);
         }
     }
     groupArgMax(v, k);
@@ -1010,11 +1080,6 @@ static __device__ unsigned long long g_satStage[16];
 #define MW_SAT_TICK(i) do {} while (0)
 #endif
 #if defined(MW_SAT_CUTS)
-// Timing build only (make BUILD=build_cut EXTRA=-DMW_SAT_CUTS): with
-// mw_debug_set_sat_exp(c), c > 0, every pair is declared separated after
-// staging (1), the face queries (2), the Minkowski tables (3) or the edge
-// query (4); the phases' times by difference (eager node timing).
-static __device__ int32_t g_satExp;
 #define MW_SAT_CUT(i) do { if (g_satExp == (i)) return kSatFaceSeparated; } while (0)
 #else
 #define MW_SAT_CUT(i) do {} while (0)
@@ -1385,9 +1450,27 @@ size_t narrowphaseGlobalSharedBytes(const PhysArgs &P)
     return kOrderSortBytes + P.satGeoBytes;
 }
 
+// One lane's clip buffers (two polygons and the depths), padded to an odd
+// number of dwords: lanes touch the same element of their own buffers
+// together, and with an even dword stride those accesses share LDS banks
+// (a 56-dword stride -- 8-point polygons -- put every fourth lane of a
+// 32-lane half on one bank).
+#ifndef MW_CONTACT_BANK_PAD
+#define MW_CONTACT_BANK_PAD 1
+#endif
+__host__ __device__ inline size_t contactLaneBytes(int32_t clip_cap)
+{
+    const size_t b = 2 * a16(sizeof(Vector3) * clip_cap) + a16(4 * clip_cap);
+#if MW_CONTACT_BANK_PAD
+    return (b / 4) % 2 == 0 ? b + 4 : b;
+#else
+    return b;
+#endif
+}
+
 __host__ __device__ inline size_t contactLDSBytes(int32_t clip_cap)
 {
-    return (size_t)kContactBlock * (2 * a16(sizeof(Vector3) * clip_cap) + a16(4 * clip_cap));
+    return a16((size_t)kContactBlock * contactLaneBytes(clip_cap));
 }
 
 size_t contactSharedBytes(const PhysArgs &P)
@@ -1412,7 +1495,7 @@ __device__ __forceinline__ void narrowContactBlock(const PhysArgs &P)
     const ObjDev &O = P.objs;
     const int32_t cap = P.clipCap;
     char *base = kGlobal ? P.clipImage + (size_t)blockIdx.x * contactLDSBytes(cap) : smem;
-    char *mine = base + (size_t)threadIdx.x * (2 * a16(sizeof(Vector3) * cap) + a16(4 * cap));
+    char *mine = base + (size_t)threadIdx.x * contactLaneBytes(cap);
     Vector3 *clip0 = (Vector3 *)mine;
     Vector3 *clip1 = (Vector3 *)(mine + a16(sizeof(Vector3) * cap));
     float *depths = (float *)(mine + 2 * a16(sizeof(Vector3) * cap));

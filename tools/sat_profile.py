@@ -32,8 +32,8 @@ def main():
         lib.mw_debug_time_sat.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
         lib.mw_debug_time_sat.restype = ctypes.c_double
         sim.sync()
-        names = ["full", "staging", "+faces", "+tables", "+edges", "full"]
-        for cut, nm in zip((0, 1, 2, 3, 4, 0), names):
+        names = ["full", "staging", "+faces", "+tables", "+masks", "+edges", "full"]
+        for cut, nm in zip((0, 1, 2, 3, 5, 4, 0), names):
             ms = lib.mw_debug_time_sat(cut, 20, 3)
             print(f"narrowSATKernel cut {cut} ({nm:8s}) {ms:.4f} ms/launch (last substep's list, 20 launches)")
         return
