@@ -230,10 +230,13 @@ MW_PHYS_NODE(FindOverlappingNode,
 // them to the accumulators.  Launched only behind a node whose kernels are
 // bound to a timing event pair (hipx::tlTimed), outside that pair, so the
 // replayed (untimed) steps never run it.
-__global__ void __launch_bounds__(256) unitProbeKernel(PhysArgs P, int32_t from_solver,
+constexpr int32_t kProbeThreads = 256;
+constexpr int32_t kProbeBlocks = 256;
+
+__global__ void __launch_bounds__(kProbeThreads) unitProbeKernel(PhysArgs P, int32_t from_solver,
                                                        int32_t fused_extra)
 {
-    // one wave per world (grid-stride), one pair of atomics per wave
+    // one wave per world (grid-stride), one set of atomics per block
     const int32_t lane = threadIdx.x & 63;
     const int32_t waves = (int32_t)(gridDim.x * blockDim.x) >> 6;
     unsigned long long cands = 0, contacts = 0, survivors = 0;
@@ -256,10 +259,20 @@ __global__ void __launch_bounds__(256) unitProbeKernel(PhysArgs P, int32_t from_
         contacts += __shfl_down(contacts, o, 64);
         survivors += __shfl_down(survivors, o, 64);
     }
+    // the block's waves summed in LDS, one set of atomics per block (one
+    // per wave, all on three addresses, serialised into ~0.2 ms)
+    __shared__ unsigned long long s_sum[3][kProbeThreads / 64];
+    const int32_t wave = threadIdx.x >> 6;
     if (lane == 0) {
-        if (cands) atomicAdd(P.unitAccum + 1, cands);
-        if (contacts) atomicAdd(P.unitAccum + 2, contacts);
-        if (survivors) atomicAdd(P.unitAccum + 4, survivors);
+        s_sum[0][wave] = cands;
+        s_sum[1][wave] = contacts;
+        s_sum[2][wave] = survivors;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        unsigned long long x = 0;
+        for (int32_t i = 0; i < kProbeThreads / 64; i++) x += s_sum[threadIdx.x][i];
+        if (x) atomicAdd(P.unitAccum + (threadIdx.x == 0 ? 1 : threadIdx.x == 1 ? 2 : 4), x);
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(P.unitAccum + 0, 1ull);
@@ -273,7 +286,8 @@ static void probeUnits(const PhysArgs &P, LaunchCtx &lc, bool from_solver, bool 
     hipx::TimedLaunch *t = hipx::tlTimed;
     hipx::tlTimed = nullptr;        // not part of the node's timed span
     try {
-        MW_LAUNCH(unitProbeKernel, dim3((uint32_t)std::min((P.numWorlds + 3) / 4, 2048)), dim3(256), 0,
+        MW_LAUNCH(unitProbeKernel, dim3((uint32_t)std::min((P.numWorlds + 3) / 4, kProbeBlocks)),
+                  dim3(kProbeThreads), 0,
                   (hipStream_t)lc.stream, P,
                   from_solver ? 1 : 0, fused_extra ? 1 : 0);
     } catch (...) {
