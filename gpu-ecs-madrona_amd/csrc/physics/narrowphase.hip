@@ -928,24 +928,7 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
             S = 0;
             break;
         }
-        // hull-hull pairs whose last SAT passed the face queries (satHint)
-        // take the back of the chunk's reservation, the others its front
-        const int32_t thh = (total >> 10) & 1023;
-        int32_t heavy = 0;
-        {
-            int32_t sl = S + (off & 1023);
-#pragma unroll
-            for (int32_t j = 0; j < kFilterPer; j++) {
-                if (!keep[j]) continue;
-                if (wk[j].test == kHull && P.satHint && P.satHint[(size_t)w * cap + sl] != 0)
-                    heavy |= 1 << j;
-                sl++;
-            }
-        }
-        int32_t heavy_total;
-        const int32_t hoff = blockExclusiveScan(__popc((uint32_t)heavy), s_scan, &heavy_total);
-        int32_t lpos = s_base[0] + ((off >> 10) & 1023) - hoff;      // light pairs before mine
-        int32_t hpos = s_base[0] + thh - 1 - hoff;
+        int32_t hpos = s_base[0] + ((off >> 10) & 1023);
         int32_t ppos = s_base[1] + (off >> 20);
         int32_t slot = S + (off & 1023);
 #pragma unroll
@@ -954,8 +937,7 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
             wk[j].slot = slot;
             info[slot] = kNoManifold;
             if (wk[j].test == kHull) {
-                if ((heavy >> j) & 1) list[hpos--] = packWork(wk[j]);
-                else list[lpos++] = packWork(wk[j]);
+                list[hpos++] = packWork(wk[j]);
             } else if (wk[j].test == kHullPlane) {
                 *(list_back - ppos++) = packWork(wk[j]);
             }
@@ -1089,8 +1071,7 @@ static __device__ unsigned long long g_satStage[16];
 #define MW_SAT_SPLIT_STAGE 0
 #endif
 
-// How a pair's SAT ended (satHint: the pairs that got past the face queries
-// are the expensive ones).
+// How a pair's SAT ended.
 enum : int32_t { kSatFaceSeparated = 0, kSatEdgeSeparated = 1, kSatContact = 2 };
 
 // The SAT of one pair after its hulls are known (doSAT, narrowphase.cpp:
@@ -1408,11 +1389,7 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
         ContactJob job;
         job.kind = kJobNone;
         if (ok) {
-            const int32_t how = hullHullSAT(O, (int32_t)(pw.objs & 0xffffu), (int32_t)(pw.objs >> 16),
-                                            pa, pb, g, lane, job);
-            if (lane == 0 && P.hhJobs && P.satHint)
-                P.satHint[(size_t)pw.world * P.candCapacity + (pw.slotTest & 0xffffu)] =
-                    how != kSatFaceSeparated;
+            hullHullSAT(O, (int32_t)(pw.objs & 0xffffu), (int32_t)(pw.objs >> 16), pa, pb, g, lane, job);
         } else if (lane == 0) {
             atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
         }

@@ -99,9 +99,6 @@ void PhysicsModule::upload(void *stream_ptr)
     // MADRONA_MW_SAT_TABLES=0: the SAT edge query without its Minkowski-test
     // tables (the per-pair form; parity tests of both)
     if (const char *t = std::getenv("MADRONA_MW_SAT_TABLES"); t && t[0] == '0') P.objs.minkStride = 0;
-    // MADRONA_MW_SAT_HINTS=0: work lists in candidate order, without the
-    // last SAT's outcome ordering them (satHint; A/B and parity of both)
-    if (const char *t = std::getenv("MADRONA_MW_SAT_HINTS"); t && t[0] == '0') P.satHint = nullptr;
     P.satImage = nullptr;
     P.satImageBlocks = 0;
     if (fitsLDS((const void *)&narrowSATKernel, kNarrowBlock, narrowphaseSharedBytes(P))) {

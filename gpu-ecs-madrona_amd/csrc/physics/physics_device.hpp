@@ -464,8 +464,7 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
         }
         return;
     }
-    const uint8_t *hint = P.satHint ? P.satHint + (size_t)w * cap : nullptr;
-    int32_t S = 0, n_light = 0, n_heavy = 0;
+    int32_t S = 0;
     for (int32_t b0 = 0; b0 < num; b0 += kBatch) {
         uint64_t s[kFilterBatch];
 #pragma unroll
@@ -496,24 +495,16 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
             const BodyBox B = boxes[(uint32_t)(s[j] >> 32) & 0xffffu];
             const uint32_t t = A.type | B.type;
             const bool hh = keep && t == kHull, hp = keep && t == kHullPlane;
-            const uint64_t mk = __ballot(keep);
-            const int32_t slot = S + __popcll(mk & lt);
-            // hull-hull pairs whose last SAT passed the face queries go to
-            // the back of the world's run (satHint): the SAT kernel's waves
-            // then hold pairs of one kind
-            const bool heavy = hh && hint && hint[min(slot, cap - 1)] != 0;
-            const uint64_t ml = __ballot(hh && !heavy), mh = __ballot(heavy), mp = __ballot(hp);
+            const uint64_t mk = __ballot(keep), mh = __ballot(hh), mp = __ballot(hp);
             if (keep) {
                 SatWork wk = candWork(c[j], s[j], A, B, w);
-                wk.slot = slot;
+                wk.slot = S + __popcll(mk & lt);
                 info[wk.slot] = kNoManifold;
-                if (hh && !heavy) list[b_hh + n_light + __popcll(ml & lt)] = packWork(wk);
-                if (heavy) list[b_hh + n_hh - 1 - (n_heavy + __popcll(mh & lt))] = packWork(wk);
+                if (hh) list[b_hh + __popcll(mh & lt)] = packWork(wk);
                 if (hp) *(list_back - (b_hp + __popcll(mp & lt))) = packWork(wk);
             }
             S += __popcll(mk);
-            n_light += __popcll(ml);
-            n_heavy += __popcll(mh);
+            b_hh += __popcll(mh);
             b_hp += __popcll(mp);
         }
     }

@@ -189,10 +189,6 @@ struct PhysArgs {
     int32_t *nextSatWorkCount;
     ContactJob *hhJobs;           // [W * candCapacity] SAT verdict per satWork entry (only
                                   // the kind when separated)
-    uint8_t *satHint;             // [W][candCapacity] per survivor slot: 1 when the last SAT
-                                  // of the pair in that slot passed both face queries; the
-                                  // filters put such pairs after the others in the world's
-                                  // run of the work list (ordering only)
     int32_t contactGrid;          // persistent contact-kernel grid (blocks)
     int32_t planeGeoBytes;        // plane kernel's LDS copy of the hull tables (0: read
                                   // them from HBM; tables too large)

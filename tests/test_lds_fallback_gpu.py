@@ -94,17 +94,14 @@ def test_forced_global_images_bit_exact(monkeypatch):
     _lockstep(sim, orc, W, 40)
 
 
-@pytest.mark.parametrize("tables,hints", [("1", "1"), ("0", "1"), ("1", "0")])
-def test_sat_edge_query_forms_bit_exact(monkeypatch, tables, hints):
+@pytest.mark.parametrize("tables", ["1", "0"])
+def test_sat_edge_query_forms_bit_exact(monkeypatch, tables):
     """The SAT edge query's two forms (narrowphase.hip groupEdgeQueryTables:
     the Minkowski-test dot products tabulated per (edge, face), passes
     compacted per lane; groupEdgeQuery: the test per edge pair) on cube
-    worlds and on a cube + wedge hull set, with and without the work lists
-    ordered by the last SAT's outcome (satHint): the same bits as the oracle
-    every step (MADRONA_MW_SAT_TABLES=0 selects the per-pair form,
-    MADRONA_MW_SAT_HINTS=0 candidate order)."""
+    worlds and on a cube + wedge hull set: the same bits as the oracle every
+    step (MADRONA_MW_SAT_TABLES=0 selects the per-pair form)."""
     monkeypatch.setenv("MADRONA_MW_SAT_TABLES", tables)
-    monkeypatch.setenv("MADRONA_MW_SAT_HINTS", hints)
     W, n = 4, 128
     pos, rot = gen_collisions_inits(W, n, seed=11)
     sim, orc = _pair(W, n, pos, rot)
