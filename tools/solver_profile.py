@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Solver phase profile (experiment tool): run with the profiling build,
-  MADRONA_MW_LIB=gpu-ecs-madrona_amd/build_prof/libmadrona_mw.so python tools/solver_profile.py
+  MADRONA_MW_LIB=gpu-ecs-madrona_amd/build_prof/libmadrona_mw.so python tools/solver_profile.py [W] [collisions|simple]
 (build: make -C gpu-ecs-madrona_amd BUILD=build_prof EXTRA=-DMW_SOLVER_PROFILE).
 Prints the mean time per solver block in each phase over 10 settled steps."""
 import ctypes
@@ -19,9 +19,11 @@ PHASES = ["load+count", "order+level", "count sort", "positions", "setVelocities
 
 def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
-    cfg = mw.default_collisions_config(128, 4, 4096, 4096)
-    pos, rot = mw.gen_collisions_inits(W, 128, seed=0)
-    sim = mw.CollisionsSim(W, pos, rot, cfg)
+    wl = sys.argv[2] if len(sys.argv) > 2 else "collisions"      # or simple (configs[1])
+    n = 100 if wl == "simple" else 128
+    cfg = mw.default_collisions_config(n, 4, 4096, 4096)
+    pos, rot = mw.gen_collisions_inits(W, n, seed=0)
+    sim = (mw.SimpleSim if wl == "simple" else mw.CollisionsSim)(W, pos, rot, cfg)
     lib = mw.library()
     out = np.zeros(16, np.uint64)
     sim.step(int(os.environ.get('SETTLE', '220')))
