@@ -1427,6 +1427,11 @@ size_t narrowphaseGlobalSharedBytes(const PhysArgs &P)
     return kOrderSortBytes + P.satGeoBytes;
 }
 
+#ifndef MW_CONTACT_CHUNK
+#define MW_CONTACT_CHUNK 4
+#endif
+constexpr int32_t kContactChunk = MW_CONTACT_CHUNK;     // SAT entries per lane per gather
+
 // One lane's clip buffers (two polygons and the depths), padded to an odd
 // number of dwords: lanes touch the same element of their own buffers
 // together, and with an even dword stride those accesses share LDS banks
@@ -1481,10 +1486,31 @@ __device__ __forceinline__ void narrowContactBlock(const PhysArgs &P)
     __shared__ int32_t s_pre[kNarrowBins + 1];
     loadBinPrefix(P, 0, s_pre);
     const int32_t total = min(s_pre[kNarrowBins], P.numWorlds * P.candCapacity);
-    for (int32_t i = blockIdx.x * kContactBlock + threadIdx.x; i < total;
-         i += gridDim.x * kContactBlock) {
-        if (P.hhJobs[i].kind == kJobNone) continue;   // separated: only the kind was written
-        const ContactJob job = P.hhJobs[i];
+    // Chunks of kContactChunk entries per lane: the block first gathers the
+    // chunk's jobs (most entries are separated pairs: kJobNone) into LDS,
+    // then its lanes take the jobs densely -- otherwise a wave's lanes wait
+    // on the few that drew a job.  Which lane solves a job does not matter:
+    // each writes its own survivor slot.
+    __shared__ int32_t s_jobs[kContactBlock * kContactChunk];
+    __shared__ int32_t s_njobs;
+    const int32_t chunk = kContactBlock * kContactChunk;
+    for (int32_t c0 = blockIdx.x * chunk; c0 < total; c0 += gridDim.x * chunk) {
+    if (threadIdx.x == 0) s_njobs = 0;
+    __syncthreads();
+#pragma unroll
+    for (int32_t q = 0; q < kContactChunk; q++) {
+        const int32_t i = c0 + q * kContactBlock + threadIdx.x;
+        const bool has = i < total && P.hhJobs[i].kind != kJobNone;   // separated: only the kind was written
+        const uint64_t m = __ballot(has);
+        int32_t wb = 0;
+        if ((threadIdx.x & 63) == 0 && m) wb = atomicAdd(&s_njobs, (int32_t)__popcll(m));
+        wb = __shfl(wb, 0, 64);
+        if (has) s_jobs[wb + __popcll(m & __lanemask_lt())] = i;
+    }
+    __syncthreads();
+    const int32_t njobs = s_njobs;
+    for (int32_t k = threadIdx.x; k < njobs; k += kContactBlock) {
+        const ContactJob job = P.hhJobs[s_jobs[k]];
         const SatWork &wk = job.pair;
         if ((uint32_t)wk.world >= (uint32_t)P.numWorlds || (uint32_t)wk.slot >= (uint32_t)P.candCapacity ||
             (uint32_t)wk.aObj >= (uint32_t)P.objs.numObjects || (uint32_t)wk.bObj >= (uint32_t)P.objs.numObjects) {
@@ -1587,6 +1613,9 @@ __device__ __forceinline__ void narrowContactBlock(const PhysArgs &P)
             recordManifold(P, w, wk.slot, slotOf(P, wk.aArch, wk.a), slotOf(P, wk.bArch, wk.b));
         }
     }
+    __syncthreads();
+    }
+
 }
 
 __global__ void __launch_bounds__(kContactBlock) narrowContactKernel(PhysArgs P)
