@@ -1308,7 +1308,9 @@ __device__ __forceinline__ SatWork unpackSat(const PhysArgs &P, const SatArch *a
 // kGlobal: the groups' hull staging exceeds a workgroup's LDS and lives in
 // the block's slab of P.satImage (narrowSATGlobalKernel); the world sort
 // still uses kOrderSortBytes of LDS.
-template <bool kGlobal>
+// kGeo: the hull tables are staged into LDS (P.satGeoBytes > 0) -- a
+// template parameter so that their reads are LDS loads, not generic ones.
+template <bool kGlobal, bool kGeo>
 __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1328,7 +1330,7 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
         sortWorldsForSolver(P, (int32_t *)smem, s_sort_scan);
     }
     ObjDev O = P.objs;
-    if (P.satGeoBytes > 0) {
+    if constexpr (kGeo) {
         char *dst = smem + (kGlobal ? kOrderSortBytes : satStageBytes(P.objs));
         O.hulls = (HullDev *)stageTable(dst, P.objs.hulls, sizeof(HullDev) * O.numObjects);
         O.vertices = (Vector3 *)stageTable(dst, P.objs.vertices, sizeof(Vector3) * O.numVertsTotal);
@@ -1408,13 +1410,19 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
 __global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
-    narrowSATBlock<false>(P);
+    narrowSATBlock<false, true>(P);
+}
+
+__global__ void __launch_bounds__(kNarrowBlock, MW_SAT_MIN_BLOCKS) narrowSATNoGeoKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    narrowSATBlock<false, false>(P);
 }
 
 __global__ void __launch_bounds__(kNarrowBlock) narrowSATGlobalKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
-    narrowSATBlock<true>(P);
+    narrowSATBlock<true, false>(P);
 }
 
 size_t narrowphaseImageBytes(const PhysArgs &P)
@@ -1422,9 +1430,9 @@ size_t narrowphaseImageBytes(const PhysArgs &P)
     return kGroupsPerBlock * groupLDSBytes(P.objs);
 }
 
-size_t narrowphaseGlobalSharedBytes(const PhysArgs &P)
+size_t narrowphaseGlobalSharedBytes(const PhysArgs &)
 {
-    return kOrderSortBytes + P.satGeoBytes;
+    return kOrderSortBytes;
 }
 
 #ifndef MW_CONTACT_CHUNK

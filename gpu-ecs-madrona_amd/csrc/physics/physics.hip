@@ -101,8 +101,10 @@ void PhysicsModule::upload(void *stream_ptr)
     if (const char *t = std::getenv("MADRONA_MW_SAT_TABLES"); t && t[0] == '0') P.objs.minkStride = 0;
     P.satImage = nullptr;
     P.satImageBlocks = 0;
-    if (fitsLDS((const void *)&narrowSATKernel, kNarrowBlock, narrowphaseSharedBytes(P))) {
-        P.satGrid = cus * hipx::residentBlocks((const void *)&narrowSATKernel, "narrowSATKernel",
+    const bool sat_geo = P.satGeoBytes > 0;
+    const void *sat_lds = sat_geo ? (const void *)&narrowSATKernel : (const void *)&narrowSATNoGeoKernel;
+    if (fitsLDS(sat_lds, kNarrowBlock, narrowphaseSharedBytes(P))) {
+        P.satGrid = cus * hipx::residentBlocks(sat_lds, sat_geo ? "narrowSATKernel" : "narrowSATNoGeoKernel",
                                                kNarrowBlock, narrowphaseSharedBytes(P));
     } else {
         const int32_t per_cu = hipx::residentBlocks((const void *)&narrowSATGlobalKernel,
@@ -328,8 +330,12 @@ extern "C" double mw_debug_time_sat(int32_t cut, int32_t reps, int32_t substep)
     (void)hipEventCreate(&b);
     (void)hipEventRecord(a, nullptr);
     for (int32_t r = 0; r < reps; r++)
-        hipLaunchKernelGGL(narrowSATKernel, dim3(Q.satGrid), dim3(kNarrowBlock),
-                           narrowphaseSharedBytes(Q), nullptr, Q);
+        if (Q.satGeoBytes > 0)
+            hipLaunchKernelGGL(narrowSATKernel, dim3(Q.satGrid), dim3(kNarrowBlock),
+                               narrowphaseSharedBytes(Q), nullptr, Q);
+        else
+            hipLaunchKernelGGL(narrowSATNoGeoKernel, dim3(Q.satGrid), dim3(kNarrowBlock),
+                               narrowphaseSharedBytes(Q), nullptr, Q);
     (void)hipEventRecord(b, nullptr);
     float ms = -1.f;
     if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = -1.f;
@@ -405,8 +411,12 @@ struct NarrowphaseNode : PhysNodeBase {
             MW_LAUNCH(narrowSATGlobalKernel, dim3(g), dim3(kNarrowBlock),
                       narrowphaseGlobalSharedBytes(Q), stream, Q);
         } else {
-            MW_LAUNCH(narrowSATKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
-                      narrowphaseSharedBytes(Q), stream, Q);
+            if (Q.satGeoBytes > 0)
+                MW_LAUNCH(narrowSATKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
+                          narrowphaseSharedBytes(Q), stream, Q);
+            else
+                MW_LAUNCH(narrowSATNoGeoKernel, dim3(lc.persistentGrid(Q.satGrid)), dim3(kNarrowBlock),
+                          narrowphaseSharedBytes(Q), stream, Q);
         }
         if (Q.clipImage) {
             const uint32_t g = std::min<uint32_t>(lc.persistentGrid(Q.contactGrid), Q.clipImageBlocks);

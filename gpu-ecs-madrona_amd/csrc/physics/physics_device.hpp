@@ -140,7 +140,8 @@ __global__ void refitKernel(PhysArgs P);
 __global__ void findOverlapsKernel(PhysArgs P);
 __global__ void integrateKernel(PhysArgs P);
 __global__ void narrowFilterKernel(PhysArgs P);
-__global__ void narrowSATKernel(PhysArgs P);
+__global__ void narrowSATKernel(PhysArgs P);         // hull tables in LDS (satGeoBytes > 0)
+__global__ void narrowSATNoGeoKernel(PhysArgs P);    // hull tables read from HBM
 __global__ void narrowPlaneKernel(PhysArgs P);
 __global__ void narrowContactKernel(PhysArgs P);
 __global__ void solverKernel(PhysArgs P, int32_t integrate_next);

@@ -33,6 +33,7 @@ NODE_OF = {
     "narrowFilterKernel": ("NarrowphaseNode", 1),         # substep 0 only (later: solver tail)
     "solverOrderKernel": ("NarrowphaseNode", 4),
     "narrowSATKernel": ("NarrowphaseNode", 4),
+    "narrowSATNoGeoKernel": ("NarrowphaseNode", 4),      # hull tables read from HBM
     "narrowPlaneKernel": ("NarrowphaseNode", 4),
     "narrowContactKernel": ("NarrowphaseNode", 4),
     "solverKernel": ("SolverNode", 4),
