@@ -155,6 +155,17 @@ def parse():
                    help="time the dominant kernel's launches in every N-th timed step (the "
                         "graph is split at that node only in those steps)")
     p.add_argument("--no-handoff", action="store_true")
+    p.add_argument("--backend", choices=("gpu", "cpu"), default="gpu",
+                   help="cpu: the framework's CPU back end with a gloo hand-off -- a rehearsal of "
+                        "the multi-rank path without a GPU (tests/test_bench_launch.py), never "
+                        "the headline")
+    p.add_argument("--dry-launch", action="store_true",
+                   help="spawn the ranks as for a real run; each prints its launch environment "
+                        "and exits without touching a GPU")
+    p.add_argument("--ref-ticks", type=int, default=1000,
+                   help="the reference's own timing definition (examples/collisions/gpu.cpp:32-43): "
+                        "a fresh executor, this many synchronous steps from init, wall time; "
+                        "reported beside the headline (0 = skip)")
     args = p.parse_args()
     if args.cubes <= 0:
         args.cubes = 128 if args.workload == "collisions" else 100
@@ -294,15 +305,83 @@ def cpu_baselines(args, legs):
     return out
 
 
+LAUNCH_VARS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N` without a launcher: start N rank processes of this script
+    (one per GPU, LOCAL_RANK = GPU ordinal; the environment
+    torch.distributed.run would give them, rendezvous on 127.0.0.1) and exit
+    with the first non-zero status among them.  Called before this process
+    imports the framework or torch, so the parent never touches a GPU.  A
+    rank that fails takes the others down (they would wait at a barrier)."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench: rank {procs.index(p)} exited with status {code}; stopping the "
+                      "other ranks", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+    for p in procs:
+        p.wait()
+    return rc
+
+
 def main():
     args = parse()
     if args.cpu_child:
         return _cpu_child(args)
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            raise SystemExit(f"bench: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher "
+                             f"disagrees with --gpus {args.gpus}")
+    elif args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world_size != args.gpus and world_size > 1:
-        print(f"warning: WORLD_SIZE={world_size} != --gpus {args.gpus}", file=sys.stderr)
+    if args.dry_launch:
+        print(json.dumps({"dry_launch": {k: os.environ.get(k) for k in LAUNCH_VARS},
+                          "pid": os.getpid(), "gpus": args.gpus}), flush=True)
+        return None
+    cpu_backend = args.backend == "cpu"
+    if cpu_backend:
+        # rehearsal of the rank / hand-off plumbing: no per-node GPU timing,
+        # no CPU-baseline legs, no reference-definition leg
+        args.no_roofline = args.no_cpu_baseline = True
+        args.ref_ticks = 0
+    breakdown_steps = 0 if args.no_roofline else 2 * len(NODE_KINDS)
+    startup_steps = 0 if args.no_roofline else 20
+    if args.settle < breakdown_steps + startup_steps:
+        raise SystemExit(f"--settle must be >= {breakdown_steps + startup_steps} "
+                         "(the start-up and per-node breakdown steps)")
 
     # The framework owns the step stream and the hand-off collective (RCCL
     # over xGMI from the C ABI, enqueued right behind the step); the hand-off
@@ -311,39 +390,53 @@ def main():
     # the timing barrier / max-reduce run over gloo on the CPU.
     import madrona_mi355x as mw
     import torch
-    from madrona_mi355x.sharding import bootstrap_rccl, world_shard
+    from madrona_mi355x.sharding import bootstrap_rccl, gather_world_returns, world_shard
     dist = None
     if world_size > 1:
         import torch.distributed as dist
         dist.init_process_group(backend="gloo")
-    torch.cuda.set_device(local_rank)
+    if not cpu_backend:
+        torch.cuda.set_device(local_rank)
 
     cfg = mw.default_collisions_config(args.cubes, args.substeps, max_contacts=4096,
                                        max_candidates=4096)
     first_world, W = world_shard(rank, args.worlds)
-    pos, rot = mw.gen_collisions_inits(W, args.cubes, seed=0, first_world=first_world)
     simple = args.workload == "simple"
     Sim = mw.SimpleSim if simple else mw.CollisionsSim
-    sim = Sim(W, pos, rot, cfg, gpu_id=local_rank)
-    del pos, rot
+
+    def make_sim():
+        pos, rot = mw.gen_collisions_inits(W, args.cubes, seed=0, first_world=first_world)
+        if cpu_backend:
+            return Sim(W, pos, rot, cfg, backend="cpu", num_workers=max(1, args.cpu_threads))
+        return Sim(W, pos, rot, cfg, gpu_id=local_rank)
+
+    sim = make_sim()
     # the training hand-off: collisions -- the per-world episode return
     # (export slot 2, 1 float); simple -- the agent's position (slot 0, 3)
     ho_slot, ho_floats = (0, 3) if simple else (2, 1)
 
-    if dist is not None:
+    if dist is not None and not cpu_backend:
         bootstrap_rccl(sim, rank, world_size)
     # per-world returns of every rank, in world order: a torch tensor
-    returns = torch.empty(W * world_size * ho_floats, dtype=torch.float32, device=f"cuda:{local_rank}")
+    returns = torch.empty(W * world_size * ho_floats, dtype=torch.float32,
+                          device="cpu" if cpu_backend else f"cuda:{local_rank}")
     handoff = returns.data_ptr()
 
     # Every step is enqueued without a host round trip: the step graph, then
     # the hand-off (D2D copy / RCCL all-gather of the returns into the torch
     # tensor) on the same stream; the timed region ends with a device sync.
+    # The CPU back end steps synchronously and gathers over gloo.
     def step():
         sim.step_async(1)
         if args.no_handoff:
             return
-        if dist is not None:
+        if cpu_backend:
+            local = torch.from_numpy(sim.exported_array(ho_slot, np.float32).copy())
+            if dist is not None:
+                gather_world_returns(local, out=returns)
+            else:
+                returns.copy_(local)
+        elif dist is not None:
             sim.allgather_exported(ho_slot, handoff, 4 * ho_floats * W)
         else:
             sim.copy_exported_async(ho_slot, handoff, 4 * ho_floats * W)
@@ -363,11 +456,6 @@ def main():
                 "CustomParallelForNode": 1, "ParallelForNode": 1}
     node_table = {}
     dom = None
-    breakdown_steps = 0 if args.no_roofline else 2 * len(NODE_KINDS)
-    startup_steps = 0 if args.no_roofline else 20
-    if args.settle < breakdown_steps + startup_steps:
-        raise SystemExit(f"--settle must be >= {breakdown_steps + startup_steps} "
-                         "(the start-up and per-node breakdown steps)")
     # Start-up cost (untimed, part of the settle pre-roll): step 1 carries the
     # forced BVH rebuild (its kernel timed with HIP events), then the wall
     # time of steps 2-20, each synchronised, while the cubes fall and land.
@@ -468,6 +556,35 @@ def main():
             "mean_candidates_per_world": round(units["cand"] / W, 1),
             "mean_contacts_per_world": round(units["contact"] / W, 1),
         }
+        if traffic:
+            # the counters' HBM bytes over the same launches: the model counts
+            # reads that LDS / L2 serve, so this rate is the HBM-true one
+            roofline["frac_pmc"] = round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+            roofline["model_over_pmc"] = round(nbytes / traffic, 3)
+
+    assert bool(torch.isfinite(returns).all()), "non-finite returns in the hand-off tensor"
+    sim.close()
+
+    # The reference's own definition (examples/collisions/gpu.cpp:32-43): a
+    # fresh executor, ref_ticks synchronous run() calls from init (start-up
+    # transient included), wall time; beside the settled-window headline.
+    ref_def = None
+    if rank == 0 and world_size == 1 and args.ref_ticks > 0:
+        sim = make_sim()
+        sim.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.ref_ticks):
+            sim.step(1)
+        dt = time.perf_counter() - t0
+        ref_def = {"value": round(W * args.ref_ticks / dt, 1), "unit": "env-steps/s",
+                   "ticks": f"1-{args.ref_ticks}", "seconds": round(dt, 4),
+                   "ms_per_step": round(dt / args.ref_ticks * 1e3, 4),
+                   "definition": "examples/collisions/gpu.cpp:32-43: a fresh executor, "
+                                 f"{args.ref_ticks} synchronous steps from init timed by wall clock "
+                                 "(each mw_step waits for its step, as run() syncs its stream; "
+                                 "no hand-off)",
+                   "error_flags": sim.error_flags()}
+        sim.close()
 
     cpu = cpu_exec = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -502,19 +619,21 @@ def main():
                 "timed_steps": f"{args.settle + args.warmup + 1}-{args.settle + args.warmup + args.steps}",
                 "parallelism": f"world-sharded x{world_size}" +
                                ("" if args.no_handoff else ", per-step return hand-off"
-                                + (" (RCCL all-gather over xGMI)" if world_size > 1 else "")),
+                                + ((" (gloo all-gather)" if cpu_backend else " (RCCL all-gather over xGMI)")
+                                   if world_size > 1 else "")),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
             "cpu_executor": cpu_exec,
+            "reference_definition": ref_def,
             "error_flags": flags,
             "nodes": node_table,
             "startup": startup,
         }
-        print(json.dumps(out))
-    assert bool(torch.isfinite(returns).all()), "non-finite returns in the hand-off tensor"
+        if cpu_backend:
+            out["backend"] = "cpu (rehearsal of the rank plumbing, not a GPU measurement)"
+        print(json.dumps(out), flush=True)
     del returns
-    sim.close()
     if dist is not None:
         dist.destroy_process_group()
 
