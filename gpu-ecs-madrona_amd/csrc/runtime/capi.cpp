@@ -125,6 +125,7 @@ using namespace madrona;
 struct mw_exec {
     Executor *exec;
 #if !defined(MW_CPU_BACKEND)
+    int32_t gpu = 0;              // HIP device of the executor (mw_config.gpu_id)
     ncclComm_t comm = nullptr;    // RCCL communicator for the world-shard hand-off
     hipEvent_t stepDone = nullptr; // mw_stream_wait: recorded behind the enqueued steps
 #endif
@@ -179,6 +180,16 @@ mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
 {
     MW_TRY({
         if (!env || !cfg) throw std::runtime_error("mw_create: null argument");
+        // ABI check: a caller built against another include/madrona_mw.h
+        // (or one that left the header fields unset) is refused before any
+        // other field is read
+        if (cfg->struct_size != sizeof(mw_config) || cfg->abi_version != MW_ABI_VERSION) {
+            throw std::runtime_error(
+                "mw_create: mw_config.struct_size " + std::to_string(cfg->struct_size) +
+                " / abi_version " + std::to_string(cfg->abi_version) + " not supported (this "
+                "library: struct_size " + std::to_string(sizeof(mw_config)) + ", abi_version " +
+                std::to_string(MW_ABI_VERSION) + "); initialise with MW_CONFIG_INIT");
+        }
         EnvFactory f = findEnv(env);
         if (!f) throw std::runtime_error(std::string("mw_create: unknown environment '") + env + "'");
         if (cfg->num_worlds <= 0) throw std::runtime_error("mw_create: num_worlds must be > 0");
@@ -211,7 +222,11 @@ mw_exec *mw_create(const char *env, const mw_config *cfg, const void *user_cfg,
             throw std::runtime_error("mw_create: tmp_alloc_bytes >= -1 and 0 <= max_deferred_destroys <= 65536");
         }
         Executor *e = f(ec, user_cfg, user_cfg_bytes, inits, init_stride);
-        return new mw_exec { e };
+        mw_exec *x = new mw_exec { e };
+#if !defined(MW_CPU_BACKEND)
+        x->gpu = cfg->gpu_id;
+#endif
+        return x;
     }, nullptr)
 }
 
@@ -367,6 +382,8 @@ int mw_rccl_init(mw_exec *exec, const void *id, int32_t nranks, int32_t rank)
         if (exec->comm) throw std::runtime_error("mw_rccl_init: communicator already set");
         ncclUniqueId uid;
         memcpy(&uid, id, sizeof(uid));
+        // the communicator binds to the calling thread's current device
+        MW_HIP_OK(hipSetDevice(exec->gpu));
         MW_NCCL_OK(rccl().commInitRank(&exec->comm, nranks, uid, rank));
         return 0;
     }, -1)

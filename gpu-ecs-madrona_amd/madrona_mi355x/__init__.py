@@ -51,8 +51,12 @@ if len(_mapped_hip_runtimes()) > 1:
                       f"({_mapped_hip_runtimes()}); import torch before loading the library")
 
 
+MW_ABI_VERSION = 1     # include/madrona_mw.h
+
+
 class MwConfig(ctypes.Structure):
-    _fields_ = [("num_worlds", ctypes.c_int32), ("gpu_id", ctypes.c_int32),
+    _fields_ = [("struct_size", ctypes.c_uint32), ("abi_version", ctypes.c_uint32),
+                ("num_worlds", ctypes.c_int32), ("gpu_id", ctypes.c_int32),
                 ("default_capacity", ctypes.c_int32), ("use_graph", ctypes.c_int32),
                 ("tmp_alloc_bytes", ctypes.c_int32), ("max_deferred_destroys", ctypes.c_int32),
                 ("num_workers", ctypes.c_int32), ("serial_nodes", ctypes.c_int32),
@@ -377,7 +381,8 @@ class Executor:
             raise ValueError(f"backend must be 'gpu' or 'cpu', not {backend!r}")
         self._lib = backend_library(backend)
         self.backend = backend
-        cfg = MwConfig(num_worlds, gpu_id, default_capacity, 1 if use_graph else 0,
+        cfg = MwConfig(ctypes.sizeof(MwConfig), MW_ABI_VERSION,
+                       num_worlds, gpu_id, default_capacity, 1 if use_graph else 0,
                        tmp_alloc_bytes, max_deferred_destroys, num_workers,
                        1 if serial_nodes else 0, tmp_pool_bytes)
         self._keep = (user_cfg, inits)

@@ -43,8 +43,20 @@ extern "C" {
 
 typedef struct mw_exec mw_exec;
 
-/* Executor configuration (reference StateConfig, mw_gpu.hpp:20-32). */
+/* ABI version of mw_config (bumped when a field changes meaning or place).
+ * Version 1 = round 5: struct_size / abi_version added in front.           */
+#define MW_ABI_VERSION 1u
+
+/* Executor configuration (reference StateConfig, mw_gpu.hpp:20-32).  The
+ * first two fields identify the layout the caller was compiled against:
+ * mw_create refuses a struct_size / abi_version it does not know (status
+ * NULL + mw_last_error), so a stale caller fails instead of being misread.
+ * Initialise with MW_CONFIG_INIT (C: `mw_config c = MW_CONFIG_INIT;
+ * c.num_worlds = ...`).  The environment's own config struct is checked the
+ * same way through mw_create's user_cfg_bytes.                             */
 typedef struct mw_config {
+    uint32_t struct_size;      /* sizeof(mw_config)                          */
+    uint32_t abi_version;      /* MW_ABI_VERSION                             */
     int32_t num_worlds;        /* worlds stepped by this executor (this GPU) */
     int32_t gpu_id;            /* HIP device ordinal                         */
     int32_t default_capacity;  /* rows per world for archetypes w/o a size   */
@@ -74,6 +86,8 @@ typedef struct mw_config {
                                   0: default (2 x the arenas, 16 MiB - 1 GiB),
                                   -1: none (exhaustion flags the world)     */
 } mw_config;
+
+#define MW_CONFIG_INIT { (uint32_t)sizeof(mw_config), MW_ABI_VERSION }
 
 /* "collisions": rigid-body workload of SURVEY.md §8(d) C3/C4 (128 unit cube
  * hulls + one static plane per world, src/physics).                        */

@@ -107,3 +107,66 @@ def test_missing_native_library_fails_loudly():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
     assert r.returncode != 0
     assert "libmadrona_mw.so" in r.stderr
+
+
+def test_mw_config_size_and_version_are_checked():
+    # a caller compiled against another mw_config layout is
+    # refused with a message instead of being misread (CPU library: no GPU)
+    import madrona_mi355x as mw
+    lib = mw.cpu_library()
+    ccfg = mw.default_collisions_config(4, 1, 64, 64)
+    pos, rot = mw.gen_collisions_inits(1, 4, seed=0)
+    inits = (mw.CollisionsInit * 1)(mw.CollisionsInit(pos[0].ctypes.data, rot[0].ctypes.data))
+
+    def create(size, version):
+        cfg = mw.MwConfig(size, version, 1, 0, 0, 1, 0, 0, 1, 0, 0)
+        return lib.mw_create(b"collisions", ctypes.byref(cfg), ctypes.byref(ccfg),
+                             ctypes.sizeof(ccfg), ctypes.cast(inits, ctypes.c_void_p),
+                             ctypes.sizeof(mw.CollisionsInit))
+
+    for size, version in ((ctypes.sizeof(mw.MwConfig) - 8, mw.MW_ABI_VERSION),
+                          (ctypes.sizeof(mw.MwConfig), mw.MW_ABI_VERSION + 1),
+                          (1, 0)):   # a pre-round-5 struct: num_worlds where struct_size is
+        assert not create(size, version)
+        assert b"struct_size" in lib.mw_last_error()
+    h = create(ctypes.sizeof(mw.MwConfig), mw.MW_ABI_VERSION)
+    assert h, lib.mw_last_error()
+    assert lib.mw_step(h, 1) == 0
+    lib.mw_destroy(h)
+    # the environment's own config is checked through user_cfg_bytes
+    cfg = mw.MwConfig(ctypes.sizeof(mw.MwConfig), mw.MW_ABI_VERSION, 1, 0, 0, 1, 0, 0, 1, 0, 0)
+    assert not lib.mw_create(b"collisions", ctypes.byref(cfg), ctypes.byref(ccfg),
+                             ctypes.sizeof(ccfg) - 4, ctypes.cast(inits, ctypes.c_void_p),
+                             ctypes.sizeof(mw.CollisionsInit))
+    assert b"user config" in lib.mw_last_error()
+
+
+def test_c_caller_with_mw_config_init(tmp_path):
+    # the header's initialiser from C, against the CPU library
+    import madrona_mi355x as mw
+    prog = tmp_path / "cfg.c"
+    prog.write_text(textwrap.dedent("""
+        #include <stdio.h>
+        #include "madrona_mw.h"
+        int main(void) {
+            mw_config c = MW_CONFIG_INIT;
+            c.num_worlds = 2; c.use_graph = 1; c.num_workers = 1;
+            mw_collisions_config cc = { .num_cubes = 8, .num_substeps = 1, .delta_t = 1.f / 60.f,
+                .gravity_z = -9.8f, .max_contacts = 256, .max_candidates = 256,
+                .cube_inv_mass = 1.f, .cube_inv_inertia = 0.375f, .mu_s = 0.5f, .mu_d = 0.5f };
+            static float pos[2 * 8 * 3], rot[2 * 8 * 4];
+            mw_gen_collisions_inits(0, 2, 8, 0, pos, rot);
+            mw_collisions_init in[2] = { { pos, rot }, { pos + 24, rot + 32 } };
+            mw_exec *e = mw_create("collisions", &c, &cc, sizeof(cc), in, sizeof(in[0]));
+            if (!e) { printf("ERR %s\\n", mw_last_error()); return 1; }
+            if (mw_step(e, 3)) { printf("ERR %s\\n", mw_last_error()); return 1; }
+            printf("OK %d\\n", mw_num_worlds(e));
+            return mw_destroy(e);
+        }
+    """))
+    exe = tmp_path / "cfg"
+    libdir = os.path.dirname(mw.CPU_LIB_PATH)
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(prog), "-o",
+                    str(exe), "-L", libdir, "-lmadrona_cpu", "-Wl,-rpath," + libdir], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0 and out.stdout.strip() == "OK 2", (out.stdout, out.stderr)
