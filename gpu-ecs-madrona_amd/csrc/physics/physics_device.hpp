@@ -279,7 +279,11 @@ __device__ __forceinline__ int32_t *binCounter(const PhysArgs &P, int32_t bin, i
 // hull-hull list grows up from the bin's front and the hull-plane list down
 // from its back; every reservation sees all earlier ones of both lists, so
 // refusing any whose two ends would cross (b_hh + n_hh + b_hp + n_hp >
-// binCap) keeps the two lists from ever overwriting each other.
+// binCap) keeps the two lists from ever overwriting each other.  A refused
+// reservation stays counted (undoing it would race with the reservations
+// made meanwhile), so the bin's counts no longer describe written entries:
+// the refusal poisons the bin (counts[2]) and its readers treat it as empty
+// and flag every world of it (loadBinPrefix) -- never stale entries.
 __device__ __forceinline__ bool reserveBin(int32_t *counts, int32_t n_hh, int32_t n_hp,
                                            int32_t bin_cap, int32_t &b_hh, int32_t &b_hp)
 {
@@ -287,7 +291,9 @@ __device__ __forceinline__ bool reserveBin(int32_t *counts, int32_t n_hh, int32_
     const unsigned long long old = add ? atomicAdd((unsigned long long *)counts, add) : 0ull;
     b_hh = (int32_t)(uint32_t)old;
     b_hp = (int32_t)(uint32_t)(old >> 32);
-    return (int64_t)b_hh + n_hh + b_hp + n_hp <= (int64_t)bin_cap;
+    const bool fits = (int64_t)b_hh + n_hh + b_hp + n_hp <= (int64_t)bin_cap;
+    if (!fits) atomicOr(counts + 2, 1);
+    return fits;
 }
 
 // Reset the counters of a list set (`counts`: satWorkCount or
@@ -295,8 +301,8 @@ __device__ __forceinline__ bool reserveBin(int32_t *counts, int32_t n_hh, int32_
 // substep's SAT / plane / contact kernels, have finished.
 __device__ __forceinline__ void resetNarrowLists(int32_t *counts, int32_t tid, int32_t nthreads)
 {
-    for (int32_t i = tid; i < 2 * kNarrowBins; i += nthreads)
-        counts[(i >> 1) * kBinStride + (i & 1)] = 0;
+    for (int32_t i = tid; i < 3 * kNarrowBins; i += nthreads)
+        counts[(i / 3) * kBinStride + i % 3] = 0;
 }
 
 // Exclusive prefix of the bins' counts of list `which` into s_pre[0..64]
@@ -305,9 +311,15 @@ __device__ __forceinline__ void loadBinPrefix(const PhysArgs &P, int32_t which, 
 {
     static_assert(kNarrowBins == 64, "one wave scans the bins");
     if (threadIdx.x < 64) {
-        // a count past the bin (a filter's reservation that overran it was
-        // refused and flagged) is read as the full bin: entries stay in bounds
-        const int32_t v = min(*(volatile int32_t *)binCounter(P, threadIdx.x, which), P.binCap);
+        // a poisoned bin (a filter's reservation overran it, reserveBin) is
+        // read as empty and its worlds are flagged; the clamp keeps any other
+        // count that is ever wrong inside the bin
+        const bool poisoned = *(volatile int32_t *)binCounter(P, threadIdx.x, 2) != 0;
+        const int32_t v = poisoned ? 0 : min(*(volatile int32_t *)binCounter(P, threadIdx.x, which), P.binCap);
+        if (poisoned && blockIdx.x == 0) {
+            for (int32_t w = threadIdx.x; w < P.numWorlds; w += kNarrowBins)
+                atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardList << 8));
+        }
         int32_t x = v;
 #pragma unroll
         for (int32_t o = 1; o < 64; o <<= 1) {

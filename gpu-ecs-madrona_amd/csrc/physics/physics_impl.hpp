@@ -246,7 +246,7 @@ MW_INLINE int32_t numInternalNodes(int32_t num_leaves)   // broadphase.cpp:33-40
 
 // Narrowphase work-list bins (narrowphase.hip; world w in bin w % kNarrowBins).
 constexpr int32_t kNarrowBins = 64;
-constexpr int32_t kBinStride = 32;        // ints per bin (own cache lines): hull-hull at 0, hull-plane at 1 (one 64-bit counter)
+constexpr int32_t kBinStride = 32;        // ints per bin (own cache lines): hull-hull at 0, hull-plane at 1 (one 64-bit counter), poison at 2
 
 // Error flag bits (StateView::errorFlags)
 inline constexpr int32_t kErrIDStoreFull = 1;

@@ -148,16 +148,26 @@ public:
 
     // Row-parallel mode (set by the row-parallel node kernels): the lane's
     // position in the reference's serial walk, (query archetype << 24) | row,
-    // the archetype the lane's row lives in and the node's query-component
-    // mask (queryComponentMask): get / getUnsafe of one of those components
-    // at another row is a cross-row access the serial walk would order and
-    // the row-parallel launch does not, so it raises kErrFlagCrossRow.
-    MW_INLINE void setRowParallel(uint32_t row_key, int32_t own_arch = -1, uint64_t query_mask = 0)
+    // the archetype the lane's row lives in and the exact type keys of the
+    // query components the node's function takes by non-const reference
+    // (rowWriteKeys): get / getUnsafe of one of those components at another
+    // row reads or writes a row another lane of the launch is writing -- an
+    // access the serial walk would order and the row-parallel launch does
+    // not -- so it raises kErrFlagCrossRow.  Components the node only reads
+    // are not flagged (no lane writes them through the query).
+    MW_INLINE void setRowParallel(uint32_t row_key, int32_t own_arch, const RowWriteKeys &keys)
     {
         rowKey_ = row_key;
         seq_ = 0;
         ownArch_ = own_arch;
-        queryMask_ = query_mask;
+        writeKeys_ = keys;
+    }
+    MW_INLINE void setRowParallel(uint32_t row_key)
+    {
+        rowKey_ = row_key;
+        seq_ = 0;
+        ownArch_ = -1;
+        writeKeys_.n = 0;
     }
     // The lane's wave index among the waves covering this world's rows, the
     // world's finished-wave marks (StateView::makeTurn) and the node's epoch.
@@ -251,7 +261,7 @@ protected:
     uint32_t rowKey_ = kSerialRowKey;
     uint32_t seq_ = 0;
     int32_t ownArch_ = -1;
-    uint64_t queryMask_ = 0;
+    RowWriteKeys writeKeys_ {};
     int32_t *turn_ = nullptr;
     int32_t turnChunk_ = 0;
     int32_t turnEpoch_ = 0;
@@ -489,19 +499,50 @@ MW_INLINE void Context::resetTmpAlloc()
 #endif
 }
 
-// One bit per component type (its type key mod 64): the components a
-// row-parallel node's query iterates (the Entity column is the engine's).
-template <typename ComponentT>
-constexpr MW_INLINE uint64_t componentBit()
+namespace detail {
+// Parameter list of a node function (a plain function pointer
+// `void (*)(Ctx &, Cs &...)`); other callables are not introspected.
+template <typename F> struct NodeFnSig { static constexpr bool known = false; };
+template <typename R, typename C, typename... Ps>
+struct NodeFnSig<R (*)(C, Ps...)> {
+    static constexpr bool known = true;
+    template <size_t I> using Param = std::tuple_element_t<I, std::tuple<Ps...>>;
+};
+template <typename T> inline constexpr bool kMutRef = false;
+template <typename T> inline constexpr bool kMutRef<T &> = !std::is_const_v<T>;
+
+template <auto Fn, size_t I, typename ComponentT>
+constexpr bool nodeWrites()
 {
-    return std::is_same_v<std::remove_cv_t<ComponentT>, Entity> ? 0
-               : (1ull << (typeKey<std::remove_cv_t<ComponentT>>() & 63));
+    using Sig = NodeFnSig<decltype(Fn)>;
+    if constexpr (std::is_same_v<std::remove_cv_t<ComponentT>, Entity> ||
+                  std::is_const_v<ComponentT>) {
+        return false;
+    } else if constexpr (Sig::known) {
+        return kMutRef<typename Sig::template Param<I>>;
+    } else {
+        return true;     // unknown signature: every non-const query component
+    }
+}
 }
 
-template <typename... ComponentTs>
-constexpr MW_INLINE uint64_t queryComponentMask()
+// The exact type keys of the query components a row node's function may
+// write (non-const reference parameters), for Context::checkCrossRow.
+template <auto Fn, typename... ComponentTs, size_t... Is>
+constexpr RowWriteKeys rowWriteKeysImpl(std::index_sequence<Is...>)
 {
-    return (uint64_t(0) | ... | componentBit<ComponentTs>());
+    RowWriteKeys r {};
+    ((detail::nodeWrites<Fn, Is, ComponentTs>() && r.n < kMaxRowWriteKeys
+          ? (void)(r.key[r.n++] = typeKey<ComponentTs>())
+          : (void)0),
+     ...);
+    return r;
+}
+
+template <auto Fn, typename... ComponentTs>
+constexpr RowWriteKeys rowWriteKeys()
+{
+    return rowWriteKeysImpl<Fn, ComponentTs...>(std::index_sequence_for<ComponentTs...> {});
 }
 
 template <typename ComponentT>
@@ -511,7 +552,7 @@ MW_INLINE void Context::checkCrossRow(Loc loc)
     // Another lane of the same launch owns that row and may be writing it
     // (the reference walks the world's rows serially, taskgraph.inl:63-71):
     // flag it so an unported world fails loudly instead of racing.
-    if ((queryMask_ & componentBit<ComponentT>()) != 0 && rowParallel() &&
+    if (writeKeys_.has(typeKey<ComponentT>()) && rowParallel() &&
         ((int32_t)loc.archetype != ownArch_ || loc.row != (int32_t)(rowKey_ & 0xFFFFFFu))) {
         raiseFlag(kErrFlagCrossRow);
     }

@@ -248,6 +248,26 @@ inline constexpr int32_t kErrFlagCrossRow = 1 << 23;       // row-parallel get/g
 inline constexpr uint64_t kNoAppendKey = ~0ull;
 inline constexpr uint32_t kSerialRowKey = 0xFFFF'FFFFu;
 
+// Exact type keys of the query components a row-parallel node writes
+// (Context::setRowParallel / checkCrossRow); at most kMaxRowWriteKeys are
+// tracked, further written components go unchecked.
+inline constexpr int32_t kMaxRowWriteKeys = 8;
+struct RowWriteKeys {
+    uint64_t key[kMaxRowWriteKeys];
+    int32_t n;
+
+    // constant indices only (no loop the backend could leave in scratch)
+    template <size_t... Is>
+    MW_INLINE bool hasImpl(uint64_t k, std::index_sequence<Is...>) const
+    {
+        return (((int32_t)Is < n && key[Is] == k) || ...);
+    }
+    MW_INLINE bool has(uint64_t k) const
+    {
+        return hasImpl(k, std::make_index_sequence<kMaxRowWriteKeys> {});
+    }
+};
+
 // Destroy requested by a row-parallel lane; applied by the commit after the
 // node, in key order (= the reference's serial destroy order).
 struct DeferredDestroy {

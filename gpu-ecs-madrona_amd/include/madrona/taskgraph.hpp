@@ -550,7 +550,7 @@ parallelForKernel(const StateView *__restrict__ st_in, int32_t arch, int32_t que
 #pragma unroll 1
             for (int32_t k = 0; k < items && first + k < n; k++) {
                 ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k), arch,
-                                   queryComponentMask<ComponentTs...>());
+                                   rowWriteKeys<Fn, ComponentTs...>());
                 invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, first + k,
                                                         std::index_sequence_for<ComponentTs...> {});
             }
@@ -609,7 +609,7 @@ parallelForWorldKernel(const StateView *__restrict__ st_in, int32_t arch, int32_
 #pragma unroll 1
                 for (int32_t k = 0; k < items && first + k < n; k++) {
                     ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k), arch,
-                                       queryComponentMask<ComponentTs...>());
+                                       rowWriteKeys<Fn, ComponentTs...>());
                     invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, cols, w, first + k,
                                                             std::index_sequence_for<ComponentTs...> {});
                 }
@@ -645,7 +645,7 @@ __device__ inline void rowWorldMulti(StateView *st, const MultiColArgs<sizeof...
 #pragma unroll 1
                 for (int32_t k = 0; k < items && first + k < n; k++) {
                     ctx.setRowParallel(((uint32_t)query_arch << 24) | (uint32_t)(first + k), arch,
-                                       queryComponentMask<ComponentTs...>());
+                                       rowWriteKeys<Fn, ComponentTs...>());
                     invokeRow<ContextT, Fn, ComponentTs...>(ctx, st, arch, m.cols[a], w, first + k,
                                                             std::index_sequence_for<ComponentTs...> {});
                 }

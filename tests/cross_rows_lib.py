@@ -56,10 +56,14 @@ def load_env(backend=None):
 
 
 class CrossSim:
-    def __init__(self, num_worlds, per_node_serial=False, first_world=0, **kw):
+    def __init__(self, num_worlds, per_node_serial=False, first_world=0, graph=None, **kw):
+        # graph: None = the world's row nodes; "peek" / "poke" = the
+        # cross-row check's one-node graphs (cross_rows.hip peekSystem /
+        # pokeSystem)
         mw = load_env(kw.get("backend"))
         inits = (CrossInit * num_worlds)(*[CrossInit(first_world + w) for w in range(num_worlds)])
-        self.exec = mw.Executor(ENV_NAME, num_worlds, CrossConfig(NUM_CELLS, 1 if per_node_serial else 0),
+        mode = {None: 1 if per_node_serial else 0, "peek": 2, "poke": 3}[graph]
+        self.exec = mw.Executor(ENV_NAME, num_worlds, CrossConfig(NUM_CELLS, mode),
                                 inits, ctypes.sizeof(CrossInit), **kw)
         self.num_worlds = num_worlds
 

@@ -42,7 +42,10 @@ struct SparkArch : Archetype<Spark> {};
 
 struct Config {
     int32_t numCells;
-    int32_t perNodeSerial;      // 1: WorldSerialForNode for the three row nodes
+    int32_t perNodeSerial;      // 1: WorldSerialForNode for the three row nodes;
+                                // 2 / 3: the cross-row check's own graphs (one
+                                // neighbour-reading row node + tick: 2 reads
+                                // Cell const, 3 takes Cell by non-const ref)
 };
 struct Init {
     int32_t worldIndex;
@@ -60,6 +63,8 @@ struct World : public WorldBase {
     static MW_HD void churnSystem(Engine &ctx, Entity e, Cell &c);
     static MW_HD void splitSystem(Engine &ctx, Spark &sp);
     static MW_HD void tickSystem(Engine &ctx);
+    static MW_HD void peekSystem(Engine &ctx, Entity e, const Cell &c);
+    static MW_HD void pokeSystem(Engine &ctx, Entity e, Cell &c);
 };
 
 class Engine : public CustomContext<Engine, World> {
@@ -127,6 +132,18 @@ MW_HD void World::tickSystem(Engine &ctx)
     st.running = 0;
 }
 
+// The same neighbour read in a node that only reads Cell (no lane writes a
+// Cell row: not a race, must not flag) and in one that may write it (flags).
+MW_HD void World::peekSystem(Engine &ctx, Entity, const Cell &c)
+{
+    (void)ctx.get<Cell>(c.next);
+}
+
+MW_HD void World::pokeSystem(Engine &ctx, Entity, Cell &c)
+{
+    (void)ctx.get<Cell>(c.next);
+}
+
 void World::registerTypes(ECSRegistry &reg, const Config &)
 {
     reg.registerComponent<Cell>();
@@ -156,7 +173,12 @@ static void setupRowNodes(TaskGraph::Builder &builder)
 
 void World::setupTasks(TaskGraph::Builder &builder, const Config &cfg)
 {
-    if (cfg.perNodeSerial) {
+    if (cfg.perNodeSerial == 2 || cfg.perNodeSerial == 3) {
+        auto peek = cfg.perNodeSerial == 2
+                        ? builder.addToGraph<ParallelForNode<Engine, World::peekSystem, Entity, Cell>>({})
+                        : builder.addToGraph<ParallelForNode<Engine, World::pokeSystem, Entity, Cell>>({});
+        builder.addToGraph<PerWorldNode<Engine, World::tickSystem>>({ peek });
+    } else if (cfg.perNodeSerial) {
         setupRowNodes<true>(builder);
     } else {
         setupRowNodes<false>(builder);

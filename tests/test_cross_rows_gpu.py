@@ -90,6 +90,21 @@ def test_row_parallel_mode_raises_cross_row_flag():
     assert diverged
 
 
+def test_cross_row_flag_only_for_components_the_node_writes():
+    """the check compares exact type keys of the components the
+    node's function takes by non-const reference.  The same neighbour read
+    of Cell flags in a node whose function may write Cell (pokeSystem) and
+    not in one that only reads it (peekSystem: no lane writes a Cell row, so
+    the read does not race)."""
+    import madrona_mi355x as mw
+    peek = cl.CrossSim(64, graph="peek")
+    poke = cl.CrossSim(64, graph="poke")
+    peek.step(3)
+    poke.step(3)
+    assert peek.error_flags() == 0, peek.error_flags()
+    assert poke.error_flags() & mw.ERR_CROSS_ROW, poke.error_flags()
+
+
 def test_ecs_ops_serial_nodes_entity_ids_exact_and_repeatable():
     """Row-parallel, ecs_ops' IDs differ from the reference's: a row makes
     several entities, and its destroys release IDs at the commit, not
