@@ -542,8 +542,9 @@ def main():
             "traffic_source": traffic_src,
             "bytes_per_launch": int(nbytes), "ms_per_launch": round(ms, 4),
             "timed_launches": int(ev_n1 - ev_n0),
-            "timing": ("a HIP event pair bound to the kernel (hipExtLaunchKernelGGL: kernel start to "
-                       "kernel end, no dispatch gap) on every launch of the node in "
+            "timing": ("a HIP event pair bound to each of the node's kernels (hipExtLaunchKernelGGL: "
+                       "kernel start to kernel end, summed over the node's kernels, no dispatch gap) "
+                       "on every launch of the node in "
                        + ("every timed step" if args.timed_every <= 1 else
                           f"every {args.timed_every}th timed step (the first of each run of "
                           f"{args.timed_every}; the step graph is split at that node in those "

@@ -597,6 +597,11 @@ int32_t mw_world_walk_runs(mw_exec *exec)
     MW_TRY({ return exec->exec->worldWalkRuns(); }, -1)
 }
 
+int32_t mw_walk_run_end(mw_exec *exec, int32_t node)
+{
+    MW_TRY({ return exec->exec->walkRunEnd(node); }, -1)
+}
+
 const char *mw_node_name(mw_exec *exec, int32_t node)
 {
     MW_TRY({ return exec->exec->nodeName(node); }, nullptr)

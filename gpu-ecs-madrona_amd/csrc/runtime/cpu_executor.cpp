@@ -513,6 +513,7 @@ const char *Executor::traceFuncName(int32_t) { return nullptr; }
 
 int32_t Executor::numNodes() const { return impl_->graph.numNodes(); }
 int32_t Executor::worldWalkRuns() const { return 0; }
+int32_t Executor::walkRunEnd(int32_t node) const { return node + 1; }
 
 const char *Executor::nodeName(int32_t node) const
 {

@@ -361,6 +361,7 @@ struct Executor::Impl {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
         int32_t timedNode = -1;   // node launched (timed) after this segment
+        int32_t timedEnd = -1;    // ... with the rest of the walk run it starts: [timedNode, timedEnd)
     };
     std::vector<Segment> segs;
     // Sampled live timing (timedEvery > 1): the unsplit step graph, replayed
@@ -378,9 +379,10 @@ struct Executor::Impl {
     int32_t timedIndex = -1;        // setTimedNodeIndex: one node only
     // One event pair per timed launch per enqueued step: a burst of
     // runAsync steps keeps every step's pairs until the next sync.
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> timedPool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timedPool;   // one pair per timed kernel
+    size_t timedNext = 0;           // pairs used since the last sync
+    int64_t timedUnits = 0;         // timed launches (nodes / walk runs) since the last sync
     int32_t timedPerStep = 0;       // timed launches in one step
-    int32_t pendingSteps = 0;       // steps enqueued since the last sync
     double timedMs = 0.0;
     int64_t timedLaunches = 0;
 
@@ -410,7 +412,7 @@ struct Executor::Impl {
     // per node 1 = walkable with walkKernel[i] / resumeKernel[i] and entries
     // [walkOff[i], walkOff[i + 1]) of walkEntriesDev, 2 = a no-op that may sit
     // inside a run (an elided reset), 0 = launched on its own.
-    bool walkEnabled = false;
+    bool walkEnabled = true;
     std::vector<uint8_t> walkable;
     std::vector<uint8_t> walkCommits;        // the node's entries include a commit point
     std::vector<const void *> walkKernel;
@@ -684,37 +686,62 @@ static void traceStepEnd(Executor::Impl &I)
     }
 }
 
-// Event pair `ev` of the step being enqueued (created on first use).
-static std::pair<hipEvent_t, hipEvent_t> &timedPair(Executor::Impl &I, int32_t ev)
+// The next free event pair of the timing pool (created on first use); the
+// pool is read back and recycled at the next sync.
+static std::pair<hipEvent_t, hipEvent_t> &timedPair(Executor::Impl &I)
 {
-    const size_t i = (size_t)I.pendingSteps * I.timedPerStep + ev;
-    while (I.timedPool.size() <= i) {
+    while (I.timedPool.size() <= I.timedNext) {
         hipEvent_t a, b;
         MW_HIP_CHECK(hipEventCreate(&a));
         MW_HIP_CHECK(hipEventCreate(&b));
         I.timedPool.push_back({ a, b });
     }
-    return I.timedPool[i];
+    return I.timedPool[I.timedNext++];
 }
 
-// Node `i` with its kernels bound to the event pair (hipx::TimedLaunch):
-// `start` is first recorded in stream order and then re-bound to the first
-// kernel's start; a node none of whose kernels took the binding (a world
-// library launching through its own calls) keeps the stream-order pair.
-static void launchNodeTimed(Executor::Impl &I, int32_t i, LaunchCtx &lc,
-                            hipEvent_t start, hipEvent_t stop)
+static void nextTimedPair(void *ctx, hipEvent_t *a, hipEvent_t *b)
 {
-    MW_HIP_CHECK(hipEventRecord(start, I.stream));
-    hipx::TimedLaunch t { start, stop };
+    const auto &pr = timedPair(*(Executor::Impl *)ctx);
+    *a = pr.first;
+    *b = pr.second;
+}
+
+// Sum of the elapsed times of the pool's used pairs (after a stream sync);
+// recycles them.
+static double drainTimedPairs(Executor::Impl &I)
+{
+    double total = 0.0;
+    for (size_t i = 0; i < I.timedNext; i++) {
+        float ms = 0;
+        MW_HIP_CHECK(hipEventElapsedTime(&ms, I.timedPool[i].first, I.timedPool[i].second));
+        total += ms;
+    }
+    I.timedNext = 0;
+    return total;
+}
+
+static void launchUnit(Executor::Impl &I, int32_t k, int32_t j, LaunchCtx &lc);
+
+// Node i (or the walk run [i, j) it starts: timed as one unit, its walk and
+// resume kernels) with each of its kernels bound to an event pair of the
+// pool (hipx::TimedLaunch: the unit's time is the sum of its kernels').  A
+// unit none of whose kernels took a binding (a world library launching
+// through its own calls) is timed by a stream-order pair around it.
+static void launchNodeTimed(Executor::Impl &I, int32_t i, int32_t j, LaunchCtx &lc)
+{
+    const auto &pr = timedPair(I);
+    MW_HIP_CHECK(hipEventRecord(pr.first, I.stream));
+    hipx::TimedLaunch t { pr.first, pr.second, &nextTimedPair, &I };
     hipx::tlTimed = &t;
     try {
-        launchNode(I, i, lc);
+        launchUnit(I, i, j, lc);
     } catch (...) {
         hipx::tlTimed = nullptr;
         throw;
     }
     hipx::tlTimed = nullptr;
-    if (t.start) MW_HIP_CHECK(hipEventRecord(stop, I.stream));
+    if (t.kernels == 0) MW_HIP_CHECK(hipEventRecord(pr.second, I.stream));
+    I.timedUnits++;
 }
 
 // World walk planning (before any capture: a node's walk plan may read a
@@ -779,6 +806,11 @@ static void planWorldWalk(Executor::Impl &I, LaunchCtx &lc)
         }
         const int32_t per_cu = hipx::residentBlocks(k, resume ? "worldResumeKernel" : "worldWalkKernel", 64, 0);
         int64_t grid = std::min<int64_t>(I.cfg.numWorlds, (int64_t)per_cu * std::max(I.numCUs, 1));
+        // the walk: one block per world -- the hardware dispatcher balances
+        // the worlds (fantasy_vs: 120 vs 118 M env-steps/s for the resident
+        // grid striding over them); MADRONA_MW_WALK_FULL_GRID=0: resident grid
+        const char *fg = getenv("MADRONA_MW_WALK_FULL_GRID");
+        if (!resume && !(fg && atoi(fg) == 0)) grid = I.cfg.numWorlds;
         if (resume) {
             // enough blocks for the usual handful of stopped worlds; slabs
             // bounded to 256 MiB
@@ -833,30 +865,41 @@ static void launchWorldWalk(Executor::Impl &I, LaunchCtx &lc, int32_t b, int32_t
     hipx::checkLaunched("worldResumeKernel");
 }
 
-// Nodes [b, e) in order: maximal runs of walkable nodes of one walk kernel
-// with at least two real nodes become one walk launch each; the rest are
-// launched node by node.  Tracing keeps per-node launches (its markers).
+// The end of the walk run starting at node k within [k, e): a maximal run of
+// walkable nodes of one walk kernel with at least two real nodes; k + 1 when
+// node k starts none (tracing keeps per-node launches, for its markers).
+static int32_t walkRunEnd(const Executor::Impl &I, int32_t k, int32_t e)
+{
+    if (I.trace || k >= (int32_t)I.walkable.size() || I.walkable[k] != 1) return k + 1;
+    const void *kern = I.walkKernel[k];
+    int32_t j = k, real = 0;
+    while (j < e && (I.walkable[j] == 2 || (I.walkable[j] == 1 && I.walkKernel[j] == kern))) {
+        real += I.walkable[j] == 1;
+        j++;
+    }
+    return real >= 2 ? j : k + 1;
+}
+
+// Nodes [k, j) as one unit: a walk run (walkRunEnd) or the single node k.
+static void launchUnit(Executor::Impl &I, int32_t k, int32_t j, LaunchCtx &lc)
+{
+    if (j > k + 1) {
+        bool commits = false;
+        for (int32_t q = k; q < j; q++) commits |= I.walkCommits[q] != 0;
+        launchWorldWalk(I, lc, k, j, commits);
+    } else {
+        launchNode(I, k, lc);
+    }
+}
+
+// Nodes [b, e) in order, walk runs as one walk launch each, the rest node by
+// node.
 static void launchRange(Executor::Impl &I, int32_t b, int32_t e, LaunchCtx &lc)
 {
-    int32_t k = b;
-    while (k < e) {
-        if (!I.trace && k < (int32_t)I.walkable.size() && I.walkable[k] == 1) {
-            const void *kern = I.walkKernel[k];
-            int32_t j = k, real = 0;
-            while (j < e && (I.walkable[j] == 2 || (I.walkable[j] == 1 && I.walkKernel[j] == kern))) {
-                real += I.walkable[j] == 1;
-                j++;
-            }
-            if (real >= 2) {
-                bool commits = false;
-                for (int32_t q = k; q < j; q++) commits |= I.walkCommits[q] != 0;
-                launchWorldWalk(I, lc, k, j, commits);
-                k = j;
-                continue;
-            }
-        }
-        launchNode(I, k, lc);
-        k++;
+    for (int32_t k = b; k < e;) {
+        const int32_t j = walkRunEnd(I, k, e);
+        launchUnit(I, k, j, lc);
+        k = j;
     }
 }
 
@@ -864,15 +907,14 @@ static void launchRange(Executor::Impl &I, int32_t b, int32_t e, LaunchCtx &lc)
 // gathers.  Nodes of the timed kind are bracketed by their own event pair.
 static void launchStep(Executor::Impl &I, LaunchCtx &lc, const StateView &dv)
 {
-    int32_t ev = 0;
     traceStepBegin(I);
     int32_t start = 0;
     for (int32_t i = 0; i < I.graph.numNodes(); i++) {
-        if (isTimed(I, i)) {
+        if (i >= start && isTimed(I, i)) {
             launchRange(I, start, i, lc);
-            const auto &pr = timedPair(I, ev++);
-            launchNodeTimed(I, i, lc, pr.first, pr.second);
-            start = i + 1;
+            const int32_t j = walkRunEnd(I, i, I.graph.numNodes());
+            launchNodeTimed(I, i, j, lc);
+            start = j;
         }
     }
     launchRange(I, start, I.graph.numNodes(), lc);
@@ -916,9 +958,10 @@ static void captureSegments(Executor::Impl &I, LaunchCtx &lc, const StateView &d
     int32_t start = 0;
     for (int32_t i = 0; i <= n; i++) {
         const bool last = i == n;
-        if (!last && !(split && isTimed(I, i))) continue;
+        if (!last && !(split && i >= start && isTimed(I, i))) continue;
         Executor::Impl::Segment sg;
         sg.timedNode = last ? -1 : i;
+        sg.timedEnd = last ? -1 : walkRunEnd(I, i, n);
         if (i > start || last || (start == 0 && I.trace)) {
             MW_HIP_CHECK(hipStreamBeginCapture(I.stream, hipStreamCaptureModeThreadLocal));
             try {
@@ -941,7 +984,7 @@ static void captureSegments(Executor::Impl &I, LaunchCtx &lc, const StateView &d
             MW_HIP_CHECK(hipGraphInstantiate(&sg.exec, sg.graph, nullptr, nullptr, 0));
         }
         I.segs.push_back(sg);
-        start = i + 1;
+        start = last ? n + 1 : sg.timedEnd;
     }
 }
 
@@ -986,24 +1029,20 @@ int32_t Executor::worldWalkRuns() const
 {
     const Impl &I = *impl_;
     const int32_t n = (int32_t)I.walkable.size();
-    int32_t runs = 0, k = 0;
-    while (k < n) {
-        if (I.walkable[k] == 1) {
-            int32_t j = k, real = 0;
-            while (j < n && (I.walkable[j] == 2 ||
-                             (I.walkable[j] == 1 && I.walkKernel[j] == I.walkKernel[k]))) {
-                real += I.walkable[j] == 1;
-                j++;
-            }
-            if (real >= 2) {
-                runs++;
-                k = j;
-                continue;
-            }
-        }
-        k++;
+    int32_t runs = 0;
+    for (int32_t k = 0; k < n;) {
+        const int32_t j = ::madrona::walkRunEnd(I, k, n);
+        runs += j > k + 1;
+        k = j;
     }
     return runs;
+}
+
+int32_t Executor::walkRunEnd(int32_t node) const
+{
+    const int32_t n = impl_->graph.numNodes();
+    if (node < 0 || node >= n) throw std::runtime_error("walkRunEnd: node index past the graph");
+    return ::madrona::walkRunEnd(*impl_, node, n);
 }
 const char *Executor::nodeName(int32_t node) const
 {
@@ -1089,18 +1128,13 @@ void Executor::runAsync()
     const bool sampled = I.plainSegs.empty() || I.stepIndex % I.timedEvery == 0;
     I.stepIndex++;
     if (!I.segs.empty()) {
-        int32_t ev = 0;
         for (auto &sg : sampled ? I.segs : I.plainSegs) {
             if (sg.exec) MW_HIP_CHECK(hipGraphLaunch(sg.exec, I.stream));
-            if (sg.timedNode >= 0) {
-                const auto &pr = timedPair(I, ev++);
-                launchNodeTimed(I, sg.timedNode, lc, pr.first, pr.second);
-            }
+            if (sg.timedNode >= 0) launchNodeTimed(I, sg.timedNode, sg.timedEnd, lc);
         }
     } else {
         launchStep(I, lc, dv);
     }
-    if (I.timedPerStep > 0 && sampled) I.pendingSteps++;
 }
 
 void Executor::runSteps(int32_t n)
@@ -1113,14 +1147,9 @@ void Executor::sync()
     Impl &I = *impl_;
     MW_HIP_CHECK(hipStreamSynchronize(I.stream));
     // every enqueued step's timed launches since the last sync
-    const size_t n = (size_t)I.pendingSteps * I.timedPerStep;
-    for (size_t i = 0; i < n; i++) {
-        float ms = 0;
-        MW_HIP_CHECK(hipEventElapsedTime(&ms, I.timedPool[i].first, I.timedPool[i].second));
-        I.timedMs += ms;
-        I.timedLaunches++;
-    }
-    I.pendingSteps = 0;
+    I.timedMs += drainTimedPairs(I);
+    I.timedLaunches += I.timedUnits;
+    I.timedUnits = 0;
 }
 
 void Executor::run()
@@ -1340,34 +1369,25 @@ int32_t Executor::numRows(int32_t archetype, int32_t world)
 
 double Executor::timeNode(const char *name, int32_t num_steps)
 {
-    const StateView &dv = impl_->mgr->deviceViewHost();
-    LaunchCtx lc = makeLaunchCtx(*impl_, this);
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+    Impl &I = *impl_;
+    sync();        // live timing so far is accounted before the pool is reused
+    const StateView &dv = I.mgr->deviceViewHost();
+    LaunchCtx lc = makeLaunchCtx(I, this);
     for (int32_t s = 0; s < num_steps; s++) {
-        for (int32_t i = 0; i < impl_->graph.numNodes(); i++) {
-            bool match = strcmp(impl_->graph.nodeName(i), name) == 0;
-            if (match) {
-                hipEvent_t a = nullptr, b = nullptr;
-                MW_HIP_CHECK(hipEventCreate(&a));
-                MW_HIP_CHECK(hipEventCreate(&b));
-                evs.push_back({ a, b });
-                launchNodeTimed(*impl_, i, lc, a, b);
+        for (int32_t i = 0; i < I.graph.numNodes(); i++) {
+            if (strcmp(I.graph.nodeName(i), name) == 0) {
+                launchNodeTimed(I, i, i + 1, lc);
             } else {
-                launchNode(*impl_, i, lc);
+                launchNode(I, i, lc);
             }
         }
-        launchExports(*impl_, dv);
+        launchExports(I, dv);
     }
-    MW_HIP_CHECK(hipStreamSynchronize(impl_->stream));
-    double total = 0;
-    for (auto &e : evs) {
-        float ms = 0;
-        MW_HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
-        total += ms;
-        (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
-    }
-    return evs.empty() ? -1.0 : total / (double)evs.size();
+    MW_HIP_CHECK(hipStreamSynchronize(I.stream));
+    const int64_t units = I.timedUnits;
+    const double total = drainTimedPairs(I);
+    I.timedUnits = 0;
+    return units == 0 ? -1.0 : total / (double)units;
 }
 
 bool Executor::entityLoc(int32_t world, Entity e, Loc *out)

@@ -37,15 +37,32 @@ int32_t residentBlocksNoThrow(const void *fn, int32_t threads, size_t dyn_lds);
 void checkLaunched(const char *name);
 
 // Live node timing (Executor::setTimedNode / timeNode).  While a
-// TimedLaunch is installed on this thread, MW_LAUNCH binds its events to the
-// kernels it launches (hipExtLaunchKernelGGL): `start` to the first kernel's
-// start (then cleared), `stop` to every kernel's end, the last one winning.
-// The pair then spans the node's kernels only, not the dispatch gap between
-// the preceding graph segment and the node's first kernel that stream-order
-// hipEventRecord markers include (≈30 us per solver launch on the MI355X box).
+// TimedLaunch is installed on this thread, MW_LAUNCH / launchKernel bind an
+// event pair to every kernel they launch (hipExtLaunchKernelGGL: the pair
+// records that kernel's start and end): the first kernel takes (start,
+// stop), each further kernel a fresh pair from next(ctx).  The timed time of
+// a node (or walk run) is the SUM of its kernels' durations -- what a
+// rocprofv3 kernel trace sums -- not the span from the first kernel's start
+// to the last one's end, which for eagerly launched multi-kernel units
+// includes the dispatch gaps between them (a walk run's walk and resume
+// kernels: ~70 us of gap on the MI355X box against ~100 us of kernels).
 struct TimedLaunch {
     hipEvent_t start = nullptr;
     hipEvent_t stop = nullptr;
+    void (*next)(void *ctx, hipEvent_t *start, hipEvent_t *stop) = nullptr;
+    void *ctx = nullptr;
+    int32_t kernels = 0;          // kernels bound so far
+
+    // the pair of the next kernel
+    void bind(hipEvent_t *a, hipEvent_t *b)
+    {
+        if (kernels++ == 0 || !next) {
+            *a = kernels == 1 ? start : nullptr;
+            *b = stop;
+        } else {
+            next(ctx, a, b);
+        }
+    }
 };
 inline thread_local TimedLaunch *tlTimed = nullptr;
 
@@ -55,9 +72,9 @@ inline hipError_t launchKernel(const void *fn, dim3 grid, dim3 block, void **arg
                                hipStream_t stream)
 {
     if (TimedLaunch *t = tlTimed) {
-        const hipEvent_t start = t->start;
-        t->start = nullptr;
-        return hipExtLaunchKernel(fn, grid, block, args, lds, stream, start, t->stop, 0);
+        hipEvent_t a, b;
+        t->bind(&a, &b);
+        return hipExtLaunchKernel(fn, grid, block, args, lds, stream, a, b, 0);
     }
     return hipLaunchKernel(fn, grid, block, args, lds, stream);
 }
@@ -77,9 +94,9 @@ inline hipError_t launchKernel(const void *fn, dim3 grid, dim3 block, void **arg
         ::madrona::hipx::residentBlocks((const void *)&(kernel), #kernel,              \
                                         (int32_t)(blk__.x * blk__.y * blk__.z), (lds)); \
         if (::madrona::hipx::TimedLaunch *tl__ = ::madrona::hipx::tlTimed) {             \
-            const hipEvent_t start__ = tl__->start;                                     \
-            tl__->start = nullptr;                                                      \
-            hipExtLaunchKernelGGL(kernel, grid, blk__, lds, stream, start__, tl__->stop, \
+            hipEvent_t start__, stop__;                                                 \
+            tl__->bind(&start__, &stop__);                                              \
+            hipExtLaunchKernelGGL(kernel, grid, blk__, lds, stream, start__, stop__,    \
                                   0u, __VA_ARGS__);                                     \
         } else {                                                                        \
             hipLaunchKernelGGL(kernel, grid, blk__, lds, stream, __VA_ARGS__);         \

@@ -165,6 +165,9 @@ public:
     // persistent kernel; MADRONA_MW_WORLD_WALK=1 when the graph is set).
     // 0 when off or on the CPU back end.
     int32_t worldWalkRuns() const;
+    // The end of the walk run node `node` starts (one launch for nodes
+    // [node, end)); node + 1 when it starts none.
+    int32_t walkRunEnd(int32_t node) const;
     const char *nodeName(int32_t node) const;
     int32_t nodeBlocksPerCU(int32_t node) const;
     void setNodeBlocksPerCU(int32_t node, int32_t blocks_per_cu);

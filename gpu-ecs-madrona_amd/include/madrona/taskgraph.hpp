@@ -742,6 +742,54 @@ __device__ inline int32_t walkUniform(int32_t x)
     return __builtin_amdgcn_readfirstlane(x);
 }
 
+// A world function's arguments: under the generated dispatch the function
+// inlines into the walk kernel, whose state pointer is its own
+// `const __restrict__` argument -- left untouched, the backend keeps it (and
+// the column pointers loaded from it) in the global address space and reads
+// the state view with scalar loads; an integer round trip through
+// readfirstlane would make every such access a flat vector load (measured:
+// 4.8x the vector memory reads of the per-node kernels).  Called through a
+// pointer, the arguments arrive in VGPRs and walkUniform makes them scalar.
+template <typename T>
+__device__ inline T walkArg(T x)
+{
+#if defined(MW_WALK_DISPATCH)
+    return x;
+#else
+    return walkUniform(x);
+#endif
+}
+
+// How the walk calls an entry's world function.  A world source compiled
+// through its generated wrapper (MW_WALK_DISPATCH, tools/gen_walk_dispatch.py,
+// the analogue of the reference's generated dispatch() switch) gets
+// walkDispatch: direct calls to every world function of this translation
+// unit, which inline into the walk kernel.  Otherwise (an out-of-tree world
+// built without the generator) the call goes through the device pointer.
+#if defined(MW_WALK_DISPATCH)
+namespace {
+__device__ void walkDispatch(const WalkEntry &e, const WalkCtx &c, int32_t w);
+}
+#endif
+__device__ inline void walkCall(const WalkEntry &e, const WalkCtx &c, int32_t w)
+{
+#if defined(MW_WALK_DISPATCH)
+    walkDispatch(e, c, w);
+#else
+    e.fn(e, c, w);
+#endif
+}
+
+// World functions under the generated dispatch inline into the walk kernel;
+// MW_WALK_NOINLINE keeps each its own function, called directly (measured
+// slower: the caster's row code takes 97 VGPRs under the function ABI
+// against 68 inlined, fantasy_vs 63 vs 74 M env-steps/s).
+#if defined(MW_WALK_DISPATCH) && defined(MW_WALK_NOINLINE)
+#define MW_WALK_FN_ATTR __attribute__((noinline))
+#else
+#define MW_WALK_FN_ATTR
+#endif
+
 __device__ inline void walkSync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -757,15 +805,34 @@ __device__ inline void walkSync()
 // is not reachable from this kernel, so its register budget is the world
 // functions' (the commit alone needs ~120 VGPRs; most nodes of most worlds
 // never reach it).
+// Waves per SIMD the walk kernel is compiled for (its register budget).
+#ifndef MW_WALK_WAVES
+#define MW_WALK_WAVES 1
+#endif
+// Walk profile (experiments only, -DMW_WALK_PROFILE): per entry the summed
+// wall-clock ticks (100 MHz) its world function took, over every world and
+// launch, and the calls (g_walkProf[64 + i]); the generated wrapper exports
+// the reader (mw_debug_walk_profile_<world source>).
+#if defined(MW_WALK_PROFILE)
+namespace {
+__device__ unsigned long long g_walkProf[128];
+}
+#endif
+
 template <typename Tag>
-__global__ void __launch_bounds__(64)
-worldWalkKernel(const WalkEntry *__restrict__ entries, int32_t n, StateView *st, int32_t *resume)
+__global__ void __launch_bounds__(64, MW_WALK_WAVES)
+worldWalkKernel(const WalkEntry *__restrict__ entries, int32_t n, const StateView *__restrict__ st_in,
+                int32_t *resume)
 {
     MW_TRACE_BLOCK(0);
+    StateView *st = const_cast<StateView *>(st_in);
     const WalkCtx c { st };
     for (int32_t w = (int32_t)blockIdx.x; w < st->numWorlds; w += (int32_t)gridDim.x) {
 #pragma unroll 1
         for (int32_t i = 0; i < n; i++) {
+#if defined(MW_WALK_PROFILE)
+            const long long t0 = wall_clock64();
+#endif
             const WalkEntry &e = entries[i];
             if (e.kind == kWalkCommit) {
                 if (commitLoad(st->appendDirty + w) != 0 || commitLoad(st->deferCount + w) != 0) {
@@ -774,8 +841,14 @@ worldWalkKernel(const WalkEntry *__restrict__ entries, int32_t n, StateView *st,
                 }
                 continue;
             }
-            e.fn(e, c, w);
+            walkCall(e, c, w);
             walkSync();
+#if defined(MW_WALK_PROFILE)
+            if (threadIdx.x == 0 && i < 64 && (w & 15) == 0) {   // sampled: 1 world in 16
+                atomicAdd(&g_walkProf[i], (unsigned long long)(wall_clock64() - t0));
+                atomicAdd(&g_walkProf[64 + i], 1ull);
+            }
+#endif
         }
     }
 }
@@ -787,10 +860,11 @@ worldWalkKernel(const WalkEntry *__restrict__ entries, int32_t n, StateView *st,
 // does; a step where no world stopped costs one pass of loads.
 template <typename Tag>
 __global__ void __launch_bounds__(64)
-worldResumeKernel(const WalkEntry *__restrict__ entries, int32_t n, StateView *st, int32_t *resume,
-                  char *scratch, uint64_t per_block, CommitShape shape, uint64_t ws_bytes)
+worldResumeKernel(const WalkEntry *__restrict__ entries, int32_t n, const StateView *__restrict__ st_in,
+                  int32_t *resume, char *scratch, uint64_t per_block, CommitShape shape, uint64_t ws_bytes)
 {
     MW_TRACE_BLOCK(0);
+    StateView *st = const_cast<StateView *>(st_in);
     char *ws = scratch + (size_t)blockIdx.x * per_block;
     char *moves = ws + ws_bytes;
     const WalkCtx c { st };
@@ -810,7 +884,7 @@ worldResumeKernel(const WalkEntry *__restrict__ entries, int32_t n, StateView *s
                         commitWorld(*st, shape, ws, moves, w);
                     }
                 } else {
-                    e.fn(e, c, w);
+                    walkCall(e, c, w);
                 }
                 walkSync();
             }
@@ -850,17 +924,20 @@ struct RowWalkParams {
 // (rowWorldMulti, as parallelForWorldMultiKernel), or the world-serial walk
 // on threads_per_invocation lanes (serialForKernel's body).
 template <typename ContextT, auto Fn, int32_t threads, int32_t items, typename... ComponentTs>
-__device__ void rowWalkEntry(const WalkEntry &e_in, const WalkCtx &c, int32_t w_in)
+__device__ MW_WALK_FN_ATTR void rowWalkEntry(const WalkEntry &e_in, const WalkCtx &c, int32_t w_in)
 {
-    const WalkEntry &e = *walkUniform(&e_in);
-    const int32_t w = walkUniform(w_in);
+    const WalkEntry &e = *walkArg(&e_in);
+    const int32_t w = walkArg(w_in);
     const auto &p = *reinterpret_cast<const RowWalkParams<sizeof...(ComponentTs)> *>(e.params);
     const int32_t lane = (int32_t)(threadIdx.x & 63);
-    StateView *st = walkUniform(c.st);
+    StateView *st = walkArg(c.st);
     if (!p.serial) {
         rowWorldMulti<ContextT, Fn, threads, items, ComponentTs...>(st, p.m, w, lane);
         return;
     }
+#if defined(MW_WALK_NO_SERIAL)
+    return;
+#endif
     if (lane >= threads) return;
     ContextT ctx = worldContext<ContextT>(st, w);
     for (int32_t a = 0; a < p.m.n; a++) {
@@ -881,10 +958,10 @@ __device__ void rowWalkEntry(const WalkEntry &e_in, const WalkCtx &c, int32_t w_
 
 // PerWorldNode: Fn(ctx) on the world's lane 0 (world-serial context).
 template <typename ContextT, auto Fn>
-__device__ void perWorldWalkEntry(const WalkEntry &, const WalkCtx &c, int32_t w_in)
+__device__ MW_WALK_FN_ATTR void perWorldWalkEntry(const WalkEntry &, const WalkCtx &c, int32_t w_in)
 {
-    const int32_t w = walkUniform(w_in);
-    StateView *st = walkUniform(c.st);
+    const int32_t w = walkArg(w_in);
+    StateView *st = walkArg(c.st);
     if ((threadIdx.x & 63) != 0) return;
     ContextT ctx = worldContext<ContextT>(st, w);
     Fn(ctx);
@@ -900,10 +977,10 @@ struct NodeFnWalkParams {
 };
 
 template <typename NodeT, auto fn>
-__device__ void nodeFnWalkEntry(const WalkEntry &e_in, const WalkCtx &, int32_t w_in)
+__device__ MW_WALK_FN_ATTR void nodeFnWalkEntry(const WalkEntry &e_in, const WalkCtx &, int32_t w_in)
 {
-    const WalkEntry &e = *walkUniform(&e_in);
-    const int32_t w = walkUniform(w_in);
+    const WalkEntry &e = *walkArg(&e_in);
+    const int32_t w = walkArg(w_in);
     const auto &p = *reinterpret_cast<const NodeFnWalkParams<NodeT> *>(e.params);
     const int32_t total = (int32_t)(p.count * p.threads);
     for (int32_t base = 0; base < total; base += 64) {
@@ -1171,7 +1248,17 @@ TaskGraph::NodeID TaskGraph::Builder::addNodeFn(TypedDataID<NodeT> data,
 #endif
     };
 #if defined(__HIPCC__)
-    if (fixed_num_invocations > 0 && fixed_num_invocations != 0xFFFF'FFFFu) {
+    // A device node joins a world walk only when it declares itself
+    // world-local (static constexpr bool kWorldLocal = true: invocation
+    // w * count + k touches world w only).  The per-node launch orders the
+    // node after every world of the previous node; the walk does not, so a
+    // node reading another world's state, or state other nodes accumulate
+    // across worlds, must stay out of it (the default).
+    constexpr bool world_local = [] {
+        if constexpr (requires { NodeT::kWorldLocal; }) return (bool)NodeT::kWorldLocal;
+        else return false;
+    }();
+    if (world_local && fixed_num_invocations > 0 && fixed_num_invocations != 0xFFFF'FFFFu) {
         fns.walk = [](void *d, LaunchCtx &lc, detail::WalkEntry *out, const void **kernels) -> int32_t {
             const Desc &dd = *(const Desc *)d;
             detail::NodeFnWalkParams<NodeT> p { (NodeT *)(lc.nodeData + (size_t)dd.dataIdx * maxNodeDataBytes),

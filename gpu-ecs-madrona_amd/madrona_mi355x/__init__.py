@@ -171,6 +171,7 @@ def _declare(lib):
     lib.mw_timed_node_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
     lib.mw_num_nodes.argtypes = [ctypes.c_void_p]
     lib.mw_world_walk_runs.argtypes = [ctypes.c_void_p]
+    lib.mw_walk_run_end.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     lib.mw_node_name.restype = ctypes.c_char_p
     lib.mw_node_name.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     lib.mw_node_blocks_per_cu.argtypes = [ctypes.c_void_p, ctypes.c_int32]
@@ -214,7 +215,7 @@ C_ABI_SYMBOLS = (
     "mw_rccl_get_unique_id", "mw_rccl_init", "mw_allgather_exported", "mw_device_alloc",
     "mw_device_free", "mw_gen_fvs_inits", "mw_stream_wait", "mw_load_hull",
     "mw_trace_enable", "mw_trace_read", "mw_trace_func_name", "mw_trace_block_records",
-    "mw_num_nodes", "mw_world_walk_runs", "mw_node_name", "mw_node_blocks_per_cu", "mw_set_node_blocks_per_cu",
+    "mw_num_nodes", "mw_world_walk_runs", "mw_walk_run_end", "mw_node_name", "mw_node_blocks_per_cu", "mw_set_node_blocks_per_cu",
     "mw_parse_exec_config_override", "mw_parse_exec_config_file",
     "mw_export_row_bytes", "mw_load_env", "mw_num_envs", "mw_env_name",
     "mw_entity_loc", "mw_copy_exported_async", "mw_phys_kernel_variants",
@@ -510,8 +511,15 @@ class Executor:
         """Node kinds of the sorted step graph, by node index."""
         return [self._lib.mw_node_name(self.h, i).decode() for i in range(self._lib.mw_num_nodes(self.h))]
 
+    def walk_run_end(self, node):
+        """End of the walk run node `node` starts (node + 1: none)."""
+        n = self._lib.mw_walk_run_end(self.h, node)
+        if n < 0:
+            raise _err(self._lib)
+        return n
+
     def world_walk_runs(self):
-        """World-walk launches per step (MADRONA_MW_WORLD_WALK=1 at creation)."""
+        """World-walk launches per step (0 with MADRONA_MW_WORLD_WALK=0 at creation)."""
         n = self._lib.mw_world_walk_runs(self.h)
         if n < 0:
             raise _err(self._lib)

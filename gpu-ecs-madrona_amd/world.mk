@@ -20,6 +20,22 @@ MW_HIPFLAGS := -std=c++20 -O3 -fPIC --offload-arch=$(MW_ARCH) -mcode-object-vers
                -I$(MADRONA_MW)/include
 MW_LDFLAGS := -L$(MADRONA_MW)/$(MW_BUILD) -lmadrona_mw -Wl,-rpath,$(abspath $(MADRONA_MW)/$(MW_BUILD))
 
+# The world walk's generated dispatch (MADRONA_MW_WORLD_WALK=1; the
+# reference's generated megakernel dispatch, src/mw/cuda_exec.cpp:560-700):
+# list the world's walk functions from its device IR, then compile the
+# generated wrapper (it includes the source) instead of the source.  A world
+# built directly from its source still walks, through device function
+# pointers (slower: the indirect-call register budget).
+#
+#     build/myworld.ll: myworld.hip
+#     	$(MW_HIPCC) $(MW_HIPFLAGS) $(MW_WALK_IR_FLAGS) $< -o $@
+#     build/myworld_walk.hip: build/myworld.ll
+#     	$(MW_WALK_GEN) myworld.hip $< $@
+#     libmyworld.so: build/myworld_walk.hip
+#     	$(MW_HIPCC) $(MW_HIPFLAGS) -shared -o $@ $< $(MW_LDFLAGS)
+MW_WALK_IR_FLAGS := --cuda-device-only -S -emit-llvm -Xclang -disable-llvm-passes
+MW_WALK_GEN := python3 $(MADRONA_MW)/tools/gen_walk_dispatch.py
+
 # The same world for the CPU back end (libmadrona_cpu.so): g++, no HIP.
 #
 #     libmyworld_cpu.so: myworld.hip

@@ -305,13 +305,19 @@ typedef struct mw_jobs_collisions_config {
  * node reverts it to the default; re-captures the step graph.             */
 int32_t mw_num_nodes(mw_exec *exec);
 /* World walk (the persistent megakernel, reference src/mw/device/
- * megakernel_impl.inl:29-55): with MADRONA_MW_WORLD_WALK=1 in the
- * environment at mw_create, runs of consecutive world-local nodes (row nodes
- * over small tables with their ordered commits, world-serial row nodes,
- * per-world nodes, fixed-count device nodes) are walked by one kernel, a
- * wave per world calling each node's world function in graph order; same
- * results.  Returns the walk launches per step (0: off / CPU back end).    */
+ * megakernel_impl.inl:29-55): runs of consecutive world-local nodes (row
+ * nodes over small tables with their ordered commits, world-serial row
+ * nodes, per-world nodes, device nodes that declare kWorldLocal) are walked
+ * by one kernel, a wave per world calling each node's world function in
+ * graph order through the dispatch generated at build time from the world
+ * source; same results.  On by default; MADRONA_MW_WORLD_WALK=0 in the
+ * environment at mw_create launches every node on its own.  Returns the
+ * walk launches per step (0: off / CPU back end).                          */
 int32_t mw_world_walk_runs(mw_exec *exec);
+/* The end of the walk run that node `node` starts: nodes [node, end) are one
+ * walk launch (and one unit for mw_set_timed_node_index); node + 1 when it
+ * starts none.  -1 on a bad index.                                         */
+int32_t mw_walk_run_end(mw_exec *exec, int32_t node);
 const char *mw_node_name(mw_exec *exec, int32_t node);
 int32_t mw_node_blocks_per_cu(mw_exec *exec, int32_t node);
 int mw_set_node_blocks_per_cu(mw_exec *exec, int32_t node, int32_t blocks_per_cu);

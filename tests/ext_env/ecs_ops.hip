@@ -170,8 +170,10 @@ MW_HD void World::spawnSystem(Engine &ctx, Entity e, Counter &c)
     }
 }
 
-// One-off node, one invocation per world (reference addOneOffNode).
+// One-off node, one invocation per world (reference addOneOffNode).  It only
+// touches its own world, so it may run inside a world walk (kWorldLocal).
 struct StatsNode : NodeBase {
+    static constexpr bool kWorldLocal = true;
     MW_HD void run(int32_t world)
     {
 #if MW_EXEC_PASS

@@ -1,7 +1,9 @@
 """GPU: the world walk (the persistent megakernel; reference
-src/mw/device/megakernel_impl.inl:29-55).  With MADRONA_MW_WORLD_WALK=1 at
-creation, runs of consecutive world-local nodes are walked by one kernel,
-a wave per world calling each node's world function in graph order; a world
+src/mw/device/megakernel_impl.inl:29-55).  By default (MADRONA_MW_WORLD_WALK=0
+turns it off at creation) runs of consecutive world-local nodes are walked by
+one kernel, a wave per world calling each node's world function in graph
+order through the dispatch generated from the world source at build time
+(tools/gen_walk_dispatch.py: direct calls, no function pointers); a world
 with structural work stops at the commit point and worldResumeKernel commits
 and finishes it.  Every state must equal the per-node launches bit for bit:
   * fantasy_vs through its deaths (every fvs node is world-local: the tick is
@@ -86,3 +88,33 @@ def test_cross_rows_serial_walk_matches_reference(monkeypatch):
             assert cl.worlds_equal(sim, plain, w), (s, w)
             if ref is not None:
                 assert cl.worlds_equal(sim, ref, w), ("reference", s, w)
+
+
+def test_walk_is_default_and_times_as_one_unit(monkeypatch):
+    """The walk is on without the variable; timing the node that starts a
+    walk run (mw_set_timed_node_index) times the whole run as one launch
+    (walk + resume kernels bound to the event pair) and leaves the state
+    bit-exact with the untimed per-node run."""
+    import madrona_mi355x as mw
+    monkeypatch.delenv("MADRONA_MW_WORLD_WALK", raising=False)
+    W = 32
+    inits = ol.gen_fvs_inits(W, 50, 200, seed=5)
+    a = mw.FvsSim(W, inits)
+    assert a.world_walk_runs() == 1
+    end = a.walk_run_end(0)
+    assert end == len(a.nodes())          # the whole tick is one run
+    assert a.walk_run_end(end - 1) == end  # a node inside it starts none
+    _walk(monkeypatch, False)
+    b = mw.FvsSim(W, inits)
+    assert b.world_walk_runs() == 0 and b.walk_run_end(0) == 1
+    a.set_timed_node_index(0, every=3)
+    a.step(30)
+    b.step(30)
+    ms, n = a.timed_node()
+    assert n == 10 and ms > 0
+    a.set_timed_node(None)
+    a.step(20)
+    b.step(20)
+    for w in range(W):
+        for arch in (0, 1):
+            assert a.table(w, arch).tobytes() == b.table(w, arch).tobytes(), (w, arch)

@@ -172,11 +172,25 @@ def main():
     sim = mw.FvsSim(W, inits)
 
     systems = node_systems(sim.nodes())
-    # untimed pre-roll: the first ticks time each modelled node in turn (its
+    # launch units: a world-walk run (the nodes one walk launch covers,
+    # mw_walk_run_end) or a single node
+    units, i = {}, 0
+    while i < len(systems):
+        units[i] = sim.walk_run_end(i)
+        i = units[i]
+
+    def unit_name(i):
+        names = [systems[k] for k in range(i, units[i])]
+        return names[0] if len(names) == 1 else "world walk: " + " + ".join(names)
+
+    def unit_bytes(i, nd, nk):
+        return sum(SYS_BYTES[systems[k]](nd, nk) for k in range(i, units[i]) if systems[k] in SYS_BYTES)
+
+    # untimed pre-roll: the first ticks time each modelled unit in turn (its
     # kernels bound to an event pair) to pick the dominant one
     node_ms = {}
-    for i, sysname in systems.items():
-        if sysname not in SYS_BYTES:
+    for i in units:
+        if not any(systems[k] in SYS_BYTES for k in range(i, units[i])):
             continue
         sim.set_timed_node_index(i)
         sim.step(5)
@@ -184,7 +198,7 @@ def main():
         node_ms[i] = ms / max(1, n)
     sim.set_timed_node(None)
     dom = max(node_ms, key=node_ms.get)
-    dom_sys = systems[dom]
+    dom_sys = unit_name(dom)
     left = args.preroll - 5 * len(node_ms)
     if left < 0:
         raise SystemExit("--preroll too short for the node timing")
@@ -227,7 +241,7 @@ def main():
     nk_mean = sum((b[0] - a[0]) * (a[2] + b[2]) / 2 for a, b in zip(rows_by_tick, rows_by_tick[1:])) / span
 
     launch_ms = (ms1 - ms0) / max(1, n1 - n0)
-    nbytes = W * SYS_BYTES[dom_sys](nd_mean, nk_mean)
+    nbytes = W * unit_bytes(dom, nd_mean, nk_mean)
     achieved = nbytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
     cpu = cpu_exec = None
     if not args.no_cpu_baseline:
@@ -244,19 +258,23 @@ def main():
         "config": {"workload": f"examples/fantasy_vs restated: {W} worlds x ({args.dragons} "
                                f"dragons + {args.knights} knights), Game::tick with cleanup",
                    "timed_ticks": f"{args.preroll + 1}-{args.preroll + args.steps}"},
-        "roofline": {"bound": "hbm", "kernel": f"{dom_sys} (node {dom}: row kernels + ordered commit)",
+        "roofline": {"bound": "hbm",
+                     "kernel": (f"{dom_sys} (nodes {dom}-{units[dom] - 1}: the walk kernel + its resume "
+                                "kernel)" if units[dom] > dom + 1 else
+                                f"{dom_sys} (node {dom}: row kernels + ordered commit)"),
                      "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": pmc_traffic(dom_sys), "ms_per_launch": round(launch_ms, 4),
                      "timed_launches": int(n1 - n0),
-                     "timing": "a HIP event pair bound to the node's kernels (first kernel start to "
-                               "last kernel end) on every 10th tick of the timed window (the step "
-                               "graph is split at that node on those ticks only)",
+                     "timing": "a HIP event pair bound to each of the unit's kernels (start to end, "
+                               "summed over its kernels) on every 10th tick of the timed window (the "
+                               "step graph is split at that unit on those ticks only)",
                      "bytes_per_launch": int(nbytes),
-                     "bytes_model": f"{W} worlds x SYS_BYTES['{dom_sys}'] at the window's mean live "
+                     "bytes_model": f"{W} worlds x SYS_BYTES of {dom_sys} at the window's mean live "
                                     f"rows per world: {nd_mean:.1f} dragons, {nk_mean:.1f} knights"},
         "cpu_baseline": cpu, "cpu_executor": cpu_exec, "error_flags": flags,
-        "nodes_ms_per_launch_preroll": {systems[i]: round(v, 4) for i, v in node_ms.items()},
+        "world_walk_runs": sim.world_walk_runs(),
+        "nodes_ms_per_launch_preroll": {unit_name(i): round(v, 4) for i, v in node_ms.items()},
         "live_rows_sampled_worlds": {"sampled_worlds": len(sampled),
                                      "at_init": [args.dragons, args.knights],
                                      "by_tick_dragons_knights_per_world":
