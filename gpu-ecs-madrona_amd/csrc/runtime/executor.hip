@@ -425,6 +425,7 @@ struct Executor::Impl {
     char *walkScratch = nullptr;
     uint64_t walkPerBlock = 0;
     uint64_t walkWsBytes = 0;
+    size_t walkLds = 0;             // resume kernel: dynamic LDS for the commit working set (0: in the slab)
     std::vector<std::pair<const void *, int32_t>> walkGrid;   // kernel -> grid
 };
 
@@ -794,9 +795,18 @@ static void planWorldWalk(Executor::Impl &I, LaunchCtx &lc)
         MW_HIP_CHECK(hipMemset(I.walkResume, 0xFF, sizeof(int32_t) * std::max(I.cfg.numWorlds, 1)));
     }
     // resident grids (one wave per block); the resume kernel's blocks each
-    // own a global scratch slab for the commit
+    // own a global scratch slab for the commit's row moves and keep its
+    // working set in LDS, as the ordered-commit kernel does (in the slab
+    // too when it does not fit: measured 43 vs ~20 us per fantasy_vs tick)
     const CommitArgs &A = I.commit;
-    I.walkWsBytes = (detail::commitWorkingBytes(A.shape) + 255) / 256 * 256;
+    const size_t ws = detail::commitWorkingBytes(A.shape);
+    bool ws_in_lds = A.shape.capMax > 0;
+    for (int32_t i = 0; i < n && ws_in_lds; i++) {
+        if (I.walkable[i] == 1)
+            ws_in_lds = hipx::residentBlocksNoThrow(I.resumeKernel[i], 64, ws) > 0;
+    }
+    I.walkLds = ws_in_lds ? ws : 0;
+    I.walkWsBytes = ws_in_lds ? 0 : (ws + 255) / 256 * 256;
     I.walkPerBlock = I.walkWsBytes + (A.scratchPerBlock + 255) / 256 * 256;
     int64_t max_resume = 1;
     I.walkGrid.clear();
@@ -804,7 +814,8 @@ static void planWorldWalk(Executor::Impl &I, LaunchCtx &lc)
         for (auto &g : I.walkGrid) {
             if (g.first == k) return;
         }
-        const int32_t per_cu = hipx::residentBlocks(k, resume ? "worldResumeKernel" : "worldWalkKernel", 64, 0);
+        const int32_t per_cu = hipx::residentBlocks(k, resume ? "worldResumeKernel" : "worldWalkKernel", 64,
+                                                    resume ? I.walkLds : 0);
         int64_t grid = std::min<int64_t>(I.cfg.numWorlds, (int64_t)per_cu * std::max(I.numCUs, 1));
         // the walk: one block per world -- the hardware dispatcher balances
         // the worlds (fantasy_vs: 120 vs 118 M env-steps/s for the resident
@@ -859,9 +870,9 @@ static void launchWorldWalk(Executor::Impl &I, LaunchCtx &lc, int32_t b, int32_t
     uint64_t per_block = I.walkPerBlock, ws_bytes = I.walkWsBytes;
     detail::CommitShape shape = I.commit.shape;
     void *args[] = { &entries, &n, &st, &res, &scratch, &per_block, &shape, &ws_bytes };
-    hipx::residentBlocks(resume, "worldResumeKernel", 64, 0);
-    MW_HIP_CHECK(hipx::launchKernel(resume, dim3((uint32_t)walkGridOf(I, resume)), dim3(64), args, 0,
-                                    I.stream));
+    hipx::residentBlocks(resume, "worldResumeKernel", 64, I.walkLds);
+    MW_HIP_CHECK(hipx::launchKernel(resume, dim3((uint32_t)walkGridOf(I, resume)), dim3(64), args,
+                                    I.walkLds, I.stream));
     hipx::checkLaunched("worldResumeKernel");
 }
 

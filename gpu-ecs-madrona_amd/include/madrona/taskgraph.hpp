@@ -854,7 +854,7 @@ worldWalkKernel(const WalkEntry *__restrict__ entries, int32_t n, const StateVie
 }
 
 // The worlds a walk stopped at a commit point: commit (the executor's ordered
-// commit, working set in this block's global slab), then the rest of the
+// commit, working set in LDS when it fits), then the rest of the
 // world's entries, committing again wherever the world is dirty.  Blocks
 // (one wave) check 64 worlds per round with one ballot, as the commit kernel
 // does; a step where no world stopped costs one pass of loads.
@@ -865,8 +865,12 @@ worldResumeKernel(const WalkEntry *__restrict__ entries, int32_t n, const StateV
 {
     MW_TRACE_BLOCK(0);
     StateView *st = const_cast<StateView *>(st_in);
-    char *ws = scratch + (size_t)blockIdx.x * per_block;
-    char *moves = ws + ws_bytes;
+    // the commit's working set: in this block's dynamic LDS (ws_bytes == 0,
+    // as the ordered-commit kernel keeps it), else in its global slab
+    extern __shared__ __align__(16) char resume_lds[];
+    char *slab = scratch + (size_t)blockIdx.x * per_block;
+    char *ws = ws_bytes == 0 ? resume_lds : slab;
+    char *moves = slab + ws_bytes;
     const WalkCtx c { st };
     const int32_t lane = (int32_t)(threadIdx.x & 63);
     for (int64_t base = blockIdx.x; base < st->numWorlds; base += (int64_t)gridDim.x * 64) {
