@@ -329,6 +329,10 @@ struct RefWorld {
     TaskGraph *graph;
     bool logCandidates = false;
     std::vector<CandidateCollision> candidates;   // logCandidates mode only
+    int32_t numSubsteps = 0;
+    // logCandidates mode: SolverData::numContacts right after the last
+    // substep's narrowphase node (-1 when the node layout check fails)
+    int32_t lastContactCount = -1;
 };
 
 // Mirror of TaskGraph's private layout (include/madrona/taskgraph.hpp:15-27,
@@ -359,23 +363,46 @@ static_assert(sizeof(TaskGraphMirror) == sizeof(TaskGraph));
 // (src/physics/physics.cpp:1184-1185) empties it (Table::clear,
 // src/common/table.cpp:83-86), so that copy is the step's full candidate
 // list in emission order.  Nothing is written to world state.
+//
+// The step's contact count: the nodes are sorted in registration order
+// (src/core/taskgraph.cpp:18-108), so after findOverlapping (node F, the one
+// after which the candidate table is first non-empty) each substep adds 8
+// nodes -- collectConstraints, substepRigidBodies, narrowphase and its
+// ResetTmpAllocNode (narrowphase.cpp:1766-1785), solvePositions,
+// setVelocities, solveVelocities, ResetTmpAlloc (src/physics/physics.cpp:
+// 1157-1183) -- and SolverData::numContacts, which only narrowphase raises
+// (narrowphase.cpp:1127) and solveVelocities resets (physics.cpp:1007), is
+// read right after the last substep's narrowphase node (F + 3 + 8 (S - 1)).
+// Layout checks: the count is 0 just before that node and again after its
+// substep's solveVelocities (4 nodes later); otherwise -1.
 static void runLogged(RefWorld *rw)
 {
     auto *g = (TaskGraphMirror *)rw->graph;
     Engine &ctx = *rw->ctx;
+    SolverData &solver = ctx.getSingleton<SolverData>();
     auto q = ctx.query<CandidateCollision>();
     bool done = false;
+    CountT last_np = -1;
     rw->candidates.clear();
+    rw->lastContactCount = 0;      // no candidates: no contacts
+    bool layout_ok = true;
     for (CountT i = 0; i < g->numNodes; i++) {
         if (!done) {
             ctx.forEach(q, [&](CandidateCollision &c) {
                 rw->candidates.push_back(c);
             });
             done = !rw->candidates.empty();
+            if (done) last_np = i + 2 + 8 * (CountT)(rw->numSubsteps - 1);
         }
+        if (i == last_np) layout_ok = layout_ok && solver.numContacts.load_relaxed() == 0;
         const auto &n = g->nodes[i];
         n.fn((NodeBase *)&g->datas[n.dataIDX].userData[0], rw->ctx);
+        if (i == last_np) rw->lastContactCount = (int32_t)solver.numContacts.load_relaxed();
+        if (last_np >= 0 && i == last_np + 4) {
+            layout_ok = layout_ok && solver.numContacts.load_relaxed() == 0;
+        }
     }
+    if (!layout_ok || (done && last_np + 4 >= g->numNodes)) rw->lastContactCount = -1;
 }
 
 // Set before ref_phys_create: worlds created afterwards log their candidate
@@ -456,6 +483,7 @@ static void * createWorlds(bool simple, int32_t num_worlds,
         };
         new (rw->world) PhysWorld(*rw->ctx, h->mgr, *cfg, init, simple, num_hulls);
         rw->logCandidates = g_logCandidates && !simple;
+        rw->numSubsteps = cfg->numSubsteps;
 
         TaskGraph::Builder builder(*rw->ctx);
         if (simple) setupSimpleTasks(builder, cfg->numSubsteps);
@@ -679,6 +707,15 @@ MADRONA_EXPORT int32_t ref_phys_read_candidates(void *handle, int32_t world,
     memcpy(out, rw->candidates.data(),
            sizeof(CandidateCollision) * (size_t)(n < cap ? n : cap));
     return n;
+}
+
+// The last step's last-substep contact count (logCandidates worlds; -1
+// otherwise, or when runLogged's node layout check failed).
+MADRONA_EXPORT int32_t ref_phys_last_contact_count(void *handle, int32_t world)
+{
+    auto *h = (RefPhys *)handle;
+    RefWorld *rw = h->worlds[world];
+    return rw->logCandidates ? rw->lastContactCount : -1;
 }
 
 MADRONA_EXPORT int32_t ref_sizeof(int32_t what)

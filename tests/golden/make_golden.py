@@ -13,8 +13,10 @@ Worlds 0, 1, 4095 and 8191 of BASELINE.json configs[2] (8192 worlds drawn
 with seed 0, serially in world order, then sliced) stepped by the reference
 to steps 130, 145 (the driver's timed steps 126-145) and 330 (the end of
 bench.py's default window 131-330): bodies, the step's candidate pairs (the
-harness's read-only candidate log, oracle/ref_harness.cpp runLogged) and the
-last substep's contact prefix.  The GPU test loads it at full size
+harness's read-only candidate log, oracle/ref_harness.cpp runLogged), the
+last substep's contact count as the reference counted it (numContacts right
+after that narrowphase node, runLogged) and exactly those contacts.  The GPU
+test loads it at full size
 (tests/test_collisions_gpu.py::test_collisions_full_size_vs_reference_window).
 """
 import os
@@ -57,7 +59,13 @@ def make_window():
             out[f"candidates_{step}_{i}"] = ref.candidates(i)
             raw = ref.contacts_raw(i)
             n = int((raw["ref"][:, 0] != 0xFFFFFFFF).sum())
-            out[f"contacts_{step}_{i}"] = raw[:n].view(np.uint8).reshape(n, -1)
+            # the last substep's own count (numContacts right after its
+            # narrowphase node): the raw prefix also holds rows earlier
+            # substeps wrote past it (the array is poisoned once per step)
+            count = ref.last_contact_count(i)
+            assert count <= n, (step, i, count, n)
+            out[f"contacts_{step}_{i}"] = raw[:count].view(np.uint8).reshape(count, -1)
+            out[f"contact_count_{step}_{i}"] = np.int32(count)
     path = os.path.join(HERE, "collisions_window_ref.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")

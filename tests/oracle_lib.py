@@ -389,6 +389,16 @@ class ReferencePhys:
         self.lib.ref_phys_read_contacts(self.h, w, _vp(out))
         return out
 
+    def last_contact_count(self, w):
+        """SolverData::numContacts right after the last step's last
+        narrowphase node (log_candidates worlds; oracle/ref_harness.cpp
+        runLogged)."""
+        self.lib.ref_phys_last_contact_count.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        n = self.lib.ref_phys_last_contact_count(self.h, w)
+        if n < 0:
+            raise RuntimeError("no contact count (not a log_candidates world, or the node layout check failed)")
+        return n
+
 
 # ---------------------------------------------------------------------------
 # fantasy_vs (C5): oracle/fvs_oracle.cpp and the reference ECS (oracle/ref_fvs.cpp)

@@ -107,7 +107,10 @@ def test_oracle_bit_exact_vs_live_reference():
             assert orc.candidates(w).tobytes() == ref.candidates(w).tobytes(), (step, w)
             raw = ref.contacts_raw(w)
             raw = raw[raw["ref"][:, 0] != 0xFFFFFFFF]
-            assert _contact_prefix_equal(orc.contacts(w), raw) is None, (step, w)
+            got = orc.contacts(w)
+            # the reference's own count of the last substep's manifolds
+            assert len(got) == ref.last_contact_count(w), (step, w, len(got))
+            assert _contact_prefix_equal(got, raw) is None, (step, w)
             if step % 10 == 0:
                 n_o, a_o, p_o, s_o = orc.bvh(w)
                 n_r, a_r, p_r, s_r = ref.bvh(w)
@@ -139,10 +142,10 @@ def test_oracle_bit_exact_vs_reference_window_golden():
             want = g[f"bodies_{step}_{i}"].view(BODY_DTYPE)
             assert orc.bodies(i).tobytes() == want.tobytes(), (step, worlds[i])
             assert orc.candidates(i).tobytes() == g[f"candidates_{step}_{i}"].tobytes()
-            raw = g[f"contacts_{step}_{i}"].view(CONTACT_DTYPE).reshape(-1)
+            want_c = g[f"contacts_{step}_{i}"].view(CONTACT_DTYPE).reshape(-1)
             got = orc.contacts(i)
-            assert len(got) > 0
-            assert _contact_prefix_equal(got, raw) is None, (step, worlds[i])
+            assert len(got) == int(g[f"contact_count_{step}_{i}"]) == len(want_c) > 0
+            assert _contact_prefix_equal(got, want_c) is None, (step, worlds[i])
 
 
 def test_oracle_small_world_counts_and_threads_agree():
