@@ -160,6 +160,7 @@ void PhysicsModule::buildArgs(void *stream)
     for (int32_t i = 0; i < n; i++) {
         BodyArch &B = P.body[i];
         B.archetype = archs[i];
+        mgr->pinCapacity(archs[i]);       // PhysArgs keeps its slab pointers and capacity
         const ArchetypeView &av = dv.arch[archs[i]];
         B.capacity = av.capacity;
         B.numRows = av.numRows;
@@ -255,6 +256,7 @@ void PhysicsModule::buildArgs(void *stream)
     P.maxContacts = maxContacts;
     P.contactOrder = alloc<int32_t>((size_t)W * P.candCapacity, stream);
     const int32_t joint_arch = mgr->archetypeIndex(typeKey<ConstraintData>());
+    mgr->pinCapacity(joint_arch);         // PhysArgs keeps its slab pointer and capacity
     P.jointCapacity = dv.arch[joint_arch].capacity;
     P.numJointRows = dv.arch[joint_arch].numRows;
     P.joints = (JointConstraint *)dv.arch[joint_arch].cols[1];

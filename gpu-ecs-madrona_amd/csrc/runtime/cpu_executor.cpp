@@ -328,6 +328,28 @@ void packExports(Executor::Impl &I)
 
 }
 
+// Table growth between steps (the GPU executor's growTables, at every
+// step here: the CPU back end steps synchronously): a growable table past
+// half its capacity in any world doubles until at most half full.
+static void growTables(Executor::Impl &I)
+{
+    StateView &v = I.mgr->hostView();
+    for (int32_t a = 0; a < v.numArchetypes; a++) {
+        if (!(v.arch[a].flags & kArchGrowable) || !I.mgr->growable(a)) continue;
+        int32_t m = 0;
+        for (int32_t w = 0; w < v.numWorlds; w++) m = std::max(m, v.arch[a].numRows[w]);
+        const int32_t cap = v.arch[a].capacity;
+        if ((int64_t)m * 2 <= cap) continue;
+        int64_t nc = std::max(cap, 1);
+        while ((int64_t)m * 2 > nc) nc *= 2;
+        if (nc > (1 << 28)) throw std::runtime_error("table growth past 2^28 rows per world");
+        I.mgr->growArchetype(a, (int32_t)nc, nullptr);
+        for (CpuExport &b : I.exports) {
+            if (b.archetype == a) b.buf.resize((size_t)v.numWorlds * nc * b.bytes, 0);
+        }
+    }
+}
+
 void Executor::runAsync()
 {
     Impl &I = *impl_;
@@ -357,6 +379,7 @@ void Executor::runAsync()
         I.pool->parallelFor(I.cfg.numWorlds, 1, runWorlds, &arg);
     }
     packExports(I);
+    growTables(I);
 }
 
 // Several steps world-major (every node world-local): each world runs n
@@ -388,6 +411,7 @@ void Executor::runSteps(int32_t n)
         }
     }, &arg);
     packExports(I);
+    growTables(I);
 }
 
 void Executor::sync() {}

@@ -337,6 +337,11 @@ __global__ void traceMarkerKernel(TraceDev *t, uint32_t ev, uint32_t func, uint3
 // ---------------------------------------------------------------------------
 // Executor
 // ---------------------------------------------------------------------------
+struct GrowSet {
+    int32_t n;
+    int32_t arch[kMaxArchetypes];
+};
+
 struct ExportBuf {
     int32_t slot, archetype, column;
     uint32_t bytes;
@@ -426,6 +431,10 @@ struct Executor::Impl {
     uint64_t walkPerBlock = 0;
     uint64_t walkWsBytes = 0;
     size_t walkLds = 0;             // resume kernel: dynamic LDS for the commit working set (0: in the slab)
+    // table growth (growTables): the growable archetypes, their row maxima
+    GrowSet growable {};
+    int32_t *growProbe = nullptr;
+    int64_t growths = 0;
     std::vector<std::pair<const void *, int32_t>> walkGrid;   // kernel -> grid
 };
 
@@ -489,6 +498,7 @@ Executor::~Executor()
     if (impl_->hostRowsTotal) (void)hipHostFree(impl_->hostRowsTotal);
     if (impl_->nodeDataDev) (void)hipFree(impl_->nodeDataDev);
     if (impl_->commit.scratch) (void)hipFree(impl_->commit.scratch);
+    if (impl_->growProbe) (void)hipFree(impl_->growProbe);
     if (impl_->walkEntriesDev) (void)hipFree(impl_->walkEntriesDev);
     if (impl_->walkScratch) (void)hipFree(impl_->walkScratch);
     if (impl_->walkResume) (void)hipFree(impl_->walkResume);
@@ -525,16 +535,19 @@ char *Executor::hostWorldData(int32_t world)
     return v.worldData + (size_t)world * v.worldDataStride;
 }
 
-void Executor::uploadState()
+// Ordered-commit sizing (StateManager: the largest table that takes entity
+// rows or row-parallel appends); one scratch slab per commit block holds a
+// column of it.  Again after a table grows.
+static void setupCommit(Executor::Impl &I)
 {
-    impl_->mgr->uploadToDevice(impl_->stream);
-
-    // Ordered-commit sizing (StateManager: the largest table that takes
-    // entity rows or row-parallel appends); one scratch slab per commit block
-    // holds a column of it.
     {
+        Executor::Impl *impl_ = &I;
         const StateView &dv = impl_->mgr->deviceViewHost();
         CommitArgs &A = impl_->commit;
+        if (A.scratch) {
+            MW_HIP_CHECK(hipFree(A.scratch));
+            A.scratch = nullptr;
+        }
         A.st = impl_->mgr->deviceView();
         A.shape = detail::CommitShape { dv.commitCapMax, dv.commitSortA, dv.commitSortO };
         A.scratchPerBlock = ((uint64_t)dv.commitCapMax * dv.commitColMax + 255) / 256 * 256;
@@ -562,6 +575,33 @@ void Executor::uploadState()
             MW_HIP_CHECK(hipMalloc(&A.scratch, std::max<size_t>(A.scratchPerBlock * A.grid, 256)));
         }
     }
+}
+
+// Growable tables (registerArchetype, StateManager::growable) and the
+// per-archetype row-count maxima the growth check reads.
+__global__ void __launch_bounds__(256) maxRowsKernel(const StateView *__restrict__ st, GrowSet g, int32_t *out)
+{
+    for (int32_t i = 0; i < g.n; i++) {
+        const int32_t *rows = st->arch[g.arch[i]].numRows;
+        int32_t m = 0;
+        for (int32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < st->numWorlds; w += gridDim.x * blockDim.x)
+            m = max(m, rows[w]);
+#pragma unroll
+        for (int32_t o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+        if ((threadIdx.x & 63) == 0 && m > 0) atomicMax(out + i, m);
+    }
+}
+
+void Executor::uploadState()
+{
+    impl_->mgr->uploadToDevice(impl_->stream);
+    setupCommit(*impl_);
+    // growable tables: known once the modules have pinned theirs (upload)
+    impl_->growable.n = 0;
+    for (int32_t a = 0; a < impl_->mgr->numArchetypes(); a++) {
+        if (impl_->mgr->growable(a) && impl_->growable.n < kMaxArchetypes) impl_->growable.arch[impl_->growable.n++] = a;
+    }
+    if (impl_->growable.n > 0) MW_HIP_CHECK(hipMalloc(&impl_->growProbe, sizeof(int32_t) * kMaxArchetypes));
 
     int32_t num_exports = 0;
     const StateManager::ExportDesc *ex = impl_->mgr->exports(&num_exports);
@@ -1153,6 +1193,52 @@ void Executor::runSteps(int32_t n)
     for (int32_t i = 0; i < n; i++) runAsync();
 }
 
+// Table growth between steps (reference Table::addRow, src/common/table.cpp:
+// 44-61, x2 when full; the reference's device runtime grows by device
+// malloc).  At every synchronisation point the growable tables' largest
+// per-world row count is read back; a table past half its capacity doubles
+// (until it is at most half full), so a table grows before it can overflow
+// unless one stretch of unsynchronised steps more than doubles it (then the
+// table-full flag is raised, as before).  A growth re-strides the slabs
+// (StateManager::growArchetype), resizes the commit scratch and the export
+// buffers of that archetype, and re-plans / re-captures the step.
+static bool growTables(Executor &E, Executor::Impl &I)
+{
+    if (I.growable.n == 0) return false;
+    const StateView &dv = I.mgr->deviceViewHost();
+    MW_HIP_CHECK(hipMemsetAsync(I.growProbe, 0, sizeof(int32_t) * kMaxArchetypes, I.stream));
+    const uint32_t blocks = (uint32_t)std::min<int64_t>(1024, (dv.numWorlds + 255) / 256);
+    MW_LAUNCH(maxRowsKernel, dim3(std::max<uint32_t>(blocks, 1)), dim3(256), 0, I.stream,
+              I.mgr->deviceView(), I.growable, I.growProbe);
+    int32_t maxes[kMaxArchetypes];
+    MW_HIP_CHECK(hipMemcpyAsync(maxes, I.growProbe, sizeof(int32_t) * I.growable.n, hipMemcpyDeviceToHost,
+                                I.stream));
+    MW_HIP_CHECK(hipStreamSynchronize(I.stream));
+    bool grown = false;
+    for (int32_t i = 0; i < I.growable.n; i++) {
+        const int32_t a = I.growable.arch[i];
+        const int32_t cap = dv.arch[a].capacity;
+        if ((int64_t)maxes[i] * 2 <= cap) continue;
+        int64_t nc = std::max(cap, 1);
+        while ((int64_t)maxes[i] * 2 > nc) nc *= 2;
+        if (nc > (1 << 28)) throw std::runtime_error("table growth past 2^28 rows per world");
+        I.mgr->growArchetype(a, (int32_t)nc, I.stream);
+        for (ExportBuf &b : I.exports) {
+            if (b.archetype != a) continue;
+            MW_HIP_CHECK(hipFree(b.buf));
+            MW_HIP_CHECK(hipMalloc(&b.buf, std::max<size_t>((size_t)dv.numWorlds * nc * b.bytes, 256)));
+        }
+        grown = true;
+    }
+    if (!grown) return false;
+    I.growths++;
+    setupCommit(I);
+    LaunchCtx lc = makeLaunchCtx(I, &E);
+    planWorldWalk(I, lc);
+    if (I.cfg.useGraph) captureGraph(I, lc, I.mgr->deviceViewHost());
+    return true;
+}
+
 void Executor::sync()
 {
     Impl &I = *impl_;
@@ -1161,6 +1247,7 @@ void Executor::sync()
     I.timedMs += drainTimedPairs(I);
     I.timedLaunches += I.timedUnits;
     I.timedUnits = 0;
+    growTables(*this, I);
 }
 
 void Executor::run()

@@ -40,6 +40,8 @@ struct ArchetypeInfo {
     int32_t capacity;
     bool temporary;
     bool moduleRows = false;
+    bool growable = false;          // registerArchetype without a size (Table::addRow grows it)
+    bool pinned = false;            // a module keeps pointers into its slabs
 };
 
 struct StateManager::Impl {
@@ -160,6 +162,74 @@ void StateManager::setModuleRows(uint64_t key)
     }
 }
 
+void StateManager::pinCapacity(int32_t archetype)
+{
+    if (archetype >= 0 && archetype < (int32_t)impl_->archetypes.size()) {
+        impl_->archetypes[archetype].pinned = true;
+    }
+}
+
+bool StateManager::growable(int32_t archetype) const
+{
+    if (archetype < 0 || archetype >= (int32_t)impl_->archetypes.size()) return false;
+    const ArchetypeInfo &ai = impl_->archetypes[archetype];
+    const bool singleton = std::find(impl_->singletons.begin(), impl_->singletons.end(), ai.key) !=
+                           impl_->singletons.end();
+    return ai.growable && !ai.pinned && !ai.moduleRows && !singleton;
+}
+
+// Entity IDs per world for the current capacities: generous slack because
+// per-cache free lists can strand up to 2 x 64 IDs per cache
+// (id_map_impl.inl:184-226).
+static int32_t idsPerWorldFor(const StateManager::Impl &I)
+{
+    int64_t needed = 64;
+    for (const ArchetypeInfo &ai : I.archetypes) {
+        if (!ai.temporary) needed += ai.capacity;
+    }
+    return (int32_t)(((needed * 2 + 4 * kIDsPerCache) + kIDsPerCache - 1) / kIDsPerCache * kIDsPerCache);
+}
+
+// The ordered commit's shape (madrona/commit.hpp): the largest table that
+// takes entity rows or row-parallel appends (at most kCommitMaxRows rows per
+// world; larger tables raise kErrFlagCommitLimit if a row-parallel node
+// mutates them), the key sorts' sizes and the widest column.
+static void setCommitShape(StateView &d)
+{
+    int32_t cap_max = 0;
+    uint32_t col_max = 4;
+    for (int32_t a = 0; a < d.numArchetypes; a++) {
+        const ArchetypeView &av = d.arch[a];
+        if (av.flags & kArchModuleRows) continue;
+        if (av.capacity > kCommitMaxRows) continue;
+        cap_max = std::max(cap_max, av.capacity);
+        for (int32_t c = 0; c < av.numColumns; c++) col_max = std::max(col_max, av.colBytes[c]);
+    }
+    d.commitCapMax = (cap_max + 63) / 64 * 64;
+    d.commitSortA = 1;
+    while (d.commitSortA < d.commitCapMax) d.commitSortA <<= 1;
+    d.commitSortO = 1;
+    while (d.commitSortO < d.deferCap) d.commitSortO <<= 1;
+    d.commitColMax = col_max;
+}
+
+// [W][old_pitch] -> [W][new_pitch] bytes (new_pitch >= old_pitch; the tail
+// of each world's new span keeps the destination's fill).
+static void restrideHost(char *dst, const char *src, int32_t W, size_t old_pitch, size_t new_pitch)
+{
+    if (!src) return;
+    for (int32_t w = 0; w < W; w++) memcpy(dst + (size_t)w * new_pitch, src + (size_t)w * old_pitch, old_pitch);
+}
+
+static void releaseHostAlloc(StateManager::Impl &I, char *p)
+{
+    auto it = std::find(I.hostAllocs.begin(), I.hostAllocs.end(), p);
+    if (it != I.hostAllocs.end()) {
+        I.hostAllocs.erase(it);
+        free(p);
+    }
+}
+
 uint32_t StateManager::registerArchetypeDesc(uint64_t key, const char *name,
                                              const TypeDesc *comps, int32_t num_comps,
                                              int32_t capacity, bool temporary)
@@ -181,6 +251,7 @@ uint32_t StateManager::registerArchetypeDesc(uint64_t key, const char *name,
         a.cols.push_back(comps[i]);
     }
     if (capacity <= 0) capacity = capacityHint(key);
+    a.growable = capacity <= 0;
     if (capacity <= 0) capacity = impl_->cfg.defaultCapacity;
     a.capacity = capacity;
     a.temporary = temporary;
@@ -246,7 +317,8 @@ void StateManager::finalizeLayout(uint32_t world_data_bytes, uint32_t world_data
         v.archKeys[a] = ai.key;
         av.numColumns = (int32_t)ai.cols.size();
         av.capacity = ai.capacity;
-        av.flags = (ai.temporary ? kArchTemporary : 0u) | (ai.moduleRows ? kArchModuleRows : 0u);
+        av.flags = (ai.temporary ? kArchTemporary : 0u) | (ai.moduleRows ? kArchModuleRows : 0u) |
+                   (ai.growable && !ai.moduleRows ? kArchGrowable : 0u);
         if (std::find(I.singletons.begin(), I.singletons.end(), ai.key) != I.singletons.end()) {
             av.flags |= kArchSingleton;
         }
@@ -263,9 +335,9 @@ void StateManager::finalizeLayout(uint32_t world_data_bytes, uint32_t world_data
         if (!ai.temporary) ids_needed += ai.capacity;
     }
 
-    // Entity IDs: per world, generous slack because per-cache free lists can
-    // strand up to 2 x 64 IDs per cache (id_map_impl.inl:184-226).
-    int64_t ids = ((ids_needed * 2 + 4 * kIDsPerCache) + kIDsPerCache - 1) / kIDsPerCache * kIDsPerCache;
+    // Entity IDs per world (idsPerWorldFor)
+    (void)ids_needed;
+    const int64_t ids = idsPerWorldFor(I);
     v.idsPerWorld = (int32_t)ids;
     v.idNodes = (IDNode *)hostAlloc(I, sizeof(IDNode) * (size_t)W * ids);
     v.idState = (IDMapState *)hostAlloc(I, sizeof(IDMapState) * W);
@@ -402,26 +474,7 @@ void StateManager::uploadToDevice(void *stream_ptr)
     d.makeTurn = (int32_t *)devAlloc(turn_bytes);
     MW_HIP_CHECK(hipMemsetAsync(d.makeTurn, 0, turn_bytes, stream));
     d.makeEpoch = (int32_t *)devAlloc(sizeof(int32_t));
-    // Ordered-commit shape: the largest table that takes entity rows or
-    // row-parallel appends (at most kCommitMaxRows rows per world; larger
-    // tables raise kErrFlagCommitLimit if a row-parallel node mutates them).
-    {
-        int32_t cap_max = 0;
-        uint32_t col_max = 4;
-        for (int32_t a = 0; a < d.numArchetypes; a++) {
-            const ArchetypeView &av = d.arch[a];
-            if (av.flags & kArchModuleRows) continue;
-            if (av.capacity > kCommitMaxRows) continue;
-            cap_max = std::max(cap_max, av.capacity);
-            for (int32_t c = 0; c < av.numColumns; c++) col_max = std::max(col_max, av.colBytes[c]);
-        }
-        d.commitCapMax = (cap_max + 63) / 64 * 64;
-        d.commitSortA = 1;
-        while (d.commitSortA < d.commitCapMax) d.commitSortA <<= 1;
-        d.commitSortO = 1;
-        while (d.commitSortO < d.deferCap) d.commitSortO <<= 1;
-        d.commitColMax = col_max;
-    }
+    setCommitShape(d);
     {
         const int32_t first_epoch = 1;
         copy(d.makeEpoch, &first_epoch, sizeof(int32_t));
@@ -482,6 +535,112 @@ void StateManager::downloadFromDevice(void *stream_ptr)
     MW_HIP_CHECK(hipStreamSynchronize(stream));
 }
 #endif
+
+// Table growth (see state.hpp).  Row i of world w moves from w * cap + i to
+// w * new_cap + i in every column; rows past a world's count keep no
+// meaning (zero-filled), appended-row keys past it stay settled.
+void StateManager::growArchetype(int32_t a, int32_t new_cap, void *stream_ptr)
+{
+    Impl &I = *impl_;
+    if (!growable(a)) throw std::runtime_error("growArchetype: archetype " + std::to_string(a) + " is not growable");
+    ArchetypeInfo &ai = I.archetypes[a];
+    const int32_t cap = ai.capacity;
+    if (new_cap <= cap) return;
+    const int32_t W = I.cfg.numWorlds;
+    StateView &h = I.host;
+    size_t ci = 0;
+    for (int32_t b = 0; b < a; b++) ci += I.archetypes[b].cols.size();
+    const int32_t old_ids = h.idsPerWorld;
+    ai.capacity = new_cap;
+    const int32_t new_ids = std::max(old_ids, idsPerWorldFor(I));
+
+    // host mirror (the arena itself on the CPU back end)
+    for (size_t c = 0; c < ai.cols.size(); c++) {
+        Impl::ColAlloc &ca = I.colAllocs[ci + c];
+        const size_t nb = ai.cols[c].numBytes, bytes = (size_t)W * new_cap * nb;
+        if (ca.host) {
+            char *nh = hostAlloc(I, bytes);
+            restrideHost(nh, ca.host, W, (size_t)cap * nb, (size_t)new_cap * nb);
+            releaseHostAlloc(I, ca.host);
+            ca.host = nh;
+            h.arch[a].cols[c] = nh;
+        }
+    }
+    h.arch[a].capacity = new_cap;
+    if (new_ids > old_ids) {
+        char *nh = hostAlloc(I, sizeof(IDNode) * (size_t)W * new_ids);
+        restrideHost(nh, (const char *)h.idNodes, W, sizeof(IDNode) * old_ids, sizeof(IDNode) * new_ids);
+        releaseHostAlloc(I, (char *)h.idNodes);
+        h.idNodes = (IDNode *)nh;
+        h.idsPerWorld = new_ids;
+    }
+
+#if defined(MW_CPU_BACKEND)
+    (void)stream_ptr;
+    for (size_t c = 0; c < ai.cols.size(); c++) I.colAllocs[ci + c].bytes = (size_t)W * new_cap * ai.cols[c].numBytes;
+    I.devHostCopy = I.host;
+#else
+    hipStream_t stream = (hipStream_t)stream_ptr;
+    StateView &d = I.devHostCopy;
+    std::vector<void *> retired;
+    // a fresh device slab filled with `fill`, registered for release
+    auto devSlab = [&](size_t bytes, int fill) -> char * {
+        void *p = nullptr;
+        MW_HIP_CHECK(hipMalloc(&p, std::max<size_t>(bytes, 256)));
+        MW_HIP_CHECK(hipMemsetAsync(p, fill, std::max<size_t>(bytes, 256), stream));
+        I.devAllocs.push_back(p);
+        I.arenaBytes += bytes;
+        return (char *)p;
+    };
+    auto retire = [&](void *old) {
+        auto it = std::find(I.devAllocs.begin(), I.devAllocs.end(), old);
+        if (it != I.devAllocs.end()) I.devAllocs.erase(it);
+        retired.push_back(old);
+    };
+    auto restride = [&](char *dst, const void *src, size_t old_pitch, size_t new_pitch) {
+        MW_HIP_CHECK(hipMemcpy2DAsync(dst, new_pitch, src, old_pitch, old_pitch, (size_t)W,
+                                      hipMemcpyDeviceToDevice, stream));
+    };
+    for (size_t c = 0; c < ai.cols.size(); c++) {
+        Impl::ColAlloc &ca = I.colAllocs[ci + c];
+        const size_t nb = ai.cols[c].numBytes, bytes = (size_t)W * new_cap * nb;
+        char *nd = devSlab(bytes, 0);
+        restride(nd, ca.dev, (size_t)cap * nb, (size_t)new_cap * nb);
+        retire(ca.dev);
+        ca.dev = nd;
+        ca.bytes = bytes;
+        d.arch[a].cols[c] = nd;
+    }
+    d.arch[a].capacity = new_cap;
+    if (d.arch[a].appendKeys) {
+        uint64_t *old = d.arch[a].appendKeys;
+        // the same limit as at upload: the ordered commit's index arrays
+        if (new_cap <= kCommitMaxRows) {
+            char *nk = devSlab(sizeof(uint64_t) * (size_t)W * new_cap, 0xFF);
+            restride(nk, old, sizeof(uint64_t) * cap, sizeof(uint64_t) * new_cap);
+            d.arch[a].appendKeys = (uint64_t *)nk;
+        } else {
+            d.arch[a].appendKeys = nullptr;     // row-parallel appends now flag (kErrFlagRowParallelOp)
+        }
+        retire(old);
+    }
+    if (new_ids > old_ids) {
+        char *ni = devSlab(sizeof(IDNode) * (size_t)W * new_ids, 0);
+        restride(ni, d.idNodes, sizeof(IDNode) * old_ids, sizeof(IDNode) * new_ids);
+        retire(d.idNodes);
+        d.idNodes = (IDNode *)ni;
+        d.idsPerWorld = new_ids;
+    }
+    setCommitShape(d);
+    h.commitCapMax = d.commitCapMax;
+    h.commitSortA = d.commitSortA;
+    h.commitSortO = d.commitSortO;
+    h.commitColMax = d.commitColMax;
+    MW_HIP_CHECK(hipMemcpyAsync(I.devView, &d, sizeof(StateView), hipMemcpyHostToDevice, stream));
+    MW_HIP_CHECK(hipStreamSynchronize(stream));
+    for (void *p : retired) MW_HIP_CHECK(hipFree(p));
+#endif
+}
 
 int32_t StateManager::resolveQuery(const uint64_t *keys, int32_t num_keys,
                                    int32_t *out_archetypes, int32_t *out_cols,

@@ -281,6 +281,7 @@ struct DeferredDestroy {
 inline constexpr uint32_t kArchTemporary = 1;     // rows have no entity IDs
 inline constexpr uint32_t kArchModuleRows = 2;    // rows written by a module's own kernels
 inline constexpr uint32_t kArchSingleton = 4;     // exactly one row per world, always
+inline constexpr uint32_t kArchGrowable = 8;      // registerArchetype table: the executor grows it
 
 struct ArchetypeView {
     int32_t numColumns;
@@ -527,6 +528,20 @@ public:
     // Rows of this archetype are written by a module's own kernels (e.g. the
     // physics candidate list): no row-parallel append keys are kept for it.
     void setModuleRows(uint64_t archetype_key);
+    // A module keeps pointers into this archetype's slabs (physics bodies):
+    // its capacity stays fixed.
+    void pinCapacity(int32_t archetype);
+
+    // Table growth (reference Table::addRow, src/common/table.cpp:44-61: x2
+    // when a per-world table is full).  Tables registered with
+    // registerArchetype (no fixed size) are growable; the executor grows one
+    // between steps, at its high-water mark, to `new_capacity` rows per
+    // world: every column slab (and the append keys) is re-strided from
+    // [world][capacity] to [world][new_capacity], the entity ID store and the
+    // ordered-commit shape are resized with it, and the device view is
+    // re-uploaded.  The caller re-captures anything that baked capacities in.
+    bool growable(int32_t archetype) const;
+    void growArchetype(int32_t archetype, int32_t new_capacity, void *stream);
 
     template <typename ComponentT>
     uint32_t registerComponent()

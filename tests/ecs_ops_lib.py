@@ -40,7 +40,7 @@ def ref_available():
 
 
 class EcsConfig(ctypes.Structure):
-    _fields_ = [("numAgents", ctypes.c_int32)]
+    _fields_ = [("numAgents", ctypes.c_int32), ("growSpawns", ctypes.c_int32)]
 
 
 class EcsInit(ctypes.Structure):
@@ -59,10 +59,13 @@ def load_env(backend=None):
 
 
 class EcsOpsSim:
-    def __init__(self, num_worlds, first_world=0, tmp_alloc_bytes=64 * 1024, **kw):
+    def __init__(self, num_worlds, first_world=0, tmp_alloc_bytes=64 * 1024, grow_spawns=False, **kw):
+        # grow_spawns: Spawn registered without a size (registerArchetype),
+        # starting at default_capacity rows per world and grown by the
+        # executor between steps
         mw = load_env(kw.get("backend"))
         inits = (EcsInit * num_worlds)(*[EcsInit(first_world + w) for w in range(num_worlds)])
-        self.exec = mw.Executor(ENV_NAME, num_worlds, EcsConfig(NUM_AGENTS), inits,
+        self.exec = mw.Executor(ENV_NAME, num_worlds, EcsConfig(NUM_AGENTS, 1 if grow_spawns else 0), inits,
                                 ctypes.sizeof(EcsInit), tmp_alloc_bytes=tmp_alloc_bytes, **kw)
         self.num_worlds = num_worlds
 

@@ -220,7 +220,11 @@ void World::registerTypes(ECSRegistry &reg, const Config &cfg)
     reg.registerComponent<SpawnInfo>();
     reg.registerFixedSizeArchetype<Agent>(cfg.numAgents);
     reg.registerFixedSizeArchetype<PairTemp>(kMaxPairs);
-    reg.registerFixedSizeArchetype<Spawn>(kMaxSpawns);
+    if (cfg.growSpawns) {
+        reg.registerArchetype<Spawn>();          // grows past mw_config.default_capacity
+    } else {
+        reg.registerFixedSizeArchetype<Spawn>(kMaxSpawns);
+    }
     reg.registerSingleton<Stats>();
     reg.exportSingleton<Stats>(0);
 }

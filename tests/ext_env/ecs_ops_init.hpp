@@ -10,6 +10,7 @@ namespace EcsOps {
 
 struct Config {
     int32_t numAgents;
+    int32_t growSpawns;     // 1: Spawn is a registerArchetype table (the executor grows it)
 };
 struct Init {
     int32_t worldIndex;
