@@ -648,6 +648,7 @@ __global__ void __launch_bounds__(kRefitBlock) refitGlobalKernel(PhysArgs P)
 
 constexpr int32_t kOverlapBuf = 12;     // candidates kept per body before a second sweep
 constexpr int32_t kOverlapMaskWords = 4; // worlds up to 256 leaves: hits as a register bitmask
+static_assert(64 * kOverlapMaskWords == kOverlapSmallLeaves);
 
 // findOverlappingEntry + BVH::findOverlaps (broadphase.cpp:897-932,
 // physics.inl:61-100) without a per-lane tree walk.  Every ancestor slot of
@@ -699,14 +700,32 @@ __host__ __device__ inline size_t overlapLDSBytes(int32_t max_leaves)
            a16b(2 * kOverlapBlock * kOverlapBuf);
 }
 
-size_t findOverlapsSharedBytes(const PhysArgs &P)
+// The bitmask path stages its (self rank, other rank) pairs in the per-lane
+// buffers' space, so the block writes the candidate run coalesced.
+constexpr int32_t kOverlapStage = kOverlapBlock * kOverlapBuf / 2;
+
+// Traversal stacks (int16 node indices, lane-interleaved) for worlds that
+// take the DFS; always in LDS, after the image when that is in LDS too.
+constexpr int32_t kOverlapStack = 64;
+
+__host__ __device__ inline bool overlapUsesDFS(const PhysArgs &P)
 {
-    return overlapLDSBytes(P.maxLeaves);
+    return P.overlapDFSLeaves >= 0 && P.maxLeaves > P.overlapDFSLeaves;
 }
 
-size_t findOverlapsImageBytes(const PhysArgs &P)
+__host__ __device__ inline size_t overlapStackBytes(const PhysArgs &P)
 {
-    return overlapLDSBytes(P.maxLeaves);
+    return overlapUsesDFS(P) ? a16b(2 * kOverlapBlock * kOverlapStack) : 0;
+}
+
+size_t findOverlapsSharedBytes(const PhysArgs &P)
+{
+    return overlapLDSBytes(P.maxLeaves) + overlapStackBytes(P);
+}
+
+size_t findOverlapsGlobalSharedBytes(const PhysArgs &P)
+{
+    return overlapStackBytes(P);
 }
 
 // Phase profile (experiments only, -DMW_SOLVER_PROFILE, the solver's
@@ -731,10 +750,125 @@ extern "C" int mw_debug_overlap_phases(unsigned long long *out)
 #else
 #define MW_OVERLAP_MARK(i) ((void)0)
 #endif
+// Event counts in the same profile: [4] BVH nodes popped, [5] DFS queries,
+// [6] wide queries (the wave sweeps for them).
+#if defined(MW_SOLVER_PROFILE)
+#define MW_OVERLAP_COUNT(i, v) atomicAdd(&g_overlapPhase[(i)], (unsigned long long)(v))
+#else
+#define MW_OVERLAP_COUNT(i, v) ((void)0)
+#endif
+
+// One query's hits (leafHit) over the leaves in emission order, the wave
+// testing 64 leaves per step: the count, and with kWrite the candidates at
+// slot0.. in that order.  q, e_id, a_static and self are the query lane's
+// (wave-uniform).
+template <bool kWrite>
+__device__ __forceinline__ int32_t waveSweep(const OrderedLeaf *leaves, int32_t nleaves,
+                                             const AABB &q, int32_t e_id, bool a_static,
+                                             int32_t self, int32_t slot0,
+                                             CandidateCollision *out, uint64_t *out_slots,
+                                             int32_t cap)
+{
+    const int32_t lane = threadIdx.x & 63;
+    int32_t n = 0;
+    for (int32_t k0 = 0; k0 < nleaves; k0 += 64) {
+        const int32_t k = k0 + lane;
+        const bool hit = k < nleaves && leafHit(leaves, k, q, e_id, a_static);
+        const uint64_t b = __ballot(hit);
+        if (kWrite && hit) {
+            const int32_t slot = slot0 + n + __popcll(b & ((1ull << lane) - 1));
+            if (slot < cap) {
+                out[slot] = CandidateCollision { leaves[self].loc, leaves[k].loc };
+                out_slots[slot] = (uint64_t)leaves[self].slot | (uint64_t)leaves[k].slot << 32;
+            }
+        }
+        n += __popcll(b);
+    }
+    return n;
+}
+
+// BVH::findOverlaps (physics.inl:61-100) for one query: pop a node, visit
+// its children in slot order -- a leaf child whose slot overlaps the query
+// (and passes the id / static filter) is emitted, an overlapping inner
+// child is pushed.  Returns false when the stack would pass
+// kOverlapStack entries (the reference's own stack holds 128), when the walk
+// would pop more than `budget` nodes, or when emit() declines a leaf; the
+// caller then sweeps the leaves, which emits the same sequence.  (A query
+// that reaches most of the tree -- a ground plane's, say, whose hits the id
+// rule drops -- is a serial chain of dependent node loads; the wave sweeps
+// its leaves 64 at a time instead.)
+typedef int32_t NodeWords4 __attribute__((ext_vector_type(4), aligned(4)));
+static_assert(offsetof(BVHNode, minY) == 16 && offsetof(BVHNode, children) == 96);
+
+template <typename Emit>
+__device__ __forceinline__ bool dfsQuery(const BVHNode *__restrict__ nodes, int32_t max_nodes,
+                                         int32_t max_leaves, const AABB &q, int32_t e_id,
+                                         bool a_static, const OrderedLeaf *leaves,
+                                         const int32_t *rank_of, int16_t *stk, int32_t *flags,
+                                         int32_t budget, Emit &&emit)
+{
+    int32_t ss = 0;
+    int32_t cur = 0;
+    int32_t visits = 0;
+#if defined(MW_SOLVER_PROFILE)
+    struct Tally {
+        int32_t &v;
+        __device__ ~Tally() { MW_OVERLAP_COUNT(4, v); }
+    } tally { visits };
+#endif
+    for (;;) {
+        if (++visits > budget) return false;
+        // The node's bounds and children into registers first, as seven
+        // 16-byte loads (nodes are 116 bytes, so only 4-byte aligned; global
+        // loads need no more): the stack pushes below are stores the
+        // compiler cannot prove disjoint from the node, so loads left in the
+        // child loop would wait behind them one slot at a time.
+        int32_t nw[28];
+        const NodeWords4 *src = (const NodeWords4 *)(nodes + cur);
+#pragma unroll
+        for (int j = 0; j < 7; j++) {
+            const NodeWords4 v = src[j];
+            nw[4 * j] = v.x; nw[4 * j + 1] = v.y; nw[4 * j + 2] = v.z; nw[4 * j + 3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int32_t child = nw[24 + i];
+            const bool hit = (child != -1) &
+                             (q.pMin.x < __int_as_float(nw[12 + i])) & (__int_as_float(nw[i]) < q.pMax.x) &
+                             (q.pMin.y < __int_as_float(nw[16 + i])) & (__int_as_float(nw[4 + i]) < q.pMax.y) &
+                             (q.pMin.z < __int_as_float(nw[20 + i])) & (__int_as_float(nw[8 + i]) < q.pMax.z);
+            if (!hit) continue;
+            if (child & 0x80000000) {
+                // the slot test above is the leaf's (the image holds the same
+                // bytes); then e.id < other.id and not both static
+                const int32_t k =
+                    rank_of[guardIndex(child & 0x7fffffff, max_leaves, flags, kGuardLeaf)];
+                const float4 hi = ((const float4 *)leaves)[3 * k + 1];   // .., id, isStatic
+                const bool keep = (e_id < __float_as_int(hi.z)) &
+                                  !(a_static & (__float_as_int(hi.w) != 0));
+                if (keep && !emit(k)) return false;
+            } else {
+                if (ss == kOverlapStack) return false;
+                stk[ss++ * kOverlapBlock] = (int16_t)guardIndex(child, max_nodes, flags, kGuardNode);
+            }
+        }
+        if (ss == 0) return true;
+        cur = stk[--ss * kOverlapBlock];
+    }
+}
+
+size_t findOverlapsImageBytes(const PhysArgs &P)
+{
+    return overlapLDSBytes(P.maxLeaves);
+}
+
 
 // kGlobal: the world's leaf image exceeds a workgroup's LDS; it is staged in
 // the world's slab of P.overlapImage instead (findOverlapsGlobalKernel).
-template <bool kGlobal>
+// kSmall: every world fits the register bitmask (maxLeaves <= 256) and none
+// traverses -- the sweep and traversal paths are compiled out, which keeps
+// this kernel's registers (and so its occupancy) to the bitmask path's own.
+template <bool kGlobal, bool kSmall = false>
 __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
 {
 #if defined(MW_SOLVER_PROFILE)
@@ -747,6 +881,7 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
     OrderedLeaf *leaves = (OrderedLeaf *)img;
     int32_t *rank_of = (int32_t *)(img + a16b(sizeof(OrderedLeaf) * P.maxLeaves));
     uint16_t *bufs = (uint16_t *)((char *)rank_of + a16b(4 * P.maxLeaves));
+    int16_t *stk = (int16_t *)(kGlobal ? smem : img + overlapLDSBytes(P.maxLeaves)) + threadIdx.x;
 
     // Stage leaf slots (from the refit tree) + identity in emission order.
     const broadphase::BVH &bvh = P.bvh[w];
@@ -754,6 +889,7 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
     const BVHNode *nodes = P.nodes + (size_t)w * P.maxNodes;
     const int32_t *order = P.leafOrder + (size_t)w * P.maxLeaves;
     int32_t *flags = P.errorFlags + w;
+    const bool dfs = !kSmall && overlapUsesDFS(P) && nleaves > P.overlapDFSLeaves;
     for (int32_t k = threadIdx.x; k < nleaves; k += kOverlapBlock) {
         const int32_t leaf = guardIndex(order[k], P.maxLeaves, flags, kGuardLeaf);
         const uint32_t lp = P.leafParents[(size_t)w * P.maxLeaves + leaf];
@@ -802,7 +938,68 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
             CandidateCollision *out = P.cands + (size_t)w * P.candCapacity;
             uint64_t *out_slots = P.candSlots + (size_t)w * P.candCapacity;
             int32_t total;
-            if (nleaves <= 64 * kOverlapMaskWords) {
+            // Runs fn(lane, its query, e_id, static, rank) with the wave, for
+            // each lane in m (wave-uniform).
+            auto forWide = [&](uint64_t m, auto &&fn) {
+                for (; m; m &= m - 1) {
+                    const int32_t h = __ffsll((unsigned long long)m) - 1;
+                    AABB qh;
+                    qh.pMin.x = __shfl(q.pMin.x, h, 64); qh.pMin.y = __shfl(q.pMin.y, h, 64);
+                    qh.pMin.z = __shfl(q.pMin.z, h, 64); qh.pMax.x = __shfl(q.pMax.x, h, 64);
+                    qh.pMax.y = __shfl(q.pMax.y, h, 64); qh.pMax.z = __shfl(q.pMax.z, h, 64);
+                    fn(h, qh, __shfl(e_id, h, 64), __shfl((int32_t)a_static, h, 64) != 0,
+                       __shfl(self, h, 64));
+                }
+            };
+            if (dfs) {
+                // BVH::findOverlaps per lane: each body's cost follows its
+                // overlaps, not the world's size.  A query with more than
+                // kOverlapBuf candidates, a deeper stack or a walk past
+                // 32 + leaves/32 nodes (about what sweeping for it costs the
+                // wave) is "wide": its lane stops, and the wave sweeps the
+                // leaves for it, 64 per step, in the same order.
+                bool wide = false;
+                if (active) {
+                    wide = !dfsQuery(nodes, P.maxNodes, P.maxLeaves, q, e_id, a_static, leaves,
+                                     rank_of, stk, flags, 32 + nleaves / 32, [&](int32_t k) {
+                                         if (cnt == kOverlapBuf) return false;
+                                         buf[cnt++] = (uint16_t)k;
+                                         return true;
+                                     });
+                }
+                const uint64_t wides = __ballot(wide);
+                if (active) MW_OVERLAP_COUNT(5, 1);
+                if (wide) MW_OVERLAP_COUNT(6, 1);
+                forWide(wides, [&](int32_t h, const AABB &qh, int32_t eh, bool sh, int32_t selfh) {
+                    const int32_t n = waveSweep<false>(leaves, nleaves, qh, eh, sh, selfh, 0,
+                                                       out, out_slots, 0);
+                    if ((int32_t)(threadIdx.x & 63) == h) cnt = n;
+                });
+                MW_OVERLAP_MARK(1);
+                const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
+                MW_OVERLAP_MARK(2);
+                if (!wide && cnt > 0) {
+                    const Loc a_loc = me.loc;
+                    const uint64_t a_slot = me.slot;
+                    for (int32_t i = 0; i < cnt; i++) {
+                        const int32_t slot = base + off + i;
+                        const OrderedLeaf &o = leaves[buf[i]];
+                        if (slot < P.candCapacity) {
+                            out[slot] = CandidateCollision { a_loc, o.loc };
+                            out_slots[slot] = a_slot | (uint64_t)o.slot << 32;
+                        }
+                    }
+                }
+                const int32_t first = base + off;
+                forWide(wides, [&](int32_t h, const AABB &qh, int32_t eh, bool sh, int32_t selfh) {
+                    waveSweep<true>(leaves, nleaves, qh, eh, sh, selfh, __shfl(first, h, 64),
+                                    out, out_slots, P.candCapacity);
+                });
+                base += total;
+                MW_OVERLAP_MARK(3);
+                continue;
+            }
+            if (kSmall || nleaves <= 64 * kOverlapMaskWords) {
                 // The hits as a leaf-rank bitmask in registers: the sweep
                 // stores nothing to LDS, so the broadcast leaf reads of
                 // successive iterations are not ordered behind a possibly
@@ -823,7 +1020,33 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
                 MW_OVERLAP_MARK(1);                       // sweep (thread 0's wave)
                 const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
                 MW_OVERLAP_MARK(2);                       // scan (waits for every wave)
-                if (cnt > 0) {
+                if (total <= kOverlapStage) {
+                    // Pairs of ranks into LDS at their run positions, then
+                    // the block writes the run in order: each wave store
+                    // covers 64 consecutive candidates instead of one lane's
+                    // run per lane.  (The scan's barriers order this against
+                    // the previous chunk's reads of the stage.)
+                    uint32_t *stage = (uint32_t *)bufs;
+                    int32_t i = off;
+#pragma unroll
+                    for (int32_t c = 0; c < kOverlapMaskWords; c++) {
+                        uint64_t bits = mask[c];
+                        while (bits) {
+                            const int32_t k = 64 * c + __ffsll((unsigned long long)bits) - 1;
+                            bits &= bits - 1;
+                            stage[i++] = (uint32_t)self | (uint32_t)k << 16;
+                        }
+                    }
+                    __syncthreads();
+                    const int32_t lim = min(total, P.candCapacity - base);
+                    for (int32_t t = threadIdx.x; t < lim; t += kOverlapBlock) {
+                        const uint32_t pr = stage[t];
+                        const OrderedLeaf &a = leaves[pr & 0xffff];
+                        const OrderedLeaf &o = leaves[pr >> 16];
+                        out[base + t] = CandidateCollision { a.loc, o.loc };
+                        out_slots[base + t] = (uint64_t)a.slot | (uint64_t)o.slot << 32;
+                    }
+                } else if (cnt > 0) {
                     const Loc a_loc = me.loc;
                     const uint64_t a_slot = me.slot;
                     int32_t slot = base + off;
@@ -846,8 +1069,8 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
                 MW_OVERLAP_MARK(3);                       // candidate writes (thread 0's)
                 continue;
             }
-            // Worlds with more leaves: sweep 1 counts hits and keeps the
-            // first kOverlapBuf ranks in LDS, a second sweep covers a body
+            // Worlds with more leaves: the sweep counts hits and keeps the
+            // first kOverlapBuf ranks in LDS; the wave re-sweeps for a body
             // with more.  The hit test is evaluated branch-free on one
             // 32-byte broadcast read per leaf.
 #pragma unroll 4
@@ -861,31 +1084,24 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
             MW_OVERLAP_MARK(1);                           // sweep (thread 0's wave)
             const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
             MW_OVERLAP_MARK(2);                           // scan (waits for every wave)
-            if (cnt > 0) {
+            if (cnt > 0 && cnt <= kOverlapBuf) {
                 const Loc a_loc = me.loc;
                 const uint64_t a_slot = me.slot;
-                if (cnt <= kOverlapBuf) {
-                    for (int32_t i = 0; i < cnt; i++) {
-                        const int32_t slot = base + off + i;
-                        const OrderedLeaf &o = leaves[buf[i]];
-                        if (slot < P.candCapacity) {
-                            out[slot] = CandidateCollision { a_loc, o.loc };
-                            out_slots[slot] = a_slot | (uint64_t)o.slot << 32;
-                        }
-                    }
-                } else {
-                    int32_t i = 0;
-                    for (int32_t k = 0; k < nleaves; k++) {
-                        if (leafHit(leaves, k, q, e_id, a_static)) {
-                            const int32_t slot = base + off + i++;
-                            if (slot < P.candCapacity) {
-                                out[slot] = CandidateCollision { a_loc, leaves[k].loc };
-                                out_slots[slot] = a_slot | (uint64_t)leaves[k].slot << 32;
-                            }
-                        }
+                for (int32_t i = 0; i < cnt; i++) {
+                    const int32_t slot = base + off + i;
+                    const OrderedLeaf &o = leaves[buf[i]];
+                    if (slot < P.candCapacity) {
+                        out[slot] = CandidateCollision { a_loc, o.loc };
+                        out_slots[slot] = a_slot | (uint64_t)o.slot << 32;
                     }
                 }
             }
+            const int32_t first = base + off;
+            forWide(__ballot(cnt > kOverlapBuf),
+                    [&](int32_t h, const AABB &qh, int32_t eh, bool sh, int32_t selfh) {
+                        waveSweep<true>(leaves, nleaves, qh, eh, sh, selfh, __shfl(first, h, 64),
+                                        out, out_slots, P.candCapacity);
+                    });
             base += total;
             MW_OVERLAP_MARK(3);                           // candidate writes (thread 0's)
         }
@@ -907,6 +1123,17 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
     findOverlapsWorld<false>(P);
+}
+
+#if defined(MW_OVERLAP_WAVES)
+#define MW_OVERLAP_SMALL_ATTR __attribute__((amdgpu_waves_per_eu(MW_OVERLAP_WAVES)))
+#else
+#define MW_OVERLAP_SMALL_ATTR
+#endif
+__global__ void __launch_bounds__(kOverlapBlock) MW_OVERLAP_SMALL_ATTR findOverlapsSmallKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    findOverlapsWorld<false, true>(P);
 }
 
 __global__ void __launch_bounds__(kOverlapBlock) findOverlapsGlobalKernel(PhysArgs P)

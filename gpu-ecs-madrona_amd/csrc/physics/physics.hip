@@ -82,10 +82,17 @@ void PhysicsModule::upload(void *stream_ptr)
     // broadphase: the BVH rebuild picks its variant per launch (<= 64 KB)
     P.refitGlobal = fitsLDS((const void *)&refitKernel, kRefitBlock, refitSharedBytes(P)) ? 0 : 1;
     if (P.refitGlobal) hipx::residentBlocks((const void *)&refitGlobalKernel, "refitGlobalKernel", kRefitBlock, 0);
+    // findOverlaps: BVH traversal for worlds past 512 leaves (the sweep is
+    // O(leaves) per body); MADRONA_MW_OVERLAP_DFS_LEAVES overrides (0: every
+    // world, -1: never) -- both forms give the same candidates in the same order
+    P.overlapDFSLeaves = 512;
+    if (const char *e = std::getenv("MADRONA_MW_OVERLAP_DFS_LEAVES")) P.overlapDFSLeaves = atoi(e);
+    if (P.maxNodes > 32767) P.overlapDFSLeaves = -1;      // int16 traversal stack
+    if (P.overlapDFSLeaves >= P.maxLeaves) P.overlapDFSLeaves = -1;   // no world traverses
     P.overlapImage = nullptr;
     if (!fitsLDS((const void *)&findOverlapsKernel, kOverlapBlock, findOverlapsSharedBytes(P))) {
         hipx::residentBlocks((const void *)&findOverlapsGlobalKernel, "findOverlapsGlobalKernel",
-                             kOverlapBlock, 0);
+                             kOverlapBlock, findOverlapsGlobalSharedBytes(P));
         P.overlapImage = alloc<char>((size_t)W * findOverlapsImageBytes(P), stream_ptr);
     }
 
@@ -217,7 +224,11 @@ MW_PHYS_NODE(RefitNode,
 
 MW_PHYS_NODE(FindOverlappingNode,
     if (P.overlapImage)
-        MW_LAUNCH(findOverlapsGlobalKernel, dim3(P.numWorlds), dim3(kOverlapBlock), 0, stream, P);
+        MW_LAUNCH(findOverlapsGlobalKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
+                  findOverlapsGlobalSharedBytes(P), stream, P);
+    else if (P.maxLeaves <= kOverlapSmallLeaves && P.overlapDFSLeaves < 0)
+        MW_LAUNCH(findOverlapsSmallKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
+                  findOverlapsSharedBytes(P), stream, P);
     else
         MW_LAUNCH(findOverlapsKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
                   findOverlapsSharedBytes(P), stream, P);)

@@ -150,6 +150,7 @@ __global__ void solverKernel(PhysArgs P, int32_t integrate_next);
 // fit a workgroup's LDS: same code, same order of operations, same bits.
 __global__ void refitGlobalKernel(PhysArgs P);
 __global__ void findOverlapsGlobalKernel(PhysArgs P);
+__global__ void findOverlapsSmallKernel(PhysArgs P);
 __global__ void narrowSATGlobalKernel(PhysArgs P);
 __global__ void narrowContactGlobalKernel(PhysArgs P);
 __global__ void solverGlobalKernel(PhysArgs P, int32_t integrate_next);
@@ -525,6 +526,7 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
 }
 
 size_t findOverlapsSharedBytes(const PhysArgs &P);
+size_t findOverlapsGlobalSharedBytes(const PhysArgs &P);
 size_t refitSharedBytes(const PhysArgs &P);
 size_t solverSharedBytes(const PhysArgs &P);
 size_t narrowphaseSharedBytes(const PhysArgs &P);
@@ -544,6 +546,7 @@ size_t contactImageBytes(const PhysArgs &P);
 #define MW_OVERLAP_BLOCK 192
 #endif
 constexpr int32_t kOverlapBlock = MW_OVERLAP_BLOCK;
+constexpr int32_t kOverlapSmallLeaves = 256;   // findOverlapsSmallKernel: the bitmask path only
 constexpr int32_t kNarrowBlock = 256;
 #ifndef MW_CONTACT_BLOCK
 #define MW_CONTACT_BLOCK 128

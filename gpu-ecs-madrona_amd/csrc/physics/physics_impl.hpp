@@ -225,6 +225,8 @@ struct PhysArgs {
     // LDS images that do not fit a workgroup live in global slabs instead
     // (null: the kernel stages them in LDS); physics.hip upload() decides.
     char *overlapImage;           // [W][findOverlapsImageBytes] leaf image per world
+    int32_t overlapDFSLeaves;     // findOverlaps: worlds with more leaves traverse the BVH
+                                  // (stack DFS) instead of sweeping every leaf; -1: never
     int32_t refitGlobal;          // refit walks the node slab in place
     char *satImage;               // [satImageBlocks][narrowphaseImageBytes] hull staging
     int32_t satImageBlocks;

@@ -14,4 +14,8 @@ timeout -k 10 400 python -u bench.py --workload simple --steps $K > $O/bench.jso
 tail -c 300 $O/bench.json
 timeout -k 10 900 bash profiles/collect.sh $R simple $K 10 || { echo COLLECTFAIL; exit 2; }
 timeout -k 10 700 bash tools/sq_lds.sh ${R}_simple_sq simple || { echo SQFAIL; exit 3; }
+python3 profiles/sq_summary.py gpurun_out/${R}_simple_sq --out gpurun_out/${R}_simple_sq/sq_summary.json > /dev/null || true
+# the raw rocpd databases are summarised (kernels.txt); gpurun copies back at most 64 MiB
+find gpurun_out -name "*.db" -delete
+du -sh gpurun_out
 echo done
