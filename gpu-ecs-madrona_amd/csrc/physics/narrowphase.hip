@@ -575,6 +575,142 @@ __device__ __forceinline__ EdgeQuery groupEdgeQueryTables(const HullRef &a, cons
     return { v, k };
 }
 
+// The edge query on sign bits (MW_SAT_BITS; hulls of at most 16 edges and
+// 32 faces, which covers every box pair).  The Minkowski-face test of pair
+// (i, j) only asks for the signs of four table entries, and a product of two
+// floats whose magnitudes are at least 2^-62 is never zero, so its sign is
+// the xor of theirs: the three products' verdicts are bit operations on
+// sign masks once every entry is either exactly zero (its test fails, as the
+// product would be zero) or at least 2^-62 in magnitude.  Per row i of a
+// (one lane, registers) the bits of sA's row (over faces of b); per face f
+// of a the column of tB's signs and zeros over the edges j of b, and per
+// face f of b which edges j of b have f as their first / second face -- both
+// built with LDS ors in the table space the float tables would use.  Then
+// row i's 16 pairs are tested by a handful of word operations:
+//   G1 / G2 = edges j whose first / second face has a negative sA[i] entry,
+//   pass_i = (G1 ^ G2) & (CB[a1] ^ CB[a2]) & ~(G1 ^ CB[a2]) & ~zeros,
+// with a1 / a2 edge i's faces, CB[f] the negative tB[., f] entries.  An
+// entry between 0 and 2^-62 (or not finite) sends the pair to the float
+// tables (returns false).
+#ifndef MW_SAT_BITS
+#define MW_SAT_BITS 1
+#endif
+constexpr int32_t kBitsMaxEdges = 16;
+constexpr int32_t kBitsMaxFaces = 32;
+constexpr int32_t kBitsRows = (kBitsMaxEdges + kGroup - 1) / kGroup;
+
+__device__ __forceinline__ bool bitsEligible(const HullRef &a, const HullRef &b)
+{
+    return a.hd.numEdges <= kBitsMaxEdges && b.hd.numEdges <= kBitsMaxEdges &&
+           a.hd.numFaces <= kBitsMaxFaces && b.hd.numFaces <= kBitsMaxFaces;
+}
+
+// Classifies a table entry: bit 0 negative, bit 1 exactly zero, bit 2 too
+// small (or not finite) for the sign rule.
+__device__ __forceinline__ uint32_t entryClass(float x)
+{
+    const float m = fabsf(x);
+    return (x < 0.0f ? 1u : 0u) | (x == 0.0f ? 2u : 0u) |
+           ((x != 0.0f && !(m >= 0x1p-62f && m <= FLT_MAX)) ? 4u : 0u);
+}
+
+__device__ __forceinline__ EdgeQuery groupEdgeQueryBits(const HullRef &a, const HullRef &b, float *sA_space,
+                                                        float *tB_space, int32_t lane, bool &ok)
+{
+    const int32_t nA = a.hd.numEdges, nB = b.hd.numEdges;
+    const int32_t fA = a.hd.numFaces, fB = b.hd.numFaces;
+    uint32_t *CB = (uint32_t *)sA_space;     // [fA]: negative tB[j][f] (bits 0-15), zero (16-31)
+    uint32_t *FB = (uint32_t *)tB_space;     // [fB]: edges with face1 == f (0-15), face2 == f (16-31)
+    for (int32_t f = lane; f < fA; f += kGroup) CB[f] = 0;
+    for (int32_t f = lane; f < fB; f += kGroup) FB[f] = 0;
+    groupSync();
+    uint32_t bad = 0;
+    // b's rows: the same expressions as buildMinkTables' tB
+    for (int32_t j = lane; j < nB; j += kGroup) {
+        const EdgeQuad eb = ldQuad(b.quads, j);
+        const Vector3 c = -b.planes[eb.face1].normal, d = -b.planes[eb.face2].normal;
+        const Vector3 dxc = d.cross(c);
+        for (int32_t f = 0; f < fA; f++) {
+            const uint32_t cls = entryClass(a.planes[f].normal.dot(dxc));
+            bad |= cls;
+            const uint32_t bits = ((cls & 1u) << j) | (((cls >> 1) & 1u) << (16 + j));
+            if (bits) atomicOr(&CB[f], bits);
+        }
+        atomicOr(&FB[eb.face1], 1u << j);
+        atomicOr(&FB[eb.face2], 1u << (16 + j));
+    }
+    // a's rows, kept by their lane: negative and zero entries over b's faces
+    uint32_t neg[kBitsRows], zero[kBitsRows];
+    EdgeQuad qa[kBitsRows];
+#pragma unroll
+    for (int32_t r = 0; r < kBitsRows; r++) {
+        const int32_t i = lane + r * kGroup;
+        neg[r] = zero[r] = 0;
+        if (i < nA) {
+            qa[r] = ldQuad(a.quads, i);
+            const Vector3 bxa = a.planes[qa[r].face2].normal.cross(a.planes[qa[r].face1].normal);
+            for (int32_t f = 0; f < fB; f++) {
+                const uint32_t cls = entryClass((-b.planes[f].normal).dot(bxa));
+                bad |= cls;
+                neg[r] |= (cls & 1u) << f;
+                zero[r] |= ((cls >> 1) & 1u) << f;
+            }
+        }
+    }
+    // any entry too small for the sign rule: the whole group falls back
+    const uint64_t any_bad = __ballot((bad & 4u) != 0);
+    const int32_t gbase = (int32_t)(threadIdx.x & 63) & ~(kGroup - 1);
+    ok = ((any_bad >> gbase) & ((1ull << kGroup) - 1)) == 0;
+    groupSync();
+    float v = __builtin_nanf("");
+    int32_t k = INT32_MAX;
+    if (ok) {
+        const uint32_t row_mask = (1u << nB) - 1u;
+#pragma unroll
+        for (int32_t r = 0; r < kBitsRows; r++) {
+            const int32_t i = lane + r * kGroup;
+            if (i >= nA) continue;
+            uint32_t g1 = 0, g2 = 0, z = 0;
+            for (int32_t f = 0; f < fB; f++) {
+                const uint32_t w = FB[f];
+                const uint32_t e = (w & 0xffffu) | (w >> 16);      // edges touching face f
+                if ((neg[r] >> f) & 1u) { g1 |= w & 0xffffu; g2 |= w >> 16; }
+                if ((zero[r] >> f) & 1u) z |= e;
+            }
+            const uint32_t c1 = CB[qa[r].face1], c2 = CB[qa[r].face2];
+            z |= (c1 | c2) >> 16;
+            const uint32_t pass = (g1 ^ g2) & (c1 ^ c2) & ~(g1 ^ c2) & ~z & row_mask;
+            const uint32_t fail = ~pass & row_mask;
+            if (fail) {
+                const int32_t p0 = i * nB + __builtin_ctz(fail);
+                if (scanWins(-FLT_MAX, p0, v, k)) { v = -FLT_MAX; k = p0; }
+            }
+            uint32_t m = pass;
+            while (m) {
+                const int32_t j = __builtin_ctz(m);
+                m &= m - 1;
+                const EdgeQuad eb = ldQuad(b.quads, j);
+                float sep = -FLT_MAX;
+                const Vector3 pa1 = a.verts[qa[r].v1], pb1 = b.verts[eb.v1];
+                Vector3 da = a.verts[qa[r].v2] - pa1, db = b.verts[eb.v2] - pb1;
+                Vector3 uc = da.cross(db);
+                float l2 = uc.length2();
+                if (l2 != 0) {
+                    float inv = 1.f / sqrtf(l2);
+                    Vector3 nrm = uc * inv;
+                    if (nrm.dot(pa1 - a.center) < 0.0f) nrm = -nrm;
+                    sep = nrm.dot(pb1 - pa1);
+                }
+                const int32_t p = i * nB + j;
+                if (scanWins(sep, p, v, k)) { v = sep; k = p; }
+            }
+        }
+    }
+    groupArgMax(v, k);
+    if (!(v > -FLT_MAX)) return { -FLT_MAX, 0 };
+    return { v, k };
+}
+
 __device__ __forceinline__ int32_t findIncidentFace(const geometry::Plane *planes, int32_t num_faces,
                                                     Vector3 ref_normal)
 {
@@ -1077,6 +1213,7 @@ enum : int32_t { kSatFaceSeparated = 0, kSatEdgeSeparated = 1, kSatContact = 2 }
 // The SAT of one pair after its hulls are known (doSAT, narrowphase.cpp:
 // 678-758): staging, face queries, edge query, contact job.  `stride` is the
 // Minkowski tables' row stride (0: the per-pair edge query).
+template <bool kBits>
 __device__ __forceinline__ int32_t satPair(const ObjDev &O, const HullRef &ha, const HullRef &hb,
                                         const BodyPose &pa, const BodyPose &pb, const GroupLDS &g,
                                         int32_t stride, int32_t lane, ContactJob &job)
@@ -1102,7 +1239,10 @@ __device__ __forceinline__ int32_t satPair(const ObjDev &O, const HullRef &ha, c
     if (fb.separation > 0.0f) { MW_SAT_COUNT(2); return kSatFaceSeparated; }
     MW_SAT_CUT(2);
     EdgeQuery eq;
-    if (stride > 0) {
+    bool bits_done = false;
+    if (kBits && stride > 0 && bitsEligible(ha, hb)) eq = groupEdgeQueryBits(ha, hb, g.sA, g.tB, lane, bits_done);
+    if (bits_done) {
+    } else if (stride > 0) {
         buildMinkTables(ha, hb, g.sA, g.tB, stride, lane);
         groupSync();
         MW_SAT_CUT(3);
@@ -1177,10 +1317,10 @@ __device__ __forceinline__ int32_t hullHullSAT(const ObjDev &O, int32_t a_obj, i
         ha.hd.numVerts = hb.hd.numVerts = 8;
         ha.hd.numFaces = hb.hd.numFaces = 6;
         ha.hd.numEdges = hb.hd.numEdges = 12;
-        return satPair(O, ha, hb, pa, pb, g, 6, lane, job);
+        return satPair<MW_SAT_BITS != 0>(O, ha, hb, pa, pb, g, 6, lane, job);
     }
 #endif
-    return satPair(O, ha, hb, pa, pb, g, O.minkStride, lane, job);
+    return satPair<false>(O, ha, hb, pa, pb, g, O.minkStride, lane, job);
 }
 
 #if defined(MW_SAT_PROFILE)
