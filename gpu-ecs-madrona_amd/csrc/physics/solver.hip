@@ -714,6 +714,12 @@ __device__ __forceinline__ void stQ(void *p, Quat q)
 // world of up to 64 * kRowBatch bodies pays one memory round trip per loop
 // instead of one per 64 rows (collisions: 129 bodies, 3 rounds -> 1).
 constexpr int32_t kRowBatch = 3;
+// The write-back's batch (it also holds each row's integration inputs for
+// the next substep, so its batch costs registers the load's does not).
+#ifndef MW_SOLVER_WRITE_BATCH
+#define MW_SOLVER_WRITE_BATCH 3
+#endif
+constexpr int32_t kWriteBatch = MW_SOLVER_WRITE_BATCH;
 
 // Load one world's bodies into its LDS image (wave `lane` 0..63) and reset
 // its ordering state.
@@ -999,23 +1005,23 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
     for (int32_t ba = 0; ba < P.numBodyArchs; ba++) {
         const BodyArch &B = P.body[ba];
         const int32_t rows = B.numRows[w];
-        for (int32_t r0 = 0; r0 < rows; r0 += kSolverBlock * kRowBatch) {
-            IntegrateIn in[kRowBatch];
-            IntegrateObj od[kRowBatch];
+        for (int32_t r0 = 0; r0 < rows; r0 += kSolverBlock * kWriteBatch) {
+            IntegrateIn in[kWriteBatch];
+            IntegrateObj od[kWriteBatch];
             if (integrate_next) {
 #pragma unroll
-                for (int32_t j = 0; j < kRowBatch; j++) {
+                for (int32_t j = 0; j < kWriteBatch; j++) {
                     const int32_t r = r0 + j * kSolverBlock + lane;
                     if (r < rows) in[j] = integrateLoad(B, w, r);
                 }
 #pragma unroll
-                for (int32_t j = 0; j < kRowBatch; j++) {
+                for (int32_t j = 0; j < kWriteBatch; j++) {
                     const int32_t r = r0 + j * kSolverBlock + lane;
                     if (r < rows) od[j] = integrateObj(P, in[j].obj);
                 }
             }
 #pragma unroll
-            for (int32_t j = 0; j < kRowBatch; j++) {
+            for (int32_t j = 0; j < kWriteBatch; j++) {
                 const int32_t r = r0 + j * kSolverBlock + lane;
                 const bool live = r < rows;
                 if (live) {
