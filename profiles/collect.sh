@@ -13,7 +13,7 @@ WARM=${4:-10}
 SETTLE=120
 WIN="$((SETTLE + WARM + 1))-$((SETTLE + WARM + STEPS))"
 OUT=$PWD/gpurun_out/prof_$R${2:+_$2}_w$WIN
-B="$PWD/bench.py --no-cpu-baseline --no-cpu-executor --workload $WL --steps $STEPS --warmup $WARM"
+B="$PWD/bench.py --no-cpu-baseline --no-cpu-executor --ref-ticks 0 --workload $WL --steps $STEPS --warmup $WARM"
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv rocpd -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1

@@ -7,7 +7,7 @@ set -euo pipefail
 T=${1:-sqlds}
 WL=${2:-simple}
 OUT=$PWD/gpurun_out/$T
-B="$PWD/bench.py --workload $WL --no-cpu-baseline --no-cpu-executor --no-roofline --settle 120 --steps 3 --warmup 1"
+B="$PWD/bench.py --workload $WL --no-cpu-baseline --no-cpu-executor --no-roofline --ref-ticks 0 --settle 120 --steps 3 --warmup 1"
 RX="narrowSATKernel|narrowContactKernel|solverKernel"
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
