@@ -662,6 +662,12 @@ __device__ __forceinline__ EdgeQuery groupEdgeQueryBits(const HullRef &a, const 
     const int32_t gbase = (int32_t)(threadIdx.x & 63) & ~(kGroup - 1);
     ok = ((any_bad >> gbase) & ((1ull << kGroup) - 1)) == 0;
     groupSync();
+#if defined(MW_SAT_CUTS)
+    if (g_satExp == 3) {                      // masks built (kept alive): separated
+        ok = true;
+        return { 1.0f + 0.0f * (float)(neg[0] ^ zero[kBitsRows - 1] ^ FB[0] ^ CB[0]), 0 };
+    }
+#endif
     float v = __builtin_nanf("");
     int32_t k = INT32_MAX;
     if (ok) {
@@ -681,6 +687,12 @@ __device__ __forceinline__ EdgeQuery groupEdgeQueryBits(const HullRef &a, const 
             z |= (c1 | c2) >> 16;
             const uint32_t pass = (g1 ^ g2) & (c1 ^ c2) & ~(g1 ^ c2) & ~z & row_mask;
             const uint32_t fail = ~pass & row_mask;
+#if defined(MW_SAT_CUTS)
+            if (g_satExp == 5) {                  // pass masks only (kept alive)
+                if (pass == 0x7fffffffu) v = 0.0f;
+                continue;
+            }
+#endif
             if (fail) {
                 const int32_t p0 = i * nB + __builtin_ctz(fail);
                 if (scanWins(-FLT_MAX, p0, v, k)) { v = -FLT_MAX; k = p0; }
