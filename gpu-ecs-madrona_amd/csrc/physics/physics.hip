@@ -85,6 +85,10 @@ void PhysicsModule::upload(void *stream_ptr)
     // findOverlaps: BVH traversal for worlds past 512 leaves (the sweep is
     // O(leaves) per body); MADRONA_MW_OVERLAP_DFS_LEAVES overrides (0: every
     // world, -1: never) -- both forms give the same candidates in the same order
+    // findOverlaps keeps leaf ranks as 16-bit values (per-lane hit buffers,
+    // the candidate stage): refuse a world it cannot index
+    if (P.maxLeaves > 65535)
+        throw std::runtime_error("physics: more than 65535 objects per world (findOverlaps leaf ranks)");
     P.overlapDFSLeaves = 512;
     if (const char *e = std::getenv("MADRONA_MW_OVERLAP_DFS_LEAVES")) P.overlapDFSLeaves = atoi(e);
     if (P.maxNodes > 32767) P.overlapDFSLeaves = -1;      // int16 traversal stack
