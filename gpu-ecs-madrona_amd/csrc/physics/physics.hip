@@ -359,6 +359,31 @@ extern "C" double mw_debug_time_sat(int32_t cut, int32_t reps, int32_t substep)
     mw_debug_set_sat_exp(0);
     return ms / reps;
 }
+
+// The solver kernel relaunched `reps` times on substep `substep`'s inputs,
+// cut after phase `cut` (solver.hip MW_SOLVER_CUT; 0: whole), without the
+// fused integration of the next substep; the mean ms per launch.
+extern "C" int mw_debug_set_solver_cut(int32_t cut);
+extern "C" double mw_debug_time_solver(int32_t cut, int32_t reps, int32_t substep)
+{
+    if (!g_cutArgs || g_cutArgs->solverImage) return -1.0;
+    const PhysArgs Q = substepArgs(*g_cutArgs, substep, true);
+    if (hipDeviceSynchronize() != hipSuccess || mw_debug_set_solver_cut(cut) != 0) return -1.0;
+    const dim3 grid((Q.numWorlds + kSolverWorlds - 1) / kSolverWorlds);
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    (void)hipEventRecord(a, nullptr);
+    for (int32_t r = 0; r < reps; r++)
+        hipLaunchKernelGGL(solverKernel, grid, dim3(kSolverThreads), solverSharedBytes(Q), nullptr, Q, 0);
+    (void)hipEventRecord(b, nullptr);
+    float ms = -1.f;
+    if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = -1.f;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    mw_debug_set_solver_cut(0);
+    return ms / reps;
+}
 #endif
 
 // substepRigidBodies.  Substeps after the first are integrated by the

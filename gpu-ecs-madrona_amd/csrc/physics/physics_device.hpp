@@ -416,6 +416,35 @@ __device__ __forceinline__ SatWork candWork(const CandidateCollision &cand, uint
     return out;
 }
 
+// Solver blocks: kSolverWorlds worlds per block, kSolverBlock lanes per
+// world.  MW_SOLVER_LANES = 32 puts two worlds on one wave (each on a half):
+// a dependency level of a collisions world holds ~33 contacts, so a wave of
+// its own leaves half its lanes idle in every level pass.
+#ifndef MW_SOLVER_LANES
+#define MW_SOLVER_LANES 64
+#endif
+constexpr int32_t kSolverBlock = MW_SOLVER_LANES;        // lanes per world
+#ifndef MW_SOLVER_WORLDS
+#define MW_SOLVER_WORLDS (64 / MW_SOLVER_LANES)
+#endif
+constexpr int32_t kSolverWorlds = MW_SOLVER_WORLDS;       // worlds per solver block
+constexpr int32_t kSolverThreads = kSolverBlock * kSolverWorlds;
+static_assert(kSolverBlock == 64 || kSolverBlock == 32, "a world's lanes: a wave or half of one");
+
+// This world's lanes (kSolverBlock of them, aligned in the wave): a ballot
+// over them (bit i = the world's lane i) and a value from one of them.
+__device__ __forceinline__ uint64_t worldBallot(bool p)
+{
+    const uint64_t m = __ballot(p);
+    if constexpr (kSolverBlock == 64) return m;
+    return (m >> (threadIdx.x & 32)) & 0xffffffffull;
+}
+template <typename T>
+__device__ __forceinline__ T worldBroadcast(T x, int32_t src)
+{
+    return __shfl(x, (int32_t)(threadIdx.x & (64 - kSolverBlock)) + src, 64);
+}
+
 // The filter for one world on one wave (the solver kernel's tail, after it
 // integrated the world's next substep into its LDS box image): the same
 // survivors, slots and list entries as narrowFilterKernel, into the
@@ -441,32 +470,32 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
     int32_t *counts = P.nextSatWorkCount + bin * kBinStride;
     constexpr uint32_t kHull = (uint32_t)CollisionPrimitive::Type::Hull;
     constexpr uint32_t kHullPlane = kHull | (uint32_t)CollisionPrimitive::Type::Plane;
-    constexpr int32_t kBatch = 64 * kFilterBatch;
+    constexpr int32_t kBatch = kSolverBlock * kFilterBatch;
     const uint64_t lt = (1ull << lane) - 1;
     int32_t n_hh = 0, n_hp = 0;
     for (int32_t b0 = 0; b0 < num; b0 += kBatch) {
         uint64_t s[kFilterBatch];
 #pragma unroll
         for (int32_t j = 0; j < kFilterBatch; j++) {
-            const int32_t i = b0 + 64 * j + lane;
+            const int32_t i = b0 + kSolverBlock * j + lane;
             s[j] = i < num ? slots[i] : 0;
         }
 #pragma unroll
         for (int32_t j = 0; j < kFilterBatch; j++) {
-            const int32_t i = b0 + 64 * j + lane;
-            if (b0 + 64 * j >= num) continue;                // wave-uniform
+            const int32_t i = b0 + kSolverBlock * j + lane;
+            if (b0 + kSolverBlock * j >= num) continue;                // wave-uniform
             BodyBox A, B;
             const bool keep = i < num && candOverlaps(P, w, s[j], boxes, A, B);
             const uint32_t t = A.type | B.type;
-            n_hh += __popcll(__ballot(keep && t == kHull));
-            n_hp += __popcll(__ballot(keep && t == kHullPlane));
+            n_hh += __popcll(worldBallot(keep && t == kHull));
+            n_hp += __popcll(worldBallot(keep && t == kHullPlane));
         }
     }
     int32_t b_hh = 0, b_hp = 0, fits = 1;
     if (lane == 0) fits = reserveBin(counts, n_hh, n_hp, P.binCap, b_hh, b_hp);
-    b_hh = __shfl(b_hh, 0);
-    b_hp = __shfl(b_hp, 0);
-    fits = __shfl(fits, 0);
+    b_hh = worldBroadcast(b_hh, 0);
+    b_hp = worldBroadcast(b_hp, 0);
+    fits = worldBroadcast(fits, 0);
     // The two lists stay inside their bin whatever the counter says (the
     // reservations fit by construction -- binCap = worlds per bin x
     // candCapacity -- while the counters were reset before this filter):
@@ -483,7 +512,7 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
         uint64_t s[kFilterBatch];
 #pragma unroll
         for (int32_t j = 0; j < kFilterBatch; j++) {
-            const int32_t i = b0 + 64 * j + lane;
+            const int32_t i = b0 + kSolverBlock * j + lane;
             s[j] = i < num ? slots[i] : 0;
         }
         // survivors of the batch first, then their candidates' Locs in one
@@ -491,25 +520,25 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
         uint32_t keep_bits = 0;
 #pragma unroll
         for (int32_t j = 0; j < kFilterBatch; j++) {
-            const int32_t i = b0 + 64 * j + lane;
-            if (b0 + 64 * j >= num) continue;
+            const int32_t i = b0 + kSolverBlock * j + lane;
+            if (b0 + kSolverBlock * j >= num) continue;
             BodyBox A, B;
             if (i < num && candOverlaps(P, w, s[j], boxes, A, B)) keep_bits |= 1u << j;
         }
         CandidateCollision c[kFilterBatch];
 #pragma unroll
         for (int32_t j = 0; j < kFilterBatch; j++) {
-            if (keep_bits & (1u << j)) c[j] = cands[b0 + 64 * j + lane];
+            if (keep_bits & (1u << j)) c[j] = cands[b0 + kSolverBlock * j + lane];
         }
 #pragma unroll
         for (int32_t j = 0; j < kFilterBatch; j++) {
-            if (b0 + 64 * j >= num) continue;
+            if (b0 + kSolverBlock * j >= num) continue;
             const bool keep = (keep_bits >> j) & 1u;
             const BodyBox A = boxes[(uint32_t)s[j] & 0xffffu];
             const BodyBox B = boxes[(uint32_t)(s[j] >> 32) & 0xffffu];
             const uint32_t t = A.type | B.type;
             const bool hh = keep && t == kHull, hp = keep && t == kHullPlane;
-            const uint64_t mk = __ballot(keep), mh = __ballot(hh), mp = __ballot(hp);
+            const uint64_t mk = worldBallot(keep), mh = worldBallot(hh), mp = worldBallot(hp);
             if (keep) {
                 SatWork wk = candWork(c[j], s[j], A, B, w);
                 wk.slot = S + __popcll(mk & lt);
@@ -552,12 +581,6 @@ constexpr int32_t kNarrowBlock = 256;
 #define MW_CONTACT_BLOCK 128
 #endif
 constexpr int32_t kContactBlock = MW_CONTACT_BLOCK;   // plane / contact kernels
-constexpr int32_t kSolverBlock = 64;      // lanes per world (one wave)
-#ifndef MW_SOLVER_WORLDS
-#define MW_SOLVER_WORLDS 1
-#endif
-constexpr int32_t kSolverWorlds = MW_SOLVER_WORLDS;       // worlds per solver block
-constexpr int32_t kSolverThreads = kSolverBlock * kSolverWorlds;
 #ifndef MW_REFIT_BLOCK
 #define MW_REFIT_BLOCK 128
 #endif

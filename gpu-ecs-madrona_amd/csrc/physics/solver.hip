@@ -813,7 +813,7 @@ __device__ __forceinline__ int32_t gatherContacts(const PhysArgs &P, int32_t w, 
         for (int32_t u = 0; u < kInfoUnroll; u++) {
             const int32_t s = chunk + u * kSolverBlock + lane;
             const bool has = v[u] != kNoManifold;
-            const uint64_t mask = __ballot(has);
+            const uint64_t mask = worldBallot(has);
             const int32_t k = k0 + __popcll(mask & lt_mask);
             if (has && k < maxK) order[k] = s;
             if (has && k < cap) {
@@ -936,7 +936,8 @@ __device__ __forceinline__ int32_t scheduleLevels(SolverLDS &L, int32_t N, RecPt
     int32_t max_level = 0;
     for (int32_t k = lane; k < N; k += kSolverBlock) max_level = max(max_level, (int32_t)recs[k].lvl);
 #pragma unroll
-    for (int32_t off = 32; off > 0; off >>= 1) max_level = max(max_level, __shfl_xor(max_level, off));
+    for (int32_t off = kSolverBlock / 2; off > 0; off >>= 1)
+        max_level = max(max_level, __shfl_xor(max_level, off));
     return max_level;
 }
 
@@ -1194,6 +1195,21 @@ __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, S
 // Occupancy: latency bound (dependent LDS / column reads per contact), so
 // residency matters more than packed math; built without SLP vectorisation
 // (Makefile) it fits 3 waves per SIMD without spills.
+// Timing build only (make BUILD=build_cut EXTRA=-DMW_SAT_CUTS): the solver
+// block returns after phase g_solverCut (1 load + count, 2 levels, 3 sort,
+// 4 positions, 5 setVelocities, 6 velocities; 0: whole), relaunched on one
+// substep's inputs by mw_debug_time_solver (physics.hip).
+#if defined(MW_SAT_CUTS)
+static __device__ int32_t g_solverCut;
+extern "C" int mw_debug_set_solver_cut(int32_t cut)
+{
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_solverCut), &cut, sizeof(cut)) == hipSuccess ? 0 : -1;
+}
+#define MW_SOLVER_CUT(i) do { if (g_solverCut == (i)) return; } while (0)
+#else
+#define MW_SOLVER_CUT(i) ((void)0)
+#endif
+
 #ifndef MW_SOLVER_WAVES_PER_EU
 #define MW_SOLVER_WAVES_PER_EU 3
 #endif
@@ -1240,6 +1256,7 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     __syncthreads();
     const bool fits = BL.scalars[1] <= kSolverLDSContacts;
     MW_SOLVER_MARK(0);
+    MW_SOLVER_CUT(1);
 
     // Levels of the world's items (contacts, then joints) in LDS, unless the
     // items overflow the LDS records or the levels the bucket table holds:
@@ -1260,6 +1277,7 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
         max_level = BL.scalars[2];
     }
     MW_SOLVER_MARK(1);
+    MW_SOLVER_CUT(2);
     if (!fits || max_level > MW_SOLVER_MAX_LEVELS) {
         if (live) {
             if (fits) {                       // scheduled once already: afresh
@@ -1306,6 +1324,7 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     }
     __syncthreads();
     MW_SOLVER_MARK(2);
+    MW_SOLVER_CUT(3);
 
     // solvePositions, level by level over the whole block
     for (int32_t l = 1; l <= max_level; l++) {
@@ -1321,9 +1340,11 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     }
 
     MW_SOLVER_MARK(3);
+    MW_SOLVER_CUT(4);
     if (live) setWorldVelocities(P, w, L, P.solver[w].h, lane);
     __syncthreads();
     MW_SOLVER_MARK(4);
+    MW_SOLVER_CUT(5);
 
     // solveVelocities, same schedule
     for (int32_t l = 1; l <= max_level; l++) {
@@ -1339,6 +1360,7 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     }
 
     MW_SOLVER_MARK(5);
+    MW_SOLVER_CUT(6);
     if (live) writeWorldBodies(P, w, L, lane, integrate_next != 0);
     __syncthreads();
     MW_SOLVER_MARK(6);

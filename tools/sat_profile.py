@@ -7,7 +7,9 @@
       several-fold: shares only);
   make -C gpu-ecs-madrona_amd BUILD=build_cut EXTRA=-DMW_SAT_CUTS
   MADRONA_MW_LIB=gpu-ecs-madrona_amd/build_cut/libmadrona_mw.so python tools/sat_profile.py [simple|collisions] --cuts
-      NarrowphaseNode time with the SAT cut after each phase."""
+      NarrowphaseNode time with the SAT cut after each phase;
+  ... python tools/sat_profile.py [simple|collisions] --solver-cuts
+      the solver kernel cut after each of its phases (same build)."""
 import ctypes
 import os
 import sys
@@ -28,6 +30,16 @@ def main():
     sim = (mw.SimpleSim if wl == "simple" else mw.CollisionsSim)(W, pos, rot, cfg)
     lib = mw.library()
     sim.step(130)
+    if "--solver-cuts" in sys.argv:
+        lib.mw_debug_time_solver.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+        lib.mw_debug_time_solver.restype = ctypes.c_double
+        sim.sync()
+        names = ["load+count", "+levels", "+sort", "+positions", "+setVelocities", "+velocities",
+                 "whole (no fused integration)"]
+        for cut, nm in zip((1, 2, 3, 4, 5, 6, 0), names):
+            ms = lib.mw_debug_time_solver(cut, 20, 3)
+            print(f"solverKernel cut {cut} ({nm:30s}) {ms:.4f} ms/launch (last substep, 20 launches)")
+        return
     if "--cuts" in sys.argv:
         lib.mw_debug_time_sat.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
         lib.mw_debug_time_sat.restype = ctypes.c_double
