@@ -1,6 +1,11 @@
 #!/bin/bash
 # Round-5 A/B batch (repo root, GPU box): findOverlaps occupancy variants and
 # the re-verification of the pre-9e95308 flag-only dead ends.
+# Variant builds it loads (built beforehand, in-tree, then removed):
+#   make -C gpu-ecs-madrona_amd BUILD=build_ow5 EXTRA=-DMW_OVERLAP_WAVES=5 (ow6, ow8 likewise),
+#   build_sol4/5 EXTRA=-DMW_SOLVER_WAVES_PER_EU=4/5, build_bits0 EXTRA=-DMW_SAT_BITS=0,
+#   build_sat_split EXTRA=-DMW_SAT_SPLIT_STAGE=1, build_sat_g16 EXTRA=-DMW_SAT_GROUP=16,
+#   build_sat_3w EXTRA=-DMW_SAT_MIN_BLOCKS=3.  Results: profiles/r05_ab_*.txt.
 set -o pipefail
 O=gpurun_out/ab2
 mkdir -p $O

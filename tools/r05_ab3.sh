@@ -2,6 +2,10 @@
 # Round-5 A/B batch 3 (repo root, GPU box): register budgets -- the solver
 # (2 waves / SIMD without spills vs 3 with), its write-back batch, and the
 # narrowphase kernels pinned to more waves per SIMD.
+# Variant builds: build_sol2 (-DMW_SOLVER_WAVES_PER_EU=2), build_wb1/2
+#   (-DMW_SOLVER_WRITE_BATCH=1/2), build_flt8 (-DMW_FILTER_WAVES=8), build_pl5/6
+#   (-DMW_PLANE_WAVES), build_ct5/6 (-DMW_CONTACT_WAVES), build_int8
+#   (-DMW_INTEGRATE_WAVES=8).  Results: profiles/r05_ab_occupancy.txt.
 set -o pipefail
 O=gpurun_out/ab3
 mkdir -p $O

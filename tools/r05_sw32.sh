@@ -1,5 +1,6 @@
 #!/bin/bash
 # Two worlds per solver wave (MW_SOLVER_LANES=32): parity, then A/B.
+# Variant build: make -C gpu-ecs-madrona_amd BUILD=build_sw32 EXTRA=-DMW_SOLVER_LANES=32
 set -o pipefail
 O=gpurun_out/sw32
 mkdir -p $O
