@@ -1095,6 +1095,11 @@ __device__ __forceinline__ int32_t solveKind(int32_t kind, const ContactIn &c)
     return kind;
 }
 
+#if defined(MW_SAT_CUTS)
+// timing build: cut 7 = the positions phase with its loads only
+static __device__ int32_t g_solverCut;
+#endif
+
 __device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w, SolverLDS &L,
                                                    const CRec r, int32_t kind)
 {
@@ -1104,6 +1109,17 @@ __device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w,
         // one round of loads: the manifold and the bodies' columns
         const ContactIn c = loadContact(cr);
         PosIn in = loadPosIn(P, w, b1, r.s1, b2, r.s2, kind == kKindStaticRef, kind == kKindStaticAlt);
+#if defined(MW_SAT_CUTS)
+        if (g_solverCut == 7) {               // every loaded word kept alive, no solve
+            float acc = (float)c.np;
+            const float *fc = (const float *)&c;
+            for (size_t i = 0; i < sizeof(ContactIn) / 4; i++) acc += fc[i];
+            const float *fi = (const float *)&in;
+            for (size_t i = 0; i < sizeof(PosIn) / 4; i++) acc += fi[i];
+            if (acc == 1.2345f) b1.x.x = acc;
+            return;
+        }
+#endif
         const int32_t k = solveKind(kind, c);
         int32_t res = kSolveNonFinite;
         if (k == kKindStaticRef) {
@@ -1200,12 +1216,11 @@ __device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, S
 // 4 positions, 5 setVelocities, 6 velocities; 0: whole), relaunched on one
 // substep's inputs by mw_debug_time_solver (physics.hip).
 #if defined(MW_SAT_CUTS)
-static __device__ int32_t g_solverCut;
 extern "C" int mw_debug_set_solver_cut(int32_t cut)
 {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_solverCut), &cut, sizeof(cut)) == hipSuccess ? 0 : -1;
 }
-#define MW_SOLVER_CUT(i) do { if (g_solverCut == (i)) return; } while (0)
+#define MW_SOLVER_CUT(i) do { if (g_solverCut == (i) || ((i) == 4 && g_solverCut == 7)) return; } while (0)
 #else
 #define MW_SOLVER_CUT(i) ((void)0)
 #endif

@@ -35,8 +35,8 @@ def main():
         lib.mw_debug_time_solver.restype = ctypes.c_double
         sim.sync()
         names = ["load+count", "+levels", "+sort", "+positions", "+setVelocities", "+velocities",
-                 "whole (no fused integration)"]
-        for cut, nm in zip((1, 2, 3, 4, 5, 6, 0), names):
+                 "whole (no fused integration)", "+positions' loads only"]
+        for cut, nm in zip((1, 2, 3, 4, 5, 6, 0, 7), names):
             ms = lib.mw_debug_time_solver(cut, 20, 3)
             print(f"solverKernel cut {cut} ({nm:30s}) {ms:.4f} ms/launch (last substep, 20 launches)")
         return
