@@ -70,3 +70,15 @@ def test_traversal_cost_is_subquadratic(monkeypatch):
           f"sweep 3200 {sweep:.4f} ms")
     assert big < 12 * small, (small, big)
     assert big * 2.5 < sweep, (big, sweep)
+
+
+def test_world_past_16bit_indices_refused():
+    """Leaf ranks (findOverlaps) and body slots (solver records) are 16-bit:
+    a world past those limits is refused at creation with the limit named,
+    not indexed wrongly (the body-slot limit, 32767, binds first)."""
+    import madrona_mi355x as mw
+    W, n = 1, 40000
+    pos, rot = _grid_world(W, n, spacing=2.5)
+    g = mw.default_collisions_config(n, 1, 1024, 1024)
+    with pytest.raises(mw.MadronaError, match="per world must be <= 32767"):
+        mw.CollisionsSim(W, pos, rot, g)
