@@ -1457,6 +1457,9 @@ __device__ __forceinline__ SatWork unpackSat(const PhysArgs &P, const SatArch *a
 #ifndef MW_SAT_PIPE
 #define MW_SAT_PIPE 0        // software pipeline depth: 0 (loads at use) or 2
 #endif
+#ifndef MW_SAT_SORT_ALONE
+#define MW_SAT_SORT_ALONE 1  // block 0 sorts the worlds and takes no pairs
+#endif
 // kGlobal: the groups' hull staging exceeds a workgroup's LDS and lives in
 // the block's slab of P.satImage (narrowSATGlobalKernel); the world sort
 // still uses kOrderSortBytes of LDS.
@@ -1481,6 +1484,13 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
         __shared__ int32_t s_sort_scan[kNarrowBlock / 64];
         sortWorldsForSolver(P, (int32_t *)smem, s_sort_scan);
     }
+    // With the sort on block 0 the pairs go to the other blocks, so the sort
+    // is not added to one block's share of them (whole block: no barrier is
+    // left behind).
+    const bool sortAlone = MW_SAT_SORT_ALONE && gridDim.x > 1;
+    if (sortAlone && blockIdx.x == 0) return;
+    const int32_t pairBlock = sortAlone ? blockIdx.x - 1 : blockIdx.x;
+    const int32_t pairBlocks = sortAlone ? gridDim.x - 1 : gridDim.x;
     ObjDev O = P.objs;
     if constexpr (kGeo) {
         char *dst = smem + (kGlobal ? kOrderSortBytes : satStageBytes(P.objs));
@@ -1502,11 +1512,11 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
     loadBinPrefix(P, 0, s_pre);            // (its barrier publishes the tables)
     // the SAT verdicts (hhJobs) are indexed by list position: never past them
     const int32_t total = min(s_pre[kNarrowBins], P.numWorlds * P.candCapacity);
-    const int32_t stride = gridDim.x * kGroupsPerBlock;
+    const int32_t stride = pairBlocks * kGroupsPerBlock;
     // Two-deep software pipeline over the group's pairs (as the plane
     // kernel's): while pair idx is tested, the body poses of pair
     // idx + stride and the work entry of pair idx + 2 stride are in flight.
-    int32_t idx = blockIdx.x * kGroupsPerBlock + group;
+    int32_t idx = pairBlock * kGroupsPerBlock + group;
     PackedSatWork w1 {}, w2 {};
     BodyPose pa1 {}, pb1 {};
     bool ok1 = false;
