@@ -1140,12 +1140,16 @@ __device__ __forceinline__ bool planeWorkOk(const PhysArgs &P, const SatWork &wk
 }
 
 // Hull-plane contacts, one lane per pair of the bins' back parts.
-__global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
+// kGeo: the hull tables are staged into LDS (P.planeGeoBytes > 0) -- a
+// template parameter so that their reads compile to LDS loads; behind a
+// run-time test the table pointers are generic and every vertex, face and
+// half-edge read is a flat load.
+template <bool kGeo>
+__device__ __forceinline__ void narrowPlaneBlock(const PhysArgs &P)
 {
-    MW_TRACE_BLOCK(0);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     ObjDev O = P.objs;
-    if (P.planeGeoBytes > 0) {
+    if constexpr (kGeo) {
         static_assert(sizeof(HullDev) % 4 == 0 && sizeof(geometry::HalfEdge) % 4 == 0, "dword copies");
         char *dst = smem;
         O.hulls = (HullDev *)stageTable(dst, P.objs.hulls, sizeof(HullDev) * O.numObjects);
@@ -1192,6 +1196,18 @@ __global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
         if (planeContact(P, O, wk.world, wk, in))
             recordManifold(P, wk.world, wk.slot, slotOf(P, wk.bArch, wk.b), slotOf(P, wk.aArch, wk.a));
     }
+}
+
+__global__ void __launch_bounds__(kContactBlock) narrowPlaneKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    narrowPlaneBlock<true>(P);
+}
+
+__global__ void __launch_bounds__(kContactBlock) narrowPlaneNoGeoKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    narrowPlaneBlock<false>(P);
 }
 
 #if defined(MW_SAT_PROFILE)

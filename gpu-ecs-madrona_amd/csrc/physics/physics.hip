@@ -155,9 +155,12 @@ void PhysicsModule::upload(void *stream_ptr)
         P.clipImage = alloc<char>((size_t)P.contactGrid * contactImageBytes(P), stream_ptr);
     }
     // plane kernel: hull tables in LDS up to 16 KB, else read from HBM
-    P.planeGeoBytes = (int32_t)planeSharedBytes(P);
-    P.planeGrid = cus * hipx::residentBlocks((const void *)&narrowPlaneKernel, "narrowPlaneKernel",
-                                             kContactBlock, P.planeGeoBytes);
+    P.planeGeoBytes = force ? 0 : (int32_t)planeSharedBytes(P);
+    P.planeGrid = cus * (P.planeGeoBytes > 0
+                             ? hipx::residentBlocks((const void *)&narrowPlaneKernel, "narrowPlaneKernel",
+                                                    kContactBlock, P.planeGeoBytes)
+                             : hipx::residentBlocks((const void *)&narrowPlaneNoGeoKernel,
+                                                    "narrowPlaneNoGeoKernel", kContactBlock, 0));
 
     P.solverImage = nullptr;
     if (!fitsLDS((const void *)&solverKernel, kSolverThreads, solverSharedBytes(P))) {
@@ -443,8 +446,12 @@ struct NarrowphaseNode : PhysNodeBase {
             MW_HIP_CHECK(hipEventRecord((hipEvent_t)lc.forkEvent, stream));
             MW_HIP_CHECK(hipStreamWaitEvent(side, (hipEvent_t)lc.forkEvent, 0));
         }
-        MW_LAUNCH(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),
-                  dim3(kContactBlock), Q.planeGeoBytes, side ? side : stream, Q);
+        if (Q.planeGeoBytes > 0)
+            MW_LAUNCH(narrowPlaneKernel, dim3(lc.persistentGrid(Q.planeGrid)),
+                      dim3(kContactBlock), Q.planeGeoBytes, side ? side : stream, Q);
+        else
+            MW_LAUNCH(narrowPlaneNoGeoKernel, dim3(lc.persistentGrid(Q.planeGrid)),
+                      dim3(kContactBlock), 0, side ? side : stream, Q);
         if (side) MW_HIP_CHECK(hipEventRecord((hipEvent_t)lc.joinEvent, side));
         if (Q.satImage) {       // the grid never exceeds the slabs of the image
             const uint32_t g = std::min<uint32_t>(lc.persistentGrid(Q.satGrid), Q.satImageBlocks);

@@ -142,7 +142,8 @@ __global__ void integrateKernel(PhysArgs P);
 __global__ void narrowFilterKernel(PhysArgs P);
 __global__ void narrowSATKernel(PhysArgs P);         // hull tables in LDS (satGeoBytes > 0)
 __global__ void narrowSATNoGeoKernel(PhysArgs P);    // hull tables read from HBM
-__global__ void narrowPlaneKernel(PhysArgs P);
+__global__ void narrowPlaneKernel(PhysArgs P);        // hull tables staged into LDS
+__global__ void narrowPlaneNoGeoKernel(PhysArgs P);   // hull tables read from HBM
 __global__ void narrowContactKernel(PhysArgs P);
 __global__ void solverKernel(PhysArgs P, int32_t integrate_next);
 // The same kernels with their per-world / per-group / per-lane LDS image in
