@@ -271,10 +271,20 @@ struct BodyPose {
     Diag3x3 s;
 };
 
+// The column pointers come out of LDS (SatArch), where the compiler no longer
+// knows they point to global memory: the loads go through address-space-1
+// pointers so that they are global loads, not flat ones (a flat load also
+// counts against the LDS wait counter).
+typedef const __attribute__((address_space(1))) float *GlobalF;
+
 __device__ __forceinline__ BodyPose loadPose(const SatArch &A, int32_t w, int32_t row)
 {
     const size_t i = (size_t)w * A.capacity + row;
-    return BodyPose { A.pos[i], A.rot[i], A.scale[i] };
+    const GlobalF p = (GlobalF)(const void *)A.pos + 3 * i;
+    const GlobalF r = (GlobalF)(const void *)A.rot + 4 * i;
+    const GlobalF s = (GlobalF)(const void *)A.scale + 3 * i;
+    return BodyPose { Vector3 { p[0], p[1], p[2] }, Quat { r[0], r[1], r[2], r[3] },
+                      Diag3x3 { s[0], s[1], s[2] } };
 }
 
 // Transform one body's hull into the group's LDS and copy its edge topology

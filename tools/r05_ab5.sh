@@ -3,8 +3,10 @@
 # tables read through LDS-typed pointers (narrowPlaneKernel, kGeo template)
 # against the generic-pointer build (build_old: HEAD before the change), then
 # the parity tests that cover the plane kernel and the forced-HBM variant.
+# Re-run with O=ab9 for the SAT kernel's pose loads through global-typed
+# pointers (loadPose) against HEAD.
 set -o pipefail
-O=gpurun_out/ab8
+O=gpurun_out/ab9
 mkdir -p $O
 timeout -k 10 300 python tools/ab_bench.py --workload collisions --steps 20 --out $O/c \
     base old:LIB=build_old base2 old2:LIB=build_old \
@@ -13,6 +15,6 @@ timeout -k 10 250 python tools/ab_bench.py --workload simple --steps 50 --out $O
     base old:LIB=build_old \
     > $O/simple.log 2>&1 || { tail -20 $O/simple.log; exit 3; }
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-    tests/test_lds_fallback_gpu.py tests/test_collisions_gpu.py > $O/tests.log 2>&1 || { tail -20 $O/tests.log; exit 4; }
+    tests/test_lds_fallback_gpu.py tests/test_collisions_gpu.py tests/test_sat_bits_gpu.py > $O/tests.log 2>&1 || { tail -20 $O/tests.log; exit 4; }
 tail -2 $O/tests.log
 echo ab-done
