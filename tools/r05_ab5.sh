@@ -4,9 +4,10 @@
 # against the generic-pointer build (build_old: HEAD before the change), then
 # the parity tests that cover the plane kernel and the forced-HBM variant.
 # Re-run with O=ab9 for the SAT kernel's pose loads through global-typed
-# pointers (loadPose) against HEAD.
+# pointers (loadPose) against HEAD, and with O=ab10 for the contact kernel
+# with its hull tables staged into LDS after the clip buffers.
 set -o pipefail
-O=gpurun_out/ab9
+O=gpurun_out/ab10
 mkdir -p $O
 timeout -k 10 300 python tools/ab_bench.py --workload collisions --steps 20 --out $O/c \
     base old:LIB=build_old base2 old2:LIB=build_old \
