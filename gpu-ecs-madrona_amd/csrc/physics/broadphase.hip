@@ -540,7 +540,7 @@ __device__ __forceinline__ float ldsAtomicMaxRef(float *addr, float v)
 
 size_t refitSharedBytes(const PhysArgs &P)
 {
-    return sizeof(BVHNode) * (size_t)P.maxNodes;
+    return sizeof(BVHNode) * (size_t)P.refitLDSNodes;
 }
 
 // kGlobal: the world's nodes exceed a workgroup's LDS; the same walk runs on
@@ -632,7 +632,11 @@ __device__ __forceinline__ void refitWorld(const PhysArgs &P)
 __global__ void __launch_bounds__(kRefitBlock) refitKernel(PhysArgs P)
 {
     MW_TRACE_BLOCK(0);
-    refitWorld<false>(P);
+    // a world whose used nodes exceed the LDS capacity refits in place
+    if (min(P.bvh[blockIdx.x].usedNodes, P.maxNodes) <= P.refitLDSNodes)
+        refitWorld<false>(P);
+    else
+        refitWorld<true>(P);
 }
 
 __global__ void __launch_bounds__(kRefitBlock) refitGlobalKernel(PhysArgs P)

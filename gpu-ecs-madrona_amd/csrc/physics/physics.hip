@@ -80,6 +80,14 @@ void PhysicsModule::upload(void *stream_ptr)
     const int32_t solver_blocks = (W + kSolverWorlds - 1) / kSolverWorlds;
 
     // broadphase: the BVH rebuild picks its variant per launch (<= 64 KB)
+    // refit: LDS for about two thirds of the node capacity -- a rebuild uses
+    // ≈0.7 nodes per leaf of the capacity's 1.33 (collisions: 81-97 of
+    // 172), so the full capacity would cost blocks per CU for nodes no world
+    // uses; a world past it refits in place in HBM inside the same kernel.
+    // MADRONA_MW_REFIT_LDS_NODES overrides (the mixed-path parity tests).
+    P.refitLDSNodes = std::min(P.maxNodes, (P.maxNodes * 2 + 2) / 3);
+    if (const char *e = std::getenv("MADRONA_MW_REFIT_LDS_NODES"))
+        P.refitLDSNodes = std::max(1, std::min(P.maxNodes, atoi(e)));
     P.refitGlobal = fitsLDS((const void *)&refitKernel, kRefitBlock, refitSharedBytes(P)) ? 0 : 1;
     if (P.refitGlobal) hipx::residentBlocks((const void *)&refitGlobalKernel, "refitGlobalKernel", kRefitBlock, 0);
     // findOverlaps: BVH traversal for worlds past 512 leaves (the sweep is

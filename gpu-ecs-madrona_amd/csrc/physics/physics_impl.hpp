@@ -227,6 +227,8 @@ struct PhysArgs {
     char *overlapImage;           // [W][findOverlapsImageBytes] leaf image per world
     int32_t overlapDFSLeaves;     // findOverlaps: worlds with more leaves traverse the BVH
                                   // (stack DFS) instead of sweeping every leaf; -1: never
+    int32_t refitLDSNodes;        // refitKernel's LDS node capacity: a world with more
+                                  // used nodes walks its slab in place (same result)
     int32_t refitGlobal;          // refit walks the node slab in place
     char *satImage;               // [satImageBlocks][narrowphaseImageBytes] hull staging
     int32_t satImageBlocks;
