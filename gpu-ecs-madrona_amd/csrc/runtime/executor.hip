@@ -242,8 +242,20 @@ exportScanKernel(const int32_t *num_rows, int32_t num_worlds, int64_t *offsets)
     const int32_t per = (num_worlds + 1023) / 1024;
     const int32_t beg = min(tid * per, num_worlds);
     const int32_t end = min(beg + per, num_worlds);
+    // up to kScanPer counts per thread held in registers: their loads issue
+    // together (the loop form waited on them one by one) and the write pass
+    // reuses them
+    constexpr int32_t kScanPer = 16;
+    int32_t v[kScanPer];
     int64_t s = 0;
-    for (int32_t w = beg; w < end; w++) s += num_rows[w];
+    if (per <= kScanPer) {
+#pragma unroll
+        for (int32_t j = 0; j < kScanPer; j++) v[j] = beg + j < end ? num_rows[beg + j] : 0;
+#pragma unroll
+        for (int32_t j = 0; j < kScanPer; j++) s += v[j];
+    } else {
+        for (int32_t w = beg; w < end; w++) s += num_rows[w];
+    }
     int64_t x = s;
 #pragma unroll
     for (int32_t off = 1; off < 64; off <<= 1) {
@@ -255,9 +267,17 @@ exportScanKernel(const int32_t *num_rows, int32_t num_worlds, int64_t *offsets)
     int64_t base = 0;
     for (int32_t i = 0; i < wave; i++) base += wave_sums[i];
     int64_t run = base + x - s;
-    for (int32_t w = beg; w < end; w++) {
-        offsets[w] = run;
-        run += num_rows[w];
+    if (per <= kScanPer) {
+#pragma unroll
+        for (int32_t j = 0; j < kScanPer; j++) {
+            if (beg + j < end) offsets[beg + j] = run;
+            run += v[j];
+        }
+    } else {
+        for (int32_t w = beg; w < end; w++) {
+            offsets[w] = run;
+            run += num_rows[w];
+        }
     }
     if (tid == 1023) offsets[num_worlds] = base + x;
 }
