@@ -67,6 +67,16 @@ struct PhysicsModule : StateExtension {
     void buildArgs(void *stream);
     // Back end: buildArgs plus its own launch sizing.
     void upload(void *stream_ptr) override;
+    // A growable non-body table can grow the entity ID store: the solver's
+    // and the narrowphase's entity lookups follow it (the graphs that hold
+    // `args` are re-captured after the growth).
+    void stateResized() override
+    {
+        if (!uploaded || !initialized) return;
+        const StateView &dv = mgr->deviceViewHost();
+        args.idNodes = dv.idNodes;
+        args.idsPerWorld = dv.idsPerWorld;
+    }
 };
 
 PhysicsModule &physicsModule(StateManager &mgr);

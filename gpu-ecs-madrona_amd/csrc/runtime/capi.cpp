@@ -382,7 +382,15 @@ int mw_rccl_init(mw_exec *exec, const void *id, int32_t nranks, int32_t rank)
         if (exec->comm) throw std::runtime_error("mw_rccl_init: communicator already set");
         ncclUniqueId uid;
         memcpy(&uid, id, sizeof(uid));
-        // the communicator binds to the calling thread's current device
+        // the communicator binds to the calling thread's current device:
+        // the executor's for the call, the caller's again afterwards (also
+        // when the init throws)
+        int prev = 0;
+        MW_HIP_OK(hipGetDevice(&prev));
+        struct Restore {
+            int dev;
+            ~Restore() { (void)hipSetDevice(dev); }
+        } restore { prev };
         MW_HIP_OK(hipSetDevice(exec->gpu));
         MW_NCCL_OK(rccl().commInitRank(&exec->comm, nranks, uid, rank));
         return 0;

@@ -390,7 +390,11 @@ void Executor::runSteps(int32_t n)
     Impl &I = *impl_;
     if (n <= 0) return;
     const bool world_local = I.segs.size() == 1 && !I.segs[0].global;
-    if (n == 1 || !world_local || !I.timedName.empty()) {
+    // growable tables grow between any two steps: one step at a time
+    bool growable = false;
+    const StateView &hv = I.mgr->hostView();
+    for (int32_t a = 0; a < hv.numArchetypes; a++) growable |= I.mgr->growable(a);
+    if (n == 1 || !world_local || !I.timedName.empty() || growable) {
         for (int32_t i = 0; i < n; i++) runAsync();
         return;
     }

@@ -385,6 +385,20 @@ struct GrowSet {
     int32_t arch[kMaxArchetypes];
 };
 
+// An export buffer of a growable archetype is a reserved device address
+// range with physical memory mapped on demand (HIP virtual memory
+// management): a table growth maps more of it behind the packed rows, so the
+// buffer keeps its address and contents, as the reference's getExported
+// pointer does (src/mw/cuda_exec.cpp:1777-1782, state.cpp exportColumn).
+// Where the range cannot be reserved (or a growth outruns it) the buffer is
+// reallocated with its packed rows copied over: then pointers handed out
+// before the growth are stale (mw_get_exported again).
+struct ExportMem {
+    size_t reserved = 0;        // bytes of address space (0: a plain hipMalloc buffer)
+    size_t mapped = 0;          // bytes backed by physical chunks from the start
+    std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks;
+};
+
 struct ExportBuf {
     int32_t slot, archetype, column;
     uint32_t bytes;
@@ -392,7 +406,109 @@ struct ExportBuf {
     int64_t *offsets;           // shared by the exports of one archetype
     bool scanOwner;             // this export launches the archetype's scan
     bool singleton;             // one row per world: offsets fixed (w), flat copy
+    ExportMem mem;
+    int64_t relocations = 0;    // growths that moved buf (0 with a reserved range)
 };
+
+static hipMemAllocationProp exportMemProp(int dev)
+{
+    hipMemAllocationProp prop {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = dev;
+    return prop;
+}
+
+static size_t exportMemGranularity(int dev)
+{
+    const hipMemAllocationProp prop = exportMemProp(dev);
+    size_t gran = 0;
+    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return gran;
+}
+
+static void releaseExportMem(ExportBuf &b)
+{
+    if (!b.buf) return;
+    if (b.mem.reserved == 0) {
+        (void)hipFree(b.buf);
+    } else {
+        size_t off = 0;
+        for (auto &c : b.mem.chunks) {
+            (void)hipMemUnmap(b.buf + off, c.second);
+            (void)hipMemRelease(c.first);
+            off += c.second;
+        }
+        (void)hipMemAddressFree(b.buf, b.mem.reserved);
+    }
+    b.buf = nullptr;
+    b.mem = ExportMem {};
+}
+
+// Back [0, bytes) of the reserved range with physical memory (the new part
+// only); false when the range or the device refuses it.
+static bool mapExportMem(ExportBuf &b, size_t bytes, int dev)
+{
+    if (bytes <= b.mem.mapped) return true;
+    const size_t gran = exportMemGranularity(dev);
+    if (gran == 0) return false;
+    const size_t need = (bytes - b.mem.mapped + gran - 1) / gran * gran;
+    if (b.mem.mapped + need > b.mem.reserved) return false;
+    const hipMemAllocationProp prop = exportMemProp(dev);
+    hipMemGenericAllocationHandle_t h {};
+    if (hipMemCreate(&h, need, &prop, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    char *at = b.buf + b.mem.mapped;
+    if (hipMemMap(at, need, 0, h, 0) != hipSuccess) {
+        (void)hipMemRelease(h);
+        (void)hipGetLastError();
+        return false;
+    }
+    hipMemAccessDesc acc {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    if (hipMemSetAccess(at, need, &acc, 1) != hipSuccess) {
+        (void)hipMemUnmap(at, need);
+        (void)hipMemRelease(h);
+        (void)hipGetLastError();
+        return false;
+    }
+    b.mem.chunks.push_back({ h, need });
+    b.mem.mapped += need;
+    return true;
+}
+
+// A new export buffer of `bytes`; a growable archetype's in a reserved range
+// of 256x that (at least 4 GiB of address space, no memory behind it).
+// MADRONA_MW_EXPORT_VMM=0: plain buffers (relocated on growth).
+static void allocExportMem(ExportBuf &b, size_t bytes, bool growable, int dev)
+{
+    bytes = std::max<size_t>(bytes, 256);
+    const char *env = getenv("MADRONA_MW_EXPORT_VMM");
+    const size_t gran = growable && !(env && atoi(env) == 0) ? exportMemGranularity(dev) : 0;
+    if (gran > 0) {
+        size_t reserve = std::max<size_t>(bytes * 256, size_t(4) << 30);
+        reserve = (reserve + gran - 1) / gran * gran;
+        void *p = nullptr;
+        if (hipMemAddressReserve(&p, reserve, 0, nullptr, 0) == hipSuccess && p) {
+            b.buf = (char *)p;
+            b.mem.reserved = reserve;
+            if (mapExportMem(b, bytes, dev)) return;
+            releaseExportMem(b);
+        }
+        (void)hipGetLastError();
+    }
+    MW_HIP_CHECK(hipMalloc(&b.buf, bytes));
+}
+
+// Growth probe ring: after every enqueued step the growable tables' largest
+// per-world row counts go to pinned host memory, behind an event.
+constexpr int32_t kGrowProbeSlots = 8;
 
 struct Executor::Impl {
     ExecConfig cfg;
@@ -483,8 +599,21 @@ struct Executor::Impl {
     uint64_t walkWsBytes = 0;
     size_t walkLds = 0;             // resume kernel: dynamic LDS for the commit working set (0: in the slab)
     // table growth (growTables): the growable archetypes, their row maxima
+    // per probe slot (device, pinned host), the slots in flight oldest first,
+    // the latest maxima read back, and how many steps may run past the
+    // newest maxima the host has seen (MADRONA_MW_GROW_LAG)
     GrowSet growable {};
-    int32_t *growProbe = nullptr;
+    int32_t *growProbe = nullptr;             // [kGrowProbeSlots][kMaxArchetypes]
+    int32_t *growProbeHost = nullptr;
+    hipEvent_t growProbeEv[kGrowProbeSlots] = {};
+    int32_t probeFifo[kGrowProbeSlots] = {};
+    int32_t probeHead = 0, probeCount = 0, probeNext = 0;
+    int64_t probeStepOf[kGrowProbeSlots] = {};
+    int64_t stepsEnqueued = 0;                // probe k follows step k (0: the upload)
+    int64_t lastProbeStep = -1;               // step of the maxima in lastMax (-1: none yet)
+    int32_t growLag = 4;
+    int32_t lastMax[kMaxArchetypes] = {};
+    int32_t maxRise[kMaxArchetypes] = {};     // largest per-step rise seen, -1: none yet
     int64_t growths = 0;
     std::vector<std::pair<const void *, int32_t>> walkGrid;   // kernel -> grid
 };
@@ -546,15 +675,20 @@ Executor::~Executor()
         (void)hipFree(impl_->trace);
         (void)hipFree(impl_->traceLogs);
     }
+    if (impl_->stream) (void)hipStreamSynchronize(impl_->stream);
     if (impl_->hostRowsTotal) (void)hipHostFree(impl_->hostRowsTotal);
     if (impl_->nodeDataDev) (void)hipFree(impl_->nodeDataDev);
     if (impl_->commit.scratch) (void)hipFree(impl_->commit.scratch);
     if (impl_->growProbe) (void)hipFree(impl_->growProbe);
+    if (impl_->growProbeHost) (void)hipHostFree(impl_->growProbeHost);
+    for (hipEvent_t e : impl_->growProbeEv) {
+        if (e) (void)hipEventDestroy(e);
+    }
     if (impl_->walkEntriesDev) (void)hipFree(impl_->walkEntriesDev);
     if (impl_->walkScratch) (void)hipFree(impl_->walkScratch);
     if (impl_->walkResume) (void)hipFree(impl_->walkResume);
     for (auto &e : impl_->exports) {
-        (void)hipFree(e.buf);
+        releaseExportMem(e);
         if (e.scanOwner) (void)hipFree(e.offsets);
     }
     impl_->mgr.reset();
@@ -630,17 +764,127 @@ static void setupCommit(Executor::Impl &I)
 
 // Growable tables (registerArchetype, StateManager::growable) and the
 // per-archetype row-count maxima the growth check reads.
-__global__ void __launch_bounds__(256) maxRowsKernel(const StateView *__restrict__ st, GrowSet g, int32_t *out)
+// One block: per growable archetype the maximum over worlds, plain stores
+// (no reset needed between probes).
+constexpr int32_t kMaxRowsThreads = 1024;
+__global__ void __launch_bounds__(kMaxRowsThreads) maxRowsKernel(const StateView *__restrict__ st, GrowSet g,
+                                                                 int32_t *out)
 {
+    __shared__ int32_t part[kMaxRowsThreads / 64];
     for (int32_t i = 0; i < g.n; i++) {
         const int32_t *rows = st->arch[g.arch[i]].numRows;
         int32_t m = 0;
-        for (int32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < st->numWorlds; w += gridDim.x * blockDim.x)
-            m = max(m, rows[w]);
+        for (int32_t w = threadIdx.x; w < st->numWorlds; w += kMaxRowsThreads) m = max(m, rows[w]);
 #pragma unroll
         for (int32_t o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-        if ((threadIdx.x & 63) == 0 && m > 0) atomicMax(out + i, m);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x / 64] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int32_t k = 1; k < kMaxRowsThreads / 64; k++) m = max(m, part[k]);
+            out[i] = m;
+        }
+        __syncthreads();
     }
+}
+
+// Enqueue a growth probe behind the steps enqueued so far.
+static void consumeOldestProbe(Executor::Impl &I, bool wait);
+static void enqueueGrowProbe(Executor::Impl &I)
+{
+    if (I.growable.n == 0) return;
+    if (I.probeCount == kGrowProbeSlots) consumeOldestProbe(I, true);
+    const int32_t s = I.probeNext;
+    I.probeNext = (I.probeNext + 1) % kGrowProbeSlots;
+    int32_t *dev = I.growProbe + s * kMaxArchetypes;
+    MW_LAUNCH(maxRowsKernel, dim3(1), dim3(kMaxRowsThreads), 0, I.stream, I.mgr->deviceView(), I.growable, dev);
+    MW_HIP_CHECK(hipMemcpyAsync(I.growProbeHost + s * kMaxArchetypes, dev, sizeof(int32_t) * I.growable.n,
+                                hipMemcpyDeviceToHost, I.stream));
+    MW_HIP_CHECK(hipEventRecord(I.growProbeEv[s], I.stream));
+    I.probeStepOf[s] = I.stepsEnqueued;
+    I.probeFifo[(I.probeHead + I.probeCount) % kGrowProbeSlots] = s;
+    I.probeCount++;
+}
+
+// Read the oldest probe in flight (waiting for it, or only if it is done);
+// the maxima of later probes replace earlier ones, and the largest per-step
+// rise between consecutive readings is kept.
+static void consumeOldestProbe(Executor::Impl &I, bool wait)
+{
+    const int32_t s = I.probeFifo[I.probeHead];
+    if (wait) {
+        MW_HIP_CHECK(hipEventSynchronize(I.growProbeEv[s]));
+    } else {
+        const hipError_t q = hipEventQuery(I.growProbeEv[s]);
+        if (q == hipErrorNotReady) {
+            (void)hipGetLastError();
+            return;
+        }
+        MW_HIP_CHECK(q);
+    }
+    const int64_t step = I.probeStepOf[s];
+    for (int32_t i = 0; i < I.growable.n; i++) {
+        const int32_t m = I.growProbeHost[s * kMaxArchetypes + i];
+        if (I.lastProbeStep >= 0 && step > I.lastProbeStep) {
+            const int64_t d = step - I.lastProbeStep;
+            const int32_t rise = (int32_t)std::max<int64_t>(0, ((int64_t)m - I.lastMax[i] + d - 1) / d);
+            I.maxRise[i] = std::max(I.maxRise[i], rise);
+        }
+        I.lastMax[i] = m;
+    }
+    I.lastProbeStep = step;
+    I.probeHead = (I.probeHead + 1) % kGrowProbeSlots;
+    I.probeCount--;
+}
+
+// Consume every finished probe; with wait, every probe.
+static void drainGrowProbes(Executor::Impl &I, bool wait)
+{
+    while (I.probeCount > 0) {
+        const int32_t before = I.probeCount;
+        consumeOldestProbe(I, wait);
+        if (I.probeCount == before) break;      // the oldest is still running
+    }
+}
+
+// May the next step be enqueued before more probes are read?  The rows of
+// the steps the host has not seen yet (those in flight and the next one)
+// are projected with the largest per-step rise seen so far; before a rise
+// is known only the step right after the newest reading is.
+static bool enqueueSafe(const Executor::Impl &I)
+{
+    if (I.lastProbeStep < 0) return false;
+    const StateView &dv = I.mgr->deviceViewHost();
+    const int64_t ahead = I.stepsEnqueued + 1 - I.lastProbeStep;
+    for (int32_t i = 0; i < I.growable.n; i++) {
+        if (I.maxRise[i] < 0) {
+            if (ahead > 1) return false;
+            continue;
+        }
+        if ((int64_t)I.lastMax[i] + (int64_t)I.maxRise[i] * ahead > dv.arch[I.growable.arch[i]].capacity)
+            return false;
+    }
+    return true;
+}
+
+// The capacity archetype i needs for the newest maxima: at most half full,
+// and room for growLag + 1 steps at the largest rise seen.
+static int64_t neededCapacity(const Executor::Impl &I, int32_t i, int64_t cap)
+{
+    const int64_t m = I.lastMax[i];
+    const int64_t ahead = I.maxRise[i] > 0 ? m + (int64_t)I.maxRise[i] * (I.growLag + 1) : 0;
+    int64_t nc = std::max<int64_t>(cap, 1);
+    while (m * 2 > nc || ahead > nc) nc *= 2;
+    return nc;
+}
+
+static bool growthDue(const Executor::Impl &I)
+{
+    const StateView &dv = I.mgr->deviceViewHost();
+    for (int32_t i = 0; i < I.growable.n; i++) {
+        const int32_t cap = dv.arch[I.growable.arch[i]].capacity;
+        if (neededCapacity(I, i, cap) > cap) return true;
+    }
+    return false;
 }
 
 void Executor::uploadState()
@@ -652,7 +896,15 @@ void Executor::uploadState()
     for (int32_t a = 0; a < impl_->mgr->numArchetypes(); a++) {
         if (impl_->mgr->growable(a) && impl_->growable.n < kMaxArchetypes) impl_->growable.arch[impl_->growable.n++] = a;
     }
-    if (impl_->growable.n > 0) MW_HIP_CHECK(hipMalloc(&impl_->growProbe, sizeof(int32_t) * kMaxArchetypes));
+    if (impl_->growable.n > 0) {
+        const size_t pb = sizeof(int32_t) * kMaxArchetypes * kGrowProbeSlots;
+        MW_HIP_CHECK(hipMalloc(&impl_->growProbe, pb));
+        MW_HIP_CHECK(hipHostMalloc(&impl_->growProbeHost, pb));
+        for (hipEvent_t &e : impl_->growProbeEv) MW_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        if (const char *e = std::getenv("MADRONA_MW_GROW_LAG")) impl_->growLag = std::max(0, atoi(e));
+        impl_->growLag = std::min(impl_->growLag, kGrowProbeSlots - 1);
+        for (int32_t &r : impl_->maxRise) r = -1;
+    }
 
     int32_t num_exports = 0;
     const StateManager::ExportDesc *ex = impl_->mgr->exports(&num_exports);
@@ -667,7 +919,7 @@ void Executor::uploadState()
         if (b.bytes % 4 != 0) {
             throw std::runtime_error("exportColumn: component size must be a multiple of 4 bytes");
         }
-        MW_HIP_CHECK(hipMalloc(&b.buf, std::max<size_t>(bytes, 256)));
+        allocExportMem(b, bytes, impl_->mgr->growable(b.archetype), impl_->cfg.gpuID);
         // offsets are per archetype: exports of one archetype share them
         for (const ExportBuf &o : impl_->exports) {
             if (o.archetype == b.archetype) { b.offsets = o.offsets; b.scanOwner = false; }
@@ -686,6 +938,7 @@ void Executor::uploadState()
         }
         impl_->exports.push_back(b);
     }
+    enqueueGrowProbe(*impl_);            // the initial rows
 }
 
 static void traceMarker(Executor::Impl &I, mwGPU::DeviceEvent ev, uint32_t func, uint32_t inv,
@@ -1259,9 +1512,12 @@ void Executor::setGraph(TaskGraph &&graph)
     if (impl_->cfg.useGraph) captureGraph(*impl_, lc, dv);
 }
 
+static bool growTables(Executor &E, Executor::Impl &I);
+
 void Executor::runAsync()
 {
     Impl &I = *impl_;
+    growTables(*this, I);
     const StateView &dv = I.mgr->deviceViewHost();
     LaunchCtx lc = makeLaunchCtx(I, this);
     // sampled timing: the first step of every run of timedEvery is the
@@ -1276,6 +1532,8 @@ void Executor::runAsync()
     } else {
         launchStep(I, lc, dv);
     }
+    I.stepsEnqueued++;
+    enqueueGrowProbe(I);
 }
 
 // Is step `idx` an unsplit step?  With live timing every step is split
@@ -1291,7 +1549,9 @@ void Executor::runSteps(int32_t n)
     Impl &I = *impl_;
     const int32_t K = I.multiK;
     for (int32_t i = 0; i < n;) {
-        bool multi = !I.multiSegs.empty() && n - i >= K;
+        // growable tables: one step per launch, so the growth check runs
+        // between any two steps
+        bool multi = !I.multiSegs.empty() && n - i >= K && I.growable.n == 0;
         for (int32_t k = 0; multi && k < K; k++) multi = plainStep(I, I.stepIndex + k);
         if (multi) {
             MW_HIP_CHECK(hipGraphLaunch(I.multiSegs[0].exec, I.stream));
@@ -1306,38 +1566,53 @@ void Executor::runSteps(int32_t n)
 
 // Table growth between steps (reference Table::addRow, src/common/table.cpp:
 // 44-61, x2 when full; the reference's device runtime grows by device
-// malloc).  At every synchronisation point the growable tables' largest
-// per-world row count is read back; a table past half its capacity doubles
-// (until it is at most half full), so a table grows before it can overflow
-// unless one stretch of unsynchronised steps more than doubles it (then the
-// table-full flag is raised, as before).  A growth re-strides the slabs
-// (StateManager::growArchetype), resizes the commit scratch and the export
-// buffers of that archetype, and re-plans / re-captures the step.
+// malloc).  Behind every enqueued step a probe copies the growable tables'
+// largest per-world row counts to pinned host memory (enqueueGrowProbe).
+// Before the next step is enqueued the host reads the probes that have
+// finished and waits for older ones only while the rows of the steps it has
+// not seen, projected at the largest per-step rise seen so far, could pass a
+// table's capacity (enqueueSafe), or more than growLag steps are unseen.  A
+// table past half full, or without room for growLag + 1 steps at that rise,
+// then doubles (neededCapacity) before the step is enqueued.  So the tables
+// grow between any two steps -- inside mw_step(n), async bursts and at every
+// sync -- without a host synchronisation per step; a step whose rows rise
+// past any rise seen before (or that fills a table inside itself) still
+// overflows and raises the table-full flag.  The growth itself is a
+// synchronisation point: it re-strides the slabs
+// (StateManager::growArchetype), extends the export buffers of that
+// archetype in place (mapping more of their reserved range), resizes the
+// commit scratch and re-plans / re-captures the step.
 static bool growTables(Executor &E, Executor::Impl &I)
 {
     if (I.growable.n == 0) return false;
-    const StateView &dv = I.mgr->deviceViewHost();
-    MW_HIP_CHECK(hipMemsetAsync(I.growProbe, 0, sizeof(int32_t) * kMaxArchetypes, I.stream));
-    const uint32_t blocks = (uint32_t)std::min<int64_t>(1024, (dv.numWorlds + 255) / 256);
-    MW_LAUNCH(maxRowsKernel, dim3(std::max<uint32_t>(blocks, 1)), dim3(256), 0, I.stream,
-              I.mgr->deviceView(), I.growable, I.growProbe);
-    int32_t maxes[kMaxArchetypes];
-    MW_HIP_CHECK(hipMemcpyAsync(maxes, I.growProbe, sizeof(int32_t) * I.growable.n, hipMemcpyDeviceToHost,
-                                I.stream));
+    drainGrowProbes(I, false);
+    while (I.probeCount > 0 && (I.probeCount > I.growLag || !enqueueSafe(I))) consumeOldestProbe(I, true);
+    if (!growthDue(I)) return false;
     MW_HIP_CHECK(hipStreamSynchronize(I.stream));
+    drainGrowProbes(I, true);                   // every step so far
+    const StateView &dv = I.mgr->deviceViewHost();
     bool grown = false;
     for (int32_t i = 0; i < I.growable.n; i++) {
         const int32_t a = I.growable.arch[i];
         const int32_t cap = dv.arch[a].capacity;
-        if ((int64_t)maxes[i] * 2 <= cap) continue;
-        int64_t nc = std::max(cap, 1);
-        while ((int64_t)maxes[i] * 2 > nc) nc *= 2;
+        const int64_t nc = neededCapacity(I, i, cap);
+        if (nc <= cap) continue;
         if (nc > (1 << 28)) throw std::runtime_error("table growth past 2^28 rows per world");
         I.mgr->growArchetype(a, (int32_t)nc, I.stream);
         for (ExportBuf &b : I.exports) {
             if (b.archetype != a) continue;
-            MW_HIP_CHECK(hipFree(b.buf));
-            MW_HIP_CHECK(hipMalloc(&b.buf, std::max<size_t>((size_t)dv.numWorlds * nc * b.bytes, 256)));
+            const size_t old_bytes = std::max<size_t>((size_t)dv.numWorlds * cap * b.bytes, 256);
+            const size_t new_bytes = std::max<size_t>((size_t)dv.numWorlds * nc * b.bytes, 256);
+            if (b.mem.reserved > 0 && mapExportMem(b, new_bytes, I.cfg.gpuID)) continue;
+            // no reserved range (or past it): a new buffer with the packed
+            // rows of the last step copied over
+            char *nb = nullptr;
+            MW_HIP_CHECK(hipMalloc(&nb, new_bytes));
+            MW_HIP_CHECK(hipMemcpyAsync(nb, b.buf, old_bytes, hipMemcpyDeviceToDevice, I.stream));
+            MW_HIP_CHECK(hipStreamSynchronize(I.stream));
+            releaseExportMem(b);
+            b.buf = nb;
+            b.relocations++;
         }
         grown = true;
     }
@@ -1358,7 +1633,9 @@ void Executor::sync()
     I.timedMs += drainTimedPairs(I);
     I.timedLaunches += I.timedUnits;
     I.timedUnits = 0;
-    growTables(*this, I);
+    // the probes behind the last step are complete: no launch, no second sync
+    drainGrowProbes(I, true);
+    if (growthDue(I)) growTables(*this, I);
 }
 
 void Executor::run()
@@ -1591,6 +1868,8 @@ double Executor::timeNode(const char *name, int32_t num_steps)
             }
         }
         launchExports(I, dv);
+        I.stepsEnqueued++;
+        enqueueGrowProbe(I);
     }
     MW_HIP_CHECK(hipStreamSynchronize(I.stream));
     const int64_t units = I.timedUnits;

@@ -579,6 +579,7 @@ void StateManager::growArchetype(int32_t a, int32_t new_cap, void *stream_ptr)
     (void)stream_ptr;
     for (size_t c = 0; c < ai.cols.size(); c++) I.colAllocs[ci + c].bytes = (size_t)W * new_cap * ai.cols[c].numBytes;
     I.devHostCopy = I.host;
+    for (auto &ext : I.extensions) ext.second->stateResized();
 #else
     hipStream_t stream = (hipStream_t)stream_ptr;
     StateView &d = I.devHostCopy;
@@ -639,6 +640,7 @@ void StateManager::growArchetype(int32_t a, int32_t new_cap, void *stream_ptr)
     MW_HIP_CHECK(hipMemcpyAsync(I.devView, &d, sizeof(StateView), hipMemcpyHostToDevice, stream));
     MW_HIP_CHECK(hipStreamSynchronize(stream));
     for (void *p : retired) MW_HIP_CHECK(hipFree(p));
+    for (auto &ext : I.extensions) ext.second->stateResized();
 #endif
 }
 

@@ -532,8 +532,8 @@ template <auto Fn, typename... ComponentTs, size_t... Is>
 constexpr RowWriteKeys rowWriteKeysImpl(std::index_sequence<Is...>)
 {
     RowWriteKeys r {};
-    ((detail::nodeWrites<Fn, Is, ComponentTs>() && r.n < kMaxRowWriteKeys
-          ? (void)(r.key[r.n++] = typeKey<ComponentTs>())
+    ((detail::nodeWrites<Fn, Is, ComponentTs>()
+          ? (r.n < kMaxRowWriteKeys ? (void)(r.key[r.n++] = typeKey<ComponentTs>()) : (void)(r.all = true))
           : (void)0),
      ...);
     return r;

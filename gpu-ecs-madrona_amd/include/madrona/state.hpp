@@ -250,11 +250,13 @@ inline constexpr uint32_t kSerialRowKey = 0xFFFF'FFFFu;
 
 // Exact type keys of the query components a row-parallel node writes
 // (Context::setRowParallel / checkCrossRow); at most kMaxRowWriteKeys are
-// tracked, further written components go unchecked.
+// tracked -- a node writing more sets `all`, and then every cross-row get
+// counts as racing (conservative: flagged rather than left unchecked).
 inline constexpr int32_t kMaxRowWriteKeys = 8;
 struct RowWriteKeys {
     uint64_t key[kMaxRowWriteKeys];
     int32_t n;
+    bool all;
 
     // constant indices only (no loop the backend could leave in scratch)
     template <size_t... Is>
@@ -264,7 +266,7 @@ struct RowWriteKeys {
     }
     MW_INLINE bool has(uint64_t k) const
     {
-        return hasImpl(k, std::make_index_sequence<kMaxRowWriteKeys> {});
+        return all || hasImpl(k, std::make_index_sequence<kMaxRowWriteKeys> {});
     }
 };
 
@@ -466,6 +468,11 @@ class StateExtension {
 public:
     virtual ~StateExtension() = default;
     virtual void upload(void *stream) = 0;
+    // After a table growth (StateManager::growArchetype): slabs the
+    // extension cached from the device view may have moved (the entity ID
+    // store grows with the tables that take entities).  Called before the
+    // executor re-captures the step.
+    virtual void stateResized() {}
 };
 
 class ECSRegistry {

@@ -155,10 +155,20 @@ int32_t mw_load_env(const char *so_path);
 int32_t mw_num_envs(void);
 const char *mw_env_name(int32_t i);
 
-/* Step every world `num_steps` times; blocks until done. */
+/* Step every world `num_steps` times; blocks until done.
+ * Growable tables (registerArchetype without a size) grow between any two
+ * steps, here and in mw_step_async: behind each step the host is sent the
+ * tables' largest row counts, and a table past half full doubles before
+ * the next step is enqueued.  The host runs at most MADRONA_MW_GROW_LAG
+ * (default 2, at most 7) steps ahead of the counts it has seen, so a table
+ * that more than doubles within that many steps + 1 (or inside one step)
+ * overflows and flags its worlds (mw_error_flags); growth itself waits for
+ * the device.  Executors with growable tables launch one step graph per
+ * step (no multi-step graphs).                                             */
 int mw_step(mw_exec *exec, int32_t num_steps);
 
-/* Enqueue `num_steps` steps on the executor stream without waiting. */
+/* Enqueue `num_steps` steps on the executor stream without waiting (beyond
+ * the bounded growth look-behind of mw_step above).                        */
 int mw_step_async(mw_exec *exec, int32_t num_steps);
 
 /* Wait for enqueued steps. */
@@ -166,7 +176,11 @@ int mw_sync(mw_exec *exec);
 
 /* Device pointer of export slot `slot`: rows of all worlds packed
  * world-major (reference getExported).  *num_rows receives the row count of
- * the last enqueued step (waits for it).                                  */
+ * the last enqueued step (waits for it).  The pointer is stable: the buffer
+ * of a growable table is a reserved address range that a growth extends in
+ * place, contents kept (HIP virtual memory; past 256x its first size, or
+ * with MADRONA_MW_EXPORT_VMM=0, a growth moves it to a new buffer with the
+ * contents copied, and earlier pointers are stale).                       */
 void *mw_get_exported(mw_exec *exec, int32_t slot, int64_t *num_rows);
 
 /* Copy up to max_bytes of export slot `slot` into buffer `dst` (device or

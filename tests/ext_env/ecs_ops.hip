@@ -227,6 +227,7 @@ void World::registerTypes(ECSRegistry &reg, const Config &cfg)
     }
     reg.registerSingleton<Stats>();
     reg.exportSingleton<Stats>(0);
+    reg.exportColumn<Spawn, SpawnInfo>(1);      // packed spawn rows (a growable table's export)
 }
 
 void World::setupTasks(TaskGraph::Builder &builder, const Config &)

@@ -16,7 +16,7 @@ struct Init {
     int32_t worldIndex;
 };
 
-// exported singleton (slot 0)
+// exported singleton (slot 0); slot 1: the Spawn table's SpawnInfo column
 struct Stats {
     int32_t tick;
     int32_t numPairs;
