@@ -497,6 +497,7 @@ def main():
     for _ in range(args.steps):
         step()
     sim.sync()
+    own_elapsed = time.perf_counter() - t0      # this rank's own steps (before the barrier)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -562,6 +563,28 @@ def main():
             # reads that LDS / L2 serve, so this rate is the HBM-true one
             roofline["frac_pmc"] = round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
             roofline["model_over_pmc"] = round(nbytes / traffic, 3)
+
+    # N > 1: every rank's own step time, error flags and dominant-kernel time
+    # (a shard imbalance or a failing shard shows here, not only in the max)
+    ranks = None
+    if dist is not None:
+        mine = torch.tensor([own_elapsed, float(flags), roofline["ms_per_launch"] if roofline else -1.0],
+                            dtype=torch.float64)
+        got = [torch.zeros_like(mine) for _ in range(world_size)]
+        dist.all_gather(got, mine)
+        per = []
+        for r, (el, fl, dms) in enumerate(x.tolist() for x in got):
+            e = {"rank": r, "worlds": W, "ms_per_step": round(el / args.steps * 1e3, 4),
+                 "value": round(W * args.steps / el, 1), "error_flags": int(fl)}
+            if dms >= 0:
+                e["dominant_ms_per_launch"] = round(dms, 4)
+            per.append(e)
+        mss = [e["ms_per_step"] for e in per]
+        ranks = {"per_rank": per,
+                 "ms_per_step": {"min": min(mss), "max": max(mss), "mean": round(sum(mss) / len(mss), 4)},
+                 "imbalance": round(max(mss) / min(mss), 4) if min(mss) > 0 else None}
+        for e in per:
+            flags |= e["error_flags"]
 
     assert bool(torch.isfinite(returns).all()), "non-finite returns in the hand-off tensor"
     sim.close()
@@ -629,6 +652,7 @@ def main():
             "reference_definition": ref_def,
             "error_flags": flags,
             "nodes": node_table,
+            **({"ranks": ranks} if ranks else {}),
             "startup": startup,
         }
         if cpu_backend:

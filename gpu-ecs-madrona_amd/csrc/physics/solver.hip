@@ -642,7 +642,7 @@ struct SolverBlockLDS {
     uint32_t *items;
     int32_t *bucketOff;   // [(Lmax + 2) * kNumKinds]
     int32_t *bucketCur;
-    int32_t *scalars;     // [1] max items, [2] max level
+    int32_t *scalars;     // [1] max items, [2] max level, [3] max level (global records)
 };
 
 __device__ __forceinline__ SolverLDS solverWorldLDS(char *smem, int32_t nb, int32_t wi)
@@ -1160,39 +1160,6 @@ __device__ __forceinline__ void solveItemVelocities(const PhysArgs &P, int32_t w
     }
 }
 
-// Fallback for a world whose items do not fit the LDS records: the whole
-// solve on its own wave, records in the global slab, level by level.
-__device__ __forceinline__ void solveWorldGlobal(const PhysArgs &P, int32_t w, SolverLDS L,
-                                                 int32_t J, int32_t lane)
-{
-    CRec *recs = (CRec *)(P.solverRecs + (size_t)w * P.recStride);
-    int32_t *prevs = P.solverPrevs + (size_t)w * P.recStride;
-    const int32_t K = gatherContacts(P, w, recs, INT32_MAX, lane);
-    appendJoints(P, w, recs, K, J, lane);
-    waveSync();
-    const int32_t N = K + J;
-    const int32_t max_level = scheduleLevels(L, N, recs, prevs, lane);
-    const SolverData &sd = P.solver[w];
-    for (int32_t l = 1; l <= max_level; l++) {
-        for (int32_t k = lane; k < N; k += kSolverBlock) {
-            const CRec r = recs[k];
-            if (r.lvl != l) continue;
-            solveItemPositions(P, w, L, r, itemKind(L, r));
-        }
-        waveSync();
-    }
-    setWorldVelocities(P, w, L, sd.h, lane);
-    waveSync();
-    for (int32_t l = 1; l <= max_level; l++) {
-        for (int32_t k = lane; k < K; k += kSolverBlock) {   // joints sort last
-            const CRec r = recs[k];
-            if (r.lvl != l) continue;
-            solveItemVelocities(P, w, L, r, itemKind(L, r));
-        }
-        waveSync();
-    }
-}
-
 // Phase profile (experiments only, -DMW_SOLVER_PROFILE): per-phase sums of
 // block time in 10 ns device-clock ticks, read by mw_debug_solver_phases.
 #if defined(MW_SOLVER_PROFILE)
@@ -1259,7 +1226,7 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     long long prof_t = wall_clock64();
     if (threadIdx.x == 0 && blockIdx.x < 16384) g_solverBlockT[2 * blockIdx.x] = (unsigned long long)prof_t;
 #endif
-    if (threadIdx.x == 0) { BL.scalars[1] = 0; BL.scalars[2] = 0; }
+    if (threadIdx.x == 0) { BL.scalars[1] = 0; BL.scalars[2] = 0; BL.scalars[3] = 0; }
     int32_t K = 0, J = 0;
     if (live) {
         loadWorldBodies(P, w, L, lane);
@@ -1275,10 +1242,12 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
 
     // Levels of the world's items (contacts, then joints) in LDS, unless the
     // items overflow the LDS records or the levels the bucket table holds:
-    // then every world of the block solves on its own wave from the global
-    // records (same bits).  One call site for that path (a second inlined
-    // copy sent the kernel arguments to scratch).
-    const int32_t N = K + J;
+    // then every world of the block takes the global records -- its items
+    // gathered and levelled again in its slab, each wave solving its own
+    // world level by level (same bits).  Both paths share the solve loops
+    // below, so the solves are inlined once (a second inlined copy had cost
+    // 20 VGPRs and 40 % of the kernel's code).
+    int32_t N = K + J;
     int32_t max_level = 0;
     if (fits) {
         int32_t my_levels = 0;
@@ -1293,63 +1262,94 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     }
     MW_SOLVER_MARK(1);
     MW_SOLVER_CUT(2);
-    if (!fits || max_level > MW_SOLVER_MAX_LEVELS) {
+    const bool global = !fits || max_level > MW_SOLVER_MAX_LEVELS;
+    CRec *grecs = (CRec *)(P.solverRecs + (size_t)w * P.recStride);
+    if (global) {
+        int32_t my_levels = 0;
+        N = 0;
         if (live) {
             if (fits) {                       // scheduled once already: afresh
                 for (int32_t b = lane; b < nb; b += kSolverBlock) L.lastItem[b] = -1;
                 waveSync();
             }
-            solveWorldGlobal(P, w, L, J, lane);
-            writeWorldBodies(P, w, L, lane, integrate_next != 0);
+            K = gatherContacts(P, w, grecs, INT32_MAX, lane);
+            appendJoints(P, w, grecs, K, J, lane);
+            waveSync();
+            N = K + J;
+            my_levels = scheduleLevels(L, N, grecs, P.solverPrevs + (size_t)w * P.recStride, lane);
         }
-        return;
-    }
-
-    // counting sort of the block's items by (level, kind)
-    const int32_t nbk = (max_level + 2) * kNumKinds;
-    for (int32_t i = threadIdx.x; i < nbk; i += kSolverThreads) {
-        BL.bucketOff[i] = 0;
-        BL.bucketCur[i] = 0;
-    }
-    __syncthreads();
-    if (live) {
-        for (int32_t k = lane; k < N; k += kSolverBlock) {
-            const CRec r = L.recs[k];
-            atomicAdd(&BL.bucketOff[r.lvl * kNumKinds + itemKind(L, r)], 1);
+        if (live && lane == 0) atomicMax(&BL.scalars[3], my_levels);
+        __syncthreads();
+        max_level = BL.scalars[3];
+    } else {
+        // counting sort of the block's items by (level, kind)
+        const int32_t nbk = (max_level + 2) * kNumKinds;
+        for (int32_t i = threadIdx.x; i < nbk; i += kSolverThreads) {
+            BL.bucketOff[i] = 0;
+            BL.bucketCur[i] = 0;
         }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int32_t run = 0;
-        for (int32_t b = 0; b < nbk; b++) {
-            const int32_t c = BL.bucketOff[b];
-            BL.bucketOff[b] = run;
-            run += c;
+        __syncthreads();
+        if (live) {
+            for (int32_t k = lane; k < N; k += kSolverBlock) {
+                const CRec r = L.recs[k];
+                atomicAdd(&BL.bucketOff[r.lvl * kNumKinds + itemKind(L, r)], 1);
+            }
         }
-    }
-    __syncthreads();
-    if (live) {
-        for (int32_t k = lane; k < N; k += kSolverBlock) {
-            const CRec r = L.recs[k];
-            const int32_t kind = itemKind(L, r);
-            const int32_t b = r.lvl * kNumKinds + kind;
-            const int32_t pos = BL.bucketOff[b] + atomicAdd(&BL.bucketCur[b], 1);
-            BL.items[pos] = ((uint32_t)wi << 16) | ((uint32_t)kind << 12) | (uint32_t)k;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int32_t run = 0;
+            for (int32_t b = 0; b < nbk; b++) {
+                const int32_t c = BL.bucketOff[b];
+                BL.bucketOff[b] = run;
+                run += c;
+            }
         }
+        __syncthreads();
+        if (live) {
+            for (int32_t k = lane; k < N; k += kSolverBlock) {
+                const CRec r = L.recs[k];
+                const int32_t kind = itemKind(L, r);
+                const int32_t b = r.lvl * kNumKinds + kind;
+                const int32_t pos = BL.bucketOff[b] + atomicAdd(&BL.bucketCur[b], 1);
+                BL.items[pos] = ((uint32_t)wi << 16) | ((uint32_t)kind << 12) | (uint32_t)k;
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
     MW_SOLVER_MARK(2);
     MW_SOLVER_CUT(3);
 
-    // solvePositions, level by level over the whole block
+    // The items of level l: the block's (level, kind)-sorted run, or
+    // (global) this wave's world's records at level l.
+    struct LevelItem {
+        int32_t iw, kind;
+        CRec r;
+    };
+    auto levelItem = [&](int32_t l, int32_t t, LevelItem &it) -> bool {
+        if (global) {
+            it.r = grecs[t];
+            if (it.r.lvl != l) return false;
+            it.iw = wi;
+            it.kind = itemKind(L, it.r);
+        } else {
+            const uint32_t e = BL.items[t];
+            it.iw = (int32_t)(e >> 16);
+            it.kind = (int32_t)((e >> 12) & 0xfu);
+            it.r = solverWorldLDS(smem, nb, it.iw).recs[e & 0xfffu];
+        }
+        return true;
+    };
+    const int32_t stride = global ? kSolverBlock : kSolverThreads;
+
+    // solvePositions, level by level
     for (int32_t l = 1; l <= max_level; l++) {
-        const int32_t beg = BL.bucketOff[l * kNumKinds], end = BL.bucketOff[(l + 1) * kNumKinds];
-        for (int32_t t = beg + threadIdx.x; t < end; t += kSolverThreads) {
-            const uint32_t it = BL.items[t];
-            const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xfffu);
-            const int32_t ww = s_worlds[iw];
-            SolverLDS LW = solverWorldLDS(smem, nb, iw);
-            solveItemPositions(P, ww, LW, LW.recs[k], (int32_t)((it >> 12) & 0xfu));
+        int32_t t = global ? lane : BL.bucketOff[l * kNumKinds] + threadIdx.x;
+        const int32_t end = global ? N : BL.bucketOff[(l + 1) * kNumKinds];
+        for (; t < end; t += stride) {
+            LevelItem it;
+            if (!levelItem(l, t, it)) continue;
+            SolverLDS LW = solverWorldLDS(smem, nb, it.iw);
+            solveItemPositions(P, s_worlds[it.iw], LW, it.r, it.kind);
         }
         __syncthreads();
     }
@@ -1361,15 +1361,16 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     MW_SOLVER_MARK(4);
     MW_SOLVER_CUT(5);
 
-    // solveVelocities, same schedule
+    // solveVelocities, same schedule (joints: positions only; in the global
+    // records they sort last, k >= K)
     for (int32_t l = 1; l <= max_level; l++) {
-        const int32_t beg = BL.bucketOff[l * kNumKinds], end = BL.bucketOff[(l + 1) * kNumKinds];
-        for (int32_t t = beg + threadIdx.x; t < end; t += kSolverThreads) {
-            const uint32_t it = BL.items[t];
-            const int32_t iw = (int32_t)(it >> 16), k = (int32_t)(it & 0xfffu);
-            const int32_t ww = s_worlds[iw];
-            SolverLDS LW = solverWorldLDS(smem, nb, iw);
-            solveItemVelocities(P, ww, LW, LW.recs[k], (int32_t)((it >> 12) & 0xfu));
+        int32_t t = global ? lane : BL.bucketOff[l * kNumKinds] + threadIdx.x;
+        const int32_t end = global ? K : BL.bucketOff[(l + 1) * kNumKinds];
+        for (; t < end; t += stride) {
+            LevelItem it;
+            if (!levelItem(l, t, it)) continue;
+            SolverLDS LW = solverWorldLDS(smem, nb, it.iw);
+            solveItemVelocities(P, s_worlds[it.iw], LW, it.r, it.kind);
         }
         __syncthreads();
     }

@@ -5,7 +5,9 @@
 
 Writes tests/golden/collisions_ref.npz: inputs (init positions / rotations,
 config) and the reference's outputs (per-body state after selected steps, the
-BVH after step 1, the last substep's contact prefix).  These pin both the C++
+BVH after step 1, the last substep's contacts: the reference's own count of
+them (numContacts right after that narrowphase node) and exactly those rows).
+These pin both the C++
 restatement (oracle/) and, through it, the HIP path.
 
 Also writes tests/golden/collisions_window_ref.npz: the bench's own window.
@@ -74,7 +76,7 @@ def make_window():
 def main():
     cfg = default_phys_config(num_cubes=128, num_substeps=4, max_contacts=1024)
     pos, rot = gen_collisions_inits(NUM_WORLDS, 128, seed=0)
-    ref = ReferencePhys(cfg, pos, rot)
+    ref = ReferencePhys(cfg, pos, rot, log_candidates=True)
     out = {
         "init_pos": pos, "init_rot": rot,
         "cfg": np.array([cfg.numCubes, cfg.numSubsteps, cfg.maxContacts], np.int32),
@@ -98,7 +100,10 @@ def main():
             for w in range(NUM_WORLDS):
                 raw = ref.contacts_raw(w)
                 n = int((raw["ref"][:, 0] != 0xFFFFFFFF).sum())
-                out[f"contacts_{step}_{w}"] = raw[:n].view(np.uint8).reshape(n, -1)
+                count = ref.last_contact_count(w)
+                assert count <= n, (step, w, count, n)
+                out[f"contacts_{step}_{w}"] = raw[:count].view(np.uint8).reshape(count, -1)
+                out[f"contact_count_{step}_{w}"] = np.int32(count)
     path = os.path.join(HERE, "collisions_ref.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")

@@ -82,3 +82,27 @@ def test_two_rank_cpu_rehearsal_prints_one_line():
     assert out["n_gpus"] == 2 and out["config"]["total_worlds"] == 6
     assert out["error_flags"] == 0 and out["value"] > 0
     assert out["reference_definition"] is None and out["cpu_baseline"] is None
+    assert len(out["ranks"]["per_rank"]) == 2
+
+
+@pytest.mark.timeout(900)
+def test_eight_rank_cpu_rehearsal_reports_every_rank():
+    """the N > 1 line carries each rank's step time and error
+    flags (min / max / mean beside the max-over-ranks value); N = 1 lines
+    have no such field."""
+    r = _run(["--gpus", "8", "--backend", "cpu", "--worlds", "2", "--cubes", "8",
+              "--steps", "2", "--warmup", "1", "--settle", "2", "--cpu-threads", "1"], timeout=840)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = lines[0]
+    assert out["n_gpus"] == 8 and out["config"]["total_worlds"] == 16
+    per = out["ranks"]["per_rank"]
+    assert [e["rank"] for e in per] == list(range(8))
+    assert all(e["worlds"] == 2 and e["ms_per_step"] > 0 and e["error_flags"] == 0 for e in per)
+    mss = [e["ms_per_step"] for e in per]
+    st = out["ranks"]["ms_per_step"]
+    assert st["min"] == min(mss) and st["max"] == max(mss)
+    # each rank's own time ends before the closing barrier, the headline's
+    # (max over ranks) after it
+    assert out["ms_per_step"] >= st["max"] - 1e-3

@@ -67,9 +67,9 @@ def test_oracle_bit_exact_vs_golden_bodies_and_contacts():
             for w in range(W):
                 want_c = g[f"contacts_{step}_{w}"].view(CONTACT_DTYPE).reshape(-1)
                 got_c = orc.contacts(w)
-                # reference prefix = last substep's contacts (longer if an
-                # earlier substep wrote more); ours is exactly the last substep
-                assert len(got_c) <= len(want_c)
+                # the last substep's manifolds, as many as the reference
+                # counted (numContacts after that narrowphase node)
+                assert len(got_c) == int(g[f"contact_count_{step}_{w}"]) == len(want_c), (step, w)
                 for i in range(len(got_c)):
                     assert contacts_equal(got_c[i], want_c[i]), (step, w, i)
 

@@ -41,37 +41,6 @@ def test_large_world_traversal_and_sweep_bit_exact(monkeypatch, dfs_leaves):
     _lockstep(sim, orc, W, 8)
 
 
-def _overlap_ms(monkeypatch, dfs_leaves, W, n, steps=6):
-    monkeypatch.setenv("MADRONA_MW_OVERLAP_DFS_LEAVES", dfs_leaves)
-    import madrona_mi355x as mw
-    pos, rot = _grid_world(W, n)
-    g = mw.default_collisions_config(n, 4, 8192, 8192)
-    sim = mw.CollisionsSim(W, pos, rot, g)
-    sim.step(2)
-    sim.set_timed_node("FindOverlappingNode")
-    sim.step(steps)
-    ms, launches = sim.timed_node()
-    sim.set_timed_node(None)
-    assert sim.error_flags() == 0 and launches > 0
-    return ms / launches
-
-
-def test_traversal_cost_is_subquadratic(monkeypatch):
-    """Per launch, 4x the bodies costs the traversal well under the 16x a
-    bodies x leaves sweep pays (measured 8x: the reference's tree over the
-    3200-cube grid is deeper, about 94 nodes per query against 23), and at
-    3200 bodies the traversal beats the sweep (measured 4x).  64 worlds, so
-    this is one block's latency, not throughput."""
-    W = 64
-    small = _overlap_ms(monkeypatch, "0", W, 800)
-    big = _overlap_ms(monkeypatch, "0", W, 3200)
-    sweep = _overlap_ms(monkeypatch, "-1", W, 3200)
-    print(f"findOverlaps per launch: dfs 800 {small:.4f} ms, dfs 3200 {big:.4f} ms, "
-          f"sweep 3200 {sweep:.4f} ms")
-    assert big < 12 * small, (small, big)
-    assert big * 2.5 < sweep, (big, sweep)
-
-
 def test_world_past_16bit_indices_refused():
     """Leaf ranks (findOverlaps) and body slots (solver records) are 16-bit:
     a world past those limits is refused at creation with the limit named,
