@@ -23,6 +23,29 @@ struct SMut {
 };
 static_assert(sizeof(SMut) == 56);
 
+// The pre-solve state of a body (PreSolvePositional, PreSolveVelocity),
+// staged in the world's LDS image by the bodies' coalesced load: the
+// contact solves read it from LDS instead of two uncoalesced column loads
+// per body side and item.  PreSolvePositional is the pose the integration
+// has just written to Position / Rotation as well (integrateApply), so it
+// comes with the pose; PreSolveVelocity (the integrated velocity, which the
+// Velocity column does not hold) is loaded with the row.
+// Off by default (MW_SOLVER_PRE_LDS=1 turns it on): the 52 B per body
+// cost residency -- 13 -> 9 worlds per CU on collisions, SolverNode 0.224
+// -> 0.269 ms per launch; the warm-up below is the cheaper way to the same
+// loads.
+#ifndef MW_SOLVER_PRE_LDS
+#define MW_SOLVER_PRE_LDS 0
+#endif
+struct SPre {
+    Vector3 x;
+    Quat q;
+    Vector3 v;
+    Vector3 omega;
+};
+static_assert(sizeof(SPre) == 52);
+constexpr int32_t kPreBytes = MW_SOLVER_PRE_LDS ? (int32_t)sizeof(SPre) : 0;
+
 __device__ __forceinline__ bool isStaticBody(uint32_t meta)
 {
     return (meta & 0xffu) == (uint32_t)ResponseType::Static;
@@ -112,13 +135,39 @@ struct VelIn {
 // skip1 / skip2: the side's per-substep columns are not read (an invariant
 // static body the solve skips); the general solve of such an item reloads
 // them (loadPosIn with both false).
-__device__ __forceinline__ PosIn loadPosIn(const PhysArgs &P, int32_t w, const SMut &b1, int32_t s1,
-                                           const SMut &b2, int32_t s2, bool skip1, bool skip2)
+__device__ __forceinline__ solver::PreSolvePositional prePos(const PhysArgs &P, const SPre *pre, int32_t w,
+                                                            int32_t s, const BodyRO &o)
+{
+#if MW_SOLVER_PRE_LDS
+    (void)P; (void)w; (void)o;
+    const float *f = (const float *)(pre + s);
+    return solver::PreSolvePositional { Vector3 { f[0], f[1], f[2] }, Quat { f[3], f[4], f[5], f[6] } };
+#else
+    (void)pre; (void)s;
+    return bcol<solver::PreSolvePositional>(P.body[o.arch], Cols::PreSolvePositional, w, o.row);
+#endif
+}
+
+__device__ __forceinline__ solver::PreSolveVelocity preVel(const PhysArgs &P, const SPre *pre, int32_t w,
+                                                         int32_t s, const BodyRO &o)
+{
+#if MW_SOLVER_PRE_LDS
+    (void)P; (void)w; (void)o;
+    const float *f = (const float *)(pre + s) + 7;
+    return solver::PreSolveVelocity { Vector3 { f[0], f[1], f[2] }, Vector3 { f[3], f[4], f[5] } };
+#else
+    (void)pre; (void)s;
+    return bcol<solver::PreSolveVelocity>(P.body[o.arch], Cols::PreSolveVelocity, w, o.row);
+#endif
+}
+
+__device__ __forceinline__ PosIn loadPosIn(const PhysArgs &P, int32_t w, const SPre *pre, const SMut &b1,
+                                           int32_t s1, const SMut &b2, int32_t s2, bool skip1, bool skip2)
 {
     const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
     PosIn in;
-    in.ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
-    in.ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
+    in.ps1 = prePos(P, pre, w, s1, o1);
+    in.ps2 = prePos(P, pre, w, s2, o2);
     in.pv1 = {};
     in.pv2 = {};
     if (!skip1) in.pv1 = bcol<solver::SubstepPrevState>(P.body[o1.arch], Cols::SubstepPrevState, w, o1.row);
@@ -128,8 +177,8 @@ __device__ __forceinline__ PosIn loadPosIn(const PhysArgs &P, int32_t w, const S
     return in;
 }
 
-__device__ __forceinline__ VelIn loadVelIn(const PhysArgs &P, int32_t w, const SMut &b1, int32_t s1,
-                                           const SMut &b2, int32_t s2, bool skip1, bool skip2)
+__device__ __forceinline__ VelIn loadVelIn(const PhysArgs &P, int32_t w, const SPre *pre, const SMut &b1,
+                                           int32_t s1, const SMut &b2, int32_t s2, bool skip1, bool skip2)
 {
     const BodyRO o1 = bodyRO(P, s1, b1.meta), o2 = bodyRO(P, s2, b2.meta);
     VelIn in;
@@ -138,12 +187,12 @@ __device__ __forceinline__ VelIn loadVelIn(const PhysArgs &P, int32_t w, const S
     in.pv1 = {};
     in.pv2 = {};
     if (!skip1) {
-        in.ps1 = bcol<solver::PreSolvePositional>(P.body[o1.arch], Cols::PreSolvePositional, w, o1.row);
-        in.pv1 = bcol<solver::PreSolveVelocity>(P.body[o1.arch], Cols::PreSolveVelocity, w, o1.row);
+        in.ps1 = prePos(P, pre, w, s1, o1);
+        in.pv1 = preVel(P, pre, w, s1, o1);
     }
     if (!skip2) {
-        in.ps2 = bcol<solver::PreSolvePositional>(P.body[o2.arch], Cols::PreSolvePositional, w, o2.row);
-        in.pv2 = bcol<solver::PreSolveVelocity>(P.body[o2.arch], Cols::PreSolveVelocity, w, o2.row);
+        in.ps2 = prePos(P, pre, w, s2, o2);
+        in.pv2 = preVel(P, pre, w, s2, o2);
     }
     in.m1 = P.objs.metadata[o1.obj];
     in.m2 = P.objs.metadata[o2.obj];
@@ -574,6 +623,39 @@ __device__ __forceinline__ bool staticInvariant(const SMut &b, Vector3 prev_x, Q
            sameBits(nq.z, b.q.z);
 }
 
+// Body states in the world's LDS image (SolverLDS::state, one int16 per
+// body slot): an ordinary body holds the latest item of the earlier chunks
+// touching it while the levels are scheduled (-1: none); an invariant static
+// body takes no ordering edges (kStateStatic); kStateStaticSkip also makes
+// every per-body phase an exact no-op for it -- its Velocity column is +0
+// (what setVelocities derives from an unchanged pose, and what the
+// write-back stores), its pre-solve pose equals its pose (the fused
+// integration's static branch rewrites pose, previous and pre-solve state
+// with the same values) and its BodyBox in P.bodyBoxes is current (computed
+// from the same pose and scale by the last integration: integrateKernel
+// each step, then each substep's tail) -- so setVelocities, the write-back
+// and the next substep's integration skip it, and the filter's LDS box image
+// takes its box from P.bodyBoxes.  collisions: the ground plane, alone in
+// the third row batch of every world, which then issues no work.  A
+// general solve that may write such a body (a joint, or the fallback of a
+// non-finite skipping solve, flagged kErrStaticSchedule) marks it
+// kStateStaticWritten: still without ordering edges, but the per-body
+// phases treat it as any body.
+constexpr int16_t kStateStatic = -3;
+constexpr int16_t kStateStaticSkip = -4;
+constexpr int16_t kStateStaticWritten = -5;
+__device__ __forceinline__ bool invariantState(int16_t v) { return v <= kStateStatic; }
+
+__device__ __forceinline__ bool staticSkippable(const SMut &b, Vector3 ps_x, Quat ps_q)
+{
+    const uint32_t vbits = __float_as_uint(b.v.x) | __float_as_uint(b.v.y) | __float_as_uint(b.v.z) |
+                           __float_as_uint(b.omega.x) | __float_as_uint(b.omega.y) |
+                           __float_as_uint(b.omega.z);
+    return vbits == 0 && sameBits(ps_x.x, b.x.x) && sameBits(ps_x.y, b.x.y) && sameBits(ps_x.z, b.x.z) &&
+           sameBits(ps_q.w, b.q.w) && sameBits(ps_q.x, b.q.x) && sameBits(ps_q.y, b.q.y) &&
+           sameBits(ps_q.z, b.q.z);
+}
+
 // Per-item solver record: body slots of ref / alt (e1 / e2 for a joint)
 // and the item's level (1 + max level of earlier items sharing a
 // non-invariant body).  Items are the world's contacts followed by its
@@ -601,9 +683,10 @@ enum : int32_t { kKindStaticRef = 0, kKindStaticAlt = 1, kKindGeneral = 2, kNumK
 // Per-world LDS image: bodies, ordering state, contact records.
 struct SolverLDS {
     SMut *bodies;         // [nb]
+    SPre *pre;            // [nb] pre-solve state (MW_SOLVER_PRE_LDS)
     uint64_t *touch;      // [nb] lanes of the current 64-item chunk touching the body
-    int16_t *flag;        // [nb] -1: invariant static body (no ordering edges), else 0
-    int16_t *lastItem;    // [nb] latest item of the earlier chunks touching the body
+    int16_t *state;       // [nb] ordinary body: latest item of the earlier chunks touching it
+                          // (-1: none); invariant static body: kStateStatic* (<= -3)
     CRec *recs;           // [kSolverLDSContacts]
     int32_t *prevs;       // [kSolverLDSContacts] (prev item on s1, on s2) as 2 x int16
 };
@@ -612,8 +695,8 @@ __host__ __device__ inline size_t solverA16(size_t b) { return (b + 15) & ~size_
 
 __host__ __device__ inline size_t solverWorldLDSBytes(int32_t nb)
 {
-    return solverA16(sizeof(SMut) * nb) + solverA16(sizeof(uint64_t) * nb) +
-           2 * solverA16(sizeof(int16_t) * nb) +
+    return solverA16(sizeof(SMut) * nb) + solverA16((size_t)kPreBytes * nb) + solverA16(sizeof(uint64_t) * nb) +
+           solverA16(sizeof(int16_t) * nb) +
            (sizeof(CRec) + sizeof(int32_t)) * kSolverLDSContacts;
 }
 
@@ -630,18 +713,33 @@ constexpr int32_t kSolverItems = kSolverWorlds * kSolverLDSContacts;
 #endif
 constexpr int32_t kSolverBuckets = kNumKinds * (MW_SOLVER_MAX_LEVELS + 2);
 
+// The block schedule: items (world << 16 | kind << 12 | k) and the bucket
+// offsets of the counting sort, then four block scalars.
+__host__ __device__ inline size_t solverScheduleBytes()
+{
+    return sizeof(uint32_t) * kSolverItems + sizeof(int32_t) * kSolverBuckets;
+}
+
+// With one world per block the schedule needs no LDS of its own: the world's
+// touch masks (bucket offsets) and predecessor records (items) are dead once
+// its levels are scheduled, and the sort comes after (touch is zeroed again
+// by the next launch's body load).  That keeps a collisions world at 10.1 KB
+// of LDS (16 blocks per CU) instead of 12.1 KB (13).
+__host__ __device__ inline bool solverAliasSchedule(int32_t nb)
+{
+    return kSolverWorlds == 1 && solverA16(sizeof(uint64_t) * nb) >= sizeof(int32_t) * kSolverBuckets &&
+           sizeof(int32_t) * kSolverLDSContacts >= sizeof(uint32_t) * kSolverItems;
+}
+
 __host__ __device__ inline size_t solverBlockLDSBytes(int32_t nb)
 {
-    return kSolverWorlds * solverWorldLDSBytes(nb) +
-           sizeof(uint32_t) * kSolverItems +               // items (world << 16 | kind << 12 | k)
-           sizeof(int32_t) * 2 * kSolverBuckets +          // bucket offsets / cursors
+    return kSolverWorlds * solverWorldLDSBytes(nb) + (solverAliasSchedule(nb) ? 0 : solverScheduleBytes()) +
            sizeof(int32_t) * 4;                            // block scalars
 }
 
 struct SolverBlockLDS {
     uint32_t *items;
-    int32_t *bucketOff;   // [(Lmax + 2) * kNumKinds]
-    int32_t *bucketCur;
+    int32_t *bucketOff;   // [(Lmax + 2) * kNumKinds]; after the sort bucketOff[b] = end of bucket b
     int32_t *scalars;     // [1] max items, [2] max level, [3] max level (global records)
 };
 
@@ -651,11 +749,11 @@ __device__ __forceinline__ SolverLDS solverWorldLDS(char *smem, int32_t nb, int3
     char *p = smem + (size_t)wi * solverWorldLDSBytes(nb);
     L.bodies = (SMut *)p;
     p += solverA16(sizeof(SMut) * nb);
+    L.pre = (SPre *)p;
+    p += solverA16((size_t)kPreBytes * nb);
     L.touch = (uint64_t *)p;
     p += solverA16(sizeof(uint64_t) * nb);
-    L.flag = (int16_t *)p;
-    p += solverA16(sizeof(int16_t) * nb);
-    L.lastItem = (int16_t *)p;
+    L.state = (int16_t *)p;
     p += solverA16(sizeof(int16_t) * nb);
     L.recs = (CRec *)p;
     p += sizeof(CRec) * kSolverLDSContacts;
@@ -664,16 +762,20 @@ __device__ __forceinline__ SolverLDS solverWorldLDS(char *smem, int32_t nb, int3
 }
 
 // p: the block schedule's LDS (after the world images, or all of the
-// dynamic LDS when the images are global)
-__device__ __forceinline__ SolverBlockLDS solverBlockLDS(char *p)
+// dynamic LDS when the images are global); alias: in world 0's dead arrays
+// (solverAliasSchedule)
+__device__ __forceinline__ SolverBlockLDS solverBlockLDS(char *p, const SolverLDS *alias)
 {
     SolverBlockLDS B;
-    B.items = (uint32_t *)p;
-    p += sizeof(uint32_t) * kSolverItems;
-    B.bucketOff = (int32_t *)p;
-    p += sizeof(int32_t) * kSolverBuckets;
-    B.bucketCur = (int32_t *)p;
-    p += sizeof(int32_t) * kSolverBuckets;
+    if (alias) {
+        B.items = (uint32_t *)alias->prevs;
+        B.bucketOff = (int32_t *)alias->touch;
+    } else {
+        B.items = (uint32_t *)p;
+        p += sizeof(uint32_t) * kSolverItems;
+        B.bucketOff = (int32_t *)p;
+        p += sizeof(int32_t) * kSolverBuckets;
+    }
     B.scalars = (int32_t *)p;
     return B;
 }
@@ -721,6 +823,21 @@ constexpr int32_t kRowBatch = 3;
 #endif
 constexpr int32_t kWriteBatch = MW_SOLVER_WRITE_BATCH;
 
+// Cache warming (MW_SOLVER_WARM, default on).  The contacts and the
+// bodies' substep columns the level passes read per item were written by
+// other kernels (narrowphase, the last substep's tail), usually on another
+// XCD, so their first reads miss L2; and a level pass issues its items'
+// loads only when it starts, one pass after the other.  So the world's
+// load touches one dword of every line those reads will need -- the
+// substep columns of every body with its coalesced row loads (no extra
+// round trip), every contact's two lines once the contacts are gathered --
+// and the values are consumed (nothing computed) only when the level passes
+// begin: the lines are in L2 by then.
+#ifndef MW_SOLVER_WARM
+#define MW_SOLVER_WARM 1
+#endif
+__device__ __forceinline__ void keepLoaded(uint32_t v) { asm volatile("" ::"v"(v)); }
+
 // Load one world's bodies into its LDS image (wave `lane` 0..63) and reset
 // its ordering state.
 __device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, SolverLDS &L,
@@ -731,10 +848,27 @@ __device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, So
         const int32_t rows = B.numRows[w];
         for (int32_t r0 = 0; r0 < rows; r0 += kSolverBlock * kRowBatch) {
             SMut s[kRowBatch];
+#if MW_SOLVER_PRE_LDS
+            Vector3 pv[kRowBatch], pw[kRowBatch];
+#endif
+#if MW_SOLVER_WARM
+            uint32_t warm[kRowBatch];
+#endif
 #pragma unroll
             for (int32_t j = 0; j < kRowBatch; j++) {
                 const int32_t r = r0 + j * kSolverBlock + lane;
                 if (r >= rows) continue;
+#if MW_SOLVER_WARM
+                // a row of 24-28 B starts in every 128-B line of the columns
+                warm[j] = *(const uint32_t *)&bcol<solver::PreSolvePositional>(B, Cols::PreSolvePositional, w, r) ^
+                          *(const uint32_t *)&bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r) ^
+                          *(const uint32_t *)&bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
+#endif
+#if MW_SOLVER_PRE_LDS
+                const auto &psv = bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
+                pv[j] = ldV3(&psv.v);
+                pw[j] = ldV3(&psv.omega);
+#endif
                 s[j].x = ldV3(&bcol<Vector3>(B, Cols::Position, w, r));
                 s[j].q = ldQ(&bcol<Quat>(B, Cols::Rotation, w, r));
                 const Velocity &vel = bcol<Velocity>(B, Cols::Velocity, w, r);
@@ -748,13 +882,18 @@ __device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, So
             for (int32_t j = 0; j < kRowBatch; j++) {
                 const int32_t r = r0 + j * kSolverBlock + lane;
                 if (r >= rows) continue;
-                bool inv = false;
+                int16_t fl = -1;
                 if ((s[j].meta & 0xffu) == (uint32_t)ResponseType::Static) {
                     const auto &pv = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
                     const auto &psv = bcol<solver::PreSolveVelocity>(B, Cols::PreSolveVelocity, w, r);
-                    inv = staticInvariant(s[j], ldV3(&pv.prevPosition), ldQ(&pv.prevRotation),
-                                          ldV3(&psv.v), ldV3(&psv.omega));
+                    const auto &psp = bcol<solver::PreSolvePositional>(B, Cols::PreSolvePositional, w, r);
+                    if (staticInvariant(s[j], ldV3(&pv.prevPosition), ldQ(&pv.prevRotation),
+                                        ldV3(&psv.v), ldV3(&psv.omega)))
+                        fl = staticSkippable(s[j], ldV3(&psp.x), ldQ(&psp.q)) ? kStateStaticSkip : kStateStatic;
                 }
+#if MW_SOLVER_WARM
+                keepLoaded(warm[j]);
+#endif
                 const int32_t slot = B.slotBase + r;
                 SMut *d = L.bodies + slot;
                 stV3(&d->x, s[j].x);
@@ -762,8 +901,16 @@ __device__ __forceinline__ void loadWorldBodies(const PhysArgs &P, int32_t w, So
                 stV3(&d->v, s[j].v);
                 stV3(&d->omega, s[j].omega);
                 d->meta = s[j].meta;
-                L.flag[slot] = inv ? (int16_t)-1 : (int16_t)0;
-                L.lastItem[slot] = -1;
+#if MW_SOLVER_PRE_LDS
+                {
+                    SPre *e = L.pre + slot;           // PreSolvePositional = the pose
+                    stV3(&e->x, s[j].x);
+                    stQ(&e->q, s[j].q);
+                    stV3(&e->v, pv[j]);
+                    stV3(&e->omega, pw[j]);
+                }
+#endif
+                L.state[slot] = fl;
                 L.touch[slot] = 0;
             }
         }
@@ -888,8 +1035,8 @@ __device__ __forceinline__ int32_t scheduleLevels(SolverLDS &L, int32_t N, RecPt
         const int32_t k = base + lane;
         const bool valid = k < N;
         const CRec r = valid ? recs[k] : CRec { 0, 0, 0, 0 };
-        const bool on1 = valid && L.flag[r.s1] >= 0;
-        const bool on2 = valid && L.flag[r.s2] >= 0 && r.s2 != r.s1;
+        const bool on1 = valid && !invariantState(L.state[r.s1]);
+        const bool on2 = valid && !invariantState(L.state[r.s2]) && r.s2 != r.s1;
         if (on1) atomicOr((unsigned long long *)&L.touch[r.s1], 1ull << lane);
         if (on2) atomicOr((unsigned long long *)&L.touch[r.s2], 1ull << lane);
         waveSync();
@@ -898,17 +1045,17 @@ __device__ __forceinline__ int32_t scheduleLevels(SolverLDS &L, int32_t N, RecPt
         if (on1) {
             m1 = L.touch[r.s1];
             const uint64_t lo = m1 & lt_mask;
-            p1 = lo ? base + 63 - __clzll(lo) : L.lastItem[r.s1];
+            p1 = lo ? base + 63 - __clzll(lo) : L.state[r.s1];
         }
         if (on2) {
             m2 = L.touch[r.s2];
             const uint64_t lo = m2 & lt_mask;
-            p2 = lo ? base + 63 - __clzll(lo) : L.lastItem[r.s2];
+            p2 = lo ? base + 63 - __clzll(lo) : L.state[r.s2];
         }
         waveSync();
         // the chunk's last item on each body becomes the body's latest
-        if (on1 && 63 - __clzll(m1) == lane) L.lastItem[r.s1] = (int16_t)k;
-        if (on2 && 63 - __clzll(m2) == lane) L.lastItem[r.s2] = (int16_t)k;
+        if (on1 && 63 - __clzll(m1) == lane) L.state[r.s1] = (int16_t)k;
+        if (on2 && 63 - __clzll(m2) == lane) L.state[r.s2] = (int16_t)k;
         if (on1) L.touch[r.s1] = 0;
         if (on2) L.touch[r.s2] = 0;
         if (valid) {
@@ -944,10 +1091,15 @@ __device__ __forceinline__ int32_t scheduleLevels(SolverLDS &L, int32_t N, RecPt
 __device__ __forceinline__ int32_t itemKind(const SolverLDS &L, const CRec r)
 {
     if (r.slot < 0) return kKindGeneral;
-    const bool i1 = L.flag[r.s1] < 0, i2 = L.flag[r.s2] < 0;
+    const bool i1 = invariantState(L.state[r.s1]), i2 = invariantState(L.state[r.s2]);
     if (i1 && !i2) return kKindStaticRef;
     if (i2 && !i1) return kKindStaticAlt;
     return kKindGeneral;
+}
+
+__device__ __forceinline__ bool bodySkips(const SolverLDS &L, int32_t slot)
+{
+    return L.state[slot] == kStateStaticSkip;
 }
 
 // setVelocities (physics.cpp:673-714) for one world, one wave.
@@ -960,10 +1112,12 @@ __device__ __forceinline__ void setWorldVelocities(const PhysArgs &P, int32_t w,
         for (int32_t r0 = 0; r0 < rows; r0 += kSolverBlock * kRowBatch) {
             Vector3 px[kRowBatch];
             Quat qp[kRowBatch];
+            bool act[kRowBatch];
 #pragma unroll
             for (int32_t j = 0; j < kRowBatch; j++) {
                 const int32_t r = r0 + j * kSolverBlock + lane;
-                if (r >= rows) continue;
+                act[j] = r < rows && !bodySkips(L, B.slotBase + r);
+                if (!act[j]) continue;
                 const auto &prev = bcol<solver::SubstepPrevState>(B, Cols::SubstepPrevState, w, r);
                 px[j] = ldV3(&prev.prevPosition);
                 qp[j] = ldQ(&prev.prevRotation);
@@ -971,7 +1125,7 @@ __device__ __forceinline__ void setWorldVelocities(const PhysArgs &P, int32_t w,
 #pragma unroll
             for (int32_t j = 0; j < kRowBatch; j++) {
                 const int32_t r = r0 + j * kSolverBlock + lane;
-                if (r >= rows) continue;
+                if (!act[j]) continue;
                 SMut *s = L.bodies + B.slotBase + r;
                 const Vector3 x = ldV3(&s->x);
                 const Quat q = ldQ(&s->q);
@@ -1009,23 +1163,37 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
         for (int32_t r0 = 0; r0 < rows; r0 += kSolverBlock * kWriteBatch) {
             IntegrateIn in[kWriteBatch];
             IntegrateObj od[kWriteBatch];
+            BodyBox kept[kWriteBatch];            // a skipped static body's current box
+            bool skip[kWriteBatch];
+#pragma unroll
+            for (int32_t j = 0; j < kWriteBatch; j++) {
+                const int32_t r = r0 + j * kSolverBlock + lane;
+                skip[j] = r < rows && bodySkips(L, B.slotBase + r);
+            }
             if (integrate_next) {
 #pragma unroll
                 for (int32_t j = 0; j < kWriteBatch; j++) {
                     const int32_t r = r0 + j * kSolverBlock + lane;
-                    if (r < rows) in[j] = integrateLoad(B, w, r);
+                    if (r < rows && !skip[j]) in[j] = integrateLoad(B, w, r);
+                    if (skip[j]) kept[j] = P.bodyBoxes[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r];
                 }
 #pragma unroll
                 for (int32_t j = 0; j < kWriteBatch; j++) {
                     const int32_t r = r0 + j * kSolverBlock + lane;
-                    if (r < rows) od[j] = integrateObj(P, in[j].obj);
+                    if (r < rows && !skip[j]) od[j] = integrateObj(P, in[j].obj);
                 }
             }
 #pragma unroll
             for (int32_t j = 0; j < kWriteBatch; j++) {
                 const int32_t r = r0 + j * kSolverBlock + lane;
-                const bool live = r < rows;
-                if (live) {
+                const bool live = r < rows && !skip[j];
+                if (skip[j]) {
+                    // every write of this body would store the value it holds
+                    if (integrate_next) {
+                        waveSync();                       // the round's SMut reads first
+                        boxes[B.slotBase + r] = kept[j];
+                    }
+                } else if (live) {
                     const SMut *s = L.bodies + B.slotBase + r;
                     const Vector3 x = ldV3(&s->x), v = ldV3(&s->v), om = ldV3(&s->omega);
                     const Quat q = ldQ(&s->q);
@@ -1100,6 +1268,15 @@ __device__ __forceinline__ int32_t solveKind(int32_t kind, const ContactIn &c)
 static __device__ int32_t g_solverCut;
 #endif
 
+// A general solve (a joint, a contact of the general kind, or the fallback of
+// a skipping solve) may write an invariant static body it touches: it then
+// takes the per-body phases again (bodySkips).
+__device__ __forceinline__ void markStaticWritten(SolverLDS &L, const CRec r)
+{
+    if (invariantState(L.state[r.s1])) L.state[r.s1] = kStateStaticWritten;
+    if (invariantState(L.state[r.s2])) L.state[r.s2] = kStateStaticWritten;
+}
+
 __device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w, SolverLDS &L,
                                                    const CRec r, int32_t kind)
 {
@@ -1108,7 +1285,7 @@ __device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w,
         SMut &b1 = L.bodies[r.s1], &b2 = L.bodies[r.s2];
         // one round of loads: the manifold and the bodies' columns
         const ContactIn c = loadContact(cr);
-        PosIn in = loadPosIn(P, w, b1, r.s1, b2, r.s2, kind == kKindStaticRef, kind == kKindStaticAlt);
+        PosIn in = loadPosIn(P, w, L.pre, b1, r.s1, b2, r.s2, kind == kKindStaticRef, kind == kKindStaticAlt);
 #if defined(MW_SAT_CUTS)
         if (g_solverCut == 7) {               // every loaded word kept alive, no solve
             float acc = (float)c.np;
@@ -1129,11 +1306,13 @@ __device__ __forceinline__ void solveItemPositions(const PhysArgs &P, int32_t w,
         }
         if (res != kSolveDone) {
             if (k != kKindGeneral) atomicOr(P.errorFlags + w, kErrStaticSchedule);
-            if (kind != kKindGeneral) in = loadPosIn(P, w, b1, r.s1, b2, r.s2, false, false);
+            if (kind != kKindGeneral) in = loadPosIn(P, w, L.pre, b1, r.s1, b2, r.s2, false, false);
+            markStaticWritten(L, r);
             solvePositionsGeneral(b1, b2, c, in, cr.lambdaN);
         }
     } else {
         const JointConstraint &j = P.joints[(size_t)w * P.jointCapacity + (-1 - r.slot)];
+        markStaticWritten(L, r);
         solveJoint(P, L.bodies[r.s1], L.bodies[r.s2], j);
     }
 }
@@ -1144,7 +1323,7 @@ __device__ __forceinline__ void solveItemVelocities(const PhysArgs &P, int32_t w
     if (r.slot < 0) return;                                // joints: positions only
     SMut &b1 = L.bodies[r.s1], &b2 = L.bodies[r.s2];
     const ContactIn c = loadContact(P.candContacts[(size_t)w * P.candCapacity + r.slot]);
-    VelIn in = loadVelIn(P, w, b1, r.s1, b2, r.s2, kind == kKindStaticRef, kind == kKindStaticAlt);
+    VelIn in = loadVelIn(P, w, L.pre, b1, r.s1, b2, r.s2, kind == kKindStaticRef, kind == kKindStaticAlt);
     const SolverData &sd = P.solver[w];
     const int32_t k = solveKind(kind, c);
     int32_t res = kSolveNonFinite;
@@ -1155,7 +1334,8 @@ __device__ __forceinline__ void solveItemVelocities(const PhysArgs &P, int32_t w
     }
     if (res != kSolveDone) {
         if (k != kKindGeneral) atomicOr(P.errorFlags + w, kErrStaticSchedule);
-        if (kind != kKindGeneral) in = loadVelIn(P, w, b1, r.s1, b2, r.s2, false, false);
+        if (kind != kKindGeneral) in = loadVelIn(P, w, L.pre, b1, r.s1, b2, r.s2, false, false);
+        markStaticWritten(L, r);
         solveVelocitiesGeneral(b1, b2, c, in, sd.h, sd.restitutionThreshold);
     }
 }
@@ -1220,7 +1400,9 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     const int32_t w = live ? P.solverOrder[wslot] : 0;
     if (lane == 0) s_worlds[wi] = w;
     SolverLDS L = solverWorldLDS(smem, nb, wi);
-    SolverBlockLDS BL = solverBlockLDS(kGlobal ? smem_raw : smem + kSolverWorlds * solverWorldLDSBytes(nb));
+    const bool alias = !kGlobal && solverAliasSchedule(nb);
+    SolverBlockLDS BL = solverBlockLDS(kGlobal ? smem_raw : smem + kSolverWorlds * solverWorldLDSBytes(nb),
+                                       alias ? &L : nullptr);
 
 #if defined(MW_SOLVER_PROFILE)
     long long prof_t = wall_clock64();
@@ -1228,10 +1410,30 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
 #endif
     if (threadIdx.x == 0) { BL.scalars[1] = 0; BL.scalars[2] = 0; BL.scalars[3] = 0; }
     int32_t K = 0, J = 0;
+#if MW_SOLVER_WARM
+    constexpr int32_t kWarmContacts = (kSolverLDSContacts + kSolverBlock - 1) / kSolverBlock;
+    uint32_t cwarm[2 * kWarmContacts];
+#pragma unroll
+    for (int32_t i = 0; i < 2 * kWarmContacts; i++) cwarm[i] = 0;
+#endif
     if (live) {
         loadWorldBodies(P, w, L, lane);
         J = worldJointCount(P, w, lane);
         K = gatherContacts(P, w, L.recs, kSolverLDSContacts, lane);
+#if MW_SOLVER_WARM
+        // the lines of the manifold words a solve reads (bytes 16-111)
+        waveSync();
+        const Contact *cbase = P.candContacts + (size_t)w * P.candCapacity;
+#pragma unroll
+        for (int32_t i = 0; i < kWarmContacts; i++) {
+            const int32_t k = lane + i * kSolverBlock;
+            if (k < min(K, kSolverLDSContacts)) {
+                const uint32_t *c = (const uint32_t *)(cbase + L.recs[k].slot);
+                cwarm[2 * i] = c[4];
+                cwarm[2 * i + 1] = c[27];
+            }
+        }
+#endif
     }
     __syncthreads();
     if (live && lane == 0) atomicMax(&BL.scalars[1], K + J);
@@ -1269,7 +1471,9 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
         N = 0;
         if (live) {
             if (fits) {                       // scheduled once already: afresh
-                for (int32_t b = lane; b < nb; b += kSolverBlock) L.lastItem[b] = -1;
+                for (int32_t b = lane; b < nb; b += kSolverBlock) {
+                    if (!invariantState(L.state[b])) L.state[b] = -1;
+                }
                 waveSync();
             }
             K = gatherContacts(P, w, grecs, INT32_MAX, lane);
@@ -1282,12 +1486,12 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
         __syncthreads();
         max_level = BL.scalars[3];
     } else {
-        // counting sort of the block's items by (level, kind)
+        // counting sort of the block's items by (level, kind), in place:
+        // counts, exclusive offsets, then each item's atomicAdd on its
+        // offset -- which leaves bucketOff[b] = the end of bucket b, i.e.
+        // the start of b + 1
         const int32_t nbk = (max_level + 2) * kNumKinds;
-        for (int32_t i = threadIdx.x; i < nbk; i += kSolverThreads) {
-            BL.bucketOff[i] = 0;
-            BL.bucketCur[i] = 0;
-        }
+        for (int32_t i = threadIdx.x; i < nbk; i += kSolverThreads) BL.bucketOff[i] = 0;
         __syncthreads();
         if (live) {
             for (int32_t k = lane; k < N; k += kSolverBlock) {
@@ -1310,7 +1514,7 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
                 const CRec r = L.recs[k];
                 const int32_t kind = itemKind(L, r);
                 const int32_t b = r.lvl * kNumKinds + kind;
-                const int32_t pos = BL.bucketOff[b] + atomicAdd(&BL.bucketCur[b], 1);
+                const int32_t pos = atomicAdd(&BL.bucketOff[b], 1);
                 BL.items[pos] = ((uint32_t)wi << 16) | ((uint32_t)kind << 12) | (uint32_t)k;
             }
         }
@@ -1340,14 +1544,33 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
         return true;
     };
     const int32_t stride = global ? kSolverBlock : kSolverThreads;
+#if MW_SOLVER_WARM
+#pragma unroll
+    for (int32_t i = 0; i < 2 * kWarmContacts; i++) keepLoaded(cwarm[i]);
+#endif
 
     // solvePositions, level by level
     for (int32_t l = 1; l <= max_level; l++) {
-        int32_t t = global ? lane : BL.bucketOff[l * kNumKinds] + threadIdx.x;
-        const int32_t end = global ? N : BL.bucketOff[(l + 1) * kNumKinds];
+        int32_t t = global ? lane : BL.bucketOff[l * kNumKinds - 1] + threadIdx.x;
+        const int32_t end = global ? N : BL.bucketOff[(l + 1) * kNumKinds - 1];
         for (; t < end; t += stride) {
             LevelItem it;
-            if (!levelItem(l, t, it)) continue;
+            const bool got = levelItem(l, t, it);
+#if defined(MW_SOLVER_PROFILE)
+            {   // item kinds per wave pass: static-side items, general ones,
+                // passes, passes mixing both (the wave runs both solves)
+                const uint64_t ms = __ballot(got && it.kind != kKindGeneral);
+                const uint64_t mg = __ballot(got && it.kind == kKindGeneral);
+                if ((threadIdx.x & 63) == 0) {
+                    atomicAdd(&g_solverPhase[9], (unsigned long long)__popcll(ms));
+                    atomicAdd(&g_solverPhase[10], (unsigned long long)__popcll(mg));
+                    atomicAdd(&g_solverPhase[11], 1ull);
+                    if (ms && mg) atomicAdd(&g_solverPhase[12], 1ull);
+                    if (__popcll(ms | mg) <= 16) atomicAdd(&g_solverPhase[13], 1ull);
+                }
+            }
+#endif
+            if (!got) continue;
             SolverLDS LW = solverWorldLDS(smem, nb, it.iw);
             solveItemPositions(P, s_worlds[it.iw], LW, it.r, it.kind);
         }
@@ -1364,8 +1587,8 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
     // solveVelocities, same schedule (joints: positions only; in the global
     // records they sort last, k >= K)
     for (int32_t l = 1; l <= max_level; l++) {
-        int32_t t = global ? lane : BL.bucketOff[l * kNumKinds] + threadIdx.x;
-        const int32_t end = global ? K : BL.bucketOff[(l + 1) * kNumKinds];
+        int32_t t = global ? lane : BL.bucketOff[l * kNumKinds - 1] + threadIdx.x;
+        const int32_t end = global ? K : BL.bucketOff[(l + 1) * kNumKinds - 1];
         for (; t < end; t += stride) {
             LevelItem it;
             if (!levelItem(l, t, it)) continue;
@@ -1422,7 +1645,7 @@ size_t solverSharedBytes(const PhysArgs &P)
 
 size_t solverGlobalSharedBytes(const PhysArgs &P)
 {
-    return solverBlockLDSBytes(P.maxBodiesPerWorld) - kSolverWorlds * solverWorldLDSBytes(P.maxBodiesPerWorld);
+    return solverScheduleBytes() + sizeof(int32_t) * 4;
 }
 
 size_t solverImageBytes(const PhysArgs &P)

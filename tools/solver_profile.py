@@ -49,8 +49,10 @@ def main():
     for q in (0.25, 0.5, 0.75, 0.9, 1.0):
         print(f"  blocks started by {q * en.max():6.1f} us: {(st <= q * en.max()).mean() * 100:5.1f} %  "
               f"finished: {(en <= q * en.max()).mean() * 100:5.1f} %")
-    print("position items: skip ref", int(out[9]), "skip alt", int(out[10]), "general", int(out[11]),
-          "| numPoints 4/1/2/3:", [int(x) for x in out[12:16]])
+    passes = max(int(out[11]), 1)
+    print(f"positions: static-side items {int(out[9])}, general items {int(out[10])}; wave passes {passes}, "
+          f"{100 * out[12] / passes:.1f} % mixing both kinds, {100 * out[13] / passes:.1f} % with <= 16 items, "
+          f"{(out[9] + out[10]) / passes:.1f} items per pass")
 
 
 if __name__ == "__main__":
