@@ -916,9 +916,29 @@ __device__ __forceinline__ PlaneIn loadPlaneIn(const PhysArgs &P, const SatWork 
                      bcol<Quat>(BB, Cols::Rotation, w, wk.b.row) };
 }
 
+// An object-space vertex of the hull tables; kPad: the LDS copy holds them
+// padded to 16 bytes (the plane kernel's staged table), so each is one
+// aligned ds_read_b128 instead of a 12-byte read at a 4-byte-aligned address
+// (SQ_LDS_UNALIGNED_STALL: 71 % of the kernel's LDS-active cycles before).
+template <bool kPad>
+__device__ __forceinline__ Vector3 objVertex(const ObjDev &O, int32_t i)
+{
+    if constexpr (kPad) {
+        const float4 v = ((const float4 *)O.vertices)[i];
+        return Vector3 { v.x, v.y, v.z };
+    } else {
+        return O.vertices[i];
+    }
+}
+
+template <bool kPad>
 __device__ __forceinline__ bool planeContact(const PhysArgs &P, const ObjDev &O, int32_t w,
                                              const SatWork &wk, const PlaneIn &in)
 {
+    // worldVertex with the table's layout (the same operations)
+    auto vertex = [&](const HullDev &hd, const HullXform &xf, int32_t i) {
+        return xf.vtx * objVertex<kPad>(O, hd.vertOffset + i) + xf.x;
+    };
     int32_t *flags = P.errorFlags + w;
     const HullDev ha = O.hulls[wk.aObj];
     const Mat3x3 unscaled_rot = Mat3x3::fromQuat(in.aRot);
@@ -929,7 +949,7 @@ __device__ __forceinline__ bool planeContact(const PhysArgs &P, const ObjDev &O,
     const geometry::Plane plane { pn, dot(pn, b_pos) };
     float min_dot = FLT_MAX;
     for (int32_t v = 0; v < ha.numVerts; v++) {
-        const float d = plane.normal.dot(worldVertex(O, ha, xa, v));
+        const float d = plane.normal.dot(vertex(ha, xa, v));
         if (d < min_dot) min_dot = d;
     }
     if (min_dot - plane.d > 0.0f) return false;
@@ -952,8 +972,7 @@ __device__ __forceinline__ bool planeContact(const PhysArgs &P, const ObjDev &O,
             hidx = guardIndex(hidx, ha.numHedges, flags, kGuardPlaneWalk);
             const geometry::HalfEdge he = hh[hidx];
             hidx = he.next;
-            const Vector3 v = worldVertex(O, ha, xa,
-                                          guardIndex(he.rootVertex, ha.numVerts, flags, kGuardVertex));
+            const Vector3 v = vertex(ha, xa, guardIndex(he.rootVertex, ha.numVerts, flags, kGuardVertex));
             const float d = distFromPlane(plane, v);
             if (d < 0.0f && n < cap) {
                 fn(n, v - d * plane.normal, -d);
@@ -1115,7 +1134,7 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
 
 __host__ __device__ inline size_t planeGeoBytesFor(const ObjDev &O)
 {
-    return a16(sizeof(HullDev) * O.numObjects) + a16(sizeof(Vector3) * O.numVertsTotal) +
+    return a16(sizeof(HullDev) * O.numObjects) + a16(sizeof(float4) * O.numVertsTotal) +
            a16(sizeof(geometry::Plane) * O.numPlanesTotal) +
            a16(sizeof(geometry::HalfEdge) * O.numHedgesTotal) +
            a16(sizeof(uint32_t) * O.numPolygonsTotal);
@@ -1163,7 +1182,14 @@ __device__ __forceinline__ void narrowPlaneBlock(const PhysArgs &P)
         static_assert(sizeof(HullDev) % 4 == 0 && sizeof(geometry::HalfEdge) % 4 == 0, "dword copies");
         char *dst = smem;
         O.hulls = (HullDev *)stageTable(dst, P.objs.hulls, sizeof(HullDev) * O.numObjects);
-        O.vertices = (Vector3 *)stageTable(dst, P.objs.vertices, sizeof(Vector3) * O.numVertsTotal);
+        {   // vertices padded to 16 B (objVertex<true>)
+            float4 *d = (float4 *)dst;
+            const float *src = (const float *)P.objs.vertices;
+            for (int32_t i = threadIdx.x; i < O.numVertsTotal; i += blockDim.x)
+                d[i] = float4 { src[3 * i], src[3 * i + 1], src[3 * i + 2], 0.f };
+            O.vertices = (Vector3 *)dst;
+            dst += a16(sizeof(float4) * O.numVertsTotal);
+        }
         O.planes = (geometry::Plane *)stageTable(dst, P.objs.planes,
                                                  sizeof(geometry::Plane) * O.numPlanesTotal);
         O.hedges = (geometry::HalfEdge *)stageTable(dst, P.objs.hedges,
@@ -1203,7 +1229,7 @@ __device__ __forceinline__ void narrowPlaneBlock(const PhysArgs &P)
             atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
             continue;
         }
-        if (planeContact(P, O, wk.world, wk, in))
+        if (planeContact<kGeo>(P, O, wk.world, wk, in))
             recordManifold(P, wk.world, wk.slot, slotOf(P, wk.bArch, wk.b), slotOf(P, wk.aArch, wk.a));
     }
 }

@@ -29,13 +29,18 @@ NODE_OF = {
     "bvhRebuildWaveKernel": ("UpdateBVHNode", 1),
     "refitKernel": ("RefitNode", 2),
     "findOverlapsKernel": ("FindOverlappingNode", 1),
+    "findOverlapsSmallKernel": ("FindOverlappingNode", 1),    # worlds of <= 256 leaves (round 5)
+    "findOverlapsGlobalKernel": ("FindOverlappingNode", 1),
     "integrateKernel": ("SubstepRigidBodiesNode", 1),     # substep 0 only (later: solver tail)
     "narrowFilterKernel": ("NarrowphaseNode", 1),         # substep 0 only (later: solver tail)
     "solverOrderKernel": ("NarrowphaseNode", 4),
     "narrowSATKernel": ("NarrowphaseNode", 4),
     "narrowSATNoGeoKernel": ("NarrowphaseNode", 4),      # hull tables read from HBM
+    "narrowSATGlobalKernel": ("NarrowphaseNode", 4),
     "narrowPlaneKernel": ("NarrowphaseNode", 4),
+    "narrowPlaneNoGeoKernel": ("NarrowphaseNode", 4),
     "narrowContactKernel": ("NarrowphaseNode", 4),
+    "narrowContactGlobalKernel": ("NarrowphaseNode", 4),
     "solverKernel": ("SolverNode", 4),
 }
 PER_STEP = {"UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
@@ -44,10 +49,10 @@ PER_STEP = {"UpdateLeafPositionsNode": 2, "RefitNode": 2, "UpdateBVHNode": 1,
 
 
 def kernel_key(name):
-    for k in NODE_OF:
-        if k in name:
-            return k
-    return None
+    # the kernel's own symbol name ("...phys::narrowSATKernel(...)"), so that
+    # findOverlapsKernel does not match findOverlapsSmallKernel
+    base = name.split("(")[0].split("::")[-1].strip()
+    return base if base in NODE_OF else None
 
 
 def find_csv(d, suffix):
@@ -105,11 +110,17 @@ def main():
             continue
         f = kper / PER_STEP[node]
         e = nodes.setdefault(node, {"kernels": [], "ms_per_launch": 0.0,
-                                    "fetch_bytes": 0.0, "write_bytes": 0.0})
+                                    "fetch_bytes": 0.0, "write_bytes": 0.0, "per_kernel": {}})
         e["kernels"].append(k)
         e["ms_per_launch"] += f * ms[k]
         e["fetch_bytes"] += f * 2.0 * fetch.get(k, 0.0)
         e["write_bytes"] += f * write.get(k, 0.0)
+        # the split: each kernel per launch of its own, and its share of a
+        # node launch (launches per step / node launches per step)
+        e["per_kernel"][k] = {"ms_per_kernel_launch": round(ms[k], 4),
+                              "bytes_per_kernel_launch": (int(2.0 * fetch.get(k, 0.0) + write.get(k, 0.0))
+                                                          if (fetch or write) else None),
+                              "share_of_node_launch": round(f, 4)}
     for e in nodes.values():
         e["ms_per_launch"] = round(e["ms_per_launch"], 4)
         e["bytes_per_launch"] = (int(e["fetch_bytes"] + e["write_bytes"])

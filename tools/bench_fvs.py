@@ -56,16 +56,27 @@ def node_systems(kinds):
             for i, k in enumerate(kinds)}
 
 
-def pmc_traffic(system):
-    """HBM bytes per launch of the system's node (row kernels + commit) over
-    the timed window, from the committed rocprofv3 PMC passes
-    (profiles/r03_fvs_traffic.json, tools/gpu_fvs_pmc.sh +
-    tools/fvs_prof_summary.py); None if absent."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "r03_fvs_traffic.json")) as f:
-            return json.load(f)["nodes"][system]["bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        return None
+# committed PMC / kernel-trace summaries of the timed window (ticks 601-1200):
+# the world-walk unit (tools/gpu_fvs_walk_pmc.sh -> profiles/r06_fvs_traffic.json),
+# per-node launches of the per-node graph (tools/gpu_fvs_pmc.sh ->
+# profiles/r03_fvs_traffic.json)
+FVS_TRAFFIC = ("r06_fvs_traffic.json", "r03_fvs_traffic.json")
+
+
+def committed_unit(system):
+    """The committed summary entry of the launch unit (None if absent) and its
+    file: HBM bytes per launch (PMC) and, for the walk, its kernel time per
+    replayed tick."""
+    key = "world walk" if system.startswith("world walk") else system
+    for name in FVS_TRAFFIC:
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                d = json.load(f)
+            if d.get("ticks", "601-1200") == "601-1200" and key in d["nodes"]:
+                return d["nodes"][key], "profiles/" + name
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
 
 
 def parse():
@@ -243,6 +254,17 @@ def main():
     launch_ms = (ms1 - ms0) / max(1, n1 - n0)
     nbytes = W * unit_bytes(dom, nd_mean, nk_mean)
     achieved = nbytes / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    unit, unit_src = committed_unit(dom_sys)
+    # the same bytes over the unit's kernel time in the replayed graph (the
+    # committed trace of this window): the split ticks the live timing reads
+    # run the unit eagerly, slower than a replayed tick
+    replayed = None
+    if unit and unit.get("kernel_us_per_launch"):
+        r_ms = unit["kernel_us_per_launch"] / 1e3
+        replayed = {"ms_per_launch": round(r_ms, 4), "achieved": round(nbytes / (r_ms * 1e-3) / 1e9, 2),
+                    "frac": round(nbytes / (r_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                    "frac_pmc": round(unit["bytes_per_launch"] / (r_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                    "source": unit_src}
     cpu = cpu_exec = None
     if not args.no_cpu_baseline:
         legs = ["reference"] + ([] if args.no_cpu_executor else ["executor"])
@@ -264,12 +286,15 @@ def main():
                                 f"{dom_sys} (node {dom}: row kernels + ordered commit)"),
                      "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                     "traffic": pmc_traffic(dom_sys), "ms_per_launch": round(launch_ms, 4),
+                     "traffic": (unit or {}).get("bytes_per_launch"),
+                     "traffic_source": unit_src,
+                     "ms_per_launch": round(launch_ms, 4),
                      "timed_launches": int(n1 - n0),
                      "timing": "a HIP event pair bound to each of the unit's kernels (start to end, "
                                "summed over its kernels) on every 10th tick of the timed window (the "
                                "step graph is split at that unit on those ticks only)",
                      "bytes_per_launch": int(nbytes),
+                     "replayed_tick": replayed,
                      "bytes_model": f"{W} worlds x SYS_BYTES of {dom_sys} at the window's mean live "
                                     f"rows per world: {nd_mean:.1f} dragons, {nk_mean:.1f} knights"},
         "cpu_baseline": cpu, "cpu_executor": cpu_exec, "error_flags": flags,
