@@ -1163,7 +1163,6 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
         for (int32_t r0 = 0; r0 < rows; r0 += kSolverBlock * kWriteBatch) {
             IntegrateIn in[kWriteBatch];
             IntegrateObj od[kWriteBatch];
-            BodyBox kept[kWriteBatch];            // a skipped static body's current box
             bool skip[kWriteBatch];
 #pragma unroll
             for (int32_t j = 0; j < kWriteBatch; j++) {
@@ -1175,7 +1174,15 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
                 for (int32_t j = 0; j < kWriteBatch; j++) {
                     const int32_t r = r0 + j * kSolverBlock + lane;
                     if (r < rows && !skip[j]) in[j] = integrateLoad(B, w, r);
-                    if (skip[j]) kept[j] = P.bodyBoxes[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r];
+                    if (skip[j]) {
+                        // a skipped static body's current box rides in the
+                        // row's integration records (an array of its own
+                        // stayed in scratch: 112 B per lane)
+                        const BodyBox bb = P.bodyBoxes[(size_t)w * P.maxBodiesPerWorld + B.slotBase + r];
+                        od[j].aabb = bb.box;
+                        in[j].obj = bb.obj;
+                        od[j].type = bb.type;
+                    }
                 }
 #pragma unroll
                 for (int32_t j = 0; j < kWriteBatch; j++) {
@@ -1191,7 +1198,7 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
                     // every write of this body would store the value it holds
                     if (integrate_next) {
                         waveSync();                       // the round's SMut reads first
-                        boxes[B.slotBase + r] = kept[j];
+                        boxes[B.slotBase + r] = BodyBox { od[j].aabb, in[j].obj, od[j].type };
                     }
                 } else if (live) {
                     const SMut *s = L.bodies + B.slotBase + r;
