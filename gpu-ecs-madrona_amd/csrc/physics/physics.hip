@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 namespace madrona::phys {
 
@@ -63,6 +64,33 @@ void PhysicsModule::rawCopy(void *dst, const void *src, size_t bytes, void *stre
 // that cannot launch either way throws here, at mw_create, naming the kernel
 // and the bytes (hip_launch.hpp).  MADRONA_MW_FORCE_GLOBAL_IMAGES=1 selects
 // the global variants everywhere (the parity tests of the fallback).
+// The solver's lane variant, once, from the level widths of the worlds' last
+// solve (the stream is idle at a poll).
+bool PhysicsModule::poll(void *stream_ptr, int64_t steps)
+{
+    if (!uploaded || solverLanesMode != 0 || steps < solverLanesNextCheck) return false;
+    const int32_t W = args.numWorlds;
+    std::vector<uint32_t> st(W);
+    MW_HIP_CHECK(hipMemcpyAsync(st.data(), args.solverLevelStats, sizeof(uint32_t) * W, hipMemcpyDeviceToHost,
+                                (hipStream_t)stream_ptr));
+    MW_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream_ptr));
+    double items = 0, levels = 0;
+    for (uint32_t v : st) {
+        items += v & 0xffffu;
+        levels += v >> 16;
+    }
+    if (levels == 0) return false;                   // no contacts yet: ask again at the next sync
+    solverLanesNextCheck = steps + kSolverLanesEvery;
+    solverItemsPerLevel = items / levels;
+    int32_t lanes = solverLanes;
+    if (solverItemsPerLevel <= kSolverNarrowLevel) lanes = 32;
+    if (solverItemsPerLevel >= kSolverWideLevel) lanes = 64;
+    if (lanes == solverLanes) return false;
+    solverLanes = lanes;
+    args.solverImage = solverImages[lanes == 32];
+    return true;
+}
+
 void PhysicsModule::upload(void *stream_ptr)
 {
     if (!initialized) return;          // physics types registered but never used
@@ -77,7 +105,6 @@ void PhysicsModule::upload(void *stream_ptr)
         return !force && hipx::residentBlocksNoThrow(fn, threads, lds) > 0;
     };
     const int32_t W = P.numWorlds;
-    const int32_t solver_blocks = (W + kSolverWorlds - 1) / kSolverWorlds;
 
     // broadphase: the BVH rebuild picks its variant per launch (<= 64 KB)
     // refit: LDS for about two thirds of the node capacity -- a rebuild uses
@@ -170,12 +197,28 @@ void PhysicsModule::upload(void *stream_ptr)
                              : hipx::residentBlocks((const void *)&narrowPlaneNoGeoKernel,
                                                     "narrowPlaneNoGeoKernel", kContactBlock, 0));
 
-    P.solverImage = nullptr;
-    if (!fitsLDS((const void *)&solverKernel, kSolverThreads, solverSharedBytes(P))) {
-        hipx::residentBlocks((const void *)&solverGlobalKernel, "solverGlobalKernel", kSolverThreads,
-                             solverGlobalSharedBytes(P));
-        P.solverImage = alloc<char>((size_t)solver_blocks * solverImageBytes(P), stream_ptr);
+    // solver: both lane variants, each with its global-image slab when its
+    // block image does not fit (SolverNode picks one per launch)
+    for (int32_t v = 0; v < 2; v++) {
+        const SolverVariant sv = v ? lanes32::solverVariant() : lanes64::solverVariant();
+        const int32_t blocks = (W + sv.worldsPerBlock - 1) / sv.worldsPerBlock;
+        solverImages[v] = nullptr;
+        if (!fitsLDS(sv.kernel, sv.threads, sv.sharedBytes(P))) {
+            hipx::residentBlocks(sv.globalKernel, v ? "solverGlobalKernel (32 lanes)" : "solverGlobalKernel",
+                                 sv.threads, sv.globalSharedBytes(P));
+            solverImages[v] = alloc<char>((size_t)blocks * sv.imageBytes(P), stream_ptr);
+        }
     }
+    P.solverLevelStats = alloc<uint32_t>(W, stream_ptr);
+    solverLanesMode = 0;
+    if (const char *e = std::getenv("MADRONA_MW_SOLVER_LANES")) {
+        const int32_t v = atoi(e);
+        if (v == 32 || v == 64) solverLanesMode = v;
+        else if (strcmp(e, "auto") != 0) throw std::runtime_error("MADRONA_MW_SOLVER_LANES: 32, 64 or auto");
+    }
+    solverLanes = solverLanesMode ? solverLanesMode : 64;
+    solverLanesNextCheck = kSolverLanesAfterSteps;
+    P.solverImage = solverImages[solverLanes == 32];
     // the remaining kernels stage nothing of variable size
     hipx::residentBlocks((const void *)&narrowFilterKernel, "narrowFilterKernel", kNarrowBlock, 0);
     uploaded = true;
@@ -380,13 +423,14 @@ extern "C" double mw_debug_time_solver(int32_t cut, int32_t reps, int32_t subste
     if (!g_cutArgs || g_cutArgs->solverImage) return -1.0;
     const PhysArgs Q = substepArgs(*g_cutArgs, substep, true);
     if (hipDeviceSynchronize() != hipSuccess || mw_debug_set_solver_cut(cut) != 0) return -1.0;
-    const dim3 grid((Q.numWorlds + kSolverWorlds - 1) / kSolverWorlds);
+    const dim3 grid((Q.numWorlds + kSolverWorlds - 1) / kSolverWorlds);   // the lanes64 variant
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
     (void)hipEventRecord(a, nullptr);
     for (int32_t r = 0; r < reps; r++)
-        hipLaunchKernelGGL(solverKernel, grid, dim3(kSolverThreads), solverSharedBytes(Q), nullptr, Q, 0);
+        hipLaunchKernelGGL(lanes64::solverKernel, grid, dim3(kSolverThreads), lanes64::solverSharedBytes(Q),
+                           nullptr, Q, 0);
     (void)hipEventRecord(b, nullptr);
     float ms = -1.f;
     if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = -1.f;
@@ -502,14 +546,27 @@ struct SolverNode : PhysNodeBase {
     static constexpr bool kNoTmpAlloc = true;
     static void launch(SolverNode *self, LaunchCtx &lc)
     {
-        const PhysArgs Q = substepArgs(self->mod->args, self->substep, true);
-        const dim3 grid((Q.numWorlds + kSolverWorlds - 1) / kSolverWorlds);
-        if (Q.solverImage)
-            MW_LAUNCH(solverGlobalKernel, grid, dim3(kSolverThreads), solverGlobalSharedBytes(Q),
-                      (hipStream_t)lc.stream, Q, self->integrateNext);
-        else
-            MW_LAUNCH(solverKernel, grid, dim3(kSolverThreads), solverSharedBytes(Q),
-                      (hipStream_t)lc.stream, Q, self->integrateNext);
+        PhysArgs Q = substepArgs(self->mod->args, self->substep, true);
+        const bool l32 = self->mod->solverLanes == 32;
+        const SolverVariant sv = l32 ? lanes32::solverVariant() : lanes64::solverVariant();
+        Q.solverImage = self->mod->solverImages[l32];
+        const dim3 grid((Q.numWorlds + sv.worldsPerBlock - 1) / sv.worldsPerBlock);
+        const hipStream_t st = (hipStream_t)lc.stream;
+        if (l32) {
+            if (Q.solverImage)
+                MW_LAUNCH(lanes32::solverGlobalKernel, grid, dim3(sv.threads), sv.globalSharedBytes(Q), st, Q,
+                          self->integrateNext);
+            else
+                MW_LAUNCH(lanes32::solverKernel, grid, dim3(sv.threads), sv.sharedBytes(Q), st, Q,
+                          self->integrateNext);
+        } else {
+            if (Q.solverImage)
+                MW_LAUNCH(lanes64::solverGlobalKernel, grid, dim3(sv.threads), sv.globalSharedBytes(Q), st, Q,
+                          self->integrateNext);
+            else
+                MW_LAUNCH(lanes64::solverKernel, grid, dim3(sv.threads), sv.sharedBytes(Q), st, Q,
+                          self->integrateNext);
+        }
         probeUnits(Q, lc, true, self->integrateNext != 0);
     }
 };

@@ -23,6 +23,8 @@ namespace madrona::phys {
 using namespace math;
 using namespace base;
 
+bool PhysicsModule::poll(void *, int64_t) { return false; }   // one world per worker: no lanes
+
 PhysicsModule::~PhysicsModule()
 {
     for (void *p : allocs) free(p);

@@ -145,7 +145,28 @@ __global__ void narrowSATNoGeoKernel(PhysArgs P);    // hull tables read from HB
 __global__ void narrowPlaneKernel(PhysArgs P);        // hull tables staged into LDS
 __global__ void narrowPlaneNoGeoKernel(PhysArgs P);   // hull tables read from HBM
 __global__ void narrowContactKernel(PhysArgs P);
+// The solver kernels, per variant (solver.hip: lanes64; solver32.hip: lanes32).
+struct SolverVariant {
+    const void *kernel;          // solverKernel (world images in LDS)
+    const void *globalKernel;    // solverGlobalKernel (world images in PhysArgs::solverImage)
+    int32_t threads, worldsPerBlock, lanesPerWorld;
+    size_t (*sharedBytes)(const PhysArgs &);
+    size_t (*globalSharedBytes)(const PhysArgs &);
+    size_t (*imageBytes)(const PhysArgs &);
+};
+namespace lanes64 {
 __global__ void solverKernel(PhysArgs P, int32_t integrate_next);
+__global__ void solverGlobalKernel(PhysArgs P, int32_t integrate_next);
+size_t solverSharedBytes(const PhysArgs &P);
+size_t solverGlobalSharedBytes(const PhysArgs &P);
+size_t solverImageBytes(const PhysArgs &P);
+SolverVariant solverVariant();
+}
+namespace lanes32 {
+__global__ void solverKernel(PhysArgs P, int32_t integrate_next);
+__global__ void solverGlobalKernel(PhysArgs P, int32_t integrate_next);
+SolverVariant solverVariant();
+}
 // The same kernels with their per-world / per-group / per-lane LDS image in
 // a global slab (PhysArgs::*Image), for worlds and hulls whose image does not
 // fit a workgroup's LDS: same code, same order of operations, same bits.
@@ -154,7 +175,6 @@ __global__ void findOverlapsGlobalKernel(PhysArgs P);
 __global__ void findOverlapsSmallKernel(PhysArgs P);
 __global__ void narrowSATGlobalKernel(PhysArgs P);
 __global__ void narrowContactGlobalKernel(PhysArgs P);
-__global__ void solverGlobalKernel(PhysArgs P, int32_t integrate_next);
 
 // substepRigidBodies (physics.cpp:79-164) for one body row, from its
 // current pose and velocity (the integrate kernel reads them from the
@@ -558,7 +578,6 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
 size_t findOverlapsSharedBytes(const PhysArgs &P);
 size_t findOverlapsGlobalSharedBytes(const PhysArgs &P);
 size_t refitSharedBytes(const PhysArgs &P);
-size_t solverSharedBytes(const PhysArgs &P);
 size_t narrowphaseSharedBytes(const PhysArgs &P);
 size_t satGeoSharedBytes(const PhysArgs &P);
 size_t contactSharedBytes(const PhysArgs &P);
@@ -566,8 +585,6 @@ size_t planeSharedBytes(const PhysArgs &P);
 // Global-image variants: dynamic LDS they still use, and image bytes per
 // world (findOverlaps, solver), per SAT block and per contact block.
 size_t findOverlapsImageBytes(const PhysArgs &P);
-size_t solverGlobalSharedBytes(const PhysArgs &P);
-size_t solverImageBytes(const PhysArgs &P);
 size_t narrowphaseGlobalSharedBytes(const PhysArgs &P);
 size_t narrowphaseImageBytes(const PhysArgs &P);
 size_t contactImageBytes(const PhysArgs &P);

@@ -235,6 +235,7 @@ struct PhysArgs {
     char *clipImage;              // [clipImageBlocks][contactImageBytes] clip polygons
     int32_t clipImageBlocks;
     char *solverImage;            // [solver blocks][solverImageBytes] body image per block
+    uint32_t *solverLevelStats;   // [W] items | dependency levels << 16 of the world's last solve
 
     ObjDev objs;
 };

@@ -43,6 +43,33 @@ struct PhysicsModule : StateExtension {
     std::vector<void *> allocs;
     bool uploaded = false;
 
+    // Solver lanes per world (SolverNode): 64 (lanes64, one world per wave)
+    // or 32 (lanes32, two worlds per wave).  MADRONA_MW_SOLVER_LANES = 64 /
+    // 32 fixes it; by default (auto) the GPU executor starts at 64 and, at
+    // synchronisations from kSolverLanesAfterSteps steps on and at most every
+    // kSolverLanesEvery steps, reads the level widths of the worlds' last
+    // solve (PhysArgs::solverLevelStats): levels of at most kSolverNarrowLevel
+    // items on average take 32 lanes -- half a wave's lanes would idle in
+    // every level pass --, of at least kSolverWideLevel 64 (the gap keeps a
+    // borderline workload from switching back and forth); a change re-captures
+    // the step (poll).  Both variants give the same bits, so a switch changes
+    // nothing but speed.
+    static constexpr int64_t kSolverLanesAfterSteps = 24;
+    static constexpr int64_t kSolverLanesEvery = 64;
+    // measured (8192 worlds, settled windows): simple_taskgraph's chains
+    // average 5.3-5.6 items per level and run 0.370 ms per solver launch on
+    // 32 lanes against 0.398 on 64; collisions' 34-35 run 0.265 on 32
+    // against 0.225 on 64 (its first 150 steps, cubes still landing, read
+    // 4-15)
+    static constexpr double kSolverNarrowLevel = 12.0;
+    static constexpr double kSolverWideLevel = 20.0;
+    int32_t solverLanes = 64;
+    int32_t solverLanesMode = 0;       // 0 auto, 32 / 64 fixed
+    int64_t solverLanesNextCheck = kSolverLanesAfterSteps;
+    double solverItemsPerLevel = 0.0;  // what the last check read
+    char *solverImages[2] = {};        // global-image slabs: [0] lanes64, [1] lanes32
+    bool poll(void *stream, int64_t steps) override;
+
     ~PhysicsModule() override;
 
     // Back-end memory (zero-filled) and host -> slab copies.

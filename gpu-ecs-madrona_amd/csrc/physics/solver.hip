@@ -1,9 +1,22 @@
 // XPBD solver kernel (reference src/physics/physics.cpp:166-1008).
+// Compiled twice: as is (namespace lanes64: one world per 64-lane wave) and
+// through solver32.hip (MW_SOLVER_LANES=32, namespace lanes32: two worlds per
+// wave, one per half).  The physics module picks one per executor from the
+// level widths the kernel reports (SolverNode, physics.hip).
 #include "physics_device.hpp"
 
 #include <cfloat>
 
+#ifndef MW_SOLVER_NS
+#define MW_SOLVER_NS lanes64
+#endif
+// the debug entry points of the 32-lane copy carry a suffix
+#ifndef MW_SOLVER_C
+#define MW_SOLVER_C(name) name
+#endif
+
 namespace madrona::phys {
+namespace MW_SOLVER_NS {
 
 // ===========================================================================
 // XPBD solver: solvePositions + setVelocities + solveVelocities
@@ -1370,7 +1383,7 @@ __device__ __forceinline__ void solveItemVelocities(const PhysArgs &P, int32_t w
 // 4 positions, 5 setVelocities, 6 velocities; 0: whole), relaunched on one
 // substep's inputs by mw_debug_time_solver (physics.hip).
 #if defined(MW_SAT_CUTS)
-extern "C" int mw_debug_set_solver_cut(int32_t cut)
+extern "C" int MW_SOLVER_C(mw_debug_set_solver_cut)(int32_t cut)
 {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_solverCut), &cut, sizeof(cut)) == hipSuccess ? 0 : -1;
 }
@@ -1466,6 +1479,7 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
             my_levels = scheduleLevels(L, N, L.recs, L.prevs, lane);
         }
         if (live && lane == 0) atomicMax(&BL.scalars[2], my_levels);
+        if (live && lane == 0 && P.solverLevelStats) P.solverLevelStats[w] = (uint32_t)N | (uint32_t)my_levels << 16;
         __syncthreads();
         max_level = BL.scalars[2];
     }
@@ -1490,6 +1504,8 @@ __device__ __forceinline__ void solverBlock(const PhysArgs &P, int32_t integrate
             my_levels = scheduleLevels(L, N, grecs, P.solverPrevs + (size_t)w * P.recStride, lane);
         }
         if (live && lane == 0) atomicMax(&BL.scalars[3], my_levels);
+        if (live && lane == 0 && P.solverLevelStats)
+            P.solverLevelStats[w] = (uint32_t)min(N, 0xffff) | (uint32_t)min(my_levels, 0xffff) << 16;
         __syncthreads();
         max_level = BL.scalars[3];
     } else {
@@ -1632,12 +1648,12 @@ __global__ void __launch_bounds__(kSolverThreads) solverGlobalKernel(PhysArgs P,
 }
 
 #if defined(MW_SOLVER_PROFILE)
-extern "C" int mw_debug_solver_block_times(unsigned long long *out, int n)
+extern "C" int MW_SOLVER_C(mw_debug_solver_block_times)(unsigned long long *out, int n)
 {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solverBlockT), sizeof(unsigned long long) * 2 * n) == hipSuccess ? 0 : -1;
 }
 
-extern "C" int mw_debug_solver_phases(unsigned long long *out)
+extern "C" int MW_SOLVER_C(mw_debug_solver_phases)(unsigned long long *out)
 {
     unsigned long long z[16] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solverPhase), sizeof(z)) != hipSuccess) return -1;
@@ -1660,4 +1676,12 @@ size_t solverImageBytes(const PhysArgs &P)
     return kSolverWorlds * solverWorldLDSBytes(P.maxBodiesPerWorld);
 }
 
+SolverVariant solverVariant()
+{
+    return SolverVariant { (const void *)&solverKernel, (const void *)&solverGlobalKernel,
+                           kSolverThreads, kSolverWorlds, kSolverBlock, &solverSharedBytes,
+                           &solverGlobalSharedBytes, &solverImageBytes };
+}
+
+}   // namespace MW_SOLVER_NS
 }

@@ -6,6 +6,7 @@
 
 #include "env_registry.hpp"
 #include "../physics/physics_impl.hpp"
+#include "../physics/physics_module.hpp"
 
 #include <madrona/mw_gpu.hpp>
 #include <madrona/launch_config.hpp>
@@ -748,7 +749,7 @@ extern "C" int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t 
     MW_TRY({
         phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
         if (!P || !out) return -1;
-        int32_t v[8];
+        int32_t v[10];
         v[0] = P->refitGlobal != 0;
         v[1] = P->overlapImage != nullptr;
         v[2] = P->satImage != nullptr;
@@ -757,7 +758,10 @@ extern "C" int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t 
         v[5] = P->planeGeoBytes > 0;
         v[6] = P->satGeoBytes > 0;
         v[7] = P->objs.minkStride > 0;
-        for (int32_t i = 0; i < n && i < 8; i++) out[i] = v[i];
-        return 8;
+        const phys::PhysicsModule &M = phys::physicsModule(exec->exec->stateManager());
+        v[8] = M.solverLanes;
+        v[9] = (int32_t)(M.solverItemsPerLevel * 100.0 + 0.5);
+        for (int32_t i = 0; i < n && i < 10; i++) out[i] = v[i];
+        return 10;
     }, -1)
 }

@@ -615,6 +615,7 @@ struct Executor::Impl {
     int32_t lastMax[kMaxArchetypes] = {};
     int32_t maxRise[kMaxArchetypes] = {};     // largest per-step rise seen, -1: none yet
     int64_t growths = 0;
+    int64_t stepsRun = 0;                     // steps enqueued since creation (extension polls)
     std::vector<std::pair<const void *, int32_t>> walkGrid;   // kernel -> grid
 };
 
@@ -1533,6 +1534,7 @@ void Executor::runAsync()
         launchStep(I, lc, dv);
     }
     I.stepsEnqueued++;
+    I.stepsRun++;
     enqueueGrowProbe(I);
 }
 
@@ -1556,6 +1558,7 @@ void Executor::runSteps(int32_t n)
         if (multi) {
             MW_HIP_CHECK(hipGraphLaunch(I.multiSegs[0].exec, I.stream));
             I.stepIndex += K;
+            I.stepsRun += K;
             i += K;
         } else {
             runAsync();
@@ -1636,6 +1639,12 @@ void Executor::sync()
     // the probes behind the last step are complete: no launch, no second sync
     drainGrowProbes(I, true);
     if (growthDue(I)) growTables(*this, I);
+    // extensions that change their launches from what the steps measured
+    // (the physics module's solver lanes) ask for a re-capture here
+    if (I.mgr->pollExtensions(I.stream, I.stepsRun)) {
+        LaunchCtx lc = makeLaunchCtx(I, this);
+        if (I.cfg.useGraph) captureGraph(I, lc, I.mgr->deviceViewHost());
+    }
 }
 
 void Executor::run()

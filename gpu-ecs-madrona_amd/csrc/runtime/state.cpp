@@ -683,6 +683,13 @@ void StateManager::setExtension(const char *name, StateExtension *ext)
     impl_->extensions.emplace_back(name, std::unique_ptr<StateExtension>(ext));
 }
 
+bool StateManager::pollExtensions(void *stream, int64_t steps)
+{
+    bool recapture = false;
+    for (auto &e : impl_->extensions) recapture |= e.second->poll(stream, steps);
+    return recapture;
+}
+
 StateExtension *StateManager::getExtension(const char *name) const
 {
     for (auto &e : impl_->extensions) {

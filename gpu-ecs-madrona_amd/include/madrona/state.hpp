@@ -473,6 +473,14 @@ public:
     // store grows with the tables that take entities).  Called before the
     // executor re-captures the step.
     virtual void stateResized() {}
+    // At every executor synchronisation (the stream is idle), with the
+    // number of steps run so far: true when the extension changed how its
+    // nodes launch and the step must be re-captured.
+    virtual bool poll(void *stream, int64_t steps)
+    {
+        (void)stream; (void)steps;
+        return false;
+    }
 };
 
 class ECSRegistry {
@@ -609,6 +617,9 @@ public:
 
     void setExtension(const char *name, StateExtension *ext);   // takes ownership
     StateExtension *getExtension(const char *name) const;
+    // StateExtension::poll of every extension; true if any asked for a
+    // re-capture of the step
+    bool pollExtensions(void *stream, int64_t steps);
 
     struct Impl;
 private:
