@@ -237,6 +237,10 @@ char *Executor::hostWorldData(int32_t world)
     return v.worldData + (size_t)world * v.worldDataStride;
 }
 
+namespace {
+void packExports(Executor::Impl &I);
+}
+
 void Executor::uploadState()
 {
     impl_->mgr->uploadToDevice(nullptr);
@@ -252,6 +256,7 @@ void Executor::uploadState()
         b.buf.assign((size_t)v.numWorlds * v.arch[b.archetype].capacity * b.bytes, 0);
         impl_->exports.push_back(std::move(b));
     }
+    packExports(*impl_);                 // the initial state's rows (as the GPU executor)
 }
 
 void Executor::setGraph(TaskGraph &&graph)

@@ -888,6 +888,8 @@ static bool growthDue(const Executor::Impl &I)
     return false;
 }
 
+static void launchExports(Executor::Impl &I, const StateView &dv);
+
 void Executor::uploadState()
 {
     impl_->mgr->uploadToDevice(impl_->stream);
@@ -939,6 +941,9 @@ void Executor::uploadState()
         }
         impl_->exports.push_back(b);
     }
+    // the packed exports of the initial state (a getExported before the
+    // first step reads the worlds as created, not uninitialised offsets)
+    launchExports(*impl_, dv);
     enqueueGrowProbe(*impl_);            // the initial rows
 }
 
