@@ -458,25 +458,33 @@ static bool mapExportMem(ExportBuf &b, size_t bytes, int dev)
     const size_t need = (bytes - b.mem.mapped + gran - 1) / gran * gran;
     if (b.mem.mapped + need > b.mem.reserved) return false;
     const hipMemAllocationProp prop = exportMemProp(dev);
+    auto refused = [&](const char *what, hipError_t e) {
+        (void)hipGetLastError();
+        if (getenv("MADRONA_MW_EXPORT_DEBUG"))
+            fprintf(stderr, "export buffer: %s refused (%s): mapped %zu need %zu gran %zu reserved %zu\n",
+                    what, hipGetErrorString(e), b.mem.mapped, need, gran, b.mem.reserved);
+        return false;
+    };
     hipMemGenericAllocationHandle_t h {};
-    if (hipMemCreate(&h, need, &prop, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
+    hipError_t e = hipMemCreate(&h, need, &prop, 0);
+    if (e != hipSuccess) return refused("hipMemCreate", e);
     char *at = b.buf + b.mem.mapped;
-    if (hipMemMap(at, need, 0, h, 0) != hipSuccess) {
+    e = hipMemMap(at, need, 0, h, 0);
+    if (e != hipSuccess) {
         (void)hipMemRelease(h);
-        (void)hipGetLastError();
-        return false;
+        return refused("hipMemMap", e);
     }
     hipMemAccessDesc acc {};
     acc.location = prop.location;
     acc.flags = hipMemAccessFlagsProtReadWrite;
-    if (hipMemSetAccess(at, need, &acc, 1) != hipSuccess) {
+    // Access is set over the whole mapped prefix: ROCm refuses a range that
+    // starts inside the reservation after an earlier chunk (measured: invalid
+    // argument at offset 12 KiB), and accepts the prefix.
+    e = hipMemSetAccess(b.buf, b.mem.mapped + need, &acc, 1);
+    if (e != hipSuccess) {
         (void)hipMemUnmap(at, need);
         (void)hipMemRelease(h);
-        (void)hipGetLastError();
-        return false;
+        return refused("hipMemSetAccess", e);
     }
     b.mem.chunks.push_back({ h, need });
     b.mem.mapped += need;
