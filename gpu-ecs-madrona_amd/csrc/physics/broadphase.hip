@@ -650,7 +650,7 @@ __global__ void __launch_bounds__(kRefitBlock) refitGlobalKernel(PhysArgs P)
 // each row's candidates, a block scan gives the reference's append order,
 // pass 2 writes them.
 
-constexpr int32_t kOverlapBuf = 12;     // candidates kept per body before a second sweep
+constexpr int32_t kOverlapBuf = kOverlapBufRanks;  // candidates kept per body before a second sweep
 constexpr int32_t kOverlapMaskWords = 4; // worlds up to 256 leaves: hits as a register bitmask
 static_assert(64 * kOverlapMaskWords == kOverlapSmallLeaves);
 
@@ -708,8 +708,8 @@ __host__ __device__ inline size_t overlapLDSBytes(int32_t max_leaves)
 // buffers' space, so the block writes the candidate run coalesced.
 constexpr int32_t kOverlapStage = kOverlapBlock * kOverlapBuf / 2;
 
-// Traversal stacks (int16 node indices, lane-interleaved) for worlds that
-// take the DFS; always in LDS, after the image when that is in LDS too.
+// Traversal stack depth (int16 node indices, lane-interleaved in LDS) of
+// the traversal kernels (dfsCountKernel).
 constexpr int32_t kOverlapStack = 64;
 
 __host__ __device__ inline bool overlapUsesDFS(const PhysArgs &P)
@@ -717,19 +717,21 @@ __host__ __device__ inline bool overlapUsesDFS(const PhysArgs &P)
     return P.overlapDFSLeaves >= 0 && P.maxLeaves > P.overlapDFSLeaves;
 }
 
-__host__ __device__ inline size_t overlapStackBytes(const PhysArgs &P)
+// A world past P.overlapDFSLeaves leaves walks the BVH (dfs*Kernel) and
+// the one-block sweep kernels skip it.
+__host__ __device__ inline bool overlapTraverses(const PhysArgs &P, int32_t nleaves)
 {
-    return overlapUsesDFS(P) ? a16b(2 * kOverlapBlock * kOverlapStack) : 0;
+    return overlapUsesDFS(P) && nleaves > P.overlapDFSLeaves;
 }
 
 size_t findOverlapsSharedBytes(const PhysArgs &P)
 {
-    return overlapLDSBytes(P.maxLeaves) + overlapStackBytes(P);
+    return overlapLDSBytes(P.maxLeaves);
 }
 
-size_t findOverlapsGlobalSharedBytes(const PhysArgs &P)
+size_t findOverlapsGlobalSharedBytes(const PhysArgs &)
 {
-    return overlapStackBytes(P);
+    return 0;
 }
 
 // Phase profile (experiments only, -DMW_SOLVER_PROFILE, the solver's
@@ -800,16 +802,21 @@ __device__ __forceinline__ int32_t waveSweep(const OrderedLeaf *leaves, int32_t 
 // caller then sweeps the leaves, which emits the same sequence.  (A query
 // that reaches most of the tree -- a ground plane's, say, whose hits the id
 // rule drops -- is a serial chain of dependent node loads; the wave sweeps
-// its leaves 64 at a time instead.)
+// its leaves 64 at a time instead.)  A leaf child's filter and emission rank
+// come from one 8-byte load of its DfsKey.
 typedef int32_t NodeWords4 __attribute__((ext_vector_type(4), aligned(4)));
 static_assert(offsetof(BVHNode, minY) == 16 && offsetof(BVHNode, children) == 96);
 
-template <typename Emit>
+struct DfsKey {
+    int32_t id;                   // entity id (the e.id < other.id rule)
+    int32_t rankStatic;           // emission rank << 1 | isStatic
+};
+
+template <int32_t kStride, typename Emit>
 __device__ __forceinline__ bool dfsQuery(const BVHNode *__restrict__ nodes, int32_t max_nodes,
                                          int32_t max_leaves, const AABB &q, int32_t e_id,
-                                         bool a_static, const OrderedLeaf *leaves,
-                                         const int32_t *rank_of, int16_t *stk, int32_t *flags,
-                                         int32_t budget, Emit &&emit)
+                                         bool a_static, const DfsKey *__restrict__ keys,
+                                         int16_t *stk, int32_t *flags, int32_t budget, Emit &&emit)
 {
     int32_t ss = 0;
     int32_t cur = 0;
@@ -845,19 +852,16 @@ __device__ __forceinline__ bool dfsQuery(const BVHNode *__restrict__ nodes, int3
             if (child & 0x80000000) {
                 // the slot test above is the leaf's (the image holds the same
                 // bytes); then e.id < other.id and not both static
-                const int32_t k =
-                    rank_of[guardIndex(child & 0x7fffffff, max_leaves, flags, kGuardLeaf)];
-                const float4 hi = ((const float4 *)leaves)[3 * k + 1];   // .., id, isStatic
-                const bool keep = (e_id < __float_as_int(hi.z)) &
-                                  !(a_static & (__float_as_int(hi.w) != 0));
-                if (keep && !emit(k)) return false;
+                const DfsKey key = keys[guardIndex(child & 0x7fffffff, max_leaves, flags, kGuardLeaf)];
+                const bool keep = (e_id < key.id) & !(a_static & ((key.rankStatic & 1) != 0));
+                if (keep && !emit(key.rankStatic >> 1)) return false;
             } else {
                 if (ss == kOverlapStack) return false;
-                stk[ss++ * kOverlapBlock] = (int16_t)guardIndex(child, max_nodes, flags, kGuardNode);
+                stk[ss++ * kStride] = (int16_t)guardIndex(child, max_nodes, flags, kGuardNode);
             }
         }
         if (ss == 0) return true;
-        cur = stk[--ss * kOverlapBlock];
+        cur = stk[--ss * kStride];
     }
 }
 
@@ -867,11 +871,56 @@ size_t findOverlapsImageBytes(const PhysArgs &P)
 }
 
 
+// The leaf of emission rank k (leafOrder) as the sweeps and the traversal
+// read it: its slot AABB from the refit tree, identity, static flag,
+// location and packed body slot.  Returns the leaf id.
+__device__ __forceinline__ int32_t stageLeaf(const PhysArgs &P, int32_t w, int32_t k,
+                                             int32_t *flags, OrderedLeaf &ol)
+{
+    const BVHNode *nodes = P.nodes + (size_t)w * P.maxNodes;
+    const int32_t leaf = guardIndex(P.leafOrder[(size_t)w * P.maxLeaves + k], P.maxLeaves, flags,
+                                    kGuardLeaf);
+    const uint32_t lp = P.leafParents[(size_t)w * P.maxLeaves + leaf];
+    const BVHNode &n = nodes[guardIndex((int32_t)(lp >> 2), P.maxNodes, flags, kGuardNode)];
+    const int sub = (int)(lp & 3);
+    const Entity e = P.leafEntities[(size_t)w * P.maxLeaves + leaf];
+    const Loc loc = entityLoc(P, w, e);
+    const int32_t oa = bodyArchIndex(P, loc.archetype);
+    const BodyArch &OB = P.body[oa];
+    const int32_t row = guardIndex(loc.row, OB.capacity, flags, kGuardLeaf);
+    ol.minX = n.minX[sub]; ol.minY = n.minY[sub]; ol.minZ = n.minZ[sub];
+    ol.maxX = n.maxX[sub]; ol.maxY = n.maxY[sub]; ol.maxZ = n.maxZ[sub];
+    ol.id = e.id;
+    ol.isStatic = bcol<ResponseType>(OB, Cols::ResponseType, w, row) == ResponseType::Static ? 1 : 0;
+    ol.loc = loc;
+    ol.slot = (uint32_t)(OB.slotBase + row) | (uint32_t)oa << 16 |
+              ((uint32_t)loc.row < (uint32_t)OB.capacity ? 0u : 1u << 24);
+    return leaf;
+}
+
+// Runs fn(lane, its query, e_id, static, rank) with the wave, for each lane
+// in m (wave-uniform).
+template <typename Fn>
+__device__ __forceinline__ void forWideLanes(uint64_t m, const AABB &q, int32_t e_id, bool a_static,
+                                             int32_t self, Fn &&fn)
+{
+    for (; m; m &= m - 1) {
+        const int32_t h = __ffsll((unsigned long long)m) - 1;
+        AABB qh;
+        qh.pMin.x = __shfl(q.pMin.x, h, 64); qh.pMin.y = __shfl(q.pMin.y, h, 64);
+        qh.pMin.z = __shfl(q.pMin.z, h, 64); qh.pMax.x = __shfl(q.pMax.x, h, 64);
+        qh.pMax.y = __shfl(q.pMax.y, h, 64); qh.pMax.z = __shfl(q.pMax.z, h, 64);
+        fn(h, qh, __shfl(e_id, h, 64), __shfl((int32_t)a_static, h, 64) != 0, __shfl(self, h, 64));
+    }
+}
+
+// The sweep worlds, one block per world (worlds that traverse return at
+// once: dfsStageKernel / dfsCountKernel / dfsWriteKernel below).
 // kGlobal: the world's leaf image exceeds a workgroup's LDS; it is staged in
 // the world's slab of P.overlapImage instead (findOverlapsGlobalKernel).
 // kSmall: every world fits the register bitmask (maxLeaves <= 256) and none
-// traverses -- the sweep and traversal paths are compiled out, which keeps
-// this kernel's registers (and so its occupancy) to the bitmask path's own.
+// traverses -- the general sweep is compiled out, which keeps this kernel's
+// registers (and so its occupancy) to the bitmask path's own.
 template <bool kGlobal, bool kSmall = false>
 __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
 {
@@ -885,34 +934,15 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
     OrderedLeaf *leaves = (OrderedLeaf *)img;
     int32_t *rank_of = (int32_t *)(img + a16b(sizeof(OrderedLeaf) * P.maxLeaves));
     uint16_t *bufs = (uint16_t *)((char *)rank_of + a16b(4 * P.maxLeaves));
-    int16_t *stk = (int16_t *)(kGlobal ? smem : img + overlapLDSBytes(P.maxLeaves)) + threadIdx.x;
 
     // Stage leaf slots (from the refit tree) + identity in emission order.
     const broadphase::BVH &bvh = P.bvh[w];
     const int32_t nleaves = min(bvh.numLeaves, P.maxLeaves);
-    const BVHNode *nodes = P.nodes + (size_t)w * P.maxNodes;
-    const int32_t *order = P.leafOrder + (size_t)w * P.maxLeaves;
     int32_t *flags = P.errorFlags + w;
-    const bool dfs = !kSmall && overlapUsesDFS(P) && nleaves > P.overlapDFSLeaves;
+    if (!kSmall && overlapTraverses(P, nleaves)) return;
     for (int32_t k = threadIdx.x; k < nleaves; k += kOverlapBlock) {
-        const int32_t leaf = guardIndex(order[k], P.maxLeaves, flags, kGuardLeaf);
-        const uint32_t lp = P.leafParents[(size_t)w * P.maxLeaves + leaf];
-        const BVHNode &n = nodes[guardIndex((int32_t)(lp >> 2), P.maxNodes, flags, kGuardNode)];
-        const int sub = (int)(lp & 3);
-        const Entity e = P.leafEntities[(size_t)w * P.maxLeaves + leaf];
-        const Loc loc = entityLoc(P, w, e);
-        const int32_t oa = bodyArchIndex(P, loc.archetype);
-        const BodyArch &OB = P.body[oa];
-        const int32_t row = guardIndex(loc.row, OB.capacity, flags, kGuardLeaf);
         OrderedLeaf ol;
-        ol.minX = n.minX[sub]; ol.minY = n.minY[sub]; ol.minZ = n.minZ[sub];
-        ol.maxX = n.maxX[sub]; ol.maxY = n.maxY[sub]; ol.maxZ = n.maxZ[sub];
-        ol.id = e.id;
-        ol.isStatic =
-            bcol<ResponseType>(OB, Cols::ResponseType, w, row) == ResponseType::Static ? 1 : 0;
-        ol.loc = loc;
-        ol.slot = (uint32_t)(OB.slotBase + row) | (uint32_t)oa << 16 |
-                  ((uint32_t)loc.row < (uint32_t)OB.capacity ? 0u : 1u << 24);
+        const int32_t leaf = stageLeaf(P, w, k, flags, ol);
         leaves[k] = ol;
         rank_of[leaf] = k;
     }
@@ -942,67 +972,6 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
             CandidateCollision *out = P.cands + (size_t)w * P.candCapacity;
             uint64_t *out_slots = P.candSlots + (size_t)w * P.candCapacity;
             int32_t total;
-            // Runs fn(lane, its query, e_id, static, rank) with the wave, for
-            // each lane in m (wave-uniform).
-            auto forWide = [&](uint64_t m, auto &&fn) {
-                for (; m; m &= m - 1) {
-                    const int32_t h = __ffsll((unsigned long long)m) - 1;
-                    AABB qh;
-                    qh.pMin.x = __shfl(q.pMin.x, h, 64); qh.pMin.y = __shfl(q.pMin.y, h, 64);
-                    qh.pMin.z = __shfl(q.pMin.z, h, 64); qh.pMax.x = __shfl(q.pMax.x, h, 64);
-                    qh.pMax.y = __shfl(q.pMax.y, h, 64); qh.pMax.z = __shfl(q.pMax.z, h, 64);
-                    fn(h, qh, __shfl(e_id, h, 64), __shfl((int32_t)a_static, h, 64) != 0,
-                       __shfl(self, h, 64));
-                }
-            };
-            if (dfs) {
-                // BVH::findOverlaps per lane: each body's cost follows its
-                // overlaps, not the world's size.  A query with more than
-                // kOverlapBuf candidates, a deeper stack or a walk past
-                // 32 + leaves/32 nodes (about what sweeping for it costs the
-                // wave) is "wide": its lane stops, and the wave sweeps the
-                // leaves for it, 64 per step, in the same order.
-                bool wide = false;
-                if (active) {
-                    wide = !dfsQuery(nodes, P.maxNodes, P.maxLeaves, q, e_id, a_static, leaves,
-                                     rank_of, stk, flags, 32 + nleaves / 32, [&](int32_t k) {
-                                         if (cnt == kOverlapBuf) return false;
-                                         buf[cnt++] = (uint16_t)k;
-                                         return true;
-                                     });
-                }
-                const uint64_t wides = __ballot(wide);
-                if (active) MW_OVERLAP_COUNT(5, 1);
-                if (wide) MW_OVERLAP_COUNT(6, 1);
-                forWide(wides, [&](int32_t h, const AABB &qh, int32_t eh, bool sh, int32_t selfh) {
-                    const int32_t n = waveSweep<false>(leaves, nleaves, qh, eh, sh, selfh, 0,
-                                                       out, out_slots, 0);
-                    if ((int32_t)(threadIdx.x & 63) == h) cnt = n;
-                });
-                MW_OVERLAP_MARK(1);
-                const int32_t off = blockExclusiveScan(cnt, scan_scratch, &total);
-                MW_OVERLAP_MARK(2);
-                if (!wide && cnt > 0) {
-                    const Loc a_loc = me.loc;
-                    const uint64_t a_slot = me.slot;
-                    for (int32_t i = 0; i < cnt; i++) {
-                        const int32_t slot = base + off + i;
-                        const OrderedLeaf &o = leaves[buf[i]];
-                        if (slot < P.candCapacity) {
-                            out[slot] = CandidateCollision { a_loc, o.loc };
-                            out_slots[slot] = a_slot | (uint64_t)o.slot << 32;
-                        }
-                    }
-                }
-                const int32_t first = base + off;
-                forWide(wides, [&](int32_t h, const AABB &qh, int32_t eh, bool sh, int32_t selfh) {
-                    waveSweep<true>(leaves, nleaves, qh, eh, sh, selfh, __shfl(first, h, 64),
-                                    out, out_slots, P.candCapacity);
-                });
-                base += total;
-                MW_OVERLAP_MARK(3);
-                continue;
-            }
             if (kSmall || nleaves <= 64 * kOverlapMaskWords) {
                 // The hits as a leaf-rank bitmask in registers: the sweep
                 // stores nothing to LDS, so the broadcast leaf reads of
@@ -1101,7 +1070,7 @@ __device__ __forceinline__ void findOverlapsWorld(const PhysArgs &P)
                 }
             }
             const int32_t first = base + off;
-            forWide(__ballot(cnt > kOverlapBuf),
+            forWideLanes(__ballot(cnt > kOverlapBuf), q, e_id, a_static, self,
                     [&](int32_t h, const AABB &qh, int32_t eh, bool sh, int32_t selfh) {
                         waveSweep<true>(leaves, nleaves, qh, eh, sh, selfh, __shfl(first, h, 64),
                                         out, out_slots, P.candCapacity);
@@ -1148,6 +1117,188 @@ __global__ void __launch_bounds__(kOverlapBlock) findOverlapsGlobalKernel(PhysAr
 {
     MW_TRACE_BLOCK(0);
     findOverlapsWorld<true>(P);
+}
+
+// ---- Traversal worlds (more than P.overlapDFSLeaves leaves) ----
+// BVH::findOverlaps per body (physics.inl:61-100), its cost following the
+// body's overlaps rather than the world's size.  One block per world made a
+// 3,200-body world the latency chain of one CU (2.31 ms per launch); the
+// work now spreads over (world, chunk of kDfsBlock body rows) blocks in three
+// launches:
+//   dfsStageKernel  the emission-order leaf image (OrderedLeaf, what the
+//                   candidate writes and the wave sweeps read) and, per leaf
+//                   id, its DfsKey (entity id, static flag, emission rank);
+//   dfsCountKernel  each lane walks its body's query into its first
+//                   kOverlapBuf hit ranks; a wide query (more hits, a deeper
+//                   stack, or a walk past 32 + leaves/32 nodes -- about what
+//                   sweeping costs the wave) is counted by its wave sweeping
+//                   the leaves, 64 per step, in the same order; each block
+//                   records its chunk's total;
+//   dfsWriteKernel  each block's first slot is the earlier chunks' totals
+//                   plus a block scan; the candidates go out in row order
+//                   (a wide query swept again by its wave).
+// Rows are numbered across the body archetypes in order, as the sweep
+// kernels visit them, so the candidate sequence is the one-block path's.
+static_assert(sizeof(DfsKey) == 8 && kOrderedLeafBytes == sizeof(OrderedLeaf));
+constexpr int32_t kDfsWide = 1 << 30;                 // dfsRows[].x: the wave sweeps this row
+
+__device__ __forceinline__ bool dfsWorld(const PhysArgs &P, int32_t w, int32_t &nleaves)
+{
+    nleaves = min(P.bvh[w].numLeaves, P.maxLeaves);
+    return overlapTraverses(P, nleaves);
+}
+
+// Row r of world w counted across the body archetypes (false past the last).
+__device__ __forceinline__ bool dfsRow(const PhysArgs &P, int32_t w, int32_t r, int32_t &ba,
+                                       int32_t &row)
+{
+    for (ba = 0; ba < P.numBodyArchs; ba++) {
+        const int32_t rows = P.body[ba].numRows[w];
+        if (r < rows) {
+            row = r;
+            return true;
+        }
+        r -= rows;
+    }
+    return false;
+}
+
+__global__ void __launch_bounds__(kDfsBlock) dfsStageKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    const int32_t w = blockIdx.x;
+    int32_t nleaves;
+    if (!dfsWorld(P, w, nleaves)) return;
+    const int32_t k = blockIdx.y * kDfsBlock + threadIdx.x;
+    if (k >= nleaves) return;
+    const size_t wl = (size_t)w * P.maxLeaves;
+    OrderedLeaf ol;
+    const int32_t leaf = stageLeaf(P, w, k, P.errorFlags + w, ol);
+    ((OrderedLeaf *)P.dfsImage)[wl + k] = ol;
+    ((DfsKey *)P.dfsKeys)[wl + leaf] = DfsKey { ol.id, k << 1 | ol.isStatic };
+}
+
+__global__ void __launch_bounds__(kDfsBlock) dfsCountKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    const int32_t w = blockIdx.x;
+    int32_t nleaves;
+    if (!dfsWorld(P, w, nleaves)) return;
+    __shared__ int16_t stacks[kOverlapStack * kDfsBlock];
+    __shared__ int32_t scan_scratch[kDfsBlock / 64];
+    int32_t *flags = P.errorFlags + w;
+    const size_t wl = (size_t)w * P.maxLeaves;
+    const OrderedLeaf *leaves = (const OrderedLeaf *)P.dfsImage + wl;
+    const DfsKey *keys = (const DfsKey *)P.dfsKeys + wl;
+    const int32_t r = blockIdx.y * kDfsBlock + threadIdx.x;
+    const size_t wr = (size_t)w * P.dfsRowCap + r;
+
+    int32_t ba = 0, row = 0, leaf = 0;
+    const bool active = dfsRow(P, w, r, ba, row);
+    AABB q = AABB::invalid();
+    DfsKey me { 0, 0 };
+    if (active) {
+        const BodyArch &B = P.body[ba];
+        leaf = guardIndex(bcol<broadphase::LeafID>(B, Cols::LeafID, w, row).id, P.maxLeaves, flags,
+                          kGuardLeaf);
+        q = P.leafAABBs[wl + leaf];
+        me = keys[leaf];
+    }
+    const int32_t e_id = me.id;
+    const bool a_static = (me.rankStatic & 1) != 0;
+    const int32_t self = me.rankStatic >> 1;
+
+    uint16_t *hits = P.dfsHits + wr * kOverlapBuf;
+    int32_t cnt = 0;
+    bool wide = false;
+    if (active) {
+        MW_OVERLAP_COUNT(5, 1);
+        wide = !dfsQuery<kDfsBlock>(P.nodes + (size_t)w * P.maxNodes, P.maxNodes, P.maxLeaves, q, e_id,
+                                    a_static, keys, stacks + threadIdx.x, flags, 32 + nleaves / 32,
+                                    [&](int32_t k) {
+                                        if (cnt == kOverlapBuf) return false;
+                                        hits[cnt++] = (uint16_t)k;
+                                        return true;
+                                    });
+    }
+    if (wide) MW_OVERLAP_COUNT(6, 1);
+    forWideLanes(__ballot(wide), q, e_id, a_static, self,
+                 [&](int32_t h, const AABB &qh, int32_t eh, bool sh, int32_t selfh) {
+                     const int32_t n = waveSweep<false>(leaves, nleaves, qh, eh, sh, selfh, 0,
+                                                        nullptr, nullptr, 0);
+                     if ((int32_t)(threadIdx.x & 63) == h) cnt = n;
+                 });
+    ((int2 *)P.dfsRows)[wr] = make_int2(wide ? (cnt | kDfsWide) : cnt, leaf);
+    int32_t total;
+    (void)blockExclusiveScan(cnt, scan_scratch, &total);
+    if (threadIdx.x == 0) P.dfsChunkTotals[(size_t)w * P.dfsChunks + blockIdx.y] = total;
+}
+
+__global__ void __launch_bounds__(kDfsBlock) dfsWriteKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    const int32_t w = blockIdx.x;
+    int32_t nleaves;
+    if (!dfsWorld(P, w, nleaves)) return;
+    __shared__ int32_t scan_scratch[kDfsBlock / 64];
+    const size_t wl = (size_t)w * P.maxLeaves;
+    const OrderedLeaf *leaves = (const OrderedLeaf *)P.dfsImage + wl;
+    const DfsKey *keys = (const DfsKey *)P.dfsKeys + wl;
+    const int32_t *totals = P.dfsChunkTotals + (size_t)w * P.dfsChunks;
+    const int32_t r = blockIdx.y * kDfsBlock + threadIdx.x;
+    const size_t wr = (size_t)w * P.dfsRowCap + r;
+
+    int32_t first = 0;
+    for (int32_t c = 0; c < (int32_t)blockIdx.y; c++) first += totals[c];
+    const int2 rec = ((const int2 *)P.dfsRows)[wr];
+    const bool wide = (rec.x & kDfsWide) != 0;
+    const int32_t cnt = rec.x & ~kDfsWide;
+    int32_t total;
+    const int32_t base = first + blockExclusiveScan(cnt, scan_scratch, &total);
+
+    const int32_t cap = P.candCapacity;
+    CandidateCollision *out = P.cands + (size_t)w * cap;
+    uint64_t *out_slots = P.candSlots + (size_t)w * cap;
+    DfsKey me { 0, 0 };
+    AABB q = AABB::invalid();
+    if (cnt > 0 || wide) me = keys[rec.y];           // a wide query's sweep filters by it
+    if (wide) q = P.leafAABBs[wl + rec.y];
+    const int32_t self = me.rankStatic >> 1;
+    if (!wide && cnt > 0) {
+        const uint16_t *hits = P.dfsHits + wr * kOverlapBuf;
+        const OrderedLeaf &a = leaves[self];
+        const Loc a_loc = a.loc;
+        const uint64_t a_slot = a.slot;
+        for (int32_t i = 0; i < cnt; i++) {
+            const int32_t slot = base + i;
+            const OrderedLeaf &o = leaves[hits[i]];
+            if (slot < cap) {
+                out[slot] = CandidateCollision { a_loc, o.loc };
+                out_slots[slot] = a_slot | (uint64_t)o.slot << 32;
+            }
+        }
+    }
+    forWideLanes(__ballot(wide), q, me.id, (me.rankStatic & 1) != 0, self,
+                 [&](int32_t h, const AABB &qh, int32_t eh, bool sh, int32_t selfh) {
+                     waveSweep<true>(leaves, nleaves, qh, eh, sh, selfh, __shfl(base, h, 64), out,
+                                     out_slots, cap);
+                 });
+
+    if (blockIdx.y == 0 && threadIdx.x == 0) {
+        int32_t all = 0, rows = 0;
+        for (int32_t c = 0; c < P.dfsChunks; c++) all += totals[c];
+        for (int32_t ba = 0; ba < P.numBodyArchs; ba++) rows += P.body[ba].numRows[w];
+        if (rows > P.dfsRowCap) atomicOr(P.errorFlags + w, kErrIndexGuard | (kGuardLeaf << 8));
+        if (all > cap) {
+            atomicOr(P.errorFlags + w, kErrCandidateOverflow);
+            all = cap;
+        }
+        P.numCands[w] = all;
+        P.lastNumCands[w] = all;
+#if defined(MW_SOLVER_PROFILE)
+        atomicAdd(&g_overlapPhase[7], 1ull);
+#endif
+    }
 }
 
 }

@@ -134,6 +134,18 @@ void PhysicsModule::upload(void *stream_ptr)
                              kOverlapBlock, findOverlapsGlobalSharedBytes(P));
         P.overlapImage = alloc<char>((size_t)W * findOverlapsImageBytes(P), stream_ptr);
     }
+    P.dfsChunks = 0;
+    P.dfsRowCap = 0;
+    if (P.overlapDFSLeaves >= 0) {
+        P.dfsChunks = (P.maxLeaves + kDfsBlock - 1) / kDfsBlock;
+        P.dfsRowCap = P.dfsChunks * kDfsBlock;
+        const size_t WL = (size_t)W * P.maxLeaves, WR = (size_t)W * P.dfsRowCap;
+        P.dfsImage = alloc<char>(WL * kOrderedLeafBytes, stream_ptr);
+        P.dfsKeys = alloc<int32_t>(WL * 2, stream_ptr);
+        P.dfsHits = alloc<uint16_t>(WR * kOverlapBufRanks, stream_ptr);
+        P.dfsRows = alloc<int32_t>(WR * 2, stream_ptr);
+        P.dfsChunkTotals = alloc<int32_t>((size_t)W * P.dfsChunks, stream_ptr);
+    }
 
     // SAT: persistent grid of exactly the blocks that can be resident (hull
     // tables in LDS up to 16 KB, else read from HBM; from HBM under
@@ -280,6 +292,8 @@ MW_PHYS_NODE(RefitNode,
     else
         MW_LAUNCH(refitKernel, dim3(P.numWorlds), dim3(kRefitBlock), refitSharedBytes(P), stream, P);)
 
+// Sweep worlds in the one-block kernels, then the traversal worlds (the
+// sweep kernels skip them, the dfs kernels skip the others).
 MW_PHYS_NODE(FindOverlappingNode,
     if (P.overlapImage)
         MW_LAUNCH(findOverlapsGlobalKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
@@ -289,7 +303,13 @@ MW_PHYS_NODE(FindOverlappingNode,
                   findOverlapsSharedBytes(P), stream, P);
     else
         MW_LAUNCH(findOverlapsKernel, dim3(P.numWorlds), dim3(kOverlapBlock),
-                  findOverlapsSharedBytes(P), stream, P);)
+                  findOverlapsSharedBytes(P), stream, P);
+    if (P.dfsChunks > 0) {
+        const dim3 grid(P.numWorlds, P.dfsChunks);
+        MW_LAUNCH(dfsStageKernel, grid, dim3(kDfsBlock), 0, stream, P);
+        MW_LAUNCH(dfsCountKernel, grid, dim3(kDfsBlock), 0, stream, P);
+        MW_LAUNCH(dfsWriteKernel, grid, dim3(kDfsBlock), 0, stream, P);
+    })
 
 // Work units of a live-timed launch (PhysArgs::unitAccum): the probe sums
 // the worlds' candidates and this substep's contact manifolds -- after a

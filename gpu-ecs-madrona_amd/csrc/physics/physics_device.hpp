@@ -172,6 +172,9 @@ SolverVariant solverVariant();
 // fit a workgroup's LDS: same code, same order of operations, same bits.
 __global__ void refitGlobalKernel(PhysArgs P);
 __global__ void findOverlapsGlobalKernel(PhysArgs P);
+__global__ void dfsStageKernel(PhysArgs P);
+__global__ void dfsCountKernel(PhysArgs P);
+__global__ void dfsWriteKernel(PhysArgs P);
 __global__ void findOverlapsSmallKernel(PhysArgs P);
 __global__ void narrowSATGlobalKernel(PhysArgs P);
 __global__ void narrowContactGlobalKernel(PhysArgs P);
@@ -594,6 +597,9 @@ size_t contactImageBytes(const PhysArgs &P);
 #endif
 constexpr int32_t kOverlapBlock = MW_OVERLAP_BLOCK;
 constexpr int32_t kOverlapSmallLeaves = 256;   // findOverlapsSmallKernel: the bitmask path only
+constexpr int32_t kDfsBlock = 256;             // dfs*Kernel: body rows per block
+constexpr size_t kOrderedLeafBytes = 48;       // broadphase.hip OrderedLeaf
+constexpr int32_t kOverlapBufRanks = 12;       // broadphase.hip kOverlapBuf
 constexpr int32_t kNarrowBlock = 256;
 #ifndef MW_CONTACT_BLOCK
 #define MW_CONTACT_BLOCK 128

@@ -227,6 +227,16 @@ struct PhysArgs {
     char *overlapImage;           // [W][findOverlapsImageBytes] leaf image per world
     int32_t overlapDFSLeaves;     // findOverlaps: worlds with more leaves traverse the BVH
                                   // (stack DFS) instead of sweeping every leaf; -1: never
+    // Traversal worlds' slabs (null unless some world can traverse): the
+    // emission-order leaf image, per-leaf keys, and per body row its first
+    // hit ranks, its count | wide flag and leaf id, per row chunk its total
+    char *dfsImage;               // [W][maxLeaves] OrderedLeaf (48 B)
+    int32_t *dfsKeys;             // [W][maxLeaves][2] entity id, rank << 1 | static
+    uint16_t *dfsHits;            // [W][dfsRowCap][kOverlapBuf]
+    int32_t *dfsRows;             // [W][dfsRowCap][2] count | kDfsWide, leaf id
+    int32_t *dfsChunkTotals;      // [W][dfsChunks]
+    int32_t dfsChunks;            // row chunks of kDfsBlock (0: no traversal kernels)
+    int32_t dfsRowCap;            // dfsChunks * kDfsBlock
     int32_t refitLDSNodes;        // refitKernel's LDS node capacity: a world with more
                                   // used nodes walks its slab in place (same result)
     int32_t refitGlobal;          // refit walks the node slab in place

@@ -6,9 +6,10 @@ findOverlapsKernel / findOverlapsGlobalKernel per launch.
   python tools/overlap_scale.py --compare      # the traversal's scaling
 
 --compare times the traversal at 800 and 3200 cubes per world and the
-sweep at 3200 (64 worlds: one block's latency, not throughput) in child
-processes and prints the ratios (round 5: 8.3x for 4x the bodies, the
-sweep 4x slower than the traversal at 3200).  A wall-clock check, so it
+sweep at 3200 (64 worlds) in child processes and prints the ratios
+(round 5, one block per world: 0.28 / 2.31 ms, 8.3x for 4x the bodies;
+round 6, the walk over (world, 256-row chunk) blocks: 0.082 / 0.256 ms,
+3.1x, the one-block sweep 38x slower than the traversal at 3200).  A wall-clock check, so it
 lives here and not in the -m gpu parity suite."""
 import os
 import sys
