@@ -1610,9 +1610,10 @@ __device__ __forceinline__ void narrowSATBlock(const PhysArgs &P)
             atomicOr(P.errorFlags, kErrIndexGuard | (kGuardWork << 8));
         }
         if (lane == 0 && P.hhJobs) {
-            if (job.kind == kJobNone) {
-                P.hhJobs[idx].kind = kJobNone;
-            } else {
+            // the kind byte always, the 80-byte job only for a contact (a
+            // separated pair's record is never read)
+            P.hhKinds[idx] = (int8_t)job.kind;
+            if (job.kind != kJobNone) {
                 job.pair = unpackSat(P, s_arch, pw);
                 P.hhJobs[idx] = job;
             }
@@ -1722,7 +1723,7 @@ __device__ __forceinline__ void narrowContactBlock(const PhysArgs &P)
 #pragma unroll
     for (int32_t q = 0; q < kContactChunk; q++) {
         const int32_t i = c0 + q * kContactBlock + threadIdx.x;
-        const bool has = i < total && P.hhJobs[i].kind != kJobNone;   // separated: only the kind was written
+        const bool has = i < total && P.hhKinds[i] != (int8_t)kJobNone;
         const uint64_t m = __ballot(has);
         int32_t wb = 0;
         if ((threadIdx.x & 63) == 0 && m) wb = atomicAdd(&s_njobs, (int32_t)__popcll(m));

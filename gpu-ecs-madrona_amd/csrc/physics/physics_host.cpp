@@ -252,6 +252,7 @@ void PhysicsModule::buildArgs(void *stream)
     P.nextSatWork = P.satWorkSet[1];
     P.nextSatWorkCount = P.satWorkCountSet[1];
     P.hhJobs = alloc<ContactJob>((size_t)W * P.candCapacity, stream);
+    P.hhKinds = alloc<int8_t>((size_t)W * P.candCapacity, stream);
     P.candContacts = alloc<Contact>((size_t)W * P.candCapacity, stream);
     P.maxContacts = maxContacts;
     P.contactOrder = alloc<int32_t>((size_t)W * P.candCapacity, stream);

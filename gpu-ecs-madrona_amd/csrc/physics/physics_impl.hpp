@@ -187,8 +187,10 @@ struct PhysArgs {
     int32_t *satWorkCountSet[2];
     struct PackedSatWork *nextSatWork;
     int32_t *nextSatWorkCount;
-    ContactJob *hhJobs;           // [W * candCapacity] SAT verdict per satWork entry (only
-                                  // the kind when separated)
+    ContactJob *hhJobs;           // [W * candCapacity] SAT verdict per satWork entry (written
+                                  // only when the pair is not separated)
+    int8_t *hhKinds;              // [W * candCapacity] the verdict's kind per entry: the
+                                  // contact kernel scans these bytes, not 80-byte jobs
     int32_t contactGrid;          // persistent contact-kernel grid (blocks)
     int32_t planeGeoBytes;        // plane kernel's LDS copy of the hull tables (0: read
                                   // them from HBM; tables too large)
