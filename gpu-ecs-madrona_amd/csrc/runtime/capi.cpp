@@ -749,7 +749,7 @@ extern "C" int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t 
     MW_TRY({
         phys::PhysArgs *P = phys::physicsArgs(exec->exec->stateManager());
         if (!P || !out) return -1;
-        int32_t v[10];
+        int32_t v[11];
         v[0] = P->refitGlobal != 0;
         v[1] = P->overlapImage != nullptr;
         v[2] = P->satImage != nullptr;
@@ -761,7 +761,8 @@ extern "C" int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t 
         const phys::PhysicsModule &M = phys::physicsModule(exec->exec->stateManager());
         v[8] = M.solverLanes;
         v[9] = (int32_t)(M.solverItemsPerLevel * 100.0 + 0.5);
-        for (int32_t i = 0; i < n && i < 10; i++) out[i] = v[i];
-        return 10;
+        v[10] = P->dfsChunks > 0;
+        for (int32_t i = 0; i < n && i < 11; i++) out[i] = v[i];
+        return 11;
     }, -1)
 }

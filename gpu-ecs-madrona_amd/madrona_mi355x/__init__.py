@@ -701,13 +701,14 @@ class CollisionsSim(Executor):
         """{kernel: True when it runs its global-image variant} (mw_create
         decides per LDS image; plane_lds / sat_lds: the plane / SAT kernel's
         LDS hull tables; sat_mink: the SAT edge query's Minkowski tables)."""
-        out = np.zeros(10, np.int32)
-        if self._lib.mw_phys_kernel_variants(self.h, out.ctypes.data_as(ctypes.c_void_p), 10) < 0:
+        out = np.zeros(11, np.int32)
+        if self._lib.mw_phys_kernel_variants(self.h, out.ctypes.data_as(ctypes.c_void_p), 11) < 0:
             raise _err(self._lib)
         keys = ("refit", "find_overlaps", "sat", "contact", "solver", "plane_lds", "sat_lds", "sat_mink")
         d = {k: bool(v) for k, v in zip(keys, out)}
         d["solver_lanes"] = int(out[8])     # lanes per world the solver runs (64 or 32)
         d["solver_items_per_level"] = out[9] / 100.0   # what the last lane check read
+        d["overlap_traversal"] = bool(out[10])  # worlds past the DFS threshold walk the BVH
         return d
 
     def bvh(self, w, cap=4096):

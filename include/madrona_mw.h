@@ -267,8 +267,9 @@ int32_t mw_phys_take_units(mw_exec *exec, int64_t *out);
  * MADRONA_MW_SAT_TABLES=0 at mw_create turns them off); out[8]: the solver's
  * lanes per world (64, or 32 once the executor has measured narrow
  * dependency levels; MADRONA_MW_SOLVER_LANES=32|64|auto), out[9]: the items
- * per dependency level (x100) the last lane check read.  Returns 10, or -1
- * without physics.
+ * per dependency level (x100) the last lane check read, out[10] = 1 when
+ * worlds past MADRONA_MW_OVERLAP_DFS_LEAVES leaves (default 512) can walk the
+ * BVH (the traversal launches exist).  Returns 11, or -1 without physics.
  * MADRONA_MW_FORCE_GLOBAL_IMAGES=1 at mw_create forces the global variants. */
 int32_t mw_phys_kernel_variants(mw_exec *exec, int32_t *out, int32_t n);
 

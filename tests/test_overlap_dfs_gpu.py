@@ -30,6 +30,40 @@ def test_dfs_forced_on_collisions_worlds_bit_exact(monkeypatch):
     assert np.all(c > 0), c
 
 
+def test_dfs_forced_on_simple_worlds_spans_body_archetypes(monkeypatch):
+    """Threshold 0 on simple_taskgraph: its bodies live in two archetypes
+    (spheres, then the agent), so one 256-row chunk of the traversal kernels
+    numbers rows across both, as the sweep does; bodies equal the oracle's
+    every step (candidate order feeds the contact order, hence the bits)."""
+    import madrona_mi355x as mw
+    import oracle_lib as ol
+    from test_collisions_gpu import _cfg_pair, _diff
+    monkeypatch.setenv("MADRONA_MW_OVERLAP_DFS_LEAVES", "0")
+    gcfg, ocfg = _cfg_pair(num_cubes=100)
+    W = 4
+    pos, rot = ol.gen_collisions_inits(W, 100, seed=3)
+    sim = mw.SimpleSim(W, pos, rot, gcfg)
+    assert sim.kernel_variants()["overlap_traversal"]
+    orc = ol.OracleSimple(ocfg, pos, rot)
+    for s in range(1, 121):
+        sim.step(1)
+        orc.step(1)
+        for w in range(W):
+            d = _diff(sim.bodies(w), orc.bodies(w))
+            assert d is None, f"step {s} world {w}: {d}"
+    assert sim.error_flags() == 0, mw.ERR_BITS
+
+
+def test_default_small_worlds_do_not_launch_the_traversal():
+    """129-leaf collisions worlds stay on the one-block sweep kernels: the
+    traversal launches are not created below the threshold."""
+    import madrona_mi355x as mw
+    W, n = 2, 128
+    pos, rot = gen_collisions_inits(W, n, seed=1)
+    sim = mw.CollisionsSim(W, pos, rot, mw.default_collisions_config(n, 4, 2048, 2048))
+    assert not sim.kernel_variants()["overlap_traversal"]
+
+
 @pytest.mark.parametrize("dfs_leaves", ["512", "-1"])
 def test_large_world_traversal_and_sweep_bit_exact(monkeypatch, dfs_leaves):
     """1200 cubes per world (past the default threshold): the traversal
