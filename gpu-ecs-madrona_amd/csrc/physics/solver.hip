@@ -515,20 +515,31 @@ __device__ __forceinline__ int32_t solveContactVelocitiesT(SMut &b1, SMut &b2, c
     Vector3 v1 = b1.v, o1v = b1.omega, v2 = b2.v, o2v = b2.omega;
     const Vector3 n = k.n;
 
+    // The world-space lever arms q.rotateVec(r_local): q is fixed during
+    // this phase, so a skipping solve (whose registers are not the kernel's
+    // peak: the general solve sets it) computes each once instead of once per
+    // use -- the same operations on the same inputs, so the same bits.
+#ifndef MW_SOLVER_VEL_ARMS
+#define MW_SOLVER_VEL_ARMS 1
+#endif
+    constexpr bool kArms = MW_SOLVER_VEL_ARMS >= 1 && sk;
+    // ... and (level 2) the moving side's angular terms of the normal
+    // impulse, ra = I^-1 (r x n_local) and w = m^-1 + ta . ra, which both
+    // iterations apply unchanged
+    constexpr bool kTerms = MW_SOLVER_VEL_ARMS >= 2 && sk;
+    Vector3 arm[4], rac[4];
+    float wc[4];
     // relVel (physics.cpp:716-722) as t1 - t2, a skipped side's term = +0
-    auto rel = [&](int32_t, Vector3 r1l, Vector3 r2l) {
+    auto rel = [&](int32_t i, Vector3 r1l, Vector3 r2l) {
         Vector3 t1 = Vector3::zero(), t2 = Vector3::zero();
-        if (!sk1) t1 = v1 + cross(o1v, q1.rotateVec(r1l));
-        if (!sk2) t2 = v2 + cross(o2v, q2.rotateVec(r2l));
+        if (!sk1) t1 = v1 + cross(o1v, kArms ? arm[i] : q1.rotateVec(r1l));
+        if (!sk2) t2 = v2 + cross(o2v, kArms ? arm[i] : q2.rotateVec(r2l));
         return t1 - t2;
     };
     // applyVelocityUpdate (physics.cpp:724-750), false on a non-finite
-    // magnitude when a side is skipped (nothing is written then)
-    auto apply = [&](Vector3 ta1, Vector3 ta2, Vector3 dv, float mag) {
-        Vector3 ra1 = Vector3::zero(), ra2 = Vector3::zero();
-        float w1 = 0.f, w2 = 0.f;
-        if (!sk1) { ra1 = multDiag(k.iI1, ta1); w1 = k.im1 + dot(ta1, ra1); }
-        if (!sk2) { ra2 = multDiag(k.iI2, ta2); w2 = k.im2 + dot(ta2, ra2); }
+    // magnitude when a side is skipped (nothing is written then); applyRW
+    // takes the sides' angular terms ready-made
+    auto applyRW = [&](Vector3 ra1, float w1, Vector3 ra2, float w2, Vector3 dv, float mag) {
         mag *= 1.f / (w1 + w2);
         if (sk && !finiteF(mag)) return false;
         if (!sk1) {
@@ -540,6 +551,13 @@ __device__ __forceinline__ int32_t solveContactVelocitiesT(SMut &b1, SMut &b2, c
             o2v -= q2.rotateVec(mag * ra2);
         }
         return true;
+    };
+    auto apply = [&](Vector3 ta1, Vector3 ta2, Vector3 dv, float mag) {
+        Vector3 ra1 = Vector3::zero(), ra2 = Vector3::zero();
+        float w1 = 0.f, w2 = 0.f;
+        if (!sk1) { ra1 = multDiag(k.iI1, ta1); w1 = k.im1 + dot(ta1, ra1); }
+        if (!sk2) { ra2 = multDiag(k.iI2, ta2); w2 = k.im2 + dot(ta2, ra2); }
+        return applyRW(ra1, w1, ra2, w2, dv, mag);
     };
 
     // Per point only the body-local lever arms and the pre-solve normal
@@ -569,6 +587,12 @@ __device__ __forceinline__ int32_t solveContactVelocitiesT(SMut &b1, SMut &b2, c
             t2 = pv2.v + cross(pv2.omega, ps2.q.rotateVec(r2l[i]));
         }
         vn_bars[i] = dot(n, t1 - t2);
+        if constexpr (kArms) arm[i] = sk1 ? q2.rotateVec(r2l[i]) : q1.rotateVec(r1l[i]);
+        if constexpr (kTerms) {
+            const Vector3 ta = sk1 ? cross(r2l[i], nl2) : cross(r1l[i], nl1);
+            rac[i] = multDiag(sk1 ? k.iI2 : k.iI1, ta);
+            wc[i] = (sk1 ? k.im2 : k.im1) + dot(ta, rac[i]);
+        }
     }
     for (int it = 0; it < 2; it++) {                       // :813-863
 #pragma unroll
@@ -579,7 +603,13 @@ __device__ __forceinline__ int32_t solveContactVelocitiesT(SMut &b1, SMut &b2, c
             float e = 0.3f;
             if (fabsf(vn_bar) <= rest_thresh) e = 0.f;
             float mag = fminRef(-e * vn_bar, 0) - vn;
-            if (!apply(cross(r1l[i], nl1), cross(r2l[i], nl2), n, mag)) return kSolveNonFinite;
+            if constexpr (kTerms) {
+                const bool ok = sk1 ? applyRW(Vector3::zero(), 0.f, rac[i], wc[i], n, mag)
+                                    : applyRW(rac[i], wc[i], Vector3::zero(), 0.f, n, mag);
+                if (!ok) return kSolveNonFinite;
+            } else {
+                if (!apply(cross(r1l[i], nl1), cross(r2l[i], nl2), n, mag)) return kSolveNonFinite;
+            }
         }
     }
 #pragma unroll
