@@ -516,24 +516,31 @@ __device__ __forceinline__ int32_t solveContactVelocitiesT(SMut &b1, SMut &b2, c
     const Vector3 n = k.n;
 
     // The world-space lever arms q.rotateVec(r_local): q is fixed during
-    // this phase, so a skipping solve (whose registers are not the kernel's
-    // peak: the general solve sets it) computes each once instead of once per
-    // use -- the same operations on the same inputs, so the same bits.
+    // this phase, so they are computed once per point instead of at each of
+    // their three uses -- the same operations on the same inputs, so the
+    // same bits -- wherever the registers are free: in the skipping solves
+    // (the general solve sets the kernel's register peak), and in the general
+    // solve too where LDS, not registers, bounds residency (the 32-lane
+    // variant: two worlds' images per block).  Level 2 also keeps each
+    // moving side's angular terms of the normal impulse, ra = I^-1 (r x n_l)
+    // and w = m^-1 + ta . ra, which both iterations apply unchanged.
 #ifndef MW_SOLVER_VEL_ARMS
 #define MW_SOLVER_VEL_ARMS 1
 #endif
-    constexpr bool kArms = MW_SOLVER_VEL_ARMS >= 1 && sk;
-    // ... and (level 2) the moving side's angular terms of the normal
-    // impulse, ra = I^-1 (r x n_local) and w = m^-1 + ta . ra, which both
-    // iterations apply unchanged
-    constexpr bool kTerms = MW_SOLVER_VEL_ARMS >= 2 && sk;
-    Vector3 arm[4], rac[4];
-    float wc[4];
+#ifndef MW_SOLVER_GENERAL_CACHE
+#define MW_SOLVER_GENERAL_CACHE (MW_SOLVER_LANES == 32)
+#endif
+    constexpr bool kCache = sk || MW_SOLVER_GENERAL_CACHE;
+    constexpr bool kArms1 = MW_SOLVER_VEL_ARMS >= 1 && kCache && !sk1;
+    constexpr bool kArms2 = MW_SOLVER_VEL_ARMS >= 1 && kCache && !sk2;
+    constexpr bool kTerms = MW_SOLVER_VEL_ARMS >= 2 && kCache;
+    Vector3 arm1[4], arm2[4], rac1[4], rac2[4];
+    float wc1[4], wc2[4];
     // relVel (physics.cpp:716-722) as t1 - t2, a skipped side's term = +0
     auto rel = [&](int32_t i, Vector3 r1l, Vector3 r2l) {
         Vector3 t1 = Vector3::zero(), t2 = Vector3::zero();
-        if (!sk1) t1 = v1 + cross(o1v, kArms ? arm[i] : q1.rotateVec(r1l));
-        if (!sk2) t2 = v2 + cross(o2v, kArms ? arm[i] : q2.rotateVec(r2l));
+        if (!sk1) t1 = v1 + cross(o1v, kArms1 ? arm1[i] : q1.rotateVec(r1l));
+        if (!sk2) t2 = v2 + cross(o2v, kArms2 ? arm2[i] : q2.rotateVec(r2l));
         return t1 - t2;
     };
     // applyVelocityUpdate (physics.cpp:724-750), false on a non-finite
@@ -587,11 +594,21 @@ __device__ __forceinline__ int32_t solveContactVelocitiesT(SMut &b1, SMut &b2, c
             t2 = pv2.v + cross(pv2.omega, ps2.q.rotateVec(r2l[i]));
         }
         vn_bars[i] = dot(n, t1 - t2);
-        if constexpr (kArms) arm[i] = sk1 ? q2.rotateVec(r2l[i]) : q1.rotateVec(r1l[i]);
+        if constexpr (kArms1) arm1[i] = q1.rotateVec(r1l[i]);
+        if constexpr (kArms2) arm2[i] = q2.rotateVec(r2l[i]);
         if constexpr (kTerms) {
-            const Vector3 ta = sk1 ? cross(r2l[i], nl2) : cross(r1l[i], nl1);
-            rac[i] = multDiag(sk1 ? k.iI2 : k.iI1, ta);
-            wc[i] = (sk1 ? k.im2 : k.im1) + dot(ta, rac[i]);
+            rac1[i] = rac2[i] = Vector3::zero();
+            wc1[i] = wc2[i] = 0.f;
+            if (!sk1) {
+                const Vector3 ta = cross(r1l[i], nl1);
+                rac1[i] = multDiag(k.iI1, ta);
+                wc1[i] = k.im1 + dot(ta, rac1[i]);
+            }
+            if (!sk2) {
+                const Vector3 ta = cross(r2l[i], nl2);
+                rac2[i] = multDiag(k.iI2, ta);
+                wc2[i] = k.im2 + dot(ta, rac2[i]);
+            }
         }
     }
     for (int it = 0; it < 2; it++) {                       // :813-863
@@ -604,9 +621,7 @@ __device__ __forceinline__ int32_t solveContactVelocitiesT(SMut &b1, SMut &b2, c
             if (fabsf(vn_bar) <= rest_thresh) e = 0.f;
             float mag = fminRef(-e * vn_bar, 0) - vn;
             if constexpr (kTerms) {
-                const bool ok = sk1 ? applyRW(Vector3::zero(), 0.f, rac[i], wc[i], n, mag)
-                                    : applyRW(rac[i], wc[i], Vector3::zero(), 0.f, n, mag);
-                if (!ok) return kSolveNonFinite;
+                if (!applyRW(rac1[i], wc1[i], rac2[i], wc2[i], n, mag)) return kSolveNonFinite;
             } else {
                 if (!apply(cross(r1l[i], nl1), cross(r2l[i], nl2), n, mag)) return kSolveNonFinite;
             }
