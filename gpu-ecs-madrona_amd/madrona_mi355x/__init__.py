@@ -823,7 +823,10 @@ class SimpleSim(CollisionsSim):
     archetypes (Sphere: objects + test object, Agent)."""
     SPHERE, AGENT = BODY_ARCHETYPE, BODY_ARCHETYPE + 1
 
-    def __init__(self, num_worlds, pos, rot, cfg=None, gpu_id=0, use_graph=True, **kw):
+    def __init__(self, num_worlds, pos, rot, cfg=None, gpu_id=0, use_graph=True,
+                 env="simple_taskgraph", **kw):
+        # env: a loaded world with simple_taskgraph's config, inits and body
+        # archetypes (tests/ext_env/phys_grow.hip)
         cfg = cfg or default_collisions_config(num_cubes=pos.shape[1])
         self._pos = np.ascontiguousarray(pos, np.float32)
         self._rot = np.ascontiguousarray(rot, np.float32)
@@ -833,9 +836,9 @@ class SimpleSim(CollisionsSim):
             inits[w].rot = self._rot.ctypes.data + w * cfg.num_cubes * 16
         self.cfg = cfg
         self.num_bodies = cfg.num_cubes + 2
-        Executor.__init__(self, "simple_taskgraph", num_worlds, cfg, inits,
-                          ctypes.sizeof(CollisionsInit), gpu_id=gpu_id, default_capacity=64,
-                          use_graph=use_graph, **kw)
+        kw.setdefault("default_capacity", 64)
+        Executor.__init__(self, env, num_worlds, cfg, inits,
+                          ctypes.sizeof(CollisionsInit), gpu_id=gpu_id, use_graph=use_graph, **kw)
 
     def bodies(self, w):
         """Sphere rows then Agent rows (the reference query order)."""
