@@ -1127,6 +1127,21 @@ __global__ void __launch_bounds__(kNarrowBlock) narrowFilterKernel(PhysArgs P)
     if (threadIdx.x == 0) P.survCount[w] = S;
 }
 
+// The same filter with one wave per world (the solver tail's
+// filterWorldOnWave on substep 0's list set, its boxes read from the
+// integration's BodyBox slab): no block barriers, and four worlds per
+// 256-lane block in flight independently -- narrowFilterKernel's world waits
+// for its whole block at the scan.  Same survivors, slots and list entries
+// (their order within a bin differs, which no reader depends on).
+__global__ void __launch_bounds__(kNarrowBlock) narrowFilterWaveKernel(PhysArgs P)
+{
+    MW_TRACE_BLOCK(0);
+    const int32_t w = blockIdx.x * (kNarrowBlock / 64) + (int32_t)(threadIdx.x >> 6);
+    if (w >= P.numWorlds) return;
+    filterWorldOnWave(P, w, P.bodyBoxes + (size_t)w * P.maxBodiesPerWorld, (int32_t)(threadIdx.x & 63),
+                      P.satWork, P.satWorkCount);
+}
+
 // The plane kernel's LDS copy of the hull tables it walks (hulls, vertices,
 // face planes, half-edges, face polygons): each pair's vertex / face scans
 // and incident-face walk are chains of dependent reads over a few hundred

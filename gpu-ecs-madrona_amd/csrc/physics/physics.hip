@@ -233,6 +233,7 @@ void PhysicsModule::upload(void *stream_ptr)
     P.solverImage = solverImages[solverLanes == 32];
     // the remaining kernels stage nothing of variable size
     hipx::residentBlocks((const void *)&narrowFilterKernel, "narrowFilterKernel", kNarrowBlock, 0);
+    hipx::residentBlocks((const void *)&narrowFilterWaveKernel, "narrowFilterWaveKernel", kNarrowBlock, 0);
     uploaded = true;
 }
 
@@ -508,8 +509,16 @@ struct NarrowphaseNode : PhysNodeBase {
     {
         const PhysArgs Q = substepArgs(self->mod->args, self->substep, false);
         hipStream_t stream = (hipStream_t)lc.stream;
-        if (self->substep == 0)
-            MW_LAUNCH(narrowFilterKernel, dim3(Q.numWorlds), dim3(kNarrowBlock), 0, stream, Q);
+        if (self->substep == 0) {
+#ifndef MW_FILTER_WAVE
+#define MW_FILTER_WAVE 1
+#endif
+            if (MW_FILTER_WAVE)
+                MW_LAUNCH(narrowFilterWaveKernel, dim3((Q.numWorlds + kNarrowBlock / 64 - 1) / (kNarrowBlock / 64)),
+                          dim3(kNarrowBlock), 0, stream, Q);
+            else
+                MW_LAUNCH(narrowFilterKernel, dim3(Q.numWorlds), dim3(kNarrowBlock), 0, stream, Q);
+        }
         // The hull-plane pairs share nothing with the hull-hull ones (own
         // list, own contact slots): their kernel runs on the side stream,
         // beside SAT + contact clipping (a parallel branch of the graph).

@@ -140,6 +140,7 @@ __global__ void refitKernel(PhysArgs P);
 __global__ void findOverlapsKernel(PhysArgs P);
 __global__ void integrateKernel(PhysArgs P);
 __global__ void narrowFilterKernel(PhysArgs P);
+__global__ void narrowFilterWaveKernel(PhysArgs P);
 __global__ void narrowSATKernel(PhysArgs P);         // hull tables in LDS (satGeoBytes > 0)
 __global__ void narrowSATNoGeoKernel(PhysArgs P);    // hull tables read from HBM
 __global__ void narrowPlaneKernel(PhysArgs P);        // hull tables staged into LDS
@@ -484,8 +485,10 @@ __device__ __forceinline__ T worldBroadcast(T x, int32_t src)
 // env-steps/s without it.)
 constexpr int32_t kFilterBatch = 8;
 
+// `sets`, `set_counts`: the list set it appends to (the solver tail: the
+// next substep's, nextSatWork; narrowFilterWaveKernel: substep 0's).
 __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, const BodyBox *boxes,
-                                                  int32_t lane)
+                                                  int32_t lane, PackedSatWork *sets, int32_t *set_counts)
 {
     const int32_t cap = P.candCapacity;
     const int32_t num = min(P.numCands[w], cap);
@@ -493,9 +496,9 @@ __device__ __forceinline__ void filterWorldOnWave(const PhysArgs &P, int32_t w, 
     const uint64_t *slots = P.candSlots + (size_t)w * cap;
     uint32_t *info = P.survInfo + (size_t)w * cap;
     const int32_t bin = w % kNarrowBins;
-    PackedSatWork *list = P.nextSatWork + (size_t)bin * P.binCap;
+    PackedSatWork *list = sets + (size_t)bin * P.binCap;
     PackedSatWork *list_back = list + P.binCap - 1;        // plane entries grow down
-    int32_t *counts = P.nextSatWorkCount + bin * kBinStride;
+    int32_t *counts = set_counts + bin * kBinStride;
     constexpr uint32_t kHull = (uint32_t)CollisionPrimitive::Type::Hull;
     constexpr uint32_t kHullPlane = kHull | (uint32_t)CollisionPrimitive::Type::Plane;
     constexpr int32_t kBatch = kSolverBlock * kFilterBatch;

@@ -1282,7 +1282,7 @@ __device__ __forceinline__ void writeWorldBodies(const PhysArgs &P, int32_t w, S
     if (lane == 0) P.solver[w].numContacts = 0;           // physics.cpp:1007
     if (integrate_next) {
         waveSync();
-        filterWorldOnWave(P, w, boxes, lane);
+        filterWorldOnWave(P, w, boxes, lane, P.nextSatWork, P.nextSatWorkCount);
     }
 }
 

@@ -33,6 +33,7 @@ NODE_OF = {
     "findOverlapsGlobalKernel": ("FindOverlappingNode", 1),
     "integrateKernel": ("SubstepRigidBodiesNode", 1),     # substep 0 only (later: solver tail)
     "narrowFilterKernel": ("NarrowphaseNode", 1),         # substep 0 only (later: solver tail)
+    "narrowFilterWaveKernel": ("NarrowphaseNode", 1),     # the same, a wave per world
     "solverOrderKernel": ("NarrowphaseNode", 4),
     "narrowSATKernel": ("NarrowphaseNode", 4),
     "narrowSATNoGeoKernel": ("NarrowphaseNode", 4),      # hull tables read from HBM
